@@ -1,0 +1,170 @@
+/* cfm.h — C ABI of the MI355X-native Conformer encoder hot path (libcfm.so).
+ *
+ * Plain C: raw device pointers, sizes and a hipStream_t passed as void*.  No torch types.
+ * Every entry point is stream-ordered (no host synchronisation), allocates no device memory
+ * (callers pass workspaces), keeps no pointer after return, and returns 0 on success or a
+ * negative CFM_ERR_* code; cfm_get_last_error() returns the thread's last message.
+ *
+ * The reference (icadriani/nn_conformer_for_speech_recognition) has no FFI: its hot path is a
+ * composition of torch.nn modules.  Each entry point below names the reference module/op it
+ * replaces (file:line under /root/reference, or torchaudio semantics restated in
+ * oracle/conformer.py); INTEGRATION.md shows the ctypes binding the host side uses.
+ *
+ * Layouts: activations are token-major (row = b*T + t, feature contiguous), matching
+ * torchaudio's (B, T, D) interface after its internal transpose.  dtype codes: CFM_F32 / CFM_BF16.
+ */
+#ifndef CFM_H
+#define CFM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CFM_F32 0
+#define CFM_BF16 1
+
+#define CFM_OK 0
+#define CFM_ERR_ARG (-1)
+#define CFM_ERR_SHAPE (-2)
+#define CFM_ERR_DTYPE (-3)
+#define CFM_ERR_ALIGN (-4)
+#define CFM_ERR_UNSUPPORTED (-5)
+#define CFM_ERR_LAUNCH (-6)
+
+#define CFM_ACT_NONE 0
+#define CFM_ACT_SILU 1
+
+int cfm_version(void);
+const char* cfm_get_last_error(void);
+
+/* y[i] = (dy)x[i] for n elements (dtype conversion; fp32 master weights -> bf16 compute copies). */
+int cfm_cast(const void* x, int dtype_x, void* y, int dtype_y, long n, void* stream);
+
+/* ---------------------------------------------------------------- SpecAugment
+ * Replaces ASRNN.SpecAugment / time_warping / frequency_masking / time_masking
+ * (lib/standard/asrnn.py:91-192).  The random draws stay on the host (python `random`, the
+ * reference's own RNG, in the reference's order); this kernel applies them in ONE pass:
+ * y[b,f,t] = x[b,f,Wt_b(t)] (warp passes composed), then the masks when intended != 0
+ * (the reference's masks are no-ops as shipped, asrnn.py:141,165).
+ * params (device int32): [n_warp, n_freq, n_time, 0,
+ *                         n_warp x B x (w, w0, tau), n_freq x (f0, f), n_time x B x (t0, t)]
+ * x, y: (B, F, T) fp32, may not alias. */
+int cfm_specaug_apply(const float* x, float* y, int B, int F, int T, const int32_t* params,
+                      int n_params, int intended, float mask_value, void* stream);
+
+/* ---------------------------------------------------------------- GEMM (MFMA)
+ * C[z][m][n] = epilogue( alpha * sum_k A(m,k) * B(n,k) )  for z in [0, batch).
+ * Serves every dense contraction of the encoder (torch.nn.Linear / 1x1 Conv1d forward,
+ * input-grad and weight-grad): FFN (torchaudio _FeedForwardModule), MHSA in/out projections
+ * (nn.MultiheadAttention), point-wise convs (_ConvolutionModule), the front-end projection
+ * (asrnn.py:208 / frame projection) and the projection block (asrnn.py:73-89).
+ *   A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]
+ *   B(n,k) = B[n*ldb + k] if b_kmajor else B[k*ldb + n]
+ * Epilogue, in order: v = alpha*acc + bias[n];  v *= act'(pre[m,n]) if act_grad;
+ *   if act == SILU { pre[m,n] = v (if pre != NULL); v = silu(v) };  v *= dropout(seed, idx);
+ *   v *= out_scale;  v += residual[m,n];  C = v  (or atomically C += v when split_k > 1).
+ * dtype_ab is the operand type (fp32 operands run on the exact-f32 MFMA path). */
+typedef struct cfm_gemm_desc {
+  int M, N, K, batch;
+  int dtype_ab;
+  const void* A; long lda; long stride_a; int a_kmajor;
+  const void* B; long ldb; long stride_b; int b_kmajor;
+  void* C; long ldc; long stride_c; int dtype_c;
+  float alpha;
+  const float* bias;
+  int act;                 /* CFM_ACT_NONE | CFM_ACT_SILU */
+  int act_grad;            /* multiply by silu'(pre) (backward of a SILU epilogue) */
+  void* pre; int dtype_pre;
+  float drop_p; uint64_t drop_seed; uint64_t drop_offset;
+  float out_scale;
+  const void* residual; long ldr; int dtype_r;
+  int split_k;             /* >1: C must be fp32 and pre-initialised; partial sums are added */
+} cfm_gemm_desc;
+int cfm_gemm(const cfm_gemm_desc* d, void* stream);
+
+/* out[n] (+)= sum_m x[m*ld + n]  — bias gradients (sum over tokens).  ws: >= 4*N*64 bytes. */
+int cfm_colsum(const void* x, int dtype_x, long M, int N, long ld, float* out, int accumulate,
+               float* ws, void* stream);
+
+/* ---------------------------------------------------------------- LayerNorm (nn.LayerNorm(D))
+ * Forward: y = (x-mean)*rstd*gamma + beta; saves mean/rstd per row.
+ * Backward: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)) + dres, g = dy*gamma;
+ * dgamma/dbeta accumulate (+=) over rows.  ws: >= 8*D*nblk bytes, see cfm_layernorm_ws_bytes. */
+int cfm_layernorm_fwd(const void* x, int dtype_x, const float* gamma, const float* beta, void* y,
+                      int dtype_y, float* mean, float* rstd, long M, int D, float eps, void* stream);
+size_t cfm_layernorm_ws_bytes(long M, int D);
+int cfm_layernorm_bwd(const void* dy, int dtype_dy, const void* x, int dtype_x, const float* gamma,
+                      const float* mean, const float* rstd, const void* dres, int dtype_dres,
+                      void* dx, int dtype_dx, float* dgamma, float* dbeta, float* ws, long M, int D,
+                      void* stream);
+
+/* y = act(x*scale [dropout]) + residual, elementwise helpers used at residual joins. */
+int cfm_scale_dropout(const void* x, int dtype_x, void* y, int dtype_y, long n, float scale,
+                      float drop_p, uint64_t seed, uint64_t offset, void* stream);
+
+/* ---------------------------------------------------------------- Convolution module
+ * _ConvolutionModule (torchaudio; restated oracle/conformer.py ConvModuleRef):
+ *   a = pw1(LN(x)) (cfm_gemm), g = GLU(a) (dim = channel), y = depthwise_conv_K(g) + b,
+ *   z = SiLU(BatchNorm1d(y)) (train: batch statistics over B*T incl. padded frames),
+ *   out = pw2(z) (cfm_gemm, + residual).
+ * a: (B*T, 2C) token-major; w_dw: (C, K) fp32; y: (B*T, C) fp32.
+ * cfm_glu_dwconv_fwd also produces per-channel partial (sum, sumsq) into ws for BN. */
+size_t cfm_convmod_ws_bytes(int B, int T, int C);
+int cfm_glu_dwconv_fwd(const void* a, int dtype_a, const float* w_dw, const float* b_dw, float* y,
+                       int B, int T, int C, int K, float* ws, void* stream);
+/* finalize BN batch stats from ws partials; update running stats (momentum, unbiased var);
+ * writes mean/invstd (C each).  z = silu(bn(y)) into z (dtype_z). */
+int cfm_bn_silu_fwd(const float* y, const float* gamma, const float* beta, float* running_mean,
+                    float* running_var, float momentum, float eps, int training, float* mean,
+                    float* invstd, void* z, int dtype_z, long M, int C, float* ws, void* stream);
+/* backward of z = silu(bn(y)): dy = BN-bwd(dz*silu'(bn(y))); dgamma, dbeta (=) written. */
+int cfm_bn_silu_bwd(const void* dz, int dtype_dz, const float* y, const float* gamma,
+                    const float* beta, const float* mean, const float* invstd, int training,
+                    float* dy, float* dgamma, float* dbeta, long M, int C, float* ws, void* stream);
+/* backward of y = dwconv(GLU(a)): da (B*T, 2C), dw (C,K) (=), db (C) (=). */
+int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dtype_a, const float* w_dw, void* da,
+                       int dtype_da, float* dw, float* db, int B, int T, int C, int K, float* ws,
+                       void* stream);
+
+/* ---------------------------------------------------------------- Attention
+ * nn.MultiheadAttention(need_weights=False, key_padding_mask) core (torchaudio ConformerLayer
+ * self_attn), optionally with Transformer-XL relative positions (transformers
+ * Wav2Vec2ConformerSelfAttention, scores=((q+u)k^T + (q+v)p_{T-1-i+j}^T)/sqrt(dk)).
+ * qkv: (B*T, 3*H*dk) rows [q | k | v]; o: (B*T, H*dk); lse: (B*H*T) fp32 log-sum-exp per query
+ * (saved for backward); lengths: (B) int32 valid keys.  pos (rel only): (2T-1, H*dk) projected
+ * table; pos_u / pos_v: (H*dk) fp32.  dtype: CFM_BF16 (MFMA) or CFM_F32. */
+int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
+                 const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
+                 float drop_p, uint64_t seed, void* stream);
+size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel);
+int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, const float* lse,
+                 const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
+                 void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H,
+                 int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream);
+
+/* ---------------------------------------------------------------- ConvSubSampling
+ * lib/convsubsampling.py:16-45: Conv2d(1->C1, 7x7, s2) -> Conv2d(C1->C2, 3x3, s2), no padding.
+ * conv1: x (B, F, T) fp32 -> h1 NHWC (B, F1, T1, C1) dtype_h; w1 (C1, 49), b1 (C1).
+ * conv2: implicit GEMM over h1 -> h2 (B, T2, F2, C2) "frame-major" (row = (b,t2), features
+ *        (f2, c2)) so the frame projection reads it as a plain (B*T2, F2*C2) matrix.
+ *        w2r: (C2, 3*3*C1) reordered [c2][kh][kw][c1], dtype of h1. */
+int cfm_conv1_fwd(const float* x, const float* w1, const float* b1, void* h1, int dtype_h, int B,
+                  int F, int T, int C1, void* stream);
+int cfm_conv2_fwd(const void* h1, const void* w2r, const float* b2, void* h2, int dtype_h2,
+                  int dtype, int B, int F1, int T1, int C1, int C2, void* stream);
+/* grads: dh1 from dh2 (transposed conv), dw2r (=), db2 via cfm_colsum; dw1 (=) and db1 (=). */
+int cfm_conv2_bwd_data(const void* dh2, const void* w2r, void* dh1, int dtype, int B, int F1,
+                       int T1, int C1, int C2, void* stream);
+int cfm_conv2_bwd_weight(const void* dh2, const void* h1, float* dw2r, int dtype, int B, int F1,
+                         int T1, int C1, int C2, void* stream);
+size_t cfm_conv1_bwd_ws_bytes(int B, int F, int T, int C1);
+int cfm_conv1_bwd_weight(const void* dh1, int dtype_h, const float* x, float* dw1, float* db1,
+                         int B, int F, int T, int C1, float* ws, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFM_H */

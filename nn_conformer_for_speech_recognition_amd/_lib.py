@@ -1,0 +1,158 @@
+"""ctypes binding of libcfm.so — the C ABI declared in include/cfm.h.
+
+The library is the product: if it is missing, or no GPU is visible, every op raises.  There
+is no CPU / PyTorch fallback anywhere on the hot path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import torch  # noqa: F401  (load torch's libamdhip64 first: libcfm resolves to the same runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcfm.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_SILU = 0, 1
+
+c_void_p, c_int, c_long, c_float, c_size_t = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_size_t
+c_u64 = ctypes.c_uint64
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("M", c_int), ("N", c_int), ("K", c_int), ("batch", c_int),
+        ("dtype_ab", c_int),
+        ("A", c_void_p), ("lda", c_long), ("stride_a", c_long), ("a_kmajor", c_int),
+        ("B", c_void_p), ("ldb", c_long), ("stride_b", c_long), ("b_kmajor", c_int),
+        ("C", c_void_p), ("ldc", c_long), ("stride_c", c_long), ("dtype_c", c_int),
+        ("alpha", c_float),
+        ("bias", c_void_p),
+        ("act", c_int),
+        ("act_grad", c_int),
+        ("pre", c_void_p), ("dtype_pre", c_int),
+        ("drop_p", c_float), ("drop_seed", c_u64), ("drop_offset", c_u64),
+        ("out_scale", c_float),
+        ("residual", c_void_p), ("ldr", c_long), ("dtype_r", c_int),
+        ("split_k", c_int),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "cfm_version": (c_int, []),
+    "cfm_get_last_error": (ctypes.c_char_p, []),
+    "cfm_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_void_p]),
+    "cfm_specaug_apply": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "cfm_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
+    "cfm_colsum": (c_int, [c_void_p, c_int, c_long, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p]),
+    "cfm_layernorm_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                  c_long, c_int, c_float, c_void_p]),
+    "cfm_layernorm_ws_bytes": (c_size_t, [c_long, c_int]),
+    "cfm_layernorm_bwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p]),
+    "cfm_scale_dropout": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_float, c_float, c_u64, c_u64,
+                                  c_void_p]),
+    "cfm_convmod_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "cfm_glu_dwconv_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                   c_void_p, c_void_p]),
+    "cfm_bn_silu_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_int,
+                                c_void_p, c_void_p, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p]),
+    "cfm_bn_silu_bwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p]),
+    "cfm_glu_dwconv_bwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                   c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "cfm_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                             c_int, c_int, c_int, c_float, c_u64, c_void_p]),
+    "cfm_attn_bwd_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "cfm_attn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
+                             c_u64, c_void_p, c_void_p]),
+    "cfm_conv1_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "cfm_conv2_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                              c_int, c_void_p]),
+    "cfm_conv2_bwd_data": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                   c_void_p]),
+    "cfm_conv2_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_void_p]),
+    "cfm_conv1_bwd_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "cfm_conv1_bwd_weight": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                     c_void_p, c_void_p]),
+}
+
+EXPORTED = sorted(k for k in _SIGS)
+
+_lib = None
+MISSING = []
+
+
+class CfmError(RuntimeError):
+    pass
+
+
+def build(verbose=False):
+    """Compile libcfm.so in-tree with hipcc for gfx950 (make -C csrc)."""
+    jobs = str(min(16, os.cpu_count() or 4))
+    r = subprocess.run(["make", "-C", CSRC, "-j", jobs], capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        raise CfmError("libcfm build failed:\n" + (r.stdout or "") + (r.stderr or ""))
+    return LIB_PATH
+
+
+def load():
+    """Load libcfm.so (no GPU work); raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CfmError(f"{LIB_PATH} not found: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                       "(hipcc, gfx950). There is no fallback path.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            MISSING.append(name)
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.cfm_get_last_error().decode(errors="replace")
+        raise CfmError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def size_call(name, *args):
+    return int(getattr(load(), name)(*args))
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL). Tensors must live on the GPU."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise CfmError("cfm ops need GPU tensors (the HIP path has no CPU fallback)")
+    return t.data_ptr()
+
+
+def dt(t):
+    if t is None:
+        return F32
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise CfmError(f"unsupported dtype {t.dtype}")
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream

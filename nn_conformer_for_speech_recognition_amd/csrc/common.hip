@@ -1,0 +1,113 @@
+// common.hip — error plumbing, version, dtype casts and small elementwise kernels.
+#include "cfm_common.h"
+
+namespace cfm {
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CFM_ERR_LAUNCH, std::string(what) + ": " + hipGetErrorString(e));
+  return CFM_OK;
+}
+}  // namespace cfm
+
+CFM_EXPORT int cfm_version(void) { return 1; }
+CFM_EXPORT const char* cfm_get_last_error(void) { return cfm::g_last_error.c_str(); }
+
+namespace {
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long n) {
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long stride = (long)gridDim.x * blockDim.x * 4;
+  for (; i < n; i += stride) {
+    if (i + 4 <= n) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[i + e] = from_f32<TO>(to_f32(x[i + e]));
+    } else {
+      for (long e = i; e < n; ++e) y[e] = from_f32<TO>(to_f32(x[e]));
+    }
+  }
+}
+
+__global__ void scale_dropout_kernel(const void* x, int dtx, void* y, int dty, long n, float scale,
+                                     float p, uint64_t seed, uint64_t off) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    float v = ld_dyn(x, dtx, i) * scale;
+    if (p > 0.f) v *= dropout_scale(p, seed, off + (uint64_t)i);
+    st_dyn(y, dty, i, v);
+  }
+}
+}  // namespace
+
+static int grid_for(long n, int per_thread) {
+  long blocks = (n / per_thread + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 8192) blocks = 8192;
+  return (int)blocks;
+}
+
+CFM_EXPORT int cfm_cast(const void* x, int dtx, void* y, int dty, long n, void* stream) {
+  CFM_REQUIRE(x && y && n >= 0, CFM_ERR_ARG, "bad args");
+  if (n == 0) return CFM_OK;
+  hipStream_t s = cfm::as_stream(stream);
+  dim3 g(grid_for(n, 4)), b(256);
+  if (dtx == CFM_F32 && dty == CFM_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), g, b, 0, s, (const float*)x, (bf16*)y, n);
+  else if (dtx == CFM_BF16 && dty == CFM_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), g, b, 0, s, (const bf16*)x, (float*)y, n);
+  else if (dtx == CFM_F32 && dty == CFM_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), g, b, 0, s, (const float*)x, (float*)y, n);
+  else if (dtx == CFM_BF16 && dty == CFM_BF16)
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), g, b, 0, s, (const bf16*)x, (bf16*)y, n);
+  else
+    return cfm::fail(CFM_ERR_DTYPE, "cfm_cast: dtype");
+  return cfm::check_launch("cfm_cast");
+}
+
+CFM_EXPORT int cfm_scale_dropout(const void* x, int dtx, void* y, int dty, long n, float scale,
+                                 float p, uint64_t seed, uint64_t off, void* stream) {
+  CFM_REQUIRE(x && y && n >= 0, CFM_ERR_ARG, "bad args");
+  if (n == 0) return CFM_OK;
+  hipLaunchKernelGGL(scale_dropout_kernel, dim3(grid_for(n, 1)), dim3(256), 0, cfm::as_stream(stream), x,
+                     dtx, y, dty, n, scale, p, seed, off);
+  return cfm::check_launch("cfm_scale_dropout");
+}
+
+// --------------------------------------------------------------------------- column sums
+namespace {
+// partial sums: grid (ceil(N/256), nblk); each block sums rows [b*rows_per, ...) for 256 cols
+__global__ void colsum_partial(const void* x, int dtx, long M, int N, long ld, long rows_per, float* ws) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const long r0 = (long)blockIdx.y * rows_per;
+  const long r1 = min(M, r0 + rows_per);
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) s += ld_dyn(x, dtx, r * ld + n);
+  ws[(long)blockIdx.y * N + n] = s;
+}
+__global__ void colsum_final(const float* ws, int nblk, int N, float* out, int acc) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += ws[(long)b * N + n];
+  out[n] = acc ? out[n] + s : s;
+}
+}  // namespace
+
+CFM_EXPORT int cfm_colsum(const void* x, int dtx, long M, int N, long ld, float* out, int accumulate,
+                          float* ws, void* stream) {
+  CFM_REQUIRE(x && out && ws && N > 0 && M >= 0 && ld >= N, CFM_ERR_ARG, "bad args");
+  const int nblk = 64;
+  const long rows_per = (M + nblk - 1) / nblk;
+  hipStream_t s = cfm::as_stream(stream);
+  hipLaunchKernelGGL(colsum_partial, dim3(cdiv(N, 256), nblk), dim3(256), 0, s, x, dtx, M, N, ld,
+                     rows_per > 0 ? rows_per : 1, ws);
+  hipLaunchKernelGGL(colsum_final, dim3(cdiv(N, 256)), dim3(256), 0, s, ws, nblk, N, out, accumulate);
+  return cfm::check_launch("cfm_colsum");
+}
