@@ -112,14 +112,16 @@ int cfm_scale_dropout(const void* x, int dtype_x, void* y, int dtype_y, long n, 
  *   out = pw2(z) (cfm_gemm, + residual).
  * a: (B*T, 2C) token-major; w_dw: (C, K) fp32; y: (B*T, C) fp32.
  * cfm_glu_dwconv_fwd also produces per-channel partial (sum, sumsq) into ws for BN. */
-size_t cfm_convmod_ws_bytes(int B, int T, int C);
+size_t cfm_convmod_ws_bytes(int B, int T, int C, int K);
 int cfm_glu_dwconv_fwd(const void* a, int dtype_a, const float* w_dw, const float* b_dw, float* y,
                        int B, int T, int C, int K, float* ws, void* stream);
-/* finalize BN batch stats from ws partials; update running stats (momentum, unbiased var);
- * writes mean/invstd (C each).  z = silu(bn(y)) into z (dtype_z). */
+/* z = silu(bn(y)).  training: batch stats finalised from the partial sums cfm_glu_dwconv_fwd left
+ * in ws (same B, T, C), running stats updated (momentum, unbiased var); eval: running stats.
+ * Writes mean/invstd (C each) for the backward. */
 int cfm_bn_silu_fwd(const float* y, const float* gamma, const float* beta, float* running_mean,
                     float* running_var, float momentum, float eps, int training, float* mean,
-                    float* invstd, void* z, int dtype_z, long M, int C, float* ws, void* stream);
+                    float* invstd, void* z, int dtype_z, int B, int T, int C, const float* ws,
+                    void* stream);
 /* backward of z = silu(bn(y)): dy = BN-bwd(dz*silu'(bn(y))); dgamma, dbeta (=) written. */
 int cfm_bn_silu_bwd(const void* dz, int dtype_dz, const float* y, const float* gamma,
                     const float* beta, const float* mean, const float* invstd, int training,
@@ -139,7 +141,7 @@ int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dtype_a, const float*
 int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
                  const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
                  float drop_p, uint64_t seed, void* stream);
-size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel);
+size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel, int dtype);
 int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, const float* lse,
                  const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                  void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H,

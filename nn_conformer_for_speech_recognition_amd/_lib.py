@@ -56,18 +56,18 @@ _SIGS = {
                                   c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p]),
     "cfm_scale_dropout": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_float, c_float, c_u64, c_u64,
                                   c_void_p]),
-    "cfm_convmod_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "cfm_convmod_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "cfm_glu_dwconv_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                    c_void_p, c_void_p]),
     "cfm_bn_silu_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_int,
-                                c_void_p, c_void_p, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p]),
+                                c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "cfm_bn_silu_bwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                 c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p]),
     "cfm_glu_dwconv_bwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                    c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "cfm_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                              c_int, c_int, c_int, c_float, c_u64, c_void_p]),
-    "cfm_attn_bwd_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "cfm_attn_bwd_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "cfm_attn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
                              c_u64, c_void_p, c_void_p]),

@@ -1,0 +1,350 @@
+"""Conformer encoder on libcfm — drop-in for ``torchaudio.models.Conformer``.
+
+Reference call sites: lib/standard/asrnn.py:29 (construction) and :214 (forward).  Signature,
+return values, error behaviour (even depthwise kernel -> ValueError) and state-dict keys are
+torchaudio's, so reference checkpoints (runner.py:48-77) load unchanged:
+
+    conformer_layers.{i}.ffn1.sequential.{0,1,4}.*     LayerNorm, Linear(d,ffn), Linear(ffn,d)
+    conformer_layers.{i}.self_attn_layer_norm.*
+    conformer_layers.{i}.self_attn.{in_proj_weight,in_proj_bias,out_proj.weight,out_proj.bias}
+    conformer_layers.{i}.conv_module.layer_norm.*, conv_module.sequential.{0,2,3,5}.*
+    conformer_layers.{i}.ffn2.sequential.{0,1,4}.*,  conformer_layers.{i}.final_layer_norm.*
+  (+ self_attn.linear_pos.weight, pos_bias_u, pos_bias_v with pos_enc='rel')
+
+Each ConformerLayer runs as ONE autograd node whose forward/backward are sequences of libcfm
+kernels (no PyTorch compute ops).  The residual stream stays fp32; GEMM operands and saved
+activations use the compute dtype (bf16 by default, fp32 for the parity mode).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._lib import ACT_SILU
+
+_EPS = 1e-5
+
+
+class _MHAParams(nn.Module):
+    """Parameter holder with nn.MultiheadAttention's names (+ rel-pos extras)."""
+
+    def __init__(self, d, H, dropout, pos_enc):
+        super().__init__()
+        self.embed_dim, self.num_heads, self.dropout, self.pos_enc = d, H, dropout, pos_enc
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d))
+        self.in_proj_bias = nn.Parameter(torch.zeros(3 * d))
+        self.out_proj = nn.Linear(d, d, bias=True)
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        nn.init.zeros_(self.out_proj.bias)
+        if pos_enc == "rel":
+            self.linear_pos = nn.Linear(d, d, bias=False)
+            self.pos_bias_u = nn.Parameter(torch.empty(H, d // H))
+            self.pos_bias_v = nn.Parameter(torch.empty(H, d // H))
+            nn.init.xavier_uniform_(self.pos_bias_u)
+            nn.init.xavier_uniform_(self.pos_bias_v)
+
+
+class _FFNParams(nn.Module):
+    def __init__(self, d, ffn, dropout):
+        super().__init__()
+        self.sequential = nn.Sequential(nn.LayerNorm(d), nn.Linear(d, ffn), nn.SiLU(), nn.Dropout(dropout),
+                                        nn.Linear(ffn, d), nn.Dropout(dropout))
+
+
+class _ConvParams(nn.Module):
+    def __init__(self, d, K, dropout, use_group_norm):
+        super().__init__()
+        self.layer_norm = nn.LayerNorm(d)
+        self.sequential = nn.Sequential(
+            nn.Conv1d(d, 2 * d, 1, bias=True), nn.GLU(dim=1),
+            nn.Conv1d(d, d, K, padding=(K - 1) // 2, groups=d, bias=True),
+            nn.GroupNorm(1, d) if use_group_norm else nn.BatchNorm1d(d), nn.SiLU(),
+            nn.Conv1d(d, d, 1, bias=True), nn.Dropout(dropout))
+
+
+def rel_pos_table(T, d, device):
+    """(2T-1, d) sinusoid, row r <-> relative position (T-1)-r (transformers
+    modeling_wav2vec2_conformer.py:168-205).  Built on the host once per length (cached)."""
+    pos = torch.arange(T - 1, -T, -1, dtype=torch.int64).float().unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2, dtype=torch.int64).float() * -(math.log(10000.0) / d))
+    pe = torch.zeros(2 * T - 1, d)
+    pe[:, 0::2] = torch.sin(pos * div)
+    pe[:, 1::2] = torch.cos(pos * div)
+    return pe.to(device)
+
+
+# parameter order of one layer (the autograd node's inputs after x)
+_PNAMES = [
+    "ffn1.sequential.0.weight", "ffn1.sequential.0.bias", "ffn1.sequential.1.weight", "ffn1.sequential.1.bias",
+    "ffn1.sequential.4.weight", "ffn1.sequential.4.bias",
+    "self_attn_layer_norm.weight", "self_attn_layer_norm.bias",
+    "self_attn.in_proj_weight", "self_attn.in_proj_bias", "self_attn.out_proj.weight", "self_attn.out_proj.bias",
+    "conv_module.layer_norm.weight", "conv_module.layer_norm.bias",
+    "conv_module.sequential.0.weight", "conv_module.sequential.0.bias",
+    "conv_module.sequential.2.weight", "conv_module.sequential.2.bias",
+    "conv_module.sequential.3.weight", "conv_module.sequential.3.bias",
+    "conv_module.sequential.5.weight", "conv_module.sequential.5.bias",
+    "ffn2.sequential.0.weight", "ffn2.sequential.0.bias", "ffn2.sequential.1.weight", "ffn2.sequential.1.bias",
+    "ffn2.sequential.4.weight", "ffn2.sequential.4.bias",
+    "final_layer_norm.weight", "final_layer_norm.bias",
+]
+_REL_PNAMES = ["self_attn.linear_pos.weight", "self_attn.pos_bias_u", "self_attn.pos_bias_v"]
+
+
+class _Cfg:
+    __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
+                 "bn_rm", "bn_rv", "bn_mom", "pe")
+
+
+def _w(t, cd):
+    """Compute-dtype view of a weight (2-D)."""
+    return t if t.dtype == cd else ops.cast(t, cd)
+
+
+def _ffn_fwd(x, P, o, cfg, seed):
+    cd = cfg.cd
+    xn, mu, rs = ops.layernorm_fwd(x, P[o], P[o + 1], _EPS, out_dtype=cd)
+    w1, w2 = _w(P[o + 2], cd), _w(P[o + 4], cd)
+    pre = torch.empty(x.shape[0], cfg.ffn, device=x.device, dtype=cd)
+    h = ops.linear(xn, w1, P[o + 3], act=ACT_SILU, pre=pre, drop_p=cfg.p, seed=seed)
+    y = ops.linear(h, w2, P[o + 5], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, out_scale=0.5, residual=x)
+    return y, (xn, mu, rs, pre, h, w1, w2)
+
+
+def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads):
+    xn, mu, rs, pre, h, w1, w2 = sv
+    cd = cfg.cd
+    g2 = ops.scale_dropout(g, 0.5, cfg.p, seed + 1, 0, out_dtype=cd)
+    grads[o + 4] = ops.linear_wgrad(g2, h)
+    grads[o + 5] = ops.colsum(g2)
+    da = ops.linear_dgrad(g2, w2, pre=pre, act_grad=True, drop_p=cfg.p, seed=seed)
+    grads[o + 2] = ops.linear_wgrad(da, xn)
+    grads[o + 3] = ops.colsum(da)
+    dxn = ops.linear_dgrad(da, w1)
+    dx, grads[o], grads[o + 1] = ops.layernorm_bwd(dxn, x, P[o], mu, rs, dres=g)
+    return dx
+
+
+def _mha_fwd(x, P, R, cfg, seed, lens):
+    cd = cfg.cd
+    B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
+    xn, mu, rs = ops.layernorm_fwd(x, P[6], P[7], _EPS, out_dtype=cd)
+    win, wout = _w(P[8], cd), _w(P[10], cd)
+    qkv = ops.linear(xn, win, P[9])
+    pos = pu = pv = None
+    if cfg.rel:
+        wpos = _w(R[0], cd)
+        pos = ops.linear(_w(cfg.pe, cd), wpos)          # (2T-1, d) projected table (no bias)
+        pu = R[1].reshape(-1).float().contiguous()
+        pv = R[2].reshape(-1).float().contiguous()
+    o, lse = ops.attn_fwd(qkv, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
+    y = ops.linear(o, wout, P[11], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, residual=x)
+    return y, (xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv)
+
+
+def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads):
+    xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv = sv
+    cd = cfg.cd
+    B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
+    g4 = ops.scale_dropout(g, 1.0, cfg.p, seed + 1, 0, out_dtype=cd)
+    grads[10] = ops.linear_wgrad(g4, o)
+    grads[11] = ops.colsum(g4)
+    do = ops.linear_dgrad(g4, wout)
+    dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
+    if cfg.rel:
+        rgrads[0] = ops.linear_wgrad(_w(dpos, cd), _w(cfg.pe, cd))
+        rgrads[1] = dpu.view(H, d // H)
+        rgrads[2] = dpv.view(H, d // H)
+    grads[8] = ops.linear_wgrad(dqkv, xn)
+    grads[9] = ops.colsum(dqkv)
+    dxn = ops.linear_dgrad(dqkv, win)
+    dx, grads[6], grads[7] = ops.layernorm_bwd(dxn, x, P[6], mu, rs, dres=g)
+    return dx
+
+
+def _conv_fwd(x, P, cfg, seed):
+    cd = cfg.cd
+    B, T, d, K = cfg.B, cfg.T, cfg.d, cfg.K
+    xn, mu, rs = ops.layernorm_fwd(x, P[12], P[13], _EPS, out_dtype=cd)
+    wp1, wp2 = _w(P[14].view(2 * d, d), cd), _w(P[20].view(d, d), cd)
+    wdw = P[16].view(d, K)
+    a = ops.linear(xn, wp1, P[15])
+    ws = ops.convmod_ws(B, T, d, K, x.device)
+    yv = ops.glu_dwconv_fwd(a, wdw, P[17], B, T, d, K, ws)
+    z, bmean, binv = ops.bn_silu_fwd(yv, P[18], P[19], cfg.bn_rm, cfg.bn_rv, cfg.bn_mom, _EPS, cfg.training, B, T,
+                                     d, ws, cd)
+    y = ops.linear(z, wp2, P[21], out_dtype=torch.float32, drop_p=cfg.p, seed=seed, residual=x)
+    return y, (xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw)
+
+
+def _conv_bwd(g, x, sv, P, cfg, seed, grads):
+    xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw = sv
+    cd = cfg.cd
+    B, T, d, K = cfg.B, cfg.T, cfg.d, cfg.K
+    g3 = ops.scale_dropout(g, 1.0, cfg.p, seed, 0, out_dtype=cd)
+    grads[20] = ops.linear_wgrad(g3, z).view(d, d, 1)
+    grads[21] = ops.colsum(g3)
+    dz = ops.linear_dgrad(g3, wp2)
+    ws = ops.convmod_ws(B, T, d, K, x.device)
+    dy, grads[18], grads[19] = ops.bn_silu_bwd(dz, yv, P[18], P[19], bmean, binv, cfg.training, ws)
+    da, dwdw, grads[17] = ops.glu_dwconv_bwd(dy, a, wdw, B, T, d, K, ws, cd)
+    grads[16] = dwdw.view(d, 1, K)
+    grads[14] = ops.linear_wgrad(da, xn).view(2 * d, d, 1)
+    grads[15] = ops.colsum(da)
+    dxn = ops.linear_dgrad(da, wp1)
+    dx, grads[12], grads[13] = ops.layernorm_bwd(dxn, x, P[12], mu, rs, dres=g)
+    return dx
+
+
+class _ConformerLayerFn(torch.autograd.Function):
+    """One torchaudio ConformerLayer as a single autograd node over libcfm."""
+
+    @staticmethod
+    def forward(ctx, x, lens, cfg, *params):
+        P = params[:len(_PNAMES)]
+        R = params[len(_PNAMES):]
+        s = cfg.seed
+        x0 = x
+        x1, sv1 = _ffn_fwd(x0, P, 0, cfg, s)
+        if cfg.conv_first:
+            xc, svc = _conv_fwd(x1, P, cfg, s + 10)
+            xa, sva = _mha_fwd(xc, P, R, cfg, s + 20, lens)
+            chain = (x1, xc)
+            x3 = xa
+        else:
+            xa, sva = _mha_fwd(x1, P, R, cfg, s + 20, lens)
+            xc, svc = _conv_fwd(xa, P, cfg, s + 10)
+            chain = (x1, xa)
+            x3 = xc
+        x4, sv4 = _ffn_fwd(x3, P, 22, cfg, s + 30)
+        out, mu5, rs5 = ops.layernorm_fwd(x4, P[28], P[29], _EPS, out_dtype=torch.float32)
+        ctx.cfg = cfg
+        ctx.sv = (sv1, sva, svc, sv4)
+        ctx.save_for_backward(x0, chain[0], chain[1], x3, x4, mu5, rs5, lens, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        cfg = ctx.cfg
+        saved = ctx.saved_tensors
+        x0, c0, c1, x3, x4, mu5, rs5, lens = saved[:8]
+        params = saved[8:]
+        P = params[:len(_PNAMES)]
+        R = params[len(_PNAMES):]
+        sv1, sva, svc, sv4 = ctx.sv
+        grads = [None] * len(_PNAMES)
+        rgrads = [None] * len(R)
+        s = cfg.seed
+        gout = gout.contiguous()
+        g, grads[28], grads[29] = ops.layernorm_bwd(gout, x4, P[28], mu5, rs5)
+        g = _ffn_bwd(g, x3, sv4, P, 22, cfg, s + 30, grads)
+        if cfg.conv_first:
+            g = _mha_bwd(g, c1, sva, P, R, cfg, s + 20, lens, grads, rgrads)
+            g = _conv_bwd(g, c0, svc, P, cfg, s + 10, grads)
+        else:
+            g = _conv_bwd(g, c1, svc, P, cfg, s + 10, grads)
+            g = _mha_bwd(g, c0, sva, P, R, cfg, s + 20, lens, grads, rgrads)
+        g = _ffn_bwd(g, x0, sv1, P, 0, cfg, s, grads)
+        ctx.sv = None
+        return (g, None, None, *grads, *rgrads)
+
+
+class ConformerLayer(nn.Module):
+    """torchaudio.models.conformer.ConformerLayer (parameter names and semantics)."""
+
+    def __init__(self, input_dim, ffn_dim, num_attention_heads, depthwise_conv_kernel_size, dropout=0.0,
+                 use_group_norm=False, convolution_first=False, pos_enc="none"):
+        super().__init__()
+        if use_group_norm:
+            raise NotImplementedError("use_group_norm=True: GroupNorm conv module is not on the MI355X path yet")
+        self.ffn1 = _FFNParams(input_dim, ffn_dim, dropout)
+        self.self_attn_layer_norm = nn.LayerNorm(input_dim)
+        self.self_attn = _MHAParams(input_dim, num_attention_heads, dropout, pos_enc)
+        self.self_attn_dropout = nn.Dropout(dropout)
+        self.conv_module = _ConvParams(input_dim, depthwise_conv_kernel_size, dropout, use_group_norm)
+        self.ffn2 = _FFNParams(input_dim, ffn_dim, dropout)
+        self.final_layer_norm = nn.LayerNorm(input_dim)
+        self.convolution_first = convolution_first
+        self.dropout = dropout
+        self.pos_enc = pos_enc
+        self.d, self.H, self.ffn, self.K = input_dim, num_attention_heads, ffn_dim, depthwise_conv_kernel_size
+
+    def params(self):
+        sd = dict(self.named_parameters())
+        ps = [sd[n] for n in _PNAMES]
+        if self.pos_enc == "rel":
+            ps += [sd[n] for n in _REL_PNAMES]
+        return ps
+
+    def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None):
+        """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device."""
+        cfg = _Cfg()
+        cfg.B, cfg.T, cfg.d, cfg.H, cfg.ffn, cfg.K = B, T, self.d, self.H, self.ffn, self.K
+        cfg.p = float(self.dropout) if self.training else 0.0
+        cfg.cd = compute_dtype
+        cfg.training = self.training
+        cfg.conv_first = self.convolution_first
+        cfg.rel = self.pos_enc == "rel"
+        cfg.seed = seed
+        bn = self.conv_module.sequential[3]
+        cfg.bn_rm, cfg.bn_rv = bn.running_mean, bn.running_var
+        cfg.bn_mom = bn.momentum if bn.momentum is not None else 0.1
+        cfg.pe = pe
+        if self.training and bn.track_running_stats:
+            bn.num_batches_tracked.add_(1)
+        return _ConformerLayerFn.apply(x, lens_i32, cfg, *self.params())
+
+
+class Conformer(nn.Module):
+    """Drop-in for torchaudio.models.Conformer (asrnn.py:29):
+    Conformer(input_dim, num_heads, ffn_dim, num_layers, depthwise_conv_kernel_size, dropout=0.0,
+              use_group_norm=False, convolution_first=False)
+    plus build knobs pos_enc ('none' | 'rel') and compute_dtype (torch.bfloat16 | torch.float32).
+    forward(input (B, T, D), lengths (B,)) -> (output (B, T, D), lengths)."""
+
+    def __init__(self, input_dim, num_heads, ffn_dim, num_layers, depthwise_conv_kernel_size, dropout=0.0,
+                 use_group_norm=False, convolution_first=False, pos_enc="none", compute_dtype=torch.bfloat16):
+        super().__init__()
+        if depthwise_conv_kernel_size % 2 != 1:
+            raise ValueError("depthwise_conv_kernel_size must be odd to achieve 'SAME' padding.")
+        if input_dim % num_heads != 0:
+            raise ValueError("input_dim must be divisible by num_heads")
+        if pos_enc not in ("none", "rel"):
+            raise ValueError(f"pos_enc must be 'none' or 'rel', got {pos_enc!r}")
+        self.conformer_layers = nn.ModuleList([
+            ConformerLayer(input_dim, ffn_dim, num_heads, depthwise_conv_kernel_size, dropout, use_group_norm,
+                           convolution_first, pos_enc) for _ in range(num_layers)])
+        self.input_dim = input_dim
+        self.pos_enc = pos_enc
+        self.compute_dtype = compute_dtype
+        self._pe_cache = {}
+        self._step = 0
+
+    def _pe(self, T, device):
+        key = (T, str(device))
+        if key not in self._pe_cache:
+            self._pe_cache[key] = rel_pos_table(T, self.input_dim, device)
+        return self._pe_cache[key]
+
+    def forward_tokens(self, x, lens_i32, B, T, seed=None):
+        if seed is None:
+            seed = (self._step * 1000003 + 12345) & 0x7FFFFFFF
+            self._step += 1
+        pe = self._pe(T, x.device) if self.pos_enc == "rel" else None
+        for i, layer in enumerate(self.conformer_layers):
+            x = layer.forward_tokens(x, lens_i32, B, T, self.compute_dtype, seed + 100 * i, pe)
+        return x
+
+    def forward(self, input, lengths):
+        if input.dim() != 3 or input.shape[-1] != self.input_dim:
+            raise ValueError(f"expected input (B, T, {self.input_dim}), got {tuple(input.shape)}")
+        if not input.is_cuda:
+            raise RuntimeError("Conformer runs on libcfm HIP kernels: move the module and inputs to the GPU")
+        B, T, d = input.shape
+        lens = lengths.to(device=input.device, dtype=torch.int32)
+        x = input.reshape(B * T, d).float().contiguous()
+        y = self.forward_tokens(x, lens, B, T)
+        return y.view(B, T, d).to(input.dtype), lengths

@@ -1,0 +1,483 @@
+// attention.hip — fused flash-style multi-head self-attention on MFMA (bf16), fwd + bwd.
+//
+// Core of nn.MultiheadAttention(need_weights=False, key_padding_mask) inside torchaudio's
+// ConformerLayer: softmax(q k^T / sqrt(dk) + mask) v per (batch, head), never materialising
+// the T x T score matrix.  qkv is the packed in_proj output (B*T, 3*H*dk); o is (B*T, H*dk).
+//
+// Forward: one workgroup = 4 waves = 128 queries of one (b, h); each wave keeps its 32 queries
+// in registers (as the B operand) and computes S^T = K Q^T (keys on the accumulator rows,
+// queries on the lanes), so the softmax row reductions are lane-local plus one lane^32
+// exchange.  The S^T accumulator feeds O^T += V^T P^T directly as an MFMA operand (no LDS
+// round trip for P); V^T comes from the V tile through ds_read_b64_tr_b16.  K/V tiles of 64
+// keys are staged in LDS (double buffered, register prefetch) and the loop stops at the
+// utterance's last valid key (key_padding_mask), so padded keys cost nothing.
+// Backward (FA2-style, deterministic, no atomics): dK/dV kernel (keys on the lanes, loops over
+// query tiles: S, dP, dV^T += dO^T P, dK^T += Q^T dS) and dQ kernel (queries on the lanes,
+// loops over key tiles: S^T, dP^T, dQ^T += K^T dS^T), plus a tiny D = rowsum(dO*O) kernel.
+// Head dims below 64 (Conformer-S: 36) are zero-padded to 64 in LDS/registers.
+// lse is saved in natural-log units of the scaled scores (same convention as attention_simt).
+#include "cfm_common.h"
+
+namespace cfm {
+int attn_simt_fwd_launch(const void*, void*, float*, const int32_t*, const void*, const float*, const float*, int,
+                         int, int, int, int, float, uint64_t, hipStream_t);
+size_t attn_simt_ws_bytes(int B, int T, int H);
+int attn_simt_bwd_launch(const void*, const void*, const void*, const float*, const int32_t*, const void*,
+                         const float*, const float*, void*, float*, float*, float*, int, int, int, int, int, float,
+                         uint64_t, float*, hipStream_t);
+}  // namespace cfm
+
+namespace {
+
+constexpr int DKP = 64;      // padded head dim
+constexpr int KS = DKP + 8;  // LDS row stride (elements): 144-B rows, conflict-free ds_read_b128
+constexpr int TILE = 64;     // keys (fwd/dQ) or queries (dK/dV) per LDS tile
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+struct AttnM {
+  const bf16* qkv;
+  int B, T, H, dk, D3, HD;
+  const int32_t* len;
+  float scale;
+  float drop_p; uint64_t seed;
+  bool vec;    // 16-B vector loads legal
+};
+
+__device__ __forceinline__ uint64_t didx(const AttnM& p, int b, int h, int i, int j) {
+  return (((uint64_t)b * p.H + h) * p.T + i) * p.T + j;
+}
+
+// 8 consecutive head-dim elements c..c+7 of row `row` of matrix base (row stride ld), zero-padded
+__device__ __forceinline__ uint4 ld8(const bf16* base, long ld, int row, int nrows, int c, int dk, bool vec) {
+  uint4 r = make_uint4(0, 0, 0, 0);
+  if (row >= nrows || c >= dk) return r;
+  const bf16* p = base + (long)row * ld + c;
+  if (vec && c + 8 <= dk) return *reinterpret_cast<const uint4*>(p);
+  unsigned short t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = (c + e < dk) ? reinterpret_cast<const unsigned short*>(p)[e] : 0;
+  r.x = t[0] | (t[1] << 16); r.y = t[2] | (t[3] << 16); r.z = t[4] | (t[5] << 16); r.w = t[6] | (t[7] << 16);
+  return r;
+}
+
+// A-operand fragment, natural k order, from a [row][KS] tile: lane (r, hh) gets row r0+r, cols k0+8hh..+7
+__device__ __forceinline__ bf16x8 rowfrag(const bf16* tile, int r0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(tile + (r0 + (lane & 31)) * KS + k0 + 8 * (lane >> 5));
+}
+
+// A-operand fragment of the TRANSPOSED tile, k order permuted to match an accumulator used as the
+// B operand (element j of lane half hh <-> tile row r0 + 8(j>>2) + 4hh + (j&3)); column c0 + (lane&31).
+__device__ __forceinline__ bf16x8 trfrag_perm(const bf16* tile, int r0, int c0, int lane) {
+  const int hh = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+  const bf16* base = tile + (r0 + 4 * hh + q) * KS + c0 + 16 * g1 + 4 * p4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 8 * KS));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// accumulator registers 8s..8s+7 -> bf16 B-operand fragment of k-step s
+__device__ __forceinline__ bf16x8 acc2frag(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
+  return r;
+}
+
+// accumulator row of register r for lane half hh
+__device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+// stage a [64 rows][64 cols] bf16 tile (row r0.., column offset col of qkv) into LDS; 2 x 16 B per thread
+__device__ __forceinline__ void tile_load(const AttnM& p, int b, int r0, int col, uint4 (&reg)[2], int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + 256 * i;
+    reg[i] = ld8(p.qkv + (long)b * p.T * p.D3 + col, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+  }
+}
+__device__ __forceinline__ void tile_store(bf16* t, const uint4 (&reg)[2], int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + 256 * i;
+    *reinterpret_cast<uint4*>(t + (v >> 3) * KS + (v & 7) * 8) = reg[i];
+  }
+}
+
+// B-operand fragments (natural k order) of a 32-row block: lane (r, hh) = row[r][16s + 8hh .. +7]
+__device__ __forceinline__ void load_bfrags(const AttnM& p, const bf16* base, long ld, int row, int nrows,
+                                            bf16x8 (&f)[4], int lane) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint4 u = ld8(base, ld, row, nrows, 16 * s + 8 * (lane >> 5), p.dk, p.vec);
+    f[s] = __builtin_bit_cast(bf16x8, u);
+  }
+}
+
+// write a wave's 64(d) x 32(cols) f32 accumulator pair (dt = 0, 1) transposed into a bf16 matrix:
+// out[(row0 + c) * ld + d] = acc[d][c] * mul_c  (c < ncols, d < dk), staged through LDS.
+__device__ void store_transposed(float* stage, const f32x16& a0, const f32x16& a1, float mulc, bf16* out, long ld,
+                                 int row0, int nvalid, int dk, int lane) {
+  const int hh = lane >> 5, c = lane & 31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    stage[c * 65 + acc_row(r, hh)] = a0[r] * mulc;
+    stage[c * 65 + 32 + acc_row(r, hh)] = a1[r] * mulc;
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int idx = lane; idx < 32 * 64; idx += 64) {
+    const int cc = idx >> 6, d = idx & 63;
+    if (cc < nvalid && d < dk) out[(long)(row0 + cc) * ld + d] = (bf16)stage[cc * 65 + d];
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnM p, bf16* __restrict__ o, float* __restrict__ lse) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];   // [buf][K,V][64][72]  36 KiB
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * 128 + wv * 32;
+  const int len = p.len[b];
+  const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
+  bf16x8 qf[4];
+  load_bfrags(p, qbase, p.D3, q0 + (lane & 31), p.T, qf, lane);
+
+  f32x16 o0 = (f32x16){0}, o1 = (f32x16){0};
+  float m = -INFINITY, l = 0.f;
+  const float c = p.scale * LOG2E;
+  const int nkt = (len + TILE - 1) / TILE;
+  uint4 rk[2], rv[2];
+  const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
+  if (nkt > 0) {
+    tile_load(p, b, 0, kcol, rk, tid);
+    tile_load(p, b, 0, vcol, rv, tid);
+    tile_store(smem, rk, tid);
+    tile_store(smem + TILE * KS, rv, tid);
+    __syncthreads();
+  }
+  const int qi = q0 + (lane & 31);
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* sK = smem + (kt & 1) * 2 * TILE * KS;
+    const bf16* sV = sK + TILE * KS;
+    if (kt + 1 < nkt) {
+      tile_load(p, b, (kt + 1) * TILE, kcol, rk, tid);
+      tile_load(p, b, (kt + 1) * TILE, vcol, rv, tid);
+    }
+    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k0 = kt * TILE + acc_row(r, hh);
+      s0[r] = (k0 < len) ? s0[r] * c : -INFINITY;
+      s1[r] = (k0 + 32 < len) ? s1[r] * c : -INFINITY;
+      mloc = fmaxf(mloc, fmaxf(s0[r], s1[r]));
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float mn = fmaxf(m, mloc);
+    const float alpha = exp2f(m - mn);
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = exp2f(s0[r] - mn);
+      s1[r] = exp2f(s1[r] - mn);
+      ls += s0[r] + s1[r];
+    }
+    ls += __shfl_xor(ls, 32, 64);
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      o0[r] *= alpha;
+      o1[r] *= alpha;
+    }
+    if (p.drop_p > 0.f) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k0 = kt * TILE + acc_row(r, hh);
+        s0[r] *= dropout_scale(p.drop_p, p.seed, didx(p, b, h, qi, k0));
+        s1[r] *= dropout_scale(p.drop_p, p.seed, didx(p, b, h, qi, k0 + 32));
+      }
+    }
+    // O^T[d][q] += sum_key V[key][d] P^T[key][q]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 0, lane), pf, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 32, lane), pf, o1, 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nkt) {
+      bf16* nK = smem + ((kt + 1) & 1) * 2 * TILE * KS;
+      tile_store(nK, rk, tid);
+      tile_store(nK + TILE * KS, rv, tid);
+    }
+    __syncthreads();
+  }
+  // epilogue: O = O^T / l (transposed through LDS), lse in natural-log units
+  float* stage = reinterpret_cast<float*>(smem) + wv * 32 * 65;
+  const float inv = 1.f / l;   // l is per query column (lane & 31); both lane halves agree
+  store_transposed(stage, o0, o1, inv, o + (long)b * p.T * p.HD + h * p.dk, p.HD, q0, min(32, p.T - q0), p.dk,
+                   lane);
+  if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
+}
+
+// ------------------------------------------------------------------------------------ D = rowsum(dO*O)
+__global__ void attn_bwd_dot_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ o, float* __restrict__ D,
+                                    int B, int T, int H, int dk) {
+  const long n = (long)B * H * T;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(i % T);
+    const long bh = i / T;
+    const int h = (int)(bh % H), b = (int)(bh / H);
+    const long base = ((long)b * T + t) * H * dk + h * dk;
+    float s = 0.f;
+    for (int d = 0; d < dk; ++d) s += (float)dout[base + d] * (float)o[base + d];
+    D[i] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------ dQ
+// grid (ceil(T/128), H, B); wave = 32 queries.  dqkv q-part written (bf16), scaled by 1/sqrt(dk).
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnM p, const bf16* __restrict__ dout,
+                                                          const float* __restrict__ lse, const float* __restrict__ Dg,
+                                                          bf16* __restrict__ dqkv) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * 128 + wv * 32;
+  const int qi = q0 + (lane & 31);
+  const int len = p.len[b];
+  bf16x8 qf[4], gf[4];
+  load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, qi, p.T, qf, lane);
+  load_bfrags(p, dout + (long)b * p.T * p.HD + h * p.dk, p.HD, qi, p.T, gf, lane);
+  const bool qvalid = qi < p.T;
+  const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : 0.f;
+  const float Dq = qvalid ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
+  const float c = p.scale * LOG2E;
+  f32x16 a0 = (f32x16){0}, a1 = (f32x16){0};
+  const int nkt = (len + TILE - 1) / TILE;
+  uint4 rk[2], rv[2];
+  const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
+  if (nkt > 0) {
+    tile_load(p, b, 0, kcol, rk, tid);
+    tile_load(p, b, 0, vcol, rv, tid);
+    tile_store(smem, rk, tid);
+    tile_store(smem + TILE * KS, rv, tid);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* sK = smem + (kt & 1) * 2 * TILE * KS;
+    const bf16* sV = sK + TILE * KS;
+    if (kt + 1 < nkt) {
+      tile_load(p, b, (kt + 1) * TILE, kcol, rk, tid);
+      tile_load(p, b, (kt + 1) * TILE, vcol, rv, tid);
+    }
+    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0}, d0 = (f32x16){0}, d1 = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
+      d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 0, 16 * s, lane), gf[s], d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32, 16 * s, lane), gf[s], d1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k0 = kt * TILE + acc_row(r, hh);
+      float p0 = (k0 < len && qvalid) ? exp2f(s0[r] * c - L2) : 0.f;
+      float p1 = (k0 + 32 < len && qvalid) ? exp2f(s1[r] * c - L2) : 0.f;
+      float g0 = d0[r], g1 = d1[r];
+      if (p.drop_p > 0.f) {
+        g0 *= dropout_scale(p.drop_p, p.seed, didx(p, b, h, qi, k0));
+        g1 *= dropout_scale(p.drop_p, p.seed, didx(p, b, h, qi, k0 + 32));
+      }
+      s0[r] = p0 * (g0 - Dq);
+      s1[r] = p1 * (g1 - Dq);
+    }
+    // dQ^T[d][q] += sum_key K[key][d] dS^T[key][q]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 0, lane), pf, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 32, lane), pf, a1, 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nkt) {
+      bf16* nK = smem + ((kt + 1) & 1) * 2 * TILE * KS;
+      tile_store(nK, rk, tid);
+      tile_store(nK + TILE * KS, rv, tid);
+    }
+    __syncthreads();
+  }
+  float* stage = reinterpret_cast<float*>(smem) + wv * 32 * 65;
+  store_transposed(stage, a0, a1, p.scale, dqkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, q0, min(32, p.T - q0),
+                   p.dk, lane);
+}
+
+// ------------------------------------------------------------------------------------ dK, dV
+// grid (ceil(T/128), H, B); wave = 32 keys on the lanes; loops over query tiles of 64.
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnM p, const bf16* __restrict__ dout,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ Dg, bf16* __restrict__ dqkv) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];   // [buf][Q, dO][64][72]
+  __shared__ float sLD[2][2][TILE];                                        // [buf][lse2, D][64]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int k0w = blockIdx.x * 128 + wv * 32;
+  const int kj = k0w + (lane & 31);
+  const int len = p.len[b];
+  const bool kvalid = kj < len;
+  bf16x8 kf[4], vf[4];
+  load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + p.HD + h * p.dk, p.D3, kj, p.T, kf, lane);
+  load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + 2 * p.HD + h * p.dk, p.D3, kj, p.T, vf, lane);
+  const float c = p.scale * LOG2E;
+  f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
+  // the whole block may be past len: still write zeros (outputs must be defined)
+  const bool block_live = blockIdx.x * 128 < len;
+  const int nqt = block_live ? (p.T + TILE - 1) / TILE : 0;
+  uint4 rq[2], rg[2];
+  float rl = 0.f, rd = 0.f;
+  auto gload = [&](int qt) {
+    const int r0 = qt * TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int v = tid + 256 * i;
+      rq[i] = ld8(p.qkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+      rg[i] = ld8(dout + (long)b * p.T * p.HD + h * p.dk, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+    }
+    if (tid < TILE) {
+      const int qi = r0 + tid;
+      rl = qi < p.T ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : INFINITY;
+      rd = qi < p.T ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
+    }
+  };
+  auto sstore = [&](int buf) {
+    bf16* t = smem + buf * 2 * TILE * KS;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int v = tid + 256 * i;
+      *reinterpret_cast<uint4*>(t + (v >> 3) * KS + (v & 7) * 8) = rq[i];
+      *reinterpret_cast<uint4*>(t + TILE * KS + (v >> 3) * KS + (v & 7) * 8) = rg[i];
+    }
+    if (tid < TILE) {
+      sLD[buf][0][tid] = rl;
+      sLD[buf][1][tid] = rd;
+    }
+  };
+  if (nqt > 0) {
+    gload(0);
+    sstore(0);
+    __syncthreads();
+  }
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int cur = qt & 1;
+    const bf16* sQ = smem + cur * 2 * TILE * KS;
+    const bf16* sG = sQ + TILE * KS;
+    if (qt + 1 < nqt) gload(qt + 1);
+    // S[q][key] (rows: 2 tiles of 32 queries), dP[q][key]
+    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0}, g0 = (f32x16){0}, g1 = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQ, 0, 16 * s, lane), kf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQ, 32, 16 * s, lane), kf[s], s1, 0, 0, 0);
+      g0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sG, 0, 16 * s, lane), vf[s], g0, 0, 0, 0);
+      g1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sG, 32, 16 * s, lane), vf[s], g1, 0, 0, 0);
+    }
+    f32x16 pd0, pd1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qa = acc_row(r, hh), qb = 32 + qa;
+      const int qia = qt * TILE + qa, qib = qt * TILE + qb;
+      const float pa = kvalid ? exp2f(s0[r] * c - sLD[cur][0][qa]) : 0.f;   // lse = +inf for q >= T
+      const float pb = kvalid ? exp2f(s1[r] * c - sLD[cur][0][qb]) : 0.f;
+      float ma = 1.f, mb = 1.f;
+      if (p.drop_p > 0.f) {
+        ma = dropout_scale(p.drop_p, p.seed, didx(p, b, h, qia, kj));
+        mb = dropout_scale(p.drop_p, p.seed, didx(p, b, h, qib, kj));
+      }
+      pd0[r] = pa * ma;
+      pd1[r] = pb * mb;
+      s0[r] = pa * (g0[r] * ma - sLD[cur][1][qa]);
+      s1[r] = pb * (g1[r] * mb - sLD[cur][1][qb]);
+    }
+    // dV^T[d][key] += sum_q dO[q][d] Pd[q][key];  dK^T[d][key] += sum_q Q[q][d] dS[q][key]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc2frag(t == 0 ? pd0 : pd1, s);
+        const bf16x8 sf = acc2frag(t == 0 ? s0 : s1, s);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s, 0, lane), pf, dv0, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s, 32, lane), pf, dv1, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQ, 32 * t + 16 * s, 0, lane), sf, dk0, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQ, 32 * t + 16 * s, 32, lane), sf, dk1, 0, 0, 0);
+      }
+    }
+    if (qt + 1 < nqt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  float* stage = reinterpret_cast<float*>(smem) + wv * 32 * 65;
+  const int nvalid = min(32, p.T - k0w);
+  bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
+  store_transposed(stage, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
+  store_transposed(stage, dv0, dv1, 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
+}
+
+bool use_mfma(int dtype, const void* pos, int dk) { return dtype == CFM_BF16 && pos == nullptr && dk <= DKP; }
+
+}  // namespace
+
+CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
+                            const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
+                            float drop_p, uint64_t seed, void* stream) {
+  CFM_REQUIRE(qkv && o && lse && lengths, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0 && dk <= 1024, CFM_ERR_SHAPE, "bad shape");
+  CFM_REQUIRE(!pos || (pos_u && pos_v), CFM_ERR_ARG, "rel-pos needs pos_u and pos_v");
+  CFM_REQUIRE(dtype == CFM_BF16 || dtype == CFM_F32, CFM_ERR_DTYPE, "dtype");
+  CFM_REQUIRE(pos || dtype == CFM_F32 || dk <= DKP, CFM_ERR_UNSUPPORTED, "bf16 head dim must be <= 64");
+  hipStream_t s = cfm::as_stream(stream);
+  if (!use_mfma(dtype, pos, dk))
+    return cfm::attn_simt_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, s);
+  AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
+          ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0)};
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (bf16*)o, lse);
+  return cfm::check_launch("cfm_attn_fwd");
+}
+
+CFM_EXPORT size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel, int dtype) {
+  if (!use_mfma(dtype, rel ? (const void*)1 : nullptr, dk)) return cfm::attn_simt_ws_bytes(B, T, H);
+  return (size_t)B * H * T * sizeof(float);
+}
+
+CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, const float* lse,
+                            const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
+                            void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
+                            int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
+  CFM_REQUIRE(qkv && o && dout && lse && lengths && dqkv && ws, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0, CFM_ERR_SHAPE, "bad shape");
+  CFM_REQUIRE(!pos || (pos_u && pos_v && dpos && dpos_u && dpos_v), CFM_ERR_ARG, "rel-pos grads need buffers");
+  hipStream_t s = cfm::as_stream(stream);
+  if (!use_mfma(dtype, pos, dk))
+    return cfm::attn_simt_bwd_launch(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B,
+                                     T, H, dk, dtype, drop_p, seed, ws, s);
+  AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
+          ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0)};
+  const long nrow = (long)B * H * T;
+  hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)min(8192L, (nrow + 255) / 256)), dim3(256), 0, s,
+                     (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse,
+                     ws, (bf16*)dqkv);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse, ws,
+                     (bf16*)dqkv);
+  return cfm::check_launch("cfm_attn_bwd");
+}

@@ -1,0 +1,357 @@
+// convmod.hip — the HBM-bound middle of torchaudio's _ConvolutionModule:
+//   GLU(dim=channel) -> depthwise Conv1d(K, 'same' zero padding, bias) -> BatchNorm1d -> SiLU
+// and its backward.  Token-major layout (row = b*T + t, channel contiguous) so every load is
+// coalesced across channels; each workgroup owns a 64-channel x TT-frame tile of one utterance
+// and stages the GLU output (or dy) with its (K-1)/2 halo in LDS.  The kernel size is a
+// template parameter for the sizes the configs use (31, 33, ...) so the tap loops unroll.
+// BatchNorm batch statistics (train mode) are per-channel sums over all B*T rows, INCLUDING
+// padded frames — exactly what torchaudio/transformers do (padding is not masked there).
+// Per-workgroup partial sums go to a workspace and are combined in double precision by a
+// finalize kernel (deterministic; no atomics).
+#include "cfm_common.h"
+
+namespace {
+constexpr int CT = 64;    // channels per workgroup (one per lane)
+constexpr int TT = 64;    // frames per workgroup
+constexpr int KMAX = 63;  // largest supported depthwise kernel
+
+__device__ __forceinline__ float glu_at(const void* a, int dta, long row, int C, int c) {
+  const float x = ld_dyn(a, dta, row * 2 * C + c);
+  const float g = ld_dyn(a, dta, row * 2 * C + C + c);
+  return x * sigmoid_f(g);
+}
+
+// grid: (ceil(C/CT), ceil(T/TT), B), block 256 = 4 waves; lane = channel, wave strides time.
+// part: [2][nparts][C] (sum, sumsq) with part index b*gridDim.y + blockIdx.y.
+template <int KT>
+__global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const void* __restrict__ a, int dta,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ bias, float* __restrict__ y,
+                                                             int T, int C, int Krt, float* __restrict__ part) {
+  const int K = KT > 0 ? KT : Krt;
+  extern __shared__ float sg[];                  // [(TT+K-1)][CT]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * CT + lane;
+  const int t0 = blockIdx.y * TT, b = blockIdx.z;
+  const int pad = (K - 1) / 2;
+  const int rows = TT + K - 1;
+  for (int r = wv; r < rows; r += 4) {
+    const int t = t0 - pad + r;
+    float v = 0.f;
+    if (c < C && t >= 0 && t < T) v = glu_at(a, dta, (long)b * T + t, C, c);
+    sg[r * CT + lane] = v;
+  }
+  __syncthreads();
+  constexpr int KR = KT > 0 ? KT : KMAX;
+  float wr[KR];
+#pragma unroll
+  for (int k = 0; k < KR; ++k) wr[k] = (c < C && k < K) ? w[c * K + k] : 0.f;
+  const float bb = c < C ? bias[c] : 0.f;
+  float s1 = 0.f, s2 = 0.f;
+  for (int tt = wv; tt < TT; tt += 4) {
+    const int t = t0 + tt;
+    if (t >= T) break;
+    float acc = bb;
+#pragma unroll
+    for (int k = 0; k < KR; ++k)
+      if (KT > 0 || k < K) acc += wr[k] * sg[(tt + k) * CT + lane];
+    if (c < C) {
+      y[((long)b * T + t) * C + c] = acc;
+      s1 += acc;
+      s2 += acc * acc;
+    }
+  }
+  __syncthreads();
+  sg[wv * CT + lane] = s1;
+  sg[(4 + wv) * CT + lane] = s2;
+  __syncthreads();
+  if (wv == 0 && c < C) {
+    const float a1 = sg[lane] + sg[CT + lane] + sg[2 * CT + lane] + sg[3 * CT + lane];
+    const float a2 = sg[4 * CT + lane] + sg[5 * CT + lane] + sg[6 * CT + lane] + sg[7 * CT + lane];
+    const long part_idx = (long)b * gridDim.y + blockIdx.y;
+    const long nparts = (long)gridDim.z * gridDim.y;
+    part[part_idx * C + c] = a1;
+    part[(nparts + part_idx) * C + c] = a2;
+  }
+}
+
+// finalize batch stats (double accumulation) + running-stat update (momentum, unbiased var).
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int nparts, long M, int C,
+                                   float* __restrict__ mean, float* __restrict__ invstd,
+                                   float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int p = 0; p < nparts; ++p) {
+    s1 += part[(long)p * C + c];
+    s2 += part[(long)(nparts + p) * C + c];
+  }
+  const double mu = s1 / (double)M;
+  double var = s2 / (double)M - mu * mu;
+  if (var < 0.0) var = 0.0;
+  mean[c] = (float)mu;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
+  if (rvar)
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(M > 1 ? var * (double)M / (double)(M - 1) : var);
+}
+
+__global__ void bn_eval_stats_kernel(const float* __restrict__ rmean, const float* __restrict__ rvar, int C,
+                                     float eps, float* __restrict__ mean, float* __restrict__ invstd) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = rmean[c];
+  invstd[c] = rsqrtf(rvar[c] + eps);
+}
+
+__global__ void bn_silu_apply_kernel(const float* __restrict__ y, const float* __restrict__ gamma,
+                                     const float* __restrict__ beta, const float* __restrict__ mean,
+                                     const float* __restrict__ invstd, void* __restrict__ z, int dtz, long M,
+                                     int C) {
+  const long n = M * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float u = (y[i] - mean[c]) * invstd[c] * gamma[c] + beta[c];
+    st_dyn(z, dtz, i, silu_f(u));
+  }
+}
+
+// per-block partial (sum du, sum du*yhat) over a row range; grid (ceil(C/256), nparts)
+__global__ void bn_silu_bwd_reduce_kernel(const void* __restrict__ dz, int dtdz, const float* __restrict__ y,
+                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                          const float* __restrict__ mean, const float* __restrict__ invstd,
+                                          long M, int C, long rows_per, float* __restrict__ part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const long r0 = (long)blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  const float mu = mean[c], is = invstd[c], g = gamma[c], bt = beta[c];
+  float sd = 0.f, sdx = 0.f;
+  for (long r = r0; r < r1; ++r) {
+    const long i = r * C + c;
+    const float yh = (y[i] - mu) * is;
+    const float du = ld_dyn(dz, dtdz, i) * silu_grad_f(yh * g + bt);
+    sd += du;
+    sdx += du * yh;
+  }
+  part[(long)blockIdx.y * C + c] = sd;
+  part[(long)(gridDim.y + blockIdx.y) * C + c] = sdx;
+}
+
+__global__ void bn_silu_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int C,
+                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int p = 0; p < nparts; ++p) {
+    a += part[(long)p * C + c];
+    b += part[(long)(nparts + p) * C + c];
+  }
+  dbeta[c] = (float)a;
+  dgamma[c] = (float)b;
+}
+
+__global__ void bn_silu_bwd_apply_kernel(const void* __restrict__ dz, int dtdz, const float* __restrict__ y,
+                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                         const float* __restrict__ mean, const float* __restrict__ invstd,
+                                         const float* __restrict__ dgamma, const float* __restrict__ dbeta,
+                                         int training, float* __restrict__ dy, long M, int C) {
+  const long n = M * C;
+  const float invM = 1.f / (float)M;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float is = invstd[c], g = gamma[c];
+    const float yh = (y[i] - mean[c]) * is;
+    const float du = ld_dyn(dz, dtdz, i) * silu_grad_f(yh * g + beta[c]);
+    float v = du;
+    if (training) v = du - dbeta[c] * invM - yh * dgamma[c] * invM;
+    dy[i] = g * is * v;
+  }
+}
+
+// backward of y = dwconv(GLU(a)).  grid (ceil(C/CT), ceil(T/TT), B)
+// part: [nparts][K+1][C] per-block partial dw (K taps) and db (tap K).
+template <int KT>
+__global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const float* __restrict__ dy,
+                                                             const void* __restrict__ a, int dta,
+                                                             const float* __restrict__ w, void* __restrict__ da,
+                                                             int dtda, int T, int C, int Krt,
+                                                             float* __restrict__ part) {
+  const int K = KT > 0 ? KT : Krt;
+  extern __shared__ float sm[];                  // sdy [(TT+K-1)][CT], sg [(TT+K-1)][CT]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * CT + lane;
+  const int t0 = blockIdx.y * TT, b = blockIdx.z;
+  const int pad = (K - 1) / 2;
+  const int rows = TT + K - 1;
+  float* sdy = sm;
+  float* sg = sm + rows * CT;
+  for (int r = wv; r < rows; r += 4) {
+    const int t = t0 - pad + r;
+    float vd = 0.f, vg = 0.f;
+    if (c < C && t >= 0 && t < T) {
+      const long row = (long)b * T + t;
+      vd = dy[row * C + c];
+      vg = glu_at(a, dta, row, C, c);
+    }
+    sdy[r * CT + lane] = vd;
+    sg[r * CT + lane] = vg;
+  }
+  __syncthreads();
+  constexpr int KR = KT > 0 ? KT : KMAX;
+  float wr[KR], dw[KR];
+#pragma unroll
+  for (int k = 0; k < KR; ++k) {
+    wr[k] = (c < C && k < K) ? w[c * K + k] : 0.f;
+    dw[k] = 0.f;
+  }
+  float db = 0.f;
+  for (int tt = wv; tt < TT; tt += 4) {
+    const int t = t0 + tt;
+    if (t >= T) break;
+    // y[t] = sum_k w[k] g[t+k-pad]  =>  dg[t] = sum_k w[k] dy[t-k+pad];  sdy[r] = dy[t0-pad+r]
+    float dg = 0.f;
+#pragma unroll
+    for (int k = 0; k < KR; ++k)
+      if (KT > 0 || k < K) dg += wr[k] * sdy[(tt - k + 2 * pad) * CT + lane];
+    // dw[k] += dy[t] * g[t+k-pad]  (sg[r] = g[t0-pad+r] -> r = tt + k)
+    const float dyt = sdy[(tt + pad) * CT + lane];
+#pragma unroll
+    for (int k = 0; k < KR; ++k)
+      if (KT > 0 || k < K) dw[k] += dyt * sg[(tt + k) * CT + lane];
+    db += dyt;
+    if (c < C) {
+      const long row = (long)b * T + t;
+      const float x = ld_dyn(a, dta, row * 2 * C + c);
+      const float s = sigmoid_f(ld_dyn(a, dta, row * 2 * C + C + c));
+      st_dyn(da, dtda, row * 2 * C + c, dg * s);
+      st_dyn(da, dtda, row * 2 * C + C + c, dg * x * s * (1.f - s));
+    }
+  }
+  __syncthreads();
+  // stage [4 waves][K+1][CT] and reduce over waves
+  float* red = sm;
+#pragma unroll
+  for (int k = 0; k < KR; ++k)
+    if (KT > 0 || k < K) red[(wv * (K + 1) + k) * CT + lane] = dw[k];
+  red[(wv * (K + 1) + K) * CT + lane] = db;
+  __syncthreads();
+  const long part_idx = (long)b * gridDim.y + blockIdx.y;
+  for (int i = threadIdx.x; i < (K + 1) * CT; i += 256) {
+    const int k = i / CT, l = i % CT;
+    const int cc = blockIdx.x * CT + l;
+    if (cc < C) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s += red[(q * (K + 1) + k) * CT + l];
+      part[(part_idx * (K + 1) + k) * C + cc] = s;
+    }
+  }
+}
+
+// dw[c][k] = sum_p part[p][k][c]; db[c] = sum_p part[p][K][c]
+__global__ void dwconv_wgrad_reduce_kernel(const float* __restrict__ part, int nparts, int C, int K,
+                                           float* __restrict__ dw, float* __restrict__ db) {
+  const int i = blockIdx.x * 256 + threadIdx.x;     // over (K+1)*C, channel fastest (coalesced)
+  if (i >= C * (K + 1)) return;
+  double s = 0.0;
+  for (int p = 0; p < nparts; ++p) s += part[(long)p * C * (K + 1) + i];
+  const int k = i / C, c = i % C;
+  if (k < K) dw[c * K + k] = (float)s;
+  else if (db) db[c] = (float)s;
+}
+
+int ew_grid(long n) {
+  long b = (n + 255) / 256;
+  return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+#define CFM_K_CASES(X) X(3) X(5) X(7) X(15) X(31) X(33)
+}  // namespace
+
+CFM_EXPORT size_t cfm_convmod_ws_bytes(int B, int T, int C, int K) {
+  const long nparts = (long)B * ((T + TT - 1) / TT);
+  const long fwd = 2 * nparts * C;
+  const long bwd = nparts * (long)C * (K + 1);
+  const long bn = 2L * 256 * C;
+  long m = fwd > bwd ? fwd : bwd;
+  if (bn > m) m = bn;
+  return (size_t)m * sizeof(float);
+}
+
+CFM_EXPORT int cfm_glu_dwconv_fwd(const void* a, int dta, const float* w, const float* bias, float* y, int B,
+                                  int T, int C, int K, float* ws, void* stream) {
+  CFM_REQUIRE(a && w && bias && y && ws, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, CFM_ERR_UNSUPPORTED, "depthwise kernel must be odd and <= 63");
+  CFM_REQUIRE(B > 0 && T > 0 && C > 0, CFM_ERR_SHAPE, "bad shape");
+  dim3 grid(cdiv(C, CT), cdiv(T, TT), B);
+  const size_t lds = (size_t)(TT + K - 1) * CT * sizeof(float);
+  hipStream_t s = cfm::as_stream(stream);
+  switch (K) {
+#define X(k) case k: hipLaunchKernelGGL(glu_dwconv_fwd_kernel<k>, grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws); break;
+    CFM_K_CASES(X)
+#undef X
+    default: hipLaunchKernelGGL(glu_dwconv_fwd_kernel<0>, grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws);
+  }
+  return cfm::check_launch("cfm_glu_dwconv_fwd");
+}
+
+CFM_EXPORT int cfm_bn_silu_fwd(const float* y, const float* gamma, const float* beta, float* running_mean,
+                               float* running_var, float momentum, float eps, int training, float* mean,
+                               float* invstd, void* z, int dtz, int B, int T, int C, const float* ws,
+                               void* stream) {
+  CFM_REQUIRE(y && gamma && beta && mean && invstd && z, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(B > 0 && T > 0 && C > 0, CFM_ERR_SHAPE, "bad shape");
+  hipStream_t s = cfm::as_stream(stream);
+  const long M = (long)B * T;
+  if (training) {
+    CFM_REQUIRE(ws, CFM_ERR_ARG, "training mode needs the partial sums of cfm_glu_dwconv_fwd");
+    const int nparts = B * cdiv(T, TT);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, ws, nparts, M, C, mean, invstd,
+                       running_mean, running_var, momentum, eps);
+  } else {
+    CFM_REQUIRE(running_mean && running_var, CFM_ERR_ARG, "eval mode needs running stats");
+    hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, running_mean, running_var, C,
+                       eps, mean, invstd);
+  }
+  hipLaunchKernelGGL(bn_silu_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z,
+                     dtz, M, C);
+  return cfm::check_launch("cfm_bn_silu_fwd");
+}
+
+CFM_EXPORT int cfm_bn_silu_bwd(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
+                               const float* mean, const float* invstd, int training, float* dy, float* dgamma,
+                               float* dbeta, long M, int C, float* ws, void* stream) {
+  CFM_REQUIRE(dz && y && gamma && beta && mean && invstd && dy && dgamma && dbeta && ws, CFM_ERR_ARG,
+              "null pointer");
+  hipStream_t s = cfm::as_stream(stream);
+  const int nparts = 256;
+  const long rows_per = (M + nparts - 1) / nparts;
+  hipLaunchKernelGGL(bn_silu_bwd_reduce_kernel, dim3(cdiv(C, 256), nparts), dim3(256), 0, s, dz, dtdz, y, gamma,
+                     beta, mean, invstd, M, C, rows_per > 0 ? rows_per : 1, ws);
+  hipLaunchKernelGGL(bn_silu_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, ws, nparts, C, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_silu_bwd_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, dz, dtdz, y, gamma, beta,
+                     mean, invstd, dgamma, dbeta, training, dy, M, C);
+  return cfm::check_launch("cfm_bn_silu_bwd");
+}
+
+CFM_EXPORT int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dta, const float* w, void* da, int dtda,
+                                  float* dw, float* db, int B, int T, int C, int K, float* ws, void* stream) {
+  CFM_REQUIRE(dy && a && w && da && dw && ws, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, CFM_ERR_UNSUPPORTED, "depthwise kernel must be odd and <= 63");
+  CFM_REQUIRE(B > 0 && T > 0 && C > 0, CFM_ERR_SHAPE, "bad shape");
+  dim3 grid(cdiv(C, CT), cdiv(T, TT), B);
+  size_t lds = (size_t)2 * (TT + K - 1) * CT * sizeof(float);
+  const size_t red = (size_t)4 * (K + 1) * CT * sizeof(float);
+  if (red > lds) lds = red;
+  hipStream_t s = cfm::as_stream(stream);
+  switch (K) {
+#define X(k) case k: hipLaunchKernelGGL(glu_dwconv_bwd_kernel<k>, grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws); break;
+    CFM_K_CASES(X)
+#undef X
+    default: hipLaunchKernelGGL(glu_dwconv_bwd_kernel<0>, grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws);
+  }
+  const int nparts = B * cdiv(T, TT);
+  hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3(cdiv((long)C * (K + 1), 256)), dim3(256), 0, s, ws, nparts, C,
+                     K, dw, db);
+  return cfm::check_launch("cfm_glu_dwconv_bwd");
+}

@@ -1,4 +1,5 @@
-// gemm.hip — MFMA GEMM with fused epilogues for every dense contraction of the encoder.
+// gemm.hip — MFMA GEMM with fused epilogues for every dense contraction of the encoder, plus the
+// implicit-GEMM forms of the second subsampling convolution (no im2col in HBM).
 //
 // Tile: 128x128 output per 256-thread workgroup (4 waves as 2x2, 64x64 per wave =
 // 2x2 MFMA 32x32 tiles).  bf16 operands: v_mfma_f32_32x32x16_bf16, BK = 32.  fp32 operands:
@@ -7,9 +8,13 @@
 // forward pass) is staged row-wise and read with ds_read_b128; MN-major (m/n contiguous, e.g.
 // the token dimension in weight-gradient GEMMs) is staged as [k][m] and read with the gfx950
 // ds_read_b64_tr_b16 transposed LDS read, so no operand is ever transposed in HBM.
+// Operands are "loader" functors: a plain strided matrix, or an on-the-fly im2col gather for
+// the 3x3/stride-2 convolution (forward, weight-grad and data-grad).
 // Global->LDS staging goes through registers with one-tile-ahead prefetch and a double-buffered
 // LDS ring (one barrier per K tile).
 #include "cfm_common.h"
+
+#include <type_traits>
 
 namespace {
 
@@ -17,8 +22,6 @@ constexpr int BM = 128, BN = 128, NT = 256;
 
 struct GemmP {
   int M, N, K;
-  const void* A; long lda, sa;
-  const void* B; long ldb, sb;
   void* C; long ldc, sc; int dtc;
   float alpha;
   const float* bias;
@@ -28,35 +31,105 @@ struct GemmP {
   float out_scale;
   const void* res; long ldr; int dtr;
   int split_k, k_per_split;
-  int vec_a, vec_b;   // 16-byte vector loads legal (alignment of base + ld)
 };
 
-// ---------------------------------------------------------------- bf16 staging helpers
-// Load 8 consecutive elements base[outer*ld + inner .. +7] with zero fill past the limits.
-__device__ __forceinline__ uint4 ld8_bf16(const bf16* __restrict__ base, long ld, int outer, int inner,
-                                          int outer_lim, int inner_lim, bool vec) {
-  uint4 r = make_uint4(0, 0, 0, 0);
-  if (outer >= outer_lim) return r;
-  const bf16* p = base + (long)outer * ld + inner;
-  if (vec && inner + 8 <= inner_lim) return *reinterpret_cast<const uint4*>(p);
-  unsigned short tmp[8];
+template <typename T> struct VecOf;
+template <> struct VecOf<bf16> { typedef uint4 type; static constexpr int W = 8; };
+template <> struct VecOf<float> { typedef float4 type; static constexpr int W = 4; };
+
+// element-wise fallback: W consecutive elements p[0..W), zero past `n_ok`
+template <typename T>
+__device__ __forceinline__ typename VecOf<T>::type ld_partial(const T* p, int n_ok) {
+  typedef typename VecOf<T>::type V;
+  constexpr int W = VecOf<T>::W;
+  if constexpr (W == 8) {
+    unsigned short t[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) tmp[e] = (inner + e < inner_lim) ? reinterpret_cast<const unsigned short*>(p)[e] : 0;
-  r.x = tmp[0] | (tmp[1] << 16); r.y = tmp[2] | (tmp[3] << 16);
-  r.z = tmp[4] | (tmp[5] << 16); r.w = tmp[6] | (tmp[7] << 16);
+    for (int e = 0; e < 8; ++e) t[e] = e < n_ok ? reinterpret_cast<const unsigned short*>(p)[e] : 0;
+    V r;
+    r.x = t[0] | (t[1] << 16); r.y = t[2] | (t[3] << 16); r.z = t[4] | (t[5] << 16); r.w = t[6] | (t[7] << 16);
+    return r;
+  } else {
+    float t[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t[e] = e < n_ok ? p[e] : 0.f;
+    return make_float4(t[0], t[1], t[2], t[3]);
+  }
+}
+template <typename T> __device__ __forceinline__ typename VecOf<T>::type vzero() {
+  typename VecOf<T>::type r;
+  if constexpr (VecOf<T>::W == 8) r = make_uint4(0, 0, 0, 0); else r = make_float4(0.f, 0.f, 0.f, 0.f);
   return r;
 }
-__device__ __forceinline__ float4 ld4_f32(const float* __restrict__ base, long ld, int outer, int inner,
-                                          int outer_lim, int inner_lim, bool vec) {
-  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (outer >= outer_lim) return r;
-  const float* p = base + (long)outer * ld + inner;
-  if (vec && inner + 4 <= inner_lim) return *reinterpret_cast<const float4*>(p);
-  float t[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) t[e] = (inner + e < inner_lim) ? p[e] : 0.f;
-  return make_float4(t[0], t[1], t[2], t[3]);
-}
+
+// Plain strided operand: element (outer, inner) at base[outer*ld + inner] (+ batch stride)
+template <typename T> struct StridedOp {
+  const T* base; long ld; long bstride; bool vec;
+  __device__ __forceinline__ void batch(int z) { base += (long)z * bstride; }
+  __device__ __forceinline__ typename VecOf<T>::type load(int outer, int inner, int outer_lim, int inner_lim) const {
+    constexpr int W = VecOf<T>::W;
+    if (outer >= outer_lim || inner >= inner_lim) return vzero<T>();
+    const T* p = base + (long)outer * ld + inner;
+    if (vec && inner + W <= inner_lim) return *reinterpret_cast<const typename VecOf<T>::type*>(p);
+    return ld_partial<T>(p, inner_lim - inner);
+  }
+};
+
+// conv2 geometry: h1 NHWC (B, F1, T1, C1); output rows m = (b, t2, f2); taps (kh, kw) 3x3 stride 2
+struct Conv2Geo { int B, F1, T1, C1, F2, T2, C2; };
+
+// forward A (K-major): A(m, k=(kh,kw,c1)) = h1[b, 2f2+kh, 2t2+kw, c1]
+template <typename T> struct Conv2FwdA {
+  const T* h1; Conv2Geo g;
+  __device__ __forceinline__ void batch(int) {}
+  __device__ __forceinline__ typename VecOf<T>::type load(int m, int k, int m_lim, int k_lim) const {
+    if (m >= m_lim || k >= k_lim) return vzero<T>();
+    const int f2 = m % g.F2, r = m / g.F2, t2 = r % g.T2, b = r / g.T2;
+    const int tap = k / g.C1, c1 = k % g.C1, kh = tap / 3, kw = tap % 3;
+    const T* p = h1 + (((long)b * g.F1 + 2 * f2 + kh) * g.T1 + 2 * t2 + kw) * g.C1 + c1;
+    return *reinterpret_cast<const typename VecOf<T>::type*>(p);
+  }
+};
+// weight-grad B (MN-major): B(n=(kh,kw,c1), k=m) = h1[b(m), 2f2+kh, 2t2+kw, c1]
+template <typename T> struct Conv2WgradB {
+  const T* h1; Conv2Geo g;
+  __device__ __forceinline__ void batch(int) {}
+  __device__ __forceinline__ typename VecOf<T>::type load(int m, int n, int m_lim, int n_lim) const {
+    if (m >= m_lim || n >= n_lim) return vzero<T>();
+    const int f2 = m % g.F2, r = m / g.F2, t2 = r % g.T2, b = r / g.T2;
+    const int tap = n / g.C1, c1 = n % g.C1, kh = tap / 3, kw = tap % 3;
+    const T* p = h1 + (((long)b * g.F1 + 2 * f2 + kh) * g.T1 + 2 * t2 + kw) * g.C1 + c1;
+    return *reinterpret_cast<const typename VecOf<T>::type*>(p);
+  }
+};
+// data-grad A (K-major): rows p = (b, f1, t1), k = (kh, kw, c2):
+//   dh2[b, t2=(t1-kw)/2, f2=(f1-kh)/2, c2] when both differences are even, >= 0 and in range
+template <typename T> struct Conv2DgradA {
+  const T* dh2; Conv2Geo g;
+  __device__ __forceinline__ void batch(int) {}
+  __device__ __forceinline__ typename VecOf<T>::type load(int pr, int k, int p_lim, int k_lim) const {
+    if (pr >= p_lim || k >= k_lim) return vzero<T>();
+    const int t1 = pr % g.T1, r = pr / g.T1, f1 = r % g.F1, b = r / g.F1;
+    const int tap = k / g.C2, c2 = k % g.C2, kh = tap / 3, kw = tap % 3;
+    const int fd = f1 - kh, td = t1 - kw;
+    if (fd < 0 || td < 0 || (fd & 1) || (td & 1)) return vzero<T>();
+    const int f2 = fd >> 1, t2 = td >> 1;
+    if (f2 >= g.F2 || t2 >= g.T2) return vzero<T>();
+    const T* p = dh2 + (((long)b * g.T2 + t2) * g.F2 + f2) * g.C2 + c2;
+    return *reinterpret_cast<const typename VecOf<T>::type*>(p);
+  }
+};
+// data-grad B (MN-major): B(n=c1, k=(kh,kw,c2)) = w2r[c2][kh][kw][c1]
+template <typename T> struct Conv2DgradB {
+  const T* w2r; Conv2Geo g;
+  __device__ __forceinline__ void batch(int) {}
+  __device__ __forceinline__ typename VecOf<T>::type load(int k, int n, int k_lim, int n_lim) const {
+    if (k >= k_lim || n >= n_lim) return vzero<T>();
+    const int tap = k / g.C2, c2 = k % g.C2;
+    const T* p = w2r + ((long)c2 * 9 + tap) * g.C1 + n;
+    return *reinterpret_cast<const typename VecOf<T>::type*>(p);
+  }
+};
 
 // bf16 LDS geometry (elements)
 constexpr int BK16 = 32;
@@ -70,8 +143,7 @@ constexpr int BK32 = 16;
 constexpr int F_STRIDE = 128 + 4;
 constexpr int TILE32 = BK32 * F_STRIDE;
 
-// Read one 32x32x16 operand fragment (8 bf16) from a staged tile.
-// row0: first row (m or n) of the 32-row MFMA block inside the tile; kk: k offset (0 / 16).
+// Read one 32x32x16 operand fragment (8 bf16, natural k order) from a staged tile.
 template <bool KMAJOR>
 __device__ __forceinline__ bf16x8 frag16(const bf16* tile, int row0, int kk, int lane) {
   if constexpr (KMAJOR) {
@@ -110,15 +182,15 @@ __device__ __forceinline__ void epilogue_store(const GemmP& p, int z, int m, int
 }
 
 // ---------------------------------------------------------------- bf16 kernel
-template <bool AK, bool BKM>
-__global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p) {
+template <bool AK, bool BKM, class OA, class OB>
+__global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
   __shared__ __attribute__((aligned(16))) bf16 lds[4 * TILE16];   // [buf][A,B] 40 KiB
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int z = blockIdx.z / p.split_k, ks = blockIdx.z % p.split_k;
-  const bf16* A = reinterpret_cast<const bf16*>(p.A) + (long)z * p.sa;
-  const bf16* B = reinterpret_cast<const bf16*>(p.B) + (long)z * p.sb;
+  oa.batch(z);
+  ob.batch(z);
   const int kbeg = ks * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg + BK16 - 1) / BK16 : 0;
@@ -135,10 +207,10 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int v = tid + NT * i;
-      if constexpr (AK) ra[i] = ld8_bf16(A, p.lda, m0 + (v >> 2), k0 + (v & 3) * 8, p.M, kend, p.vec_a);
-      else ra[i] = ld8_bf16(A, p.lda, k0 + (v >> 4), m0 + (v & 15) * 8, kend, p.M, p.vec_a);
-      if constexpr (BKM) rb[i] = ld8_bf16(B, p.ldb, n0 + (v >> 2), k0 + (v & 3) * 8, p.N, kend, p.vec_b);
-      else rb[i] = ld8_bf16(B, p.ldb, k0 + (v >> 4), n0 + (v & 15) * 8, kend, p.N, p.vec_b);
+      if constexpr (AK) ra[i] = oa.load(m0 + (v >> 2), k0 + (v & 3) * 8, p.M, kend);
+      else ra[i] = oa.load(k0 + (v >> 4), m0 + (v & 15) * 8, kend, p.M);
+      if constexpr (BKM) rb[i] = ob.load(n0 + (v >> 2), k0 + (v & 3) * 8, p.N, kend);
+      else rb[i] = ob.load(k0 + (v >> 4), n0 + (v & 15) * 8, kend, p.N);
     }
   };
   auto sstore = [&](int buf) {
@@ -194,15 +266,15 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p) {
 }
 
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
-template <bool AK, bool BKM>
-__global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p) {
+template <bool AK, bool BKM, class OA, class OB>
+__global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p, OA oa, OB ob) {
   __shared__ __attribute__((aligned(16))) float lds[4 * TILE32];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int z = blockIdx.z / p.split_k, ks = blockIdx.z % p.split_k;
-  const float* A = reinterpret_cast<const float*>(p.A) + (long)z * p.sa;
-  const float* B = reinterpret_cast<const float*>(p.B) + (long)z * p.sb;
+  oa.batch(z);
+  ob.batch(z);
   const int kbeg = ks * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg + BK32 - 1) / BK32 : 0;
@@ -220,10 +292,10 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int v = tid + NT * i;
-      if constexpr (AK) ra[i] = ld4_f32(A, p.lda, m0 + (v >> 2), k0 + (v & 3) * 4, p.M, kend, p.vec_a);
-      else ra[i] = ld4_f32(A, p.lda, k0 + (v >> 5), m0 + (v & 31) * 4, kend, p.M, p.vec_a);
-      if constexpr (BKM) rb[i] = ld4_f32(B, p.ldb, n0 + (v >> 2), k0 + (v & 3) * 4, p.N, kend, p.vec_b);
-      else rb[i] = ld4_f32(B, p.ldb, k0 + (v >> 5), n0 + (v & 31) * 4, kend, p.N, p.vec_b);
+      if constexpr (AK) ra[i] = oa.load(m0 + (v >> 2), k0 + (v & 3) * 4, p.M, kend);
+      else ra[i] = oa.load(k0 + (v >> 5), m0 + (v & 31) * 4, kend, p.M);
+      if constexpr (BKM) rb[i] = ob.load(n0 + (v >> 2), k0 + (v & 3) * 4, p.N, kend);
+      else rb[i] = ob.load(k0 + (v >> 5), n0 + (v & 31) * 4, kend, p.N);
     }
   };
   auto put = [&](float* t, bool kmaj, int v, float4 r) {
@@ -288,12 +360,30 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p) {
       }
 }
 
-template <typename F>
-void launch4(bool ak, bool bk, F f) {
-  if (ak && bk) f(std::integral_constant<int, 3>{});
-  else if (ak) f(std::integral_constant<int, 2>{});
-  else if (bk) f(std::integral_constant<int, 1>{});
-  else f(std::integral_constant<int, 0>{});
+GemmP plain_params(int M, int N, int K, void* C, long ldc, int dtc) {
+  GemmP p{};
+  p.M = M; p.N = N; p.K = K;
+  p.C = C; p.ldc = ldc; p.sc = 0; p.dtc = dtc;
+  p.alpha = 1.f; p.out_scale = 1.f;
+  p.split_k = 1; p.k_per_split = K;
+  return p;
+}
+
+int split_k_for(const GemmP& p, int bk) {
+  return ((p.K + p.split_k - 1) / p.split_k + bk - 1) / bk * bk;
+}
+
+template <bool AK, bool BKM, class OA, class OB>
+int launch_typed(int /*dtype: implied by the loaders' element type*/, GemmP p, OA oa, OB ob, int batch,
+                 hipStream_t s) {
+  dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
+  if (grid.y > 65535 || grid.z > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
+  typedef decltype(oa.load(0, 0, 0, 0)) V;
+  if constexpr (std::is_same<V, uint4>::value)
+    hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OA, OB>), grid, dim3(NT), 0, s, p, oa, ob);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, OA, OB>), grid, dim3(NT), 0, s, p, oa, ob);
+  return CFM_OK;
 }
 
 }  // namespace
@@ -314,37 +404,101 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   CFM_REQUIRE(d->ldc >= d->N, CFM_ERR_SHAPE, "ldc");
   if (d->M == 0 || d->N == 0) return CFM_OK;
 
-  GemmP p;
-  p.M = d->M; p.N = d->N; p.K = d->K;
-  p.A = d->A; p.lda = d->lda; p.sa = d->stride_a;
-  p.B = d->B; p.ldb = d->ldb; p.sb = d->stride_b;
-  p.C = d->C; p.ldc = d->ldc; p.sc = d->stride_c; p.dtc = d->dtype_c;
+  GemmP p = plain_params(d->M, d->N, d->K, d->C, d->ldc, d->dtype_c);
+  p.sc = d->stride_c;
   p.alpha = d->alpha; p.bias = d->bias; p.act = d->act; p.act_grad = d->act_grad;
   p.pre = d->pre; p.dtpre = d->dtype_pre;
   p.drop_p = d->drop_p; p.seed = d->drop_seed; p.doff = d->drop_offset;
   p.out_scale = d->out_scale; p.res = d->residual; p.ldr = d->ldr; p.dtr = d->dtype_r;
   p.split_k = split;
-  const int bk = d->dtype_ab == CFM_BF16 ? BK16 : BK32;
-  p.k_per_split = ((d->K + split - 1) / split + bk - 1) / bk * bk;
-  const int esz = d->dtype_ab == CFM_BF16 ? 2 : 4;
-  const int vlen = 16 / esz;
-  p.vec_a = ((uintptr_t)d->A % 16 == 0) && (d->lda % vlen == 0) && (d->stride_a % vlen == 0);
-  p.vec_b = ((uintptr_t)d->B % 16 == 0) && (d->ldb % vlen == 0) && (d->stride_b % vlen == 0);
-
-  dim3 grid(cdiv(d->N, BN), cdiv(d->M, BM), d->batch * split);
-  CFM_REQUIRE(grid.y <= 65535 && grid.z <= 65535, CFM_ERR_SHAPE, "grid too large");
+  const bool bf = d->dtype_ab == CFM_BF16;
+  p.k_per_split = split_k_for(p, bf ? BK16 : BK32);
+  const int vlen = bf ? 8 : 4;
+  const bool va = ((uintptr_t)d->A % 16 == 0) && (d->lda % vlen == 0) && (d->stride_a % vlen == 0);
+  const bool vb = ((uintptr_t)d->B % 16 == 0) && (d->ldb % vlen == 0) && (d->stride_b % vlen == 0);
   hipStream_t s = cfm::as_stream(stream);
   const bool ak = d->a_kmajor != 0, bkm = d->b_kmajor != 0;
-  if (d->dtype_ab == CFM_BF16) {
-    launch4(ak, bkm, [&](auto c) {
-      constexpr int v = decltype(c)::value;
-      hipLaunchKernelGGL((gemm_bf16_kernel<(v & 2) != 0, (v & 1) != 0>), grid, dim3(NT), 0, s, p);
-    });
-  } else {
-    launch4(ak, bkm, [&](auto c) {
-      constexpr int v = decltype(c)::value;
-      hipLaunchKernelGGL((gemm_f32_kernel<(v & 2) != 0, (v & 1) != 0>), grid, dim3(NT), 0, s, p);
-    });
-  }
+  int rc;
+  auto go = [&](auto tag) {
+    typedef decltype(tag) T;
+    StridedOp<T> oa{(const T*)d->A, d->lda, d->stride_a, va};
+    StridedOp<T> ob{(const T*)d->B, d->ldb, d->stride_b, vb};
+    if (ak && bkm) rc = launch_typed<true, true>(d->dtype_ab, p, oa, ob, d->batch, s);
+    else if (ak) rc = launch_typed<true, false>(d->dtype_ab, p, oa, ob, d->batch, s);
+    else if (bkm) rc = launch_typed<false, true>(d->dtype_ab, p, oa, ob, d->batch, s);
+    else rc = launch_typed<false, false>(d->dtype_ab, p, oa, ob, d->batch, s);
+  };
+  if (bf) go(bf16{}); else go(float{});
+  if (rc != CFM_OK) return rc;
   return cfm::check_launch("cfm_gemm");
+}
+
+// ---------------------------------------------------------------------------- conv2 (3x3, s2)
+static Conv2Geo conv2_geo(int B, int F1, int T1, int C1, int C2) {
+  Conv2Geo g{B, F1, T1, C1, (F1 - 3) / 2 + 1, (T1 - 3) / 2 + 1, C2};
+  return g;
+}
+
+CFM_EXPORT int cfm_conv2_fwd(const void* h1, const void* w2r, const float* b2, void* h2, int dtype_h2, int dtype,
+                             int B, int F1, int T1, int C1, int C2, void* stream) {
+  CFM_REQUIRE(h1 && w2r && h2, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(C1 % 8 == 0 && F1 >= 3 && T1 >= 3 && B > 0 && C2 > 0, CFM_ERR_SHAPE, "conv2: C1 % 8, F1/T1 >= 3");
+  CFM_REQUIRE((uintptr_t)h1 % 16 == 0 && (uintptr_t)w2r % 16 == 0, CFM_ERR_ALIGN, "16-B aligned operands");
+  const Conv2Geo g = conv2_geo(B, F1, T1, C1, C2);
+  GemmP p = plain_params(B * g.T2 * g.F2, C2, 9 * C1, h2, C2, dtype_h2);
+  p.bias = b2;
+  hipStream_t s = cfm::as_stream(stream);
+  int rc;
+  if (dtype == CFM_BF16)
+    rc = launch_typed<true, true>(dtype, p, Conv2FwdA<bf16>{(const bf16*)h1, g},
+                                  StridedOp<bf16>{(const bf16*)w2r, 9L * C1, 0, true}, 1, s);
+  else
+    rc = launch_typed<true, true>(dtype, p, Conv2FwdA<float>{(const float*)h1, g},
+                                  StridedOp<float>{(const float*)w2r, 9L * C1, 0, true}, 1, s);
+  if (rc != CFM_OK) return rc;
+  return cfm::check_launch("cfm_conv2_fwd");
+}
+
+CFM_EXPORT int cfm_conv2_bwd_weight(const void* dh2, const void* h1, float* dw2r, int dtype, int B, int F1, int T1,
+                                    int C1, int C2, void* stream) {
+  CFM_REQUIRE(dh2 && h1 && dw2r, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(C1 % 8 == 0 && C2 % 8 == 0, CFM_ERR_SHAPE, "conv2: C1 and C2 must be multiples of 8");
+  const Conv2Geo g = conv2_geo(B, F1, T1, C1, C2);
+  const int Mrows = B * g.T2 * g.F2;
+  GemmP p = plain_params(C2, 9 * C1, Mrows, dw2r, 9L * C1, CFM_F32);
+  const int tiles = cdiv(C2, BM) * cdiv(9 * C1, BN);
+  int split = 1024 / (tiles > 0 ? tiles : 1);
+  split = split < 1 ? 1 : (split > 64 ? 64 : split);
+  if (Mrows / 512 < split) split = Mrows / 512 > 1 ? Mrows / 512 : 1;
+  p.split_k = split;
+  p.k_per_split = split_k_for(p, dtype == CFM_BF16 ? BK16 : BK32);
+  hipStream_t s = cfm::as_stream(stream);
+  if (split > 1) (void)hipMemsetAsync(dw2r, 0, sizeof(float) * C2 * 9 * C1, s);
+  int rc;
+  if (dtype == CFM_BF16)
+    rc = launch_typed<false, false>(dtype, p, StridedOp<bf16>{(const bf16*)dh2, C2, 0, C2 % 8 == 0},
+                                    Conv2WgradB<bf16>{(const bf16*)h1, g}, 1, s);
+  else
+    rc = launch_typed<false, false>(dtype, p, StridedOp<float>{(const float*)dh2, C2, 0, C2 % 4 == 0},
+                                    Conv2WgradB<float>{(const float*)h1, g}, 1, s);
+  if (rc != CFM_OK) return rc;
+  return cfm::check_launch("cfm_conv2_bwd_weight");
+}
+
+CFM_EXPORT int cfm_conv2_bwd_data(const void* dh2, const void* w2r, void* dh1, int dtype, int B, int F1, int T1,
+                                  int C1, int C2, void* stream) {
+  CFM_REQUIRE(dh2 && w2r && dh1, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(C1 % 8 == 0 && C2 % 8 == 0, CFM_ERR_SHAPE, "conv2: C1 and C2 must be multiples of 8");
+  const Conv2Geo g = conv2_geo(B, F1, T1, C1, C2);
+  GemmP p = plain_params(B * F1 * T1, C1, 9 * C2, dh1, C1, dtype);
+  hipStream_t s = cfm::as_stream(stream);
+  int rc;
+  if (dtype == CFM_BF16)
+    rc = launch_typed<true, false>(dtype, p, Conv2DgradA<bf16>{(const bf16*)dh2, g},
+                                   Conv2DgradB<bf16>{(const bf16*)w2r, g}, 1, s);
+  else
+    rc = launch_typed<true, false>(dtype, p, Conv2DgradA<float>{(const float*)dh2, g},
+                                   Conv2DgradB<float>{(const float*)w2r, g}, 1, s);
+  if (rc != CFM_OK) return rc;
+  return cfm::check_launch("cfm_conv2_bwd_data");
 }

@@ -139,3 +139,112 @@ def specaug_apply(x, params_dev, intended=False, mask_value=0.0):
     L.call("cfm_specaug_apply", L.ptr(x), L.ptr(y), B, F, T, L.ptr(params_dev), params_dev.numel(),
            int(bool(intended)), float(mask_value), L.stream())
     return y
+
+
+# ----------------------------------------------------------------------------- convolution module
+def convmod_ws(B, T, C, K, device):
+    return workspace(L.size_call("cfm_convmod_ws_bytes", B, T, C, K), device)
+
+
+def glu_dwconv_fwd(a, w_dw, b_dw, B, T, C, K, ws):
+    y = torch.empty(B * T, C, device=a.device, dtype=torch.float32)
+    L.call("cfm_glu_dwconv_fwd", L.ptr(a), L.dt(a), L.ptr(w_dw), L.ptr(b_dw), L.ptr(y), B, T, C, K, L.ptr(ws),
+           L.stream())
+    return y
+
+
+def bn_silu_fwd(y, gamma, beta, running_mean, running_var, momentum, eps, training, B, T, C, ws, out_dtype):
+    mean = torch.empty(C, device=y.device, dtype=torch.float32)
+    invstd = torch.empty(C, device=y.device, dtype=torch.float32)
+    z = torch.empty(B * T, C, device=y.device, dtype=out_dtype)
+    L.call("cfm_bn_silu_fwd", L.ptr(y), L.ptr(gamma), L.ptr(beta), L.ptr(running_mean), L.ptr(running_var),
+           float(momentum), float(eps), int(bool(training)), L.ptr(mean), L.ptr(invstd), L.ptr(z), L.dt(z), B, T, C,
+           L.ptr(ws), L.stream())
+    return z, mean, invstd
+
+
+def bn_silu_bwd(dz, y, gamma, beta, mean, invstd, training, ws):
+    M, C = y.shape
+    dy = torch.empty(M, C, device=y.device, dtype=torch.float32)
+    dgamma = torch.empty(C, device=y.device, dtype=torch.float32)
+    dbeta = torch.empty(C, device=y.device, dtype=torch.float32)
+    L.call("cfm_bn_silu_bwd", L.ptr(dz), L.dt(dz), L.ptr(y), L.ptr(gamma), L.ptr(beta), L.ptr(mean), L.ptr(invstd),
+           int(bool(training)), L.ptr(dy), L.ptr(dgamma), L.ptr(dbeta), M, C, L.ptr(ws), L.stream())
+    return dy, dgamma, dbeta
+
+
+def glu_dwconv_bwd(dy, a, w_dw, B, T, C, K, ws, da_dtype):
+    da = torch.empty(B * T, 2 * C, device=a.device, dtype=da_dtype)
+    dw = torch.empty(C, K, device=a.device, dtype=torch.float32)
+    db = torch.empty(C, device=a.device, dtype=torch.float32)
+    L.call("cfm_glu_dwconv_bwd", L.ptr(dy), L.ptr(a), L.dt(a), L.ptr(w_dw), L.ptr(da), L.dt(da), L.ptr(dw),
+           L.ptr(db), B, T, C, K, L.ptr(ws), L.stream())
+    return da, dw, db
+
+
+# ----------------------------------------------------------------------------- attention
+def attn_fwd(qkv, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, drop_p=0.0, seed=0):
+    o = torch.empty(B * T, H * dk, device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty(B * H * T, device=qkv.device, dtype=torch.float32)
+    L.call("cfm_attn_fwd", L.ptr(qkv), L.ptr(o), L.ptr(lse), L.ptr(lengths_i32), L.ptr(pos), L.ptr(pos_u),
+           L.ptr(pos_v), B, T, H, dk, L.dt(qkv), float(drop_p), int(seed) & (2**64 - 1), L.stream())
+    return o, lse
+
+
+def attn_bwd(qkv, o, dout, lse, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, drop_p=0.0, seed=0):
+    rel = pos is not None
+    ws = workspace(L.size_call("cfm_attn_bwd_ws_bytes", B, T, H, dk, int(rel), L.dt(qkv)), qkv.device)
+    dqkv = torch.empty_like(qkv)
+    dpos = torch.empty(pos.shape, device=qkv.device, dtype=torch.float32) if rel else None
+    dpu = torch.empty(H * dk, device=qkv.device, dtype=torch.float32) if rel else None
+    dpv = torch.empty(H * dk, device=qkv.device, dtype=torch.float32) if rel else None
+    L.call("cfm_attn_bwd", L.ptr(qkv), L.ptr(o), L.ptr(dout), L.ptr(lse), L.ptr(lengths_i32), L.ptr(pos),
+           L.ptr(pos_u), L.ptr(pos_v), L.ptr(dqkv), L.ptr(dpos), L.ptr(dpu), L.ptr(dpv), B, T, H, dk, L.dt(qkv),
+           float(drop_p), int(seed) & (2**64 - 1), L.ptr(ws), L.stream())
+    return dqkv, dpos, dpu, dpv
+
+
+# ----------------------------------------------------------------------------- conv subsampling
+def conv1_fwd(x, w1, b1, out_dtype):
+    B, F, T = x.shape
+    C1 = w1.shape[0]
+    F1, T1 = (F - 7) // 2 + 1, (T - 7) // 2 + 1
+    h1 = torch.empty(B, F1, T1, C1, device=x.device, dtype=out_dtype)
+    L.call("cfm_conv1_fwd", L.ptr(x), L.ptr(w1), L.ptr(b1), L.ptr(h1), L.dt(h1), B, F, T, C1, L.stream())
+    return h1
+
+
+def conv1_bwd_weight(dh1, x, C1):
+    B, F, T = x.shape
+    dw1 = torch.empty(C1, 49, device=x.device, dtype=torch.float32)
+    db1 = torch.empty(C1, device=x.device, dtype=torch.float32)
+    ws = workspace(L.size_call("cfm_conv1_bwd_ws_bytes", B, F, T, C1), x.device)
+    L.call("cfm_conv1_bwd_weight", L.ptr(dh1), L.dt(dh1), L.ptr(x), L.ptr(dw1), L.ptr(db1), B, F, T, C1, L.ptr(ws),
+           L.stream())
+    return dw1, db1
+
+
+def conv2_fwd(h1, w2r, b2, out_dtype):
+    B, F1, T1, C1 = h1.shape
+    C2 = w2r.shape[0]
+    F2, T2 = (F1 - 3) // 2 + 1, (T1 - 3) // 2 + 1
+    h2 = torch.empty(B, T2, F2, C2, device=h1.device, dtype=out_dtype)
+    L.call("cfm_conv2_fwd", L.ptr(h1), L.ptr(w2r), L.ptr(b2), L.ptr(h2), L.dt(h2), L.dt(h1), B, F1, T1, C1, C2,
+           L.stream())
+    return h2
+
+
+def conv2_bwd_data(dh2, w2r, F1, T1):
+    B, T2, F2, C2 = dh2.shape
+    C1 = w2r.shape[1] // 9
+    dh1 = torch.empty(B, F1, T1, C1, device=dh2.device, dtype=dh2.dtype)
+    L.call("cfm_conv2_bwd_data", L.ptr(dh2), L.ptr(w2r), L.ptr(dh1), L.dt(dh2), B, F1, T1, C1, C2, L.stream())
+    return dh1
+
+
+def conv2_bwd_weight(dh2, h1):
+    B, F1, T1, C1 = h1.shape
+    C2 = dh2.shape[-1]
+    dw2r = torch.empty(C2, 9 * C1, device=h1.device, dtype=torch.float32)
+    L.call("cfm_conv2_bwd_weight", L.ptr(dh2), L.ptr(h1), L.ptr(dw2r), L.dt(h1), B, F1, T1, C1, C2, L.stream())
+    return dw2r

@@ -1,0 +1,140 @@
+"""Conformer parity on the GPU: the libcfm Conformer vs the golden fixtures (transformers'
+Wav2Vec2Conformer layer) and vs the CPU oracle (torchaudio semantics), fwd + bwd.
+
+Tolerances: fp32 parity mode (exact-f32 MFMA GEMMs) — relative L2 error <= 1e-4 on outputs and
+<= 1e-3 on gradients (north-star bar: 1e-3 rel); bf16 mode — <= 3e-2 relative L2 (bf16 operands,
+fp32 accumulation / residual stream)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from nn_conformer_for_speech_recognition_amd.conformer import Conformer  # noqa: E402
+from oracle import conformer as oc  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+TOL = {torch.float32: (1e-4, 1e-3), torch.bfloat16: (3e-2, 5e-2)}
+
+
+@pytest.mark.parametrize("name", ["s_none", "s_rel", "m_rel", "l_none"])
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_layer_vs_transformers_fixture(golden_dir, name, cd):
+    z = np.load(os.path.join(golden_dir, "conformer_layers.npz"))
+    p = name + "_"
+    d, H, ffn, K, B, T = [int(v) for v in z[p + "cfg"]]
+    pos = "rel" if name.endswith("rel") else "none"
+    m = Conformer(d, H, ffn, 1, K, 0.0, pos_enc=pos, compute_dtype=cd)
+    sd = {"conformer_layers.0." + k[len(p) + 2:]: torch.tensor(z[k]) for k in z.files if k.startswith(p + "w.")}
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    x = torch.tensor(z[p + "x"], device=DEV, requires_grad=True)
+    lens = torch.tensor(z[p + "lens"], device=DEV)
+    y, lo = m(x, lens)
+    tol_y, tol_g = TOL[cd]
+    assert rel_err(y.detach(), z[p + "y"]) < tol_y
+    y.backward(torch.tensor(z[p + "gy"], device=DEV))
+    assert rel_err(x.grad, z[p + "gx"]) < tol_g
+    named = dict(m.conformer_layers[0].named_parameters())
+    for k in z.files:
+        if k.startswith(p + "g."):
+            nm = k[len(p) + 2:]
+            assert rel_err(named[nm].grad.reshape(z[k].shape), z[k]) < tol_g, nm
+    bn = m.conformer_layers[0].conv_module.sequential[3]
+    assert rel_err(bn.running_mean, z[p + "bn_running_mean"]) < tol_y
+    assert rel_err(bn.running_var, z[p + "bn_running_var"]) < tol_y
+
+
+CASES = [
+    # d, H, ffn, K, layers, B, T, lens, conv_first, pos
+    (256, 4, 1024, 31, 2, 4, 200, [200, 150, 77, 1], False, "none"),
+    (144, 4, 576, 31, 2, 3, 130, [130, 129, 64], True, "none"),
+    (512, 8, 2048, 31, 1, 2, 373, [373, 300], False, "none"),
+    (128, 2, 256, 15, 1, 2, 96, [96, 50], False, "rel"),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_encoder_vs_oracle(case, cd):
+    d, H, ffn, K, L, B, T, lens, conv_first, pos = case
+    torch.manual_seed(7)
+    ref = oc.ConformerRef(d, H, ffn, L, K, 0.0, convolution_first=conv_first, pos_enc=pos).train()
+    with torch.no_grad():
+        for n, prm in ref.named_parameters():
+            if n.endswith("bias"):
+                prm.normal_(0, 0.05)
+    m = Conformer(d, H, ffn, L, K, 0.0, convolution_first=conv_first, pos_enc=pos, compute_dtype=cd)
+    m.load_state_dict(ref.state_dict())
+    m = m.to(DEV).train()
+    x = torch.randn(B, T, d)
+    ln = torch.tensor(lens)
+    xr = x.clone().requires_grad_()
+    yr, _ = ref(xr, ln)
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    xd = x.to(DEV).requires_grad_()
+    y, _ = m(xd, ln.to(DEV))
+    y.backward(gy.to(DEV))
+    tol_y, tol_g = TOL[cd]
+    assert rel_err(y.detach(), yr.detach()) < tol_y
+    assert rel_err(xd.grad, xr.grad) < tol_g
+    rp = dict(ref.named_parameters())
+    for n, prm in m.named_parameters():
+        assert prm.grad is not None, n
+        if n.endswith("conv_module.sequential.2.bias"):
+            # train-mode BatchNorm right after the depthwise conv removes its bias: the true gradient is
+            # exactly 0, both sides hold rounding noise.  Check it is noise-sized.
+            wg = dict(m.named_parameters())[n.replace(".bias", ".weight")].grad
+            assert prm.grad.norm() <= 1e-2 * wg.norm(), n
+            continue
+        assert rel_err(prm.grad, rp[n].grad) < tol_g * (3 if "pos_bias" in n else 1), n
+    for (n, b1), (_, b2) in zip(m.named_buffers(), ref.named_buffers()):
+        if "running" in n:
+            assert rel_err(b1, b2) < tol_y, n
+
+
+def test_eval_mode_uses_running_stats():
+    torch.manual_seed(3)
+    d, H, ffn, K = 64, 2, 128, 7
+    ref = oc.ConformerRef(d, H, ffn, 1, K, 0.1)
+    with torch.no_grad():
+        bn = ref.conformer_layers[0].conv_module.sequential[3]
+        bn.running_mean.normal_()
+        bn.running_var.uniform_(0.5, 2)
+    ref.eval()
+    m = Conformer(d, H, ffn, 1, K, 0.1, compute_dtype=torch.float32)
+    m.load_state_dict(ref.state_dict())
+    m = m.to(DEV).eval()
+    x = torch.randn(2, 40, d)
+    ln = torch.tensor([40, 33])
+    with torch.no_grad():
+        yr, _ = ref(x, ln)
+        y, _ = m(x.to(DEV), ln.to(DEV))
+    assert rel_err(y, yr) < 1e-4
+
+
+def test_dropout_train_is_stochastic_and_scaled():
+    torch.manual_seed(0)
+    m = Conformer(64, 2, 128, 1, 7, 0.3, compute_dtype=torch.float32).to(DEV).train()
+    x = torch.randn(2, 50, 64, device=DEV)
+    ln = torch.tensor([50, 50], device=DEV)
+    y1, _ = m(x, ln)
+    y2, _ = m(x, ln)
+    assert not torch.allclose(y1, y2)
+    assert torch.isfinite(y1).all()
+
+
+def test_even_kernel_raises():
+    with pytest.raises(ValueError):
+        Conformer(64, 2, 128, 1, 8)
