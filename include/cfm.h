@@ -105,6 +105,11 @@ int cfm_layernorm_bwd(const void* dy, int dtype_dy, const void* x, int dtype_x, 
 int cfm_scale_dropout(const void* x, int dtype_x, void* y, int dtype_y, long n, float scale,
                       float drop_p, uint64_t seed, uint64_t offset, void* stream);
 
+/* dx = dy * silu'(pre) elementwise (backward of a SILU GEMM epilogue when the gradient feeds a
+ * weight-gradient GEMM directly, e.g. the projection block asrnn.py:84-87). */
+int cfm_silu_bwd(const void* dy, int dtype_dy, const void* pre, int dtype_pre, void* dx, int dtype_dx,
+                 long n, void* stream);
+
 /* ---------------------------------------------------------------- Convolution module
  * _ConvolutionModule (torchaudio; restated oracle/conformer.py ConvModuleRef):
  *   a = pw1(LN(x)) (cfm_gemm), g = GLU(a) (dim = channel), y = depthwise_conv_K(g) + b,
@@ -126,6 +131,15 @@ int cfm_bn_silu_fwd(const float* y, const float* gamma, const float* beta, float
 int cfm_bn_silu_bwd(const void* dz, int dtype_dz, const float* y, const float* gamma,
                     const float* beta, const float* mean, const float* invstd, int training,
                     float* dy, float* dgamma, float* dbeta, long M, int C, float* ws, void* stream);
+/* Generic BatchNorm1d over (M, C) rows with optional SiLU after the normalisation (act = 1) —
+ * the projection block's BatchNorm1d(256) (lib/standard/asrnn.py:32,88).  ws: cfm_bn_ws_bytes(C). */
+size_t cfm_bn_ws_bytes(int C);
+int cfm_bn_fwd(const float* y, const float* gamma, const float* beta, float* running_mean,
+               float* running_var, float momentum, float eps, int training, float* mean, float* invstd,
+               void* z, int dtype_z, long M, int C, int act, float* ws, void* stream);
+int cfm_bn_bwd(const void* dz, int dtype_dz, const float* y, const float* gamma, const float* beta,
+               const float* mean, const float* invstd, int training, int act, float* dy, float* dgamma,
+               float* dbeta, long M, int C, float* ws, void* stream);
 /* backward of y = dwconv(GLU(a)): da (B*T, 2C), dw (C,K) (=), db (C) (=). */
 int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dtype_a, const float* w_dw, void* da,
                        int dtype_da, float* dw, float* db, int B, int T, int C, int K, float* ws,

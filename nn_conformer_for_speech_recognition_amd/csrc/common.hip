@@ -79,6 +79,22 @@ CFM_EXPORT int cfm_scale_dropout(const void* x, int dtx, void* y, int dty, long 
   return cfm::check_launch("cfm_scale_dropout");
 }
 
+namespace {
+__global__ void silu_bwd_kernel(const void* dy, int dtdy, const void* pre, int dtpre, void* dx, int dtdx, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    st_dyn(dx, dtdx, i, ld_dyn(dy, dtdy, i) * silu_grad_f(ld_dyn(pre, dtpre, i)));
+}
+}  // namespace
+
+CFM_EXPORT int cfm_silu_bwd(const void* dy, int dtdy, const void* pre, int dtpre, void* dx, int dtdx, long n,
+                            void* stream) {
+  CFM_REQUIRE(dy && pre && dx && n >= 0, CFM_ERR_ARG, "bad args");
+  if (n == 0) return CFM_OK;
+  hipLaunchKernelGGL(silu_bwd_kernel, dim3(grid_for(n, 1)), dim3(256), 0, cfm::as_stream(stream), dy, dtdy, pre,
+                     dtpre, dx, dtdx, n);
+  return cfm::check_launch("cfm_silu_bwd");
+}
+
 // --------------------------------------------------------------------------- column sums
 namespace {
 // partial sums: grid (ceil(N/256), nblk); each block sums rows [b*rows_per, ...) for 256 cols

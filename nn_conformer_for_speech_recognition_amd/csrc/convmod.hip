@@ -107,20 +107,36 @@ __global__ void bn_eval_stats_kernel(const float* __restrict__ rmean, const floa
 __global__ void bn_silu_apply_kernel(const float* __restrict__ y, const float* __restrict__ gamma,
                                      const float* __restrict__ beta, const float* __restrict__ mean,
                                      const float* __restrict__ invstd, void* __restrict__ z, int dtz, long M,
-                                     int C) {
+                                     int C, int act) {
   const long n = M * C;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
     const float u = (y[i] - mean[c]) * invstd[c] * gamma[c] + beta[c];
-    st_dyn(z, dtz, i, silu_f(u));
+    st_dyn(z, dtz, i, act ? silu_f(u) : u);
   }
+}
+
+// generic per-block row partial sums (sum, sumsq) for BatchNorm1d over (M, C); grid (ceil(C/256), nparts)
+__global__ void bn_stats_rows_kernel(const float* __restrict__ y, long M, int C, long rows_per,
+                                     float* __restrict__ part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const long r0 = (long)blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  float s1 = 0.f, s2 = 0.f;
+  for (long r = r0; r < r1; ++r) {
+    const float v = y[r * C + c];
+    s1 += v;
+    s2 += v * v;
+  }
+  part[(long)blockIdx.y * C + c] = s1;
+  part[(long)(gridDim.y + blockIdx.y) * C + c] = s2;
 }
 
 // per-block partial (sum du, sum du*yhat) over a row range; grid (ceil(C/256), nparts)
 __global__ void bn_silu_bwd_reduce_kernel(const void* __restrict__ dz, int dtdz, const float* __restrict__ y,
                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                           const float* __restrict__ mean, const float* __restrict__ invstd,
-                                          long M, int C, long rows_per, float* __restrict__ part) {
+                                          long M, int C, long rows_per, float* __restrict__ part, int act) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   const long r0 = (long)blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
@@ -129,7 +145,7 @@ __global__ void bn_silu_bwd_reduce_kernel(const void* __restrict__ dz, int dtdz,
   for (long r = r0; r < r1; ++r) {
     const long i = r * C + c;
     const float yh = (y[i] - mu) * is;
-    const float du = ld_dyn(dz, dtdz, i) * silu_grad_f(yh * g + bt);
+    const float du = ld_dyn(dz, dtdz, i) * (act ? silu_grad_f(yh * g + bt) : 1.f);
     sd += du;
     sdx += du * yh;
   }
@@ -154,14 +170,14 @@ __global__ void bn_silu_bwd_apply_kernel(const void* __restrict__ dz, int dtdz, 
                                          const float* __restrict__ gamma, const float* __restrict__ beta,
                                          const float* __restrict__ mean, const float* __restrict__ invstd,
                                          const float* __restrict__ dgamma, const float* __restrict__ dbeta,
-                                         int training, float* __restrict__ dy, long M, int C) {
+                                         int training, float* __restrict__ dy, long M, int C, int act) {
   const long n = M * C;
   const float invM = 1.f / (float)M;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
     const float is = invstd[c], g = gamma[c];
     const float yh = (y[i] - mean[c]) * is;
-    const float du = ld_dyn(dz, dtdz, i) * silu_grad_f(yh * g + beta[c]);
+    const float du = ld_dyn(dz, dtdz, i) * (act ? silu_grad_f(yh * g + beta[c]) : 1.f);
     float v = du;
     if (training) v = du - dbeta[c] * invM - yh * dgamma[c] * invM;
     dy[i] = g * is * v;
@@ -314,8 +330,21 @@ CFM_EXPORT int cfm_bn_silu_fwd(const float* y, const float* gamma, const float* 
                        eps, mean, invstd);
   }
   hipLaunchKernelGGL(bn_silu_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z,
-                     dtz, M, C);
+                     dtz, M, C, 1);
   return cfm::check_launch("cfm_bn_silu_fwd");
+}
+
+static int bn_bwd_impl(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
+                       const float* mean, const float* invstd, int training, int act, float* dy, float* dgamma,
+                       float* dbeta, long M, int C, float* ws, hipStream_t s) {
+  const int nparts = 256;
+  const long rows_per = (M + nparts - 1) / nparts;
+  hipLaunchKernelGGL(bn_silu_bwd_reduce_kernel, dim3(cdiv(C, 256), nparts), dim3(256), 0, s, dz, dtdz, y, gamma,
+                     beta, mean, invstd, M, C, rows_per > 0 ? rows_per : 1, ws, act);
+  hipLaunchKernelGGL(bn_silu_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, ws, nparts, C, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_silu_bwd_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, dz, dtdz, y, gamma, beta,
+                     mean, invstd, dgamma, dbeta, training, dy, M, C, act);
+  return CFM_OK;
 }
 
 CFM_EXPORT int cfm_bn_silu_bwd(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
@@ -323,15 +352,44 @@ CFM_EXPORT int cfm_bn_silu_bwd(const void* dz, int dtdz, const float* y, const f
                                float* dbeta, long M, int C, float* ws, void* stream) {
   CFM_REQUIRE(dz && y && gamma && beta && mean && invstd && dy && dgamma && dbeta && ws, CFM_ERR_ARG,
               "null pointer");
-  hipStream_t s = cfm::as_stream(stream);
-  const int nparts = 256;
-  const long rows_per = (M + nparts - 1) / nparts;
-  hipLaunchKernelGGL(bn_silu_bwd_reduce_kernel, dim3(cdiv(C, 256), nparts), dim3(256), 0, s, dz, dtdz, y, gamma,
-                     beta, mean, invstd, M, C, rows_per > 0 ? rows_per : 1, ws);
-  hipLaunchKernelGGL(bn_silu_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, ws, nparts, C, dgamma, dbeta);
-  hipLaunchKernelGGL(bn_silu_bwd_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, dz, dtdz, y, gamma, beta,
-                     mean, invstd, dgamma, dbeta, training, dy, M, C);
+  bn_bwd_impl(dz, dtdz, y, gamma, beta, mean, invstd, training, 1, dy, dgamma, dbeta, M, C, ws,
+              cfm::as_stream(stream));
   return cfm::check_launch("cfm_bn_silu_bwd");
+}
+
+CFM_EXPORT size_t cfm_bn_ws_bytes(int C) { return (size_t)2 * 256 * C * sizeof(float); }
+
+CFM_EXPORT int cfm_bn_fwd(const float* y, const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, float momentum, float eps, int training, float* mean, float* invstd,
+                          void* z, int dtz, long M, int C, int act, float* ws, void* stream) {
+  CFM_REQUIRE(y && gamma && beta && mean && invstd && z && ws, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(M > 0 && C > 0, CFM_ERR_SHAPE, "bad shape");
+  hipStream_t s = cfm::as_stream(stream);
+  if (training) {
+    const int nparts = 256;
+    const long rows_per = (M + nparts - 1) / nparts;
+    hipLaunchKernelGGL(bn_stats_rows_kernel, dim3(cdiv(C, 256), nparts), dim3(256), 0, s, y, M, C,
+                       rows_per > 0 ? rows_per : 1, ws);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, ws, nparts, M, C, mean, invstd,
+                       running_mean, running_var, momentum, eps);
+  } else {
+    CFM_REQUIRE(running_mean && running_var, CFM_ERR_ARG, "eval mode needs running stats");
+    hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, running_mean, running_var, C,
+                       eps, mean, invstd);
+  }
+  hipLaunchKernelGGL(bn_silu_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z,
+                     dtz, M, C, act);
+  return cfm::check_launch("cfm_bn_fwd");
+}
+
+CFM_EXPORT int cfm_bn_bwd(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
+                          const float* mean, const float* invstd, int training, int act, float* dy, float* dgamma,
+                          float* dbeta, long M, int C, float* ws, void* stream) {
+  CFM_REQUIRE(dz && y && gamma && beta && mean && invstd && dy && dgamma && dbeta && ws, CFM_ERR_ARG,
+              "null pointer");
+  bn_bwd_impl(dz, dtdz, y, gamma, beta, mean, invstd, training, act, dy, dgamma, dbeta, M, C, ws,
+              cfm::as_stream(stream));
+  return cfm::check_launch("cfm_bn_bwd");
 }
 
 CFM_EXPORT int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dta, const float* w, void* da, int dtda,

@@ -141,6 +141,35 @@ def specaug_apply(x, params_dev, intended=False, mask_value=0.0):
     return y
 
 
+def silu_bwd(dy, pre, out_dtype=None):
+    dx = torch.empty(dy.shape, device=dy.device, dtype=out_dtype or dy.dtype)
+    L.call("cfm_silu_bwd", L.ptr(dy), L.dt(dy), L.ptr(pre), L.dt(pre), L.ptr(dx), L.dt(dx), dy.numel(), L.stream())
+    return dx
+
+
+def bn_fwd(y, gamma, beta, running_mean, running_var, momentum, eps, training, act=0, out_dtype=torch.float32):
+    M, C = y.shape
+    mean = torch.empty(C, device=y.device, dtype=torch.float32)
+    invstd = torch.empty(C, device=y.device, dtype=torch.float32)
+    z = torch.empty(M, C, device=y.device, dtype=out_dtype)
+    ws = workspace(L.size_call("cfm_bn_ws_bytes", C), y.device)
+    L.call("cfm_bn_fwd", L.ptr(y), L.ptr(gamma), L.ptr(beta), L.ptr(running_mean), L.ptr(running_var),
+           float(momentum), float(eps), int(bool(training)), L.ptr(mean), L.ptr(invstd), L.ptr(z), L.dt(z), M, C,
+           int(act), L.ptr(ws), L.stream())
+    return z, mean, invstd
+
+
+def bn_bwd(dz, y, gamma, beta, mean, invstd, training, act=0):
+    M, C = y.shape
+    dy = torch.empty(M, C, device=y.device, dtype=torch.float32)
+    dgamma = torch.empty(C, device=y.device, dtype=torch.float32)
+    dbeta = torch.empty(C, device=y.device, dtype=torch.float32)
+    ws = workspace(L.size_call("cfm_bn_ws_bytes", C), y.device)
+    L.call("cfm_bn_bwd", L.ptr(dz), L.dt(dz), L.ptr(y), L.ptr(gamma), L.ptr(beta), L.ptr(mean), L.ptr(invstd),
+           int(bool(training)), int(act), L.ptr(dy), L.ptr(dgamma), L.ptr(dbeta), M, C, L.ptr(ws), L.stream())
+    return dy, dgamma, dbeta
+
+
 # ----------------------------------------------------------------------------- convolution module
 def convmod_ws(B, T, C, K, device):
     return workspace(L.size_call("cfm_convmod_ws_bytes", B, T, C, K), device)

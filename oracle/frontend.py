@@ -27,9 +27,10 @@ def convsub_forward(x, w1, b1, w2, b2, s1=(2, 2), s2=(2, 2)):
 
 
 def frame_projection(y, w, b):
-    """y (B, C2, F', T') → (B, T', d): per-subsampled-frame Linear over (c2, f') features."""
+    """y (B, C2, F', T') → (B, T', d): per-subsampled-frame Linear over the frame's (f', c2)
+    features (feature index f'*C2 + c2 — the build's 'frame' projection)."""
     B, C2, Fp, Tp = y.shape
-    feats = y.permute(0, 3, 1, 2).reshape(B, Tp, C2 * Fp)
+    feats = y.permute(0, 3, 2, 1).reshape(B, Tp, Fp * C2)
     return F.linear(feats, w, b)
 
 
