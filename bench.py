@@ -1,0 +1,269 @@
+"""Throughput benchmark: mel-frames/s of the Conformer-L encoder training step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config L15]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+One step = one utterance batch through the hot path, forward + backward:
+SpecAugment (optional, --specaug) -> ConvSubSampling -> frame projection -> 17 Conformer-L layers
+-> CTC head (Linear d->V) -> log_softmax + CTC loss -> full backward -> (N>1) RCCL gradient
+all-reduce -> optimizer step.  Inputs are synthetic 80-bin log-mel batches already resident in HBM
+(SURVEY.md §8d), weights random-init.  Weak scaling: B=32 utterances per GPU.
+
+Prints ONE JSON line (rank 0) with the contract fields plus `roofline` (dominant kernel, measured
+live with HIP events on its launch stream over the timed region) and `cpu_baseline` (the CPU
+oracle, rank 0 at N=1 only, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from nn_conformer_for_speech_recognition_amd import dist as cdist  # noqa: E402
+from nn_conformer_for_speech_recognition_amd import ops  # noqa: E402
+from nn_conformer_for_speech_recognition_amd.conformer import Conformer  # noqa: E402
+from nn_conformer_for_speech_recognition_amd.frontend import linear  # noqa: E402
+from nn_conformer_for_speech_recognition_amd.lib.convsubsampling import ConvSubSampling  # noqa: E402
+from nn_conformer_for_speech_recognition_amd.lib.hparams import HParams  # noqa: E402
+from nn_conformer_for_speech_recognition_amd.optim import Adafactor  # noqa: E402
+
+METRIC = "mel-frames/sec/GPU Conformer-L encoder fwd+bwd; 1/2/4/8-GPU scaling"
+# (name, layers, d, heads, ffn, K, batch per GPU, seconds)
+CONFIGS = {
+    "L15": ("Conformer-L", 17, 512, 8, 2048, 31, 32, 15),
+    "M15": ("Conformer-M", 16, 256, 4, 1024, 31, 32, 15),
+    "S15": ("Conformer-S", 16, 144, 4, 576, 31, 32, 15),
+}
+PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, F2, C1=512, C2=128):
+    """per-layer per-encoder-frame MACs 4*d*ffn + 4d^2 + 3d^2 + K*d + 2*T*d, the
+    front-end (conv1 + conv2 + frame projection), x2 FLOPs, fwd+bwd = 3x fwd minus conv1's dgrad."""
+    F1, T1 = (80 - 7) // 2 + 1, (T_in - 7) // 2 + 1
+    enc = L * T2 * (4 * d * ffn + 7 * d * d + K * d + 2 * T2 * d)
+    conv1 = C1 * 49 * F1 * T1
+    conv2 = C2 * C1 * 9 * F2 * T2
+    proj = T2 * F2 * C2 * d
+    fwd = 2 * (enc + conv1 + conv2 + proj)
+    fwdbwd = 3 * fwd - 2 * conv1
+    return fwd / T_in, fwdbwd / T_in
+
+
+class EncoderCTC(torch.nn.Module):
+    """Front-end + Conformer encoder + CTC head (the hot path of SURVEY.md §8a, 'frame' mode)."""
+
+    def __init__(self, L, d, H, ffn, K, V, F_bins, T_in, dropout, cd):
+        super().__init__()
+        hp = HParams(None)
+        hp.set_input_dim(F_bins, T_in)
+        self.hp = hp
+        self.cd = cd
+        self.conv_sub_sampling = ConvSubSampling(hp, 1, hp.conv_sub_2_nodes)
+        self.F1, self.T1 = (F_bins - 7) // 2 + 1, (T_in - 7) // 2 + 1
+        self.F2, self.T2 = (self.F1 - 3) // 2 + 1, (self.T1 - 3) // 2 + 1
+        self.standard_linear = torch.nn.Linear(self.F2 * hp.conv_sub_2_nodes, d)
+        self.conformers = Conformer(d, H, ffn, L, K, dropout, compute_dtype=cd)
+        self.ctc_fc = torch.nn.Linear(d, V)
+        self.dropout = dropout
+
+    def forward(self, x, lens_i32, seed):
+        B = x.shape[0]
+        h2 = self.conv_sub_sampling.forward_frames(x, self.cd)
+        p = self.dropout if self.training else 0.0
+        h = linear(h2.view(B * self.T2, -1), self.standard_linear.weight, self.standard_linear.bias, cd=self.cd,
+                   drop_p=p, seed=seed)
+        y = self.conformers.forward_tokens(h, lens_i32, B, self.T2, seed=seed + 7)
+        logits = linear(y, self.ctc_fc.weight, self.ctc_fc.bias, cd=self.cd, out_dtype=torch.float32)
+        return logits.view(B, self.T2, -1)
+
+
+class KernelProbe:
+    """HIP-event timing of one kernel family on the stream it is launched on (torch's current
+    stream, which every libcfm op uses).  Installed as ops.PROBE while the timed region runs."""
+
+    def __init__(self, match):
+        self.match = match
+        self.pairs = []
+        self.active = False
+
+    def __call__(self, kind, shape, launch):
+        if not (self.active and self.match(kind, shape)):
+            return launch()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = launch()
+        e.record()
+        self.pairs.append((s, e, shape))
+        return r
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        t = [s.elapsed_time(e) for s, e, _ in self.pairs]
+        return sum(t) / len(t) if t else float("nan"), len(t)
+
+
+def cpu_baseline(cfg, threads, steps=2):
+    """The CPU oracle (torch fp32 restatement of the same composition) on a bounded sample:
+    1 utterance x 15 s through front-end + encoder + CTC, fwd+bwd, 1 warm-up then `steps` timed."""
+    from oracle import conformer as oc
+    from oracle import frontend as of
+    name, L, d, H, ffn, K, _, secs = cfg
+    torch.set_num_threads(threads)
+    T_in = 100 * secs + 1
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(1, 1, 80, T_in, generator=g)
+    w1 = (torch.randn(512, 1, 7, 7, generator=g) * 0.1).requires_grad_()
+    b1 = torch.zeros(512, requires_grad=True)
+    w2 = (torch.randn(128, 512, 3, 3, generator=g) * 0.01).requires_grad_()
+    b2 = torch.zeros(128, requires_grad=True)
+    T2 = ((T_in - 7) // 2 + 1 - 3) // 2 + 1
+    wf = (torch.randn(d, 18 * 128, generator=g) * 0.02).requires_grad_()
+    bf = torch.zeros(d, requires_grad=True)
+    conf = oc.ConformerRef(d, H, ffn, L, K, 0.0).train()
+    wc = (torch.randn(1024, d, generator=g) * 0.02).requires_grad_()
+    tgt = torch.randint(1, 1024, (1, T2 // 4), generator=g)
+    lens = torch.tensor([T2])
+
+    def step():
+        h = of.frame_projection(of.convsub_forward(x, w1, b1, w2, b2), wf, bf)
+        y, _ = conf(h, lens)
+        lp = F.log_softmax(F.linear(y, wc), -1).transpose(0, 1)
+        loss = F.ctc_loss(lp, tgt, lens, torch.tensor([T2 // 4]), blank=0, zero_infinity=True)
+        loss.backward()
+
+    step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(T_in / dt, 1), "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "sample": f"{name} fp32 oracle (torch CPU), 1 x {secs} s utterance ({T_in} frames), front-end + "
+                      f"{L} layers + CTC, fwd+bwd, mean of {steps} steps after 1 warm-up"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="L15", choices=sorted(CONFIGS))
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-optimizer", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    rank, world, local = cdist.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = CONFIGS[args.config]
+    name, L, d, H, ffn, K, B, secs = cfg
+    T_in, Fb, V = 100 * secs + 1, 80, 1024
+    cd = torch.bfloat16
+
+    torch.manual_seed(1234)                      # identical init on every rank (then broadcast)
+    model = EncoderCTC(L, d, H, ffn, K, V, Fb, T_in, args.dropout, cd).to(dev).train()
+    cdist.broadcast_parameters(model)
+    params = [p for p in model.parameters() if p.requires_grad]
+    reducer = cdist.GradAllReducer(params)
+    opt = Adafactor(params, lr=2e-5, beta1=0.9, scale_parameter=False, relative_step=False)
+
+    # synthetic data: per-utterance min-max-normalised uniform mels, full lengths
+    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    x = torch.rand(B, Fb, T_in, generator=g)
+    x = (x - x.amin((1, 2), keepdim=True)) / (x.amax((1, 2), keepdim=True) - x.amin((1, 2), keepdim=True))
+    x = x.to(dev)
+    T2 = model.T2
+    lens_i32 = torch.full((B,), T2, dtype=torch.int32, device=dev)
+    U = T2 // 4
+    targets = torch.randint(1, V, (B, U), generator=g).to(dev)
+    in_lens = torch.full((B,), T2, dtype=torch.long)
+    tgt_lens = torch.full((B,), U, dtype=torch.long)
+
+    def step(i):
+        opt.zero_grad(set_to_none=False)
+        logits = model(x, lens_i32, seed=1000 * i + 17 * rank)
+        lp = F.log_softmax(logits, -1).transpose(0, 1)
+        loss = F.ctc_loss(lp, targets, in_lens, tgt_lens, blank=0, reduction="mean", zero_infinity=True)
+        loss.backward()
+        reducer.allreduce()
+        if not args.no_optimizer:
+            opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+
+    # dominant kernel: the FFN up-projection GEMM (M=B*T2, N=ffn, K=d, bf16, SiLU epilogue)
+    M_ffn = B * T2
+    probe = KernelProbe(lambda kind, shape: kind == "gemm" and shape == (M_ffn, ffn, d))
+    ops.PROBE = probe
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    probe.active = True
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    probe.active = False
+    ops.PROBE = None
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = tt.item()
+    ms_step = 1000.0 * elapsed / args.steps
+    frames_total = B * T_in * world * args.steps
+    value = frames_total / elapsed
+
+    gemm_ms, n_launch = probe.mean_ms()
+    gemm_flops = 2.0 * M_ffn * ffn * d
+    achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
+    _, fpf = algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, model.F2)
+    step_tflops = fpf * B * T_in / (ms_step * 1e-3) / 1e12
+
+    result = {
+        "metric": METRIC, "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (uniform min-max-normalised 80-bin mels, random init)",
+        "config": {"workload": f"{name} encoder fwd+bwd + CTC head, {B} x {secs} s utterances per GPU",
+                   "model": name, "layers": L, "d_model": d, "heads": H, "ffn": ffn, "conv_kernel": K,
+                   "global_batch": B * world, "seq_len": T_in, "enc_frames": T2, "frontend": "frame",
+                   "dropout": args.dropout, "optimizer": None if args.no_optimizer else "adafactor",
+                   "parallelism": f"dp{world}"},
+        "per_gpu_value": round(value / world, 1),
+        "step_algorithmic_tflops": round(step_tflops, 1),
+        "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
+        "loss": float(loss.item()),
+        "roofline": {"kernel": f"gemm_bf16 FFN up-projection M={M_ffn} N={ffn} K={d} (+bias+SiLU epilogue)",
+                     "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "avg_launch_ms": round(gemm_ms, 4), "launches_timed": n_launch,
+                     "flops_per_launch": gemm_flops},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

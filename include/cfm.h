@@ -180,6 +180,22 @@ size_t cfm_conv1_bwd_ws_bytes(int B, int F, int T, int C1);
 int cfm_conv1_bwd_weight(const void* dh1, int dtype_h, const float* x, float* dw1, float* db1,
                          int B, int F, int T, int C1, float* ws, void* stream);
 
+/* ---------------------------------------------------------------- Adafactor (runner.py:36)
+ * transformers.Adafactor(lr, beta1, scale_parameter=False, relative_step=False) as one
+ * multi-tensor step.  The host fills a parameter table (cfm_adafactor_fill_table into a host
+ * buffer of cfm_adafactor_table_bytes(n)), copies it to the device, and calls
+ * cfm_adafactor_step with the prefix totals (factored rows, factored columns, elementwise
+ * blocks = sum of cfm_adafactor_blocks(numel)).  col == NULL marks an unfactored (1-D) tensor,
+ * whose full second moment lives in `row`.  rowmean: >= sum(nb) floats; sumsq: n floats. */
+size_t cfm_adafactor_table_bytes(int n_params);
+int cfm_adafactor_fill_table(void* host_table, int i, float* p, const float* g, float* m, float* row,
+                             float* col, long numel, int nb, int R, int C, long row_off, long col_off,
+                             long blk_off, long rm_off);
+int cfm_adafactor_blocks(long numel);
+int cfm_adafactor_step(const void* dev_table, int n, long nrows, long ncols, long nblocks,
+                       float* rowmean, float* sumsq, float lr, float beta1, float beta2t, float eps1,
+                       float clip, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

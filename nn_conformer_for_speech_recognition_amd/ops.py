@@ -33,8 +33,14 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         out_scale=float(out_scale), residual=L.ptr(residual),
         ldr=ldr if ldr is not None else N, dtype_r=L.dt(residual) if residual is not None else F32,
         split_k=int(split_k))
-    L.call("cfm_gemm", L.ctypes.byref(d), L.stream())
+    if PROBE is not None:
+        PROBE("gemm", (M, N, K), lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
+    else:
+        L.call("cfm_gemm", L.ctypes.byref(d), L.stream())
     return C
+
+
+PROBE = None   # optional timing hook (bench.py KernelProbe): PROBE(kind, shape, launch)
 
 
 def linear(x, w, bias=None, out_dtype=None, act=ACT_NONE, pre=None, drop_p=0.0, seed=0, offset=0,

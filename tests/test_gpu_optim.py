@@ -1,0 +1,46 @@
+"""libcfm Adafactor vs transformers.Adafactor (the reference's optimizer, runner.py:36) on the
+same parameters and gradients, several steps, mixed tensor ranks (1-D, 2-D, 3-D, 4-D)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("beta1", [0.9, None])
+def test_adafactor_matches_transformers(beta1):
+    from transformers import Adafactor as HFAdafactor
+    from nn_conformer_for_speech_recognition_amd.optim import Adafactor
+    torch.manual_seed(0)
+    shapes = [(37,), (64, 48), (16, 8, 3, 3), (24, 1, 7), (512, 256), (5,)]
+    ref = [torch.randn(s, dtype=torch.float64) for s in shapes]
+    mine = [torch.nn.Parameter(r.float().cuda()) for r in ref]
+    theirs = [torch.nn.Parameter(r.clone()) for r in ref]
+    o1 = Adafactor(mine, lr=1e-2, beta1=beta1, scale_parameter=False, relative_step=False)
+    o2 = HFAdafactor(theirs, lr=1e-2, beta1=beta1, scale_parameter=False, relative_step=False)
+    for step in range(5):
+        for a, b in zip(mine, theirs):
+            g = torch.randn(a.shape, dtype=torch.float64) * (step + 1)
+            a.grad = g.float().cuda()
+            b.grad = g.clone()
+        o1.step()
+        o2.step()
+    torch.cuda.synchronize()
+    for a, b in zip(mine, theirs):
+        err = (a.detach().double().cpu() - b.detach()).norm() / b.detach().norm()
+        assert err < 1e-5, (tuple(a.shape), err.item())
+
+
+def test_adafactor_relative_step():
+    from transformers import Adafactor as HFAdafactor
+    from nn_conformer_for_speech_recognition_amd.optim import Adafactor
+    torch.manual_seed(1)
+    a = torch.nn.Parameter(torch.randn(32, 16).cuda())
+    b = torch.nn.Parameter(a.detach().cpu().double().clone())
+    o1 = Adafactor([a], lr=None, scale_parameter=False, relative_step=True)
+    o2 = HFAdafactor([b], lr=None, scale_parameter=False, relative_step=True)
+    for _ in range(3):
+        g = torch.randn(32, 16, dtype=torch.float64)
+        a.grad, b.grad = g.float().cuda(), g.clone()
+        o1.step()
+        o2.step()
+    assert ((a.detach().double().cpu() - b.detach()).norm() / b.detach().norm()) < 1e-5
