@@ -192,7 +192,7 @@ def main():
     tgt_lens = torch.full((B,), U, dtype=torch.long)
 
     def step(i):
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=True)     # autograd hands our fp32 grads over without an extra add
         logits = model(x, lens_i32, seed=1000 * i + 17 * rank)
         lp = F.log_softmax(logits, -1).transpose(0, 1)
         loss = F.ctc_loss(lp, targets, in_lens, tgt_lens, blank=0, reduction="mean", zero_infinity=True)

@@ -85,7 +85,7 @@ typedef struct cfm_gemm_desc {
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 
-/* out[n] (+)= sum_m x[m*ld + n]  — bias gradients (sum over tokens).  ws: >= 4*N*64 bytes. */
+/* out[n] (+)= sum_m x[m*ld + n]  — bias gradients (sum over tokens).  ws: >= 4*N*256 bytes. */
 int cfm_colsum(const void* x, int dtype_x, long M, int N, long ld, float* out, int accumulate,
                float* ws, void* stream);
 
@@ -189,12 +189,14 @@ int cfm_conv1_bwd_weight(const void* dh1, int dtype_h, const float* x, float* dw
  * whose full second moment lives in `row`.  rowmean: >= sum(nb) floats; sumsq: n floats. */
 size_t cfm_adafactor_table_bytes(int n_params);
 int cfm_adafactor_fill_table(void* host_table, int i, float* p, const float* g, float* m, float* row,
-                             float* col, long numel, int nb, int R, int C, long row_off, long col_off,
-                             long blk_off, long rm_off);
+                             float* col, long numel, int nb, int R, int C, long row_task_off,
+                             long col_off, long blk_off, long rm_off, long rm_task_off);
 int cfm_adafactor_blocks(long numel);
-int cfm_adafactor_step(const void* dev_table, int n, long nrows, long ncols, long nblocks,
-                       float* rowmean, float* sumsq, float lr, float beta1, float beta2t, float eps1,
-                       float clip, void* stream);
+long cfm_adafactor_row_tasks(int nb, int R, int C);
+long cfm_adafactor_rowmean_tasks(int nb, int R);
+int cfm_adafactor_step(const void* dev_table, int n, long nrow_tasks, long ncols, long nblocks,
+                       long nrowmean_tasks, float* rowmean, float* sumsq, float lr, float beta1,
+                       float beta2t, float eps1, float clip, void* stream);
 
 #ifdef __cplusplus
 }

@@ -231,17 +231,26 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnM p, bf16* __restrict
 }
 
 // ------------------------------------------------------------------------------------ D = rowsum(dO*O)
-__global__ void attn_bwd_dot_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ o, float* __restrict__ D,
-                                    int B, int T, int H, int dk) {
-  const long n = (long)B * H * T;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int t = (int)(i % T);
-    const long bh = i / T;
-    const int h = (int)(bh % H), b = (int)(bh / H);
-    const long base = ((long)b * T + t) * H * dk + h * dk;
-    float s = 0.f;
-    for (int d = 0; d < dk; ++d) s += (float)dout[base + d] * (float)o[base + d];
-    D[i] = s;
+// one wave per (b, t) token row: lanes sweep the H*dk features (coalesced), per-head sums via LDS
+__global__ __launch_bounds__(256) void attn_bwd_dot_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ o,
+                                                           float* __restrict__ D, int B, int T, int H, int dk) {
+  __shared__ float sacc[4][1024];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long row = (long)blockIdx.x * 4 + wv;          // b*T + t
+  const int HD = H * dk;
+  if (row < (long)B * T) {
+    const bf16* g = dout + row * HD;
+    const bf16* x = o + row * HD;
+    for (int c = lane; c < HD; c += 64) sacc[wv][c] = (float)g[c] * (float)x[c];
+  }
+  __syncthreads();
+  if (row < (long)B * T) {
+    const int b = (int)(row / T), t = (int)(row % T);
+    for (int h = lane; h < H; h += 64) {
+      float s = 0.f;
+      for (int d = 0; d < dk; ++d) s += sacc[wv][h * dk + d];
+      D[((long)b * H + h) * T + t] = s;
+    }
   }
 }
 
@@ -473,7 +482,9 @@ CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, co
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0)};
   const long nrow = (long)B * H * T;
-  hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)min(8192L, (nrow + 255) / 256)), dim3(256), 0, s,
+  (void)nrow;
+  CFM_REQUIRE(H * dk <= 1024, CFM_ERR_UNSUPPORTED, "H*dk must be <= 1024");
+  hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s,
                      (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse,
                      ws, (bf16*)dqkv);

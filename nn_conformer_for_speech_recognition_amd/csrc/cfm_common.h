@@ -25,6 +25,8 @@ namespace cfm {
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int check_launch(const char* what);
+// out[n] (+)= sum_p part[p*ldp + n]  (deterministic, block = 16 waves x 64 columns; ldp 0 -> N)
+void colreduce(const float* part, int nparts, long N, float* out, int accumulate, hipStream_t s, long ldp = 0);
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 }  // namespace cfm
 

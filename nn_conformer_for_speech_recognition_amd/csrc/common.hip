@@ -95,35 +95,77 @@ CFM_EXPORT int cfm_silu_bwd(const void* dy, int dtdy, const void* pre, int dtpre
   return cfm::check_launch("cfm_silu_bwd");
 }
 
-// --------------------------------------------------------------------------- column sums
+// --------------------------------------------------------------------------- column reductions
+// Deterministic two-level column sums.  Level 1 (colsum_partial): grid (ceil(N/64), NCHUNK), each
+// block = 4 waves over a contiguous row chunk, lane = column, waves interleave rows, LDS combine ->
+// one partial row per block.  Level 2 (colreduce_kernel): block = 16 waves over 64 columns, each
+// wave sums every 16th partial row, LDS combine.  Also used by LayerNorm / BatchNorm / depthwise
+// weight-gradient partial sums.
 namespace {
-// partial sums: grid (ceil(N/256), nblk); each block sums rows [b*rows_per, ...) for 256 cols
-__global__ void colsum_partial(const void* x, int dtx, long M, int N, long ld, long rows_per, float* ws) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+constexpr int COLSUM_CHUNKS = 256;
+
+__global__ __launch_bounds__(256) void colsum_partial(const void* __restrict__ x, int dtx, long M, int N, long ld,
+                                                      long rows_per, float* __restrict__ ws) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
   const long r0 = (long)blockIdx.y * rows_per;
   const long r1 = min(M, r0 + rows_per);
   float s = 0.f;
-  for (long r = r0; r < r1; ++r) s += ld_dyn(x, dtx, r * ld + n);
-  ws[(long)blockIdx.y * N + n] = s;
+  if (n < N) {
+    if (dtx == CFM_BF16) {
+      const bf16* p = reinterpret_cast<const bf16*>(x) + n;
+#pragma unroll 4
+      for (long r = r0 + wv; r < r1; r += 4) s += (float)p[r * ld];
+    } else {
+      const float* p = reinterpret_cast<const float*>(x) + n;
+#pragma unroll 4
+      for (long r = r0 + wv; r < r1; r += 4) s += p[r * ld];
+    }
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && n < N) ws[(long)blockIdx.y * N + n] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
-__global__ void colsum_final(const float* ws, int nblk, int N, float* out, int acc) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+
+__global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict__ part, int nparts, long N,
+                                                         long ldp, float* __restrict__ out, int acc) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long n = (long)blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += ws[(long)b * N + n];
-  out[n] = acc ? out[n] + s : s;
+  if (n < N) {
+#pragma unroll 4
+    for (int p = wv; p < nparts; p += 16) s += part[(long)p * ldp + n];
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][lane];
+    out[n] = acc ? out[n] + t : t;
+  }
 }
 }  // namespace
+
+namespace cfm {
+void colreduce(const float* part, int nparts, long N, float* out, int accumulate, hipStream_t s, long ldp) {
+  hipLaunchKernelGGL(colreduce_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, part, nparts, N,
+                     ldp > 0 ? ldp : N, out, accumulate);
+}
+}  // namespace cfm
 
 CFM_EXPORT int cfm_colsum(const void* x, int dtx, long M, int N, long ld, float* out, int accumulate,
                           float* ws, void* stream) {
   CFM_REQUIRE(x && out && ws && N > 0 && M >= 0 && ld >= N, CFM_ERR_ARG, "bad args");
-  const int nblk = 64;
+  int nblk = (int)((M + 63) / 64);
+  if (nblk > COLSUM_CHUNKS) nblk = COLSUM_CHUNKS;
+  if (nblk < 1) nblk = 1;
   const long rows_per = (M + nblk - 1) / nblk;
   hipStream_t s = cfm::as_stream(stream);
-  hipLaunchKernelGGL(colsum_partial, dim3(cdiv(N, 256), nblk), dim3(256), 0, s, x, dtx, M, N, ld,
+  hipLaunchKernelGGL(colsum_partial, dim3(cdiv(N, 64), nblk), dim3(256), 0, s, x, dtx, M, N, ld,
                      rows_per > 0 ? rows_per : 1, ws);
-  hipLaunchKernelGGL(colsum_final, dim3(cdiv(N, 256)), dim3(256), 0, s, ws, nblk, N, out, accumulate);
+  cfm::colreduce(ws, nblk, N, out, accumulate, s);
   return cfm::check_launch("cfm_colsum");
 }

@@ -1,19 +1,21 @@
 // convmod.hip — the HBM-bound middle of torchaudio's _ConvolutionModule:
 //   GLU(dim=channel) -> depthwise Conv1d(K, 'same' zero padding, bias) -> BatchNorm1d -> SiLU
-// and its backward.  Token-major layout (row = b*T + t, channel contiguous) so every load is
-// coalesced across channels; each workgroup owns a 64-channel x TT-frame tile of one utterance
-// and stages the GLU output (or dy) with its (K-1)/2 halo in LDS.  The kernel size is a
-// template parameter for the sizes the configs use (31, 33, ...) so the tap loops unroll.
+// and its backward, plus the generic BatchNorm1d of the projection block.
+// Token-major layout (row = b*T + t, channel contiguous) so every load is coalesced across
+// channels; each workgroup owns a 64-channel x TT-frame tile of one utterance and stages the GLU
+// output (or dy) with its (K-1)/2 halo in LDS.  The kernel size is a template parameter for the
+// sizes the configs use (31, 33, ...) so the tap loops unroll.
 // BatchNorm batch statistics (train mode) are per-channel sums over all B*T rows, INCLUDING
 // padded frames — exactly what torchaudio/transformers do (padding is not masked there).
-// Per-workgroup partial sums go to a workspace and are combined in double precision by a
-// finalize kernel (deterministic; no atomics).
+// Per-workgroup partial sums go to a workspace and are combined by cfm::colreduce
+// (deterministic two-level reduction; no atomics).
 #include "cfm_common.h"
 
 namespace {
 constexpr int CT = 64;    // channels per workgroup (one per lane)
 constexpr int TT = 64;    // frames per workgroup
 constexpr int KMAX = 63;  // largest supported depthwise kernel
+constexpr int BN_PARTS = 256;
 
 __device__ __forceinline__ float glu_at(const void* a, int dta, long row, int C, int c) {
   const float x = ld_dyn(a, dta, row * 2 * C + c);
@@ -75,19 +77,14 @@ __global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const void* __restr
   }
 }
 
-// finalize batch stats (double accumulation) + running-stat update (momentum, unbiased var).
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int nparts, long M, int C,
+// batch stats from column sums s1 (sum) and s2 (sum of squares) + running-stat update.
+__global__ void bn_finalize_kernel(const float* __restrict__ s1, const float* __restrict__ s2, long M, int C,
                                    float* __restrict__ mean, float* __restrict__ invstd,
                                    float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int p = 0; p < nparts; ++p) {
-    s1 += part[(long)p * C + c];
-    s2 += part[(long)(nparts + p) * C + c];
-  }
-  const double mu = s1 / (double)M;
-  double var = s2 / (double)M - mu * mu;
+  const double mu = (double)s1[c] / (double)M;
+  double var = (double)s2[c] / (double)M - mu * mu;
   if (var < 0.0) var = 0.0;
   mean[c] = (float)mu;
   invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
@@ -104,10 +101,10 @@ __global__ void bn_eval_stats_kernel(const float* __restrict__ rmean, const floa
   invstd[c] = rsqrtf(rvar[c] + eps);
 }
 
-__global__ void bn_silu_apply_kernel(const float* __restrict__ y, const float* __restrict__ gamma,
-                                     const float* __restrict__ beta, const float* __restrict__ mean,
-                                     const float* __restrict__ invstd, void* __restrict__ z, int dtz, long M,
-                                     int C, int act) {
+__global__ void bn_apply_kernel(const float* __restrict__ y, const float* __restrict__ gamma,
+                                const float* __restrict__ beta, const float* __restrict__ mean,
+                                const float* __restrict__ invstd, void* __restrict__ z, int dtz, long M, int C,
+                                int act) {
   const long n = M * C;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
@@ -116,61 +113,67 @@ __global__ void bn_silu_apply_kernel(const float* __restrict__ y, const float* _
   }
 }
 
-// generic per-block row partial sums (sum, sumsq) for BatchNorm1d over (M, C); grid (ceil(C/256), nparts)
-__global__ void bn_stats_rows_kernel(const float* __restrict__ y, long M, int C, long rows_per,
-                                     float* __restrict__ part) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+// row-chunk partial sums (sum, sumsq) of y over (M, C); grid (ceil(C/64), nparts), 4 waves per block
+__global__ __launch_bounds__(256) void bn_stats_rows_kernel(const float* __restrict__ y, long M, int C,
+                                                            long rows_per, float* __restrict__ part) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   const long r0 = (long)blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
   float s1 = 0.f, s2 = 0.f;
-  for (long r = r0; r < r1; ++r) {
-    const float v = y[r * C + c];
-    s1 += v;
-    s2 += v * v;
+  if (c < C)
+    for (long r = r0 + wv; r < r1; r += 4) {
+      const float v = y[r * C + c];
+      s1 += v;
+      s2 += v * v;
+    }
+  red[0][wv][lane] = s1;
+  red[1][wv][lane] = s2;
+  __syncthreads();
+  if (wv == 0 && c < C) {
+    part[(long)blockIdx.y * C + c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+    part[(long)(gridDim.y + blockIdx.y) * C + c] =
+        red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
   }
-  part[(long)blockIdx.y * C + c] = s1;
-  part[(long)(gridDim.y + blockIdx.y) * C + c] = s2;
 }
 
-// per-block partial (sum du, sum du*yhat) over a row range; grid (ceil(C/256), nparts)
-__global__ void bn_silu_bwd_reduce_kernel(const void* __restrict__ dz, int dtdz, const float* __restrict__ y,
-                                          const float* __restrict__ gamma, const float* __restrict__ beta,
-                                          const float* __restrict__ mean, const float* __restrict__ invstd,
-                                          long M, int C, long rows_per, float* __restrict__ part, int act) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+// row-chunk partials (sum du, sum du*yhat) for the BN backward; same geometry
+__global__ __launch_bounds__(256) void bn_bwd_rows_kernel(const void* __restrict__ dz, int dtdz,
+                                                          const float* __restrict__ y, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, long M, int C,
+                                                          long rows_per, float* __restrict__ part, int act) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   const long r0 = (long)blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
-  const float mu = mean[c], is = invstd[c], g = gamma[c], bt = beta[c];
   float sd = 0.f, sdx = 0.f;
-  for (long r = r0; r < r1; ++r) {
-    const long i = r * C + c;
-    const float yh = (y[i] - mu) * is;
-    const float du = ld_dyn(dz, dtdz, i) * (act ? silu_grad_f(yh * g + bt) : 1.f);
-    sd += du;
-    sdx += du * yh;
+  if (c < C) {
+    const float mu = mean[c], is = invstd[c], g = gamma[c], bt = beta[c];
+    for (long r = r0 + wv; r < r1; r += 4) {
+      const long i = r * C + c;
+      const float yh = (y[i] - mu) * is;
+      const float du = ld_dyn(dz, dtdz, i) * (act ? silu_grad_f(yh * g + bt) : 1.f);
+      sd += du;
+      sdx += du * yh;
+    }
   }
-  part[(long)blockIdx.y * C + c] = sd;
-  part[(long)(gridDim.y + blockIdx.y) * C + c] = sdx;
+  red[0][wv][lane] = sd;
+  red[1][wv][lane] = sdx;
+  __syncthreads();
+  if (wv == 0 && c < C) {
+    part[(long)blockIdx.y * C + c] = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+    part[(long)(gridDim.y + blockIdx.y) * C + c] =
+        red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+  }
 }
 
-__global__ void bn_silu_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int C,
-                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  double a = 0.0, b = 0.0;
-  for (int p = 0; p < nparts; ++p) {
-    a += part[(long)p * C + c];
-    b += part[(long)(nparts + p) * C + c];
-  }
-  dbeta[c] = (float)a;
-  dgamma[c] = (float)b;
-}
-
-__global__ void bn_silu_bwd_apply_kernel(const void* __restrict__ dz, int dtdz, const float* __restrict__ y,
-                                         const float* __restrict__ gamma, const float* __restrict__ beta,
-                                         const float* __restrict__ mean, const float* __restrict__ invstd,
-                                         const float* __restrict__ dgamma, const float* __restrict__ dbeta,
-                                         int training, float* __restrict__ dy, long M, int C, int act) {
+__global__ void bn_bwd_apply_kernel(const void* __restrict__ dz, int dtdz, const float* __restrict__ y,
+                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                                    const float* __restrict__ dgamma, const float* __restrict__ dbeta, int training,
+                                    float* __restrict__ dy, long M, int C, int act) {
   const long n = M * C;
   const float invM = 1.f / (float)M;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -244,8 +247,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const float* __rest
     }
   }
   __syncthreads();
-  // stage [4 waves][K+1][CT] and reduce over waves
-  float* red = sm;
+  float* red = sm;   // [4 waves][K+1][CT]
 #pragma unroll
   for (int k = 0; k < KR; ++k)
     if (KT > 0 || k < K) red[(wv * (K + 1) + k) * CT + lane] = dw[k];
@@ -264,16 +266,14 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const float* __rest
   }
 }
 
-// dw[c][k] = sum_p part[p][k][c]; db[c] = sum_p part[p][K][c]
-__global__ void dwconv_wgrad_reduce_kernel(const float* __restrict__ part, int nparts, int C, int K,
-                                           float* __restrict__ dw, float* __restrict__ db) {
-  const int i = blockIdx.x * 256 + threadIdx.x;     // over (K+1)*C, channel fastest (coalesced)
+// sums[k][c] (k <= K) -> dw[c][k], db[c]
+__global__ void dwconv_scatter_kernel(const float* __restrict__ sums, int C, int K, float* __restrict__ dw,
+                                      float* __restrict__ db) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= C * (K + 1)) return;
-  double s = 0.0;
-  for (int p = 0; p < nparts; ++p) s += part[(long)p * C * (K + 1) + i];
   const int k = i / C, c = i % C;
-  if (k < K) dw[c * K + k] = (float)s;
-  else if (db) db[c] = (float)s;
+  if (k < K) dw[c * K + k] = sums[i];
+  else if (db) db[c] = sums[i];
 }
 
 int ew_grid(long n) {
@@ -281,18 +281,45 @@ int ew_grid(long n) {
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
 }
 
+long conv_nparts(int B, int T) { return (long)B * ((T + TT - 1) / TT); }
+
+// fwd stats from [2][nparts][C] partials at ws; scratch (2C) right after them
+void bn_stats_finalize(const float* ws, int nparts, long M, int C, float* mean, float* invstd, float* rm, float* rv,
+                       float mom, float eps, hipStream_t s) {
+  float* sums = const_cast<float*>(ws) + 2L * nparts * C;
+  cfm::colreduce(ws, nparts, C, sums, 0, s);
+  cfm::colreduce(ws + (long)nparts * C, nparts, C, sums + C, 0, s);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, sums + C, M, C, mean, invstd,
+                     rm, rv, mom, eps);
+}
+
+int bn_bwd_impl(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta, const float* mean,
+                const float* invstd, int training, int act, float* dy, float* dgamma, float* dbeta, long M, int C,
+                float* ws, hipStream_t s) {
+  const long rows_per = (M + BN_PARTS - 1) / BN_PARTS;
+  hipLaunchKernelGGL(bn_bwd_rows_kernel, dim3(cdiv(C, 64), BN_PARTS), dim3(256), 0, s, dz, dtdz, y, gamma, beta, mean,
+                     invstd, M, C, rows_per > 0 ? rows_per : 1, ws, act);
+  cfm::colreduce(ws, BN_PARTS, C, dbeta, 0, s);
+  cfm::colreduce(ws + (long)BN_PARTS * C, BN_PARTS, C, dgamma, 0, s);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, dz, dtdz, y, gamma, beta, mean,
+                     invstd, dgamma, dbeta, training, dy, M, C, act);
+  return CFM_OK;
+}
+
 #define CFM_K_CASES(X) X(3) X(5) X(7) X(15) X(31) X(33)
 }  // namespace
 
 CFM_EXPORT size_t cfm_convmod_ws_bytes(int B, int T, int C, int K) {
-  const long nparts = (long)B * ((T + TT - 1) / TT);
-  const long fwd = 2 * nparts * C;
-  const long bwd = nparts * (long)C * (K + 1);
-  const long bn = 2L * 256 * C;
+  const long np = conv_nparts(B, T);
+  const long fwd = 2 * np * C + 2L * C;
+  const long bwd = np * (long)C * (K + 1) + (long)C * (K + 1);
+  const long bn = 2L * BN_PARTS * C;
   long m = fwd > bwd ? fwd : bwd;
   if (bn > m) m = bn;
   return (size_t)m * sizeof(float);
 }
+
+CFM_EXPORT size_t cfm_bn_ws_bytes(int C) { return (size_t)(2L * BN_PARTS * C + 2L * C) * sizeof(float); }
 
 CFM_EXPORT int cfm_glu_dwconv_fwd(const void* a, int dta, const float* w, const float* bias, float* y, int B,
                                   int T, int C, int K, float* ws, void* stream) {
@@ -321,30 +348,15 @@ CFM_EXPORT int cfm_bn_silu_fwd(const float* y, const float* gamma, const float* 
   const long M = (long)B * T;
   if (training) {
     CFM_REQUIRE(ws, CFM_ERR_ARG, "training mode needs the partial sums of cfm_glu_dwconv_fwd");
-    const int nparts = B * cdiv(T, TT);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, ws, nparts, M, C, mean, invstd,
-                       running_mean, running_var, momentum, eps);
+    bn_stats_finalize(ws, (int)conv_nparts(B, T), M, C, mean, invstd, running_mean, running_var, momentum, eps, s);
   } else {
     CFM_REQUIRE(running_mean && running_var, CFM_ERR_ARG, "eval mode needs running stats");
     hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, running_mean, running_var, C,
                        eps, mean, invstd);
   }
-  hipLaunchKernelGGL(bn_silu_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z,
-                     dtz, M, C, 1);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z, dtz,
+                     M, C, 1);
   return cfm::check_launch("cfm_bn_silu_fwd");
-}
-
-static int bn_bwd_impl(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
-                       const float* mean, const float* invstd, int training, int act, float* dy, float* dgamma,
-                       float* dbeta, long M, int C, float* ws, hipStream_t s) {
-  const int nparts = 256;
-  const long rows_per = (M + nparts - 1) / nparts;
-  hipLaunchKernelGGL(bn_silu_bwd_reduce_kernel, dim3(cdiv(C, 256), nparts), dim3(256), 0, s, dz, dtdz, y, gamma,
-                     beta, mean, invstd, M, C, rows_per > 0 ? rows_per : 1, ws, act);
-  hipLaunchKernelGGL(bn_silu_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, ws, nparts, C, dgamma, dbeta);
-  hipLaunchKernelGGL(bn_silu_bwd_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, dz, dtdz, y, gamma, beta,
-                     mean, invstd, dgamma, dbeta, training, dy, M, C, act);
-  return CFM_OK;
 }
 
 CFM_EXPORT int cfm_bn_silu_bwd(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
@@ -357,8 +369,6 @@ CFM_EXPORT int cfm_bn_silu_bwd(const void* dz, int dtdz, const float* y, const f
   return cfm::check_launch("cfm_bn_silu_bwd");
 }
 
-CFM_EXPORT size_t cfm_bn_ws_bytes(int C) { return (size_t)2 * 256 * C * sizeof(float); }
-
 CFM_EXPORT int cfm_bn_fwd(const float* y, const float* gamma, const float* beta, float* running_mean,
                           float* running_var, float momentum, float eps, int training, float* mean, float* invstd,
                           void* z, int dtz, long M, int C, int act, float* ws, void* stream) {
@@ -366,19 +376,17 @@ CFM_EXPORT int cfm_bn_fwd(const float* y, const float* gamma, const float* beta,
   CFM_REQUIRE(M > 0 && C > 0, CFM_ERR_SHAPE, "bad shape");
   hipStream_t s = cfm::as_stream(stream);
   if (training) {
-    const int nparts = 256;
-    const long rows_per = (M + nparts - 1) / nparts;
-    hipLaunchKernelGGL(bn_stats_rows_kernel, dim3(cdiv(C, 256), nparts), dim3(256), 0, s, y, M, C,
+    const long rows_per = (M + BN_PARTS - 1) / BN_PARTS;
+    hipLaunchKernelGGL(bn_stats_rows_kernel, dim3(cdiv(C, 64), BN_PARTS), dim3(256), 0, s, y, M, C,
                        rows_per > 0 ? rows_per : 1, ws);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, ws, nparts, M, C, mean, invstd,
-                       running_mean, running_var, momentum, eps);
+    bn_stats_finalize(ws, BN_PARTS, M, C, mean, invstd, running_mean, running_var, momentum, eps, s);
   } else {
     CFM_REQUIRE(running_mean && running_var, CFM_ERR_ARG, "eval mode needs running stats");
     hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, running_mean, running_var, C,
                        eps, mean, invstd);
   }
-  hipLaunchKernelGGL(bn_silu_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z,
-                     dtz, M, C, act);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z, dtz,
+                     M, C, act);
   return cfm::check_launch("cfm_bn_fwd");
 }
 
@@ -408,8 +416,9 @@ CFM_EXPORT int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dta, const
 #undef X
     default: hipLaunchKernelGGL(glu_dwconv_bwd_kernel<0>, grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws);
   }
-  const int nparts = B * cdiv(T, TT);
-  hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3(cdiv((long)C * (K + 1), 256)), dim3(256), 0, s, ws, nparts, C,
-                     K, dw, db);
+  const long np = conv_nparts(B, T);
+  float* sums = ws + np * (long)C * (K + 1);
+  cfm::colreduce(ws, (int)np, (long)C * (K + 1), sums, 0, s);
+  hipLaunchKernelGGL(dwconv_scatter_kernel, dim3(cdiv((long)C * (K + 1), 256)), dim3(256), 0, s, sums, C, K, dw, db);
   return cfm::check_launch("cfm_glu_dwconv_bwd");
 }

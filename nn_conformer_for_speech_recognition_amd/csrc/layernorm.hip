@@ -91,32 +91,25 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
       }
     }
   }
+  // combine the 4 waves' dgamma/dbeta partials in LDS -> one partial row per workgroup
+  __shared__ float red[4][2 * 64 * MAXJ];
+  const int wv = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < MAXJ; ++j) {
     const int c = lane + 64 * j;
     if (c < D) {
-      ws[(long)wglob * 2 * D + c] = pg[j];
-      ws[(long)wglob * 2 * D + D + c] = pb[j];
+      red[wv][c] = pg[j];
+      red[wv][D + c] = pb[j];
     }
   }
-}
-
-__global__ void ln_bwd_reduce(const float* __restrict__ ws, int nw, int D, float* __restrict__ dgamma,
-                              float* __restrict__ dbeta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= D) return;
-  float a = 0.f, b = 0.f;
-  for (int w = 0; w < nw; ++w) {
-    a += ws[(long)w * 2 * D + c];
-    b += ws[(long)w * 2 * D + D + c];
-  }
-  if (dgamma) dgamma[c] = a;
-  if (dbeta) dbeta[c] = b;
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += 256)
+    ws[(long)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
 int ln_bwd_blocks(long M) {
-  long b = (M + 3) / 4;
-  return (int)(b < 256 ? (b < 1 ? 1 : b) : 256);
+  long b = (M + 15) / 16;     // ~4 rows per wave
+  return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
 }
 }  // namespace
 
@@ -131,7 +124,7 @@ CFM_EXPORT int cfm_layernorm_fwd(const void* x, int dtx, const float* gamma, con
 }
 
 CFM_EXPORT size_t cfm_layernorm_ws_bytes(long M, int D) {
-  return (size_t)ln_bwd_blocks(M) * 4 * 2 * D * sizeof(float);
+  return (size_t)ln_bwd_blocks(M) * 2 * D * sizeof(float);
 }
 
 CFM_EXPORT int cfm_layernorm_bwd(const void* dy, int dtdy, const void* x, int dtx, const float* gamma,
@@ -144,6 +137,7 @@ CFM_EXPORT int cfm_layernorm_bwd(const void* dy, int dtdy, const void* x, int dt
   const int nb = ln_bwd_blocks(M);
   hipLaunchKernelGGL(ln_bwd_kernel, dim3(nb), dim3(256), 0, s, dy, dtdy, x, dtx, gamma, mean, rstd, dres,
                      dtres, dx, dtdx, ws, M, D);
-  hipLaunchKernelGGL(ln_bwd_reduce, dim3(cdiv(D, 256)), dim3(256), 0, s, ws, nb * 4, D, dgamma, dbeta);
+  if (dgamma) cfm::colreduce(ws, nb, D, dgamma, 0, s, 2L * D);
+  if (dbeta) cfm::colreduce(ws + D, nb, D, dbeta, 0, s, 2L * D);
   return cfm::check_launch("cfm_layernorm_bwd");
 }

@@ -7,7 +7,9 @@
 // mean(row)) * rsqrt(col_c) (or g * rsqrt(v)), clipped by max(1, RMS(u)/clip), scaled by lr,
 // first moment m = b1*m + (1-b1)*u, p -= m.  All parameters are handled by five launches over a
 // device-side parameter table (no per-tensor launches): row stats, column stats, row-stat means,
-// u^2 sums (one atomic per workgroup per tensor), apply.  HBM-bound.
+// u^2 sums (one atomic per workgroup per tensor), apply.  Work items are "tasks" whose shape
+// adapts to the tensor: a wide row (C >= 64) is one wave, narrow rows (e.g. the 3x3 taps of the
+// conv2 weight, nb = 65536) are packed 64 per wave (one per lane).  HBM-bound.
 #include "cfm_common.h"
 
 namespace {
@@ -18,31 +20,47 @@ constexpr int CHUNK = 4096;      // elements per block in the elementwise passes
 struct AdaP {
   float* p; const float* g; float* m; float* row; float* col;   // col == nullptr: unfactored (row = v)
   long numel; int nb, R, C, factored;
-  long row_off, col_off, blk_off, rm_off;                        // prefix offsets into global index spaces
+  long row_toff, col_off, blk_off, rm_off, rm_toff;              // prefix offsets (tasks / elements)
 };
 
+__device__ __forceinline__ long off_of(const AdaP& q, int which) {
+  return which == 0 ? q.row_toff : which == 1 ? q.col_off : which == 2 ? q.blk_off : q.rm_toff;
+}
 __device__ __forceinline__ int find_param(const AdaP* t, int n, long idx, int which) {
   int lo = 0, hi = n - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    const long off = which == 0 ? t[mid].row_off : which == 1 ? t[mid].col_off : t[mid].blk_off;
-    if (off <= idx) lo = mid; else hi = mid - 1;
+    if (off_of(t[mid], which) <= idx) lo = mid; else hi = mid - 1;
   }
   return lo;
 }
 
-// one wave per factored row: row = b2t*row + (1-b2t)*mean_c(g^2 + eps1)
-__global__ void ada_rows(const AdaP* __restrict__ t, int n, long nrows, float b2t, float eps1) {
+__device__ __forceinline__ void row_update(const AdaP& q, long lr, float s, float b2t) {
+  q.row[lr] = b2t * q.row[lr] + (1.f - b2t) * (s / q.C);
+}
+
+// row tasks: wide rows -> one wave per row; narrow rows -> 64 rows per wave (lane = row)
+__global__ void ada_rows(const AdaP* __restrict__ t, int n, long ntasks, float b2t, float eps1) {
   const int lane = threadIdx.x & 63;
-  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= nrows) return;
-  const AdaP& q = t[find_param(t, n, r, 0)];
-  const long lr = r - q.row_off;        // = b*R + i
-  const float* g = q.g + lr * q.C;
-  float s = 0.f;
-  for (int c = lane; c < q.C; c += 64) s += g[c] * g[c] + eps1;
-  s = wave_sum(s);
-  if (lane == 0) q.row[lr] = b2t * q.row[lr] + (1.f - b2t) * (s / q.C);
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= ntasks) return;
+  const AdaP& q = t[find_param(t, n, task, 0)];
+  const long lt = task - q.row_toff;
+  if (q.C >= 64) {
+    const float* g = q.g + lt * q.C;
+    float s = 0.f;
+    for (int c = lane; c < q.C; c += 64) s += g[c] * g[c] + eps1;
+    s = wave_sum(s);
+    if (lane == 0) row_update(q, lt, s, b2t);
+  } else {
+    const long lr = lt * 64 + lane;
+    if (lr < (long)q.nb * q.R) {
+      const float* g = q.g + lr * q.C;
+      float s = 0.f;
+      for (int c = 0; c < q.C; ++c) s += g[c] * g[c] + eps1;
+      row_update(q, lr, s, b2t);
+    }
+  }
 }
 
 // one thread per factored column: col = b2t*col + (1-b2t)*mean_r(g^2 + eps1)
@@ -61,17 +79,26 @@ __global__ void ada_cols(const AdaP* __restrict__ t, int n, long ncols, float b2
   q.col[lc] = b2t * q.col[lc] + (1.f - b2t) * (s / q.R);
 }
 
-// mean over R of the row state per (param, b): one wave each; rowmean[rm_off + b]
-__global__ void ada_rowmean(const AdaP* __restrict__ t, int n, float* __restrict__ rowmean) {
+// mean over R of the row state per (param, b): wide R -> one wave per b; narrow -> 64 b per wave
+__global__ void ada_rowmean(const AdaP* __restrict__ t, int n, long ntasks, float* __restrict__ rowmean) {
   const int lane = threadIdx.x & 63;
-  const int pi = blockIdx.x;
-  const AdaP& q = t[pi];
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= ntasks) return;
+  const AdaP& q = t[find_param(t, n, task, 3)];
   if (!q.factored) return;
-  for (int b = threadIdx.x >> 6; b < q.nb; b += 4) {
+  const long lt = task - q.rm_toff;
+  if (q.R >= 64) {
     float s = 0.f;
-    for (int r = lane; r < q.R; r += 64) s += q.row[(long)b * q.R + r];
+    for (int r = lane; r < q.R; r += 64) s += q.row[lt * q.R + r];
     s = wave_sum(s);
-    if (lane == 0) rowmean[q.rm_off + b] = s / q.R;
+    if (lane == 0) rowmean[q.rm_off + lt] = s / q.R;
+  } else {
+    const long b = lt * 64 + lane;
+    if (b < q.nb) {
+      float s = 0.f;
+      for (int r = 0; r < q.R; ++r) s += q.row[b * q.R + r];
+      rowmean[q.rm_off + b] = s / q.R;
+    }
   }
 }
 
@@ -137,31 +164,37 @@ __global__ void ada_apply(const AdaP* __restrict__ t, int n, const float* __rest
 
 CFM_EXPORT size_t cfm_adafactor_table_bytes(int n_params) { return (size_t)n_params * sizeof(AdaP); }
 
-/* table: device copy of n AdaP records built by cfm_adafactor_fill_table (host memory), rowmean /
- * sumsq: device scratch (n_rowmean, n_params floats). */
 CFM_EXPORT int cfm_adafactor_fill_table(void* host_table, int i, float* p, const float* g, float* m, float* row,
-                                        float* col, long numel, int nb, int R, int C, long row_off, long col_off,
-                                        long blk_off, long rm_off) {
+                                        float* col, long numel, int nb, int R, int C, long row_toff, long col_off,
+                                        long blk_off, long rm_off, long rm_toff) {
   CFM_REQUIRE(host_table && p && g && row, CFM_ERR_ARG, "null pointer");
   AdaP* t = reinterpret_cast<AdaP*>(host_table) + i;
   t->p = p; t->g = g; t->m = m; t->row = row; t->col = col;
   t->numel = numel; t->nb = nb; t->R = R; t->C = C; t->factored = col != nullptr;
-  t->row_off = row_off; t->col_off = col_off; t->blk_off = blk_off; t->rm_off = rm_off;
+  t->row_toff = row_toff; t->col_off = col_off; t->blk_off = blk_off; t->rm_off = rm_off; t->rm_toff = rm_toff;
   return CFM_OK;
 }
 
 CFM_EXPORT int cfm_adafactor_blocks(long numel) { return (int)((numel + CHUNK - 1) / CHUNK); }
 
-CFM_EXPORT int cfm_adafactor_step(const void* dev_table, int n, long nrows, long ncols, long nblocks,
-                                  float* rowmean, float* sumsq, float lr, float beta1, float beta2t, float eps1,
-                                  float clip, void* stream) {
+// number of row tasks / row-mean tasks a factored tensor contributes (see ada_rows / ada_rowmean)
+CFM_EXPORT long cfm_adafactor_row_tasks(int nb, int R, int C) { return C >= 64 ? (long)nb * R : ((long)nb * R + 63) / 64; }
+CFM_EXPORT long cfm_adafactor_rowmean_tasks(int nb, int R) { return R >= 64 ? (long)nb : ((long)nb + 63) / 64; }
+
+CFM_EXPORT int cfm_adafactor_step(const void* dev_table, int n, long nrow_tasks, long ncols, long nblocks,
+                                  long nrm_tasks, float* rowmean, float* sumsq, float lr, float beta1, float beta2t,
+                                  float eps1, float clip, void* stream) {
   CFM_REQUIRE(dev_table && rowmean && sumsq && n > 0, CFM_ERR_ARG, "bad args");
   const AdaP* t = reinterpret_cast<const AdaP*>(dev_table);
   hipStream_t s = cfm::as_stream(stream);
   (void)hipMemsetAsync(sumsq, 0, sizeof(float) * n, s);
-  if (nrows > 0) hipLaunchKernelGGL(ada_rows, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, s, t, n, nrows, beta2t, eps1);
-  if (ncols > 0) hipLaunchKernelGGL(ada_cols, dim3((unsigned)((ncols + EB - 1) / EB)), dim3(EB), 0, s, t, n, ncols, beta2t, eps1);
-  hipLaunchKernelGGL(ada_rowmean, dim3(n), dim3(256), 0, s, t, n, rowmean);
+  if (nrow_tasks > 0)
+    hipLaunchKernelGGL(ada_rows, dim3((unsigned)((nrow_tasks + 3) / 4)), dim3(256), 0, s, t, n, nrow_tasks, beta2t,
+                       eps1);
+  if (ncols > 0)
+    hipLaunchKernelGGL(ada_cols, dim3((unsigned)((ncols + EB - 1) / EB)), dim3(EB), 0, s, t, n, ncols, beta2t, eps1);
+  if (nrm_tasks > 0)
+    hipLaunchKernelGGL(ada_rowmean, dim3((unsigned)((nrm_tasks + 3) / 4)), dim3(256), 0, s, t, n, nrm_tasks, rowmean);
   hipLaunchKernelGGL(ada_sumsq, dim3((unsigned)nblocks), dim3(EB), 0, s, t, n, rowmean, beta2t, eps1, sumsq);
   hipLaunchKernelGGL(ada_apply, dim3((unsigned)nblocks), dim3(EB), 0, s, t, n, rowmean, beta2t, eps1, sumsq, lr,
                      beta1, clip);

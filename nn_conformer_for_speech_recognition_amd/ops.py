@@ -94,7 +94,7 @@ def colsum(x, out=None, accumulate=False):
     M, N = x.shape
     if out is None:
         out = torch.empty(N, device=x.device, dtype=torch.float32)
-    ws = workspace(4 * N * 64, x.device)
+    ws = workspace(4 * N * 256, x.device)
     L.call("cfm_colsum", L.ptr(x), L.dt(x), M, N, x.stride(0), L.ptr(out), int(accumulate), L.ptr(ws), L.stream())
     return out
 

@@ -81,7 +81,7 @@ class Adafactor(torch.optim.Optimizer):
                     p.grad = p.grad.contiguous()
             n = len(ps)
             host = (ctypes.c_char * L.size_call("cfm_adafactor_table_bytes", n))()
-            row_off = col_off = blk_off = rm_off = 0
+            row_off = col_off = blk_off = rm_off = rm_toff = 0
             steps = []
             for i, p in enumerate(ps):
                 st = self._ensure_state(p, group)
@@ -91,12 +91,14 @@ class Adafactor(torch.optim.Optimizer):
                 m = st.get("exp_avg")
                 row = st["exp_avg_sq_row"] if factored else st["exp_avg_sq"]
                 col = st["exp_avg_sq_col"] if factored else None
-                L.call("cfm_adafactor_fill_table", ctypes.cast(host, ctypes.c_void_p), i, L.ptr(p), L.ptr(p.grad), L.ptr(m), L.ptr(row), L.ptr(col),
-                       p.numel(), nb, R, C, row_off, col_off, blk_off, rm_off)
+                L.call("cfm_adafactor_fill_table", ctypes.cast(host, ctypes.c_void_p), i, L.ptr(p), L.ptr(p.grad),
+                       L.ptr(m), L.ptr(row), L.ptr(col), p.numel(), nb, R, C, row_off, col_off, blk_off, rm_off,
+                       rm_toff)
                 if factored:
-                    row_off += nb * R
+                    row_off += lib.cfm_adafactor_row_tasks(nb, R, C)
                     col_off += nb * C
                     rm_off += nb
+                    rm_toff += lib.cfm_adafactor_rowmean_tasks(nb, R)
                 blk_off += lib.cfm_adafactor_blocks(p.numel())
             if len(set(steps)) != 1:
                 raise L.CfmError("libcfm Adafactor: all parameters of a group must share the step count")
@@ -110,7 +112,8 @@ class Adafactor(torch.optim.Optimizer):
                 self._dev[key] = buf
             b2t = 1.0 - math.pow(step, group["decay_rate"])
             beta1 = group["beta1"] if group["beta1"] is not None else 0.0
-            L.call("cfm_adafactor_step", L.ptr(table), n, row_off, col_off, blk_off, L.ptr(buf[0]), L.ptr(buf[1]),
+            L.call("cfm_adafactor_step", L.ptr(table), n, row_off, col_off, blk_off, rm_toff, L.ptr(buf[0]),
+                   L.ptr(buf[1]),
                    float(self._lr(group, step)), float(beta1), float(b2t), float(group["eps"][0]),
                    float(group["clip_threshold"]), L.stream())
             self._keep = table      # keep the table alive until the stream has consumed it
