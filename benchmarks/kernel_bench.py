@@ -1,0 +1,84 @@
+"""Micro-benchmarks of the hot kernels at the Conformer-L / 15 s shapes (B=32, T_enc=373,
+M = 11,936 tokens).  Times each op with HIP events (median of N launches) and prints TFLOP/s or
+GB/s.  Usage: python benchmarks/kernel_bench.py [--only gemm|attn|ln|conv]"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nn_conformer_for_speech_recognition_amd import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def timeit(fn, n=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(n):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def bench_gemm():
+    M = 32 * 373
+    bf = torch.bfloat16
+    print("GEMM (bf16 operands):")
+    for (name, N, K) in [("ffn_up", 2048, 512), ("ffn_down", 512, 2048), ("qkv", 1536, 512), ("out/pw2", 512, 512),
+                         ("pw1", 1024, 512)]:
+        x = torch.randn(M, K, device=DEV, dtype=bf)
+        w = torch.randn(N, K, device=DEV, dtype=bf) * 0.05
+        b = torch.randn(N, device=DEV)
+        fl = 2.0 * M * N * K
+        y = torch.empty(M, N, device=DEV, dtype=bf)
+        t = timeit(lambda: ops.linear(x, w, b, out=y))
+        dy = torch.randn(M, N, device=DEV, dtype=bf)
+        dx = torch.empty(M, K, device=DEV, dtype=bf)
+        t2 = timeit(lambda: ops.linear_dgrad(dy, w, out=dx))
+        t3 = timeit(lambda: ops.linear_wgrad(dy, x))
+        print(f"  {name:9s} M={M} N={N} K={K}: fwd {t*1e3:7.1f}us {fl/t/1e9:6.0f} TF | dgrad {t2*1e3:7.1f}us "
+              f"{fl/t2/1e9:6.0f} TF | wgrad {t3*1e3:7.1f}us {fl/t3/1e9:6.0f} TF")
+
+
+def bench_attn():
+    B, T, H, dk = 32, 373, 8, 64
+    qkv = torch.randn(B * T, 3 * H * dk, device=DEV, dtype=torch.bfloat16)
+    lens = torch.full((B,), T, dtype=torch.int32, device=DEV)
+    o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk)
+    fl = 4.0 * B * H * T * T * dk
+    t = timeit(lambda: ops.attn_fwd(qkv, lens, B, T, H, dk))
+    do = torch.randn_like(o)
+    t2 = timeit(lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk))
+    print(f"attention B={B} T={T} H={H} dk={dk}: fwd {t*1e3:.1f}us {fl/t/1e9:.0f} TF | bwd {t2*1e3:.1f}us "
+          f"{2.5*fl/t2/1e9:.0f} TF")
+
+
+def bench_ln():
+    M, D = 32 * 373, 512
+    x = torch.randn(M, D, device=DEV)
+    g = torch.ones(D, device=DEV)
+    bt = torch.zeros(D, device=DEV)
+    y, mu, rs = ops.layernorm_fwd(x, g, bt, out_dtype=torch.bfloat16)
+    t = timeit(lambda: ops.layernorm_fwd(x, g, bt, out_dtype=torch.bfloat16))
+    dy = torch.randn(M, D, device=DEV, dtype=torch.bfloat16)
+    t2 = timeit(lambda: ops.layernorm_bwd(dy, x, g, mu, rs, dres=x))
+    print(f"layernorm M={M} D={D}: fwd {t*1e3:.1f}us {M*D*6/t/1e6:.0f} GB/s | bwd {t2*1e3:.1f}us "
+          f"{M*D*14/t2/1e6:.0f} GB/s")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    for name, fn in (("gemm", bench_gemm), ("attn", bench_attn), ("ln", bench_ln)):
+        if a.only in (None, name):
+            fn()

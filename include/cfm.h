@@ -81,7 +81,10 @@ typedef struct cfm_gemm_desc {
   float drop_p; uint64_t drop_seed; uint64_t drop_offset;
   float out_scale;
   const void* residual; long ldr; int dtype_r;
-  int split_k;             /* >1: C must be fp32 and pre-initialised; partial sums are added */
+  int split_k;             /* >1: C must be fp32 with a plain epilogue (alpha, bias) */
+  float* workspace;        /* split_k > 1: NULL -> partial sums are atomically added into a
+                              pre-initialised C; else >= split_k*batch*M*N floats of slabs that a
+                              second pass reduces into C (deterministic, no pre-initialisation) */
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 

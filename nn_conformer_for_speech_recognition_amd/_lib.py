@@ -38,6 +38,7 @@ class GemmDesc(ctypes.Structure):
         ("out_scale", c_float),
         ("residual", c_void_p), ("ldr", c_long), ("dtype_r", c_int),
         ("split_k", c_int),
+        ("workspace", c_void_p),
     ]
 
 

@@ -31,6 +31,8 @@ struct GemmP {
   float out_scale;
   const void* res; long ldr; int dtr;
   int split_k, k_per_split;
+  int vec_c;   // 8-wide epilogue legal: C/pre/residual/bias 16-B aligned rows
+  float* slab; // split-K slabs [batch*split][M][N] (nullptr: atomics into C)
 };
 
 template <typename T> struct VecOf;
@@ -132,11 +134,27 @@ template <typename T> struct Conv2DgradB {
 };
 
 // bf16 LDS geometry (elements)
-constexpr int BK16 = 32;
-constexpr int KM_STRIDE = BK16 + 8;        // K-major tile [128][40]: 80-B rows, conflict-free b128
-constexpr int MN_STRIDE = 128 + 32;        // MN-major tile [32][160]: 320-B rows, conflict-free tr16
-constexpr int TILE16 = 128 * KM_STRIDE;    // 5120 elements = 10 KiB (== 32*160)
-static_assert(TILE16 == BK16 * MN_STRIDE, "both layouts use the same LDS footprint");
+constexpr int BK16 = 64;
+constexpr int KM_STRIDE = BK16 + 8;        // K-major tile [128][72]: 144-B rows, conflict-free b128
+constexpr int MN_STRIDE = 128 + 32;        // MN-major tile [64][160]: 320-B rows, conflict-free tr16
+constexpr int TILE16 = (128 * KM_STRIDE > BK16 * MN_STRIDE) ? 128 * KM_STRIDE : BK16 * MN_STRIDE;  // 20 KiB
+constexpr int NV16 = 128 * BK16 / 8 / NT;  // 16-B vectors per thread per operand tile (4)
+constexpr int KV16 = BK16 / 8;             // vectors per K-major row (8)
+
+// XCD-aware tile order: blocks b and b+8 share an XCD under round-robin dispatch, so hand each
+// XCD a contiguous run of (row-major) tiles: neighbouring tiles then share their A panel in that
+// XCD's L2 (bijective for any tile count; speed only, never correctness).
+__device__ __forceinline__ void xcd_tile(int& tm, int& tn) {
+  const int gx = gridDim.x, nwg = gx * gridDim.y;
+  const int L = blockIdx.y * gx + blockIdx.x;
+  int id = L;
+  if (nwg > 8) {
+    const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+  }
+  tm = id / gx;
+  tn = id % gx;
+}
 
 // fp32 LDS geometry: both operands stored [BK][128+4] (k-rows)
 constexpr int BK32 = 16;
@@ -165,6 +183,10 @@ __device__ __forceinline__ void epilogue_store(const GemmP& p, int z, int m, int
   const long cidx = (long)z * p.sc + (long)m * p.ldc + n;
   float v = acc * p.alpha;
   if (p.split_k > 1) {
+    if (p.slab) {
+      p.slab[(long)blockIdx.z * p.M * p.N + (long)m * p.N + n] = v;
+      return;
+    }
     if (p.bias && blockIdx.z % p.split_k == 0) v += p.bias[n];
     atomicAdd(reinterpret_cast<float*>(p.C) + cidx, v);
     return;
@@ -181,13 +203,92 @@ __device__ __forceinline__ void epilogue_store(const GemmP& p, int z, int m, int
   st_dyn(p.C, p.dtc, cidx, v);
 }
 
+constexpr int EP_STRIDE = 128 + 4;   // f32 staging row stride: rows r and r+4 land 16 banks apart
+static_assert(128 * EP_STRIDE * 4 <= 4 * TILE16 * 2, "epilogue staging fits in the K-loop LDS");
+
+__device__ __forceinline__ void ld8_dyn(const void* p, int dt, long idx, float (&o)[8]) {
+  if (dt == CFM_BF16) {
+    const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p) + idx);
+    const bf16x8 b = __builtin_bit_cast(bf16x8, u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (float)b[e];
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + idx);
+    const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + idx + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = c.x; o[5] = c.y; o[6] = c.z; o[7] = c.w;
+  }
+}
+__device__ __forceinline__ void st8_dyn(void* p, int dt, long idx, const float (&v)[8]) {
+  if (dt == CFM_BF16) {
+    bf16x8 b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = (bf16)v[e];
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p) + idx) = __builtin_bit_cast(uint4, b);
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + idx) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + idx + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+// the epilogue of cfm_gemm_desc on 8 consecutive columns (vectorised when legal)
+__device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int m, int n, float (&v)[8]) {
+  if (m >= p.M || n >= p.N) return;
+  if (p.split_k > 1 && p.slab && n + 8 <= p.N && (p.N & 3) == 0) {
+    float* dst = p.slab + (long)blockIdx.z * p.M * p.N + (long)m * p.N + n;
+    *reinterpret_cast<float4*>(dst) = make_float4(v[0] * p.alpha, v[1] * p.alpha, v[2] * p.alpha, v[3] * p.alpha);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4] * p.alpha, v[5] * p.alpha, v[6] * p.alpha, v[7] * p.alpha);
+    return;
+  }
+  if (!p.vec_c || n + 8 > p.N || p.split_k > 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (n + e < p.N) epilogue_store(p, z, m, n + e, v[e]);
+    return;
+  }
+  const long cidx = (long)z * p.sc + (long)m * p.ldc + n;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+  if (p.bias) {
+    const float4 a = *reinterpret_cast<const float4*>(p.bias + n);
+    const float4 c = *reinterpret_cast<const float4*>(p.bias + n + 4);
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += c.x; v[5] += c.y; v[6] += c.z; v[7] += c.w;
+  }
+  if (p.act_grad) {
+    float pr[8];
+    ld8_dyn(p.pre, p.dtpre, cidx, pr);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= silu_grad_f(pr[e]);
+  }
+  if (p.act == CFM_ACT_SILU) {
+    if (p.pre) st8_dyn(p.pre, p.dtpre, cidx, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
+  }
+  if (p.drop_p > 0.f) {
+    const uint64_t base = p.doff + (uint64_t)((long)z * p.M * p.N + (long)m * p.N + n);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= dropout_scale(p.drop_p, p.seed, base + e);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
+  if (p.res) {
+    float r[8];
+    ld8_dyn(p.res, p.dtr, (long)z * p.sc + (long)m * p.ldr + n, r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += r[e];
+  }
+  st8_dyn(p.C, p.dtc, cidx, v);
+}
+
 // ---------------------------------------------------------------- bf16 kernel
 template <bool AK, bool BKM, class OA, class OB>
 __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[4 * TILE16];   // [buf][A,B] 40 KiB
+  __shared__ __attribute__((aligned(16))) bf16 lds[4 * TILE16];   // [buf][A,B] 80 KiB
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  int tm, tn;
+  xcd_tile(tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
   const int z = blockIdx.z / p.split_k, ks = blockIdx.z % p.split_k;
   oa.batch(z);
   ob.batch(z);
@@ -201,15 +302,15 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
 
-  uint4 ra[2], rb[2];
+  uint4 ra[NV16], rb[NV16];
   auto gload = [&](int kt) {
     const int k0 = kbeg + kt * BK16;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NV16; ++i) {
       const int v = tid + NT * i;
-      if constexpr (AK) ra[i] = oa.load(m0 + (v >> 2), k0 + (v & 3) * 8, p.M, kend);
+      if constexpr (AK) ra[i] = oa.load(m0 + v / KV16, k0 + (v % KV16) * 8, p.M, kend);
       else ra[i] = oa.load(k0 + (v >> 4), m0 + (v & 15) * 8, kend, p.M);
-      if constexpr (BKM) rb[i] = ob.load(n0 + (v >> 2), k0 + (v & 3) * 8, p.N, kend);
+      if constexpr (BKM) rb[i] = ob.load(n0 + v / KV16, k0 + (v % KV16) * 8, p.N, kend);
       else rb[i] = ob.load(k0 + (v >> 4), n0 + (v & 15) * 8, kend, p.N);
     }
   };
@@ -217,10 +318,10 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
     bf16* ta = lds + buf * 2 * TILE16;
     bf16* tb = ta + TILE16;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NV16; ++i) {
       const int v = tid + NT * i;
-      bf16* da = AK ? ta + (v >> 2) * KM_STRIDE + (v & 3) * 8 : ta + (v >> 4) * MN_STRIDE + (v & 15) * 8;
-      bf16* db = BKM ? tb + (v >> 2) * KM_STRIDE + (v & 3) * 8 : tb + (v >> 4) * MN_STRIDE + (v & 15) * 8;
+      bf16* da = AK ? ta + (v / KV16) * KM_STRIDE + (v % KV16) * 8 : ta + (v >> 4) * MN_STRIDE + (v & 15) * 8;
+      bf16* db = BKM ? tb + (v / KV16) * KM_STRIDE + (v % KV16) * 8 : tb + (v >> 4) * MN_STRIDE + (v & 15) * 8;
       *reinterpret_cast<uint4*>(da) = ra[i];
       *reinterpret_cast<uint4*>(db) = rb[i];
     }
@@ -253,16 +354,43 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
     __syncthreads();
   }
 
+  if (p.split_k > 1 && !p.slab) {
+    // split-K partials: atomics straight from the accumulators (32 consecutive columns per
+    // half-wave = two 128-B segments per instruction, the fast atomic shape)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int n = n0 + wn * 64 + j * 32 + (lane & 31);
+          epilogue_store(p, z, m, n, acc[i][j][r]);
+        }
+    return;
+  }
+  // epilogue: stage the 128x128 f32 tile in LDS (the staging buffers are free now), then every
+  // thread finishes 8 consecutive columns of a row -> 16-B / 32-B vector stores.
+  float* st = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int n = n0 + wn * 64 + j * 32 + (lane & 31);
-        epilogue_store(p, z, m, n, acc[i][j][r]);
+        const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = wn * 64 + j * 32 + (lane & 31);
+        st[row * EP_STRIDE + col] = acc[i][j][r];
       }
+  __syncthreads();
+#pragma unroll 2
+  for (int it = 0; it < 8; ++it) {
+    const int row = it * 16 + (tid >> 4), c8 = (tid & 15) * 8;
+    const float4 lo = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8);
+    const float4 hi = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8 + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    epilogue_store8(p, z, m0 + row, n0 + c8, v);
+  }
 }
 
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
@@ -369,6 +497,35 @@ GemmP plain_params(int M, int N, int K, void* C, long ldc, int dtc) {
   return p;
 }
 
+// C[z][m][n] = sum_s slab[z*split + s][m][n] + bias[n]   (fp32 C, 4 columns per thread)
+__global__ void splitk_reduce_kernel(const float* __restrict__ slab, int split, int batch, int M, int N,
+                                     float* __restrict__ C, long ldc, long sc, const float* __restrict__ bias) {
+  const long per = (long)M * N;
+  const long n4 = (long)batch * per / 4;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
+    const long i = q * 4;
+    const int z = (int)(i / per);
+    const long w = i % per;
+    const int m = (int)(w / N), n = (int)(w % N);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < split; ++k) {
+      const float4 a = *reinterpret_cast<const float4*>(slab + ((long)z * split + k) * per + w);
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+    if (bias) {
+      s.x += bias[n]; s.y += bias[n + 1]; s.z += bias[n + 2]; s.w += bias[n + 3];
+    }
+    float* dst = C + (long)z * sc + (long)m * ldc + n;
+    dst[0] = s.x; dst[1] = s.y; dst[2] = s.z; dst[3] = s.w;
+  }
+}
+
+int vec_epilogue_ok(const GemmP& p) {
+  auto al = [](const void* q) { return q == nullptr || (uintptr_t)q % 16 == 0; };
+  return (p.ldc % 8 == 0) && (p.sc % 8 == 0) && al(p.C) && al(p.pre) && al(p.bias) &&
+         (p.res == nullptr || (al(p.res) && p.ldr % 8 == 0));
+}
+
 int split_k_for(const GemmP& p, int bk) {
   return ((p.K + p.split_k - 1) / p.split_k + bk - 1) / bk * bk;
 }
@@ -378,6 +535,7 @@ int launch_typed(int /*dtype: implied by the loaders' element type*/, GemmP p, O
                  hipStream_t s) {
   dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
   if (grid.y > 65535 || grid.z > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
+  p.vec_c = vec_epilogue_ok(p);
   typedef decltype(oa.load(0, 0, 0, 0)) V;
   if constexpr (std::is_same<V, uint4>::value)
     hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OA, OB>), grid, dim3(NT), 0, s, p, oa, ob);
@@ -428,8 +586,19 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
     else if (bkm) rc = launch_typed<false, true>(d->dtype_ab, p, oa, ob, d->batch, s);
     else rc = launch_typed<false, false>(d->dtype_ab, p, oa, ob, d->batch, s);
   };
+  if (split > 1 && d->workspace) {
+    CFM_REQUIRE(d->N % 4 == 0 && d->ldc % 4 == 0, CFM_ERR_SHAPE, "slab split-K needs N % 4 == 0");
+    p.slab = d->workspace;
+  }
   if (bf) go(bf16{}); else go(float{});
   if (rc != CFM_OK) return rc;
+  if (p.slab) {
+    const long n4 = (long)d->batch * d->M * d->N / 4;
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p.slab, split, d->batch, d->M,
+                       d->N, (float*)d->C, d->ldc, d->stride_c, d->bias);
+  }
   return cfm::check_launch("cfm_gemm");
 }
 

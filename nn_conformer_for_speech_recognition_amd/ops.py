@@ -18,7 +18,7 @@ def _gemm_desc(**kw):
 
 def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, alpha=1.0,
          bias=None, act=ACT_NONE, act_grad=False, pre=None, drop_p=0.0, seed=0, offset=0, out_scale=1.0,
-         residual=None, ldr=None, split_k=1, batch=1, stride_a=0, stride_b=0, stride_c=0):
+         residual=None, ldr=None, split_k=1, batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None):
     """C = epilogue(alpha * A·Bᵀ) — see cfm_gemm_desc in include/cfm.h."""
     if A.dtype != B.dtype:
         raise L.CfmError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
@@ -32,7 +32,7 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         drop_p=float(drop_p), drop_seed=int(seed) & (2**64 - 1), drop_offset=int(offset),
         out_scale=float(out_scale), residual=L.ptr(residual),
         ldr=ldr if ldr is not None else N, dtype_r=L.dt(residual) if residual is not None else F32,
-        split_k=int(split_k))
+        split_k=int(split_k), workspace=L.ptr(workspace))
     if PROBE is not None:
         PROBE("gemm", (M, N, K), lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
     else:
@@ -72,13 +72,16 @@ def linear_wgrad(dy, x, out=None, split_k=None):
     K = x.shape[1]
     if split_k is None:
         tiles = ((N + 127) // 128) * ((K + 127) // 128)
-        split_k = max(1, min(32, 512 // max(tiles, 1), M // 1024))
+        split_k = max(1, min(16, 512 // max(tiles, 1), M // 1024))
     if out is None:
-        out = torch.zeros(N, K, device=dy.device, dtype=torch.float32) if split_k > 1 else \
-            torch.empty(N, K, device=dy.device, dtype=torch.float32)
-    elif split_k > 1:
-        out.zero_()
-    return gemm(dy, x, out, N, K, M, a_kmajor=False, b_kmajor=False, lda=N, ldb=K, split_k=split_k)
+        out = torch.empty(N, K, device=dy.device, dtype=torch.float32)
+    ws = None
+    if split_k > 1:
+        if K % 4 == 0:       # deterministic slab reduction (no atomics, no zero-fill)
+            ws = torch.empty(split_k * N * K, device=dy.device, dtype=torch.float32)
+        else:
+            out.zero_()
+    return gemm(dy, x, out, N, K, M, a_kmajor=False, b_kmajor=False, lda=N, ldb=K, split_k=split_k, workspace=ws)
 
 
 _ws_cache = {}
