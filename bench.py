@@ -257,6 +257,15 @@ def main():
                      "avg_launch_ms": round(gemm_ms, 4), "launches_timed": n_launch,
                      "flops_per_launch": gemm_flops},
     }
+    pmc = os.path.join(REPO, "profiles", "r01", "gemm_ffn_up_pmc.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            rec = json.load(f)
+        shp = rec.get("kernel_shape", {})
+        if (shp.get("M"), shp.get("N"), shp.get("K")) == (M_ffn, ffn, d):
+            result["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
+            result["roofline"]["traffic_source"] = "profiles/r01/gemm_ffn_up_pmc.json (rocprofv3 --pmc, fetch x2)"
+            result["roofline"]["algorithmic_bytes"] = rec["algorithmic_bytes_per_launch"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
     if rank == 0:
