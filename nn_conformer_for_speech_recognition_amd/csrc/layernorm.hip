@@ -4,12 +4,160 @@
 // self_attn_layer_norm, conv_module.layer_norm, final_layer_norm).  The residual stream is
 // fp32; the normalised output feeds the next GEMM in the compute dtype (bf16 or fp32).
 // Backward fuses the residual-gradient add (dx = LN'(dy) + dres) and produces dgamma/dbeta
-// through per-wave partial sums reduced by a second tiny kernel (deterministic, no atomics).
+// through per-workgroup partial rows reduced by cfm::colreduce (deterministic, no atomics).
+// Fast path (D = 64*V, fp32 residual stream): each lane owns V contiguous features, so every
+// load/store is a 16-B vector; other shapes/dtypes take the generic strided path.
 #include "cfm_common.h"
 
 namespace {
 constexpr int MAXJ = 16;   // D <= 1024
 
+// ---------------------------------------------------------------- vector helpers (V per lane)
+template <int V> __device__ __forceinline__ void ldv(const float* p, float (&o)[V]) {
+  if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 4; ++i) {
+      const float4 a = reinterpret_cast<const float4*>(p)[i];
+      o[4 * i] = a.x; o[4 * i + 1] = a.y; o[4 * i + 2] = a.z; o[4 * i + 3] = a.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = p[i];
+  }
+}
+template <int V> __device__ __forceinline__ void ldv(const bf16* p, float (&o)[V]) {
+  if constexpr (V % 8 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 8; ++i) {
+      const bf16x8 b = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(p)[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[8 * i + e] = (float)b[e];
+    }
+  } else if constexpr (V == 4) {
+    const bf16x4 b = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(p));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (float)b[e];
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = (float)p[i];
+  }
+}
+template <int V> __device__ __forceinline__ void stv(float* p, const float (&v)[V]) {
+  if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 4; ++i)
+      reinterpret_cast<float4*>(p)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) p[i] = v[i];
+  }
+}
+template <int V> __device__ __forceinline__ void stv(bf16* p, const float (&v)[V]) {
+  if constexpr (V % 8 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 8; ++i) {
+      bf16x8 b;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[e] = (bf16)v[8 * i + e];
+      reinterpret_cast<uint4*>(p)[i] = __builtin_bit_cast(uint4, b);
+    }
+  } else if constexpr (V == 4) {
+    bf16x4 b;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = (bf16)v[e];
+    *reinterpret_cast<uint2*>(p) = __builtin_bit_cast(uint2, b);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) p[i] = (bf16)v[i];
+  }
+}
+
+// ---------------------------------------------------------------- vectorised kernels
+template <int V, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, TY* __restrict__ y,
+                                                  float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
+                                                  float eps) {
+  constexpr int D = 64 * V;
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[V], g[V], b[V];
+  ldv<V>(x + row * D + lane * V, v);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) s += v[i];
+  const float mean = wave_sum(s) * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    v[i] -= mean;
+    q += v[i] * v[i];
+  }
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+  ldv<V>(gamma + lane * V, g);
+  ldv<V>(beta + lane * V, b);
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] = v[i] * rstd * g[i] + b[i];
+  stv<V>(y + row * D + lane * V, v);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+template <int V, typename TDY>
+__global__ __launch_bounds__(256) void ln_bwd_vec(const TDY* __restrict__ dy, const float* __restrict__ x,
+                                                  const float* __restrict__ gamma, const float* __restrict__ mean_in,
+                                                  const float* __restrict__ rstd_in, const float* __restrict__ dres,
+                                                  float* __restrict__ dx, float* __restrict__ ws, long M) {
+  constexpr int D = 64 * V;
+  __shared__ float red[4][2 * D];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wglob = blockIdx.x * 4 + wv;
+  const int nwaves = gridDim.x * 4;
+  float gm[V], pg[V], pb[V];
+  ldv<V>(gamma + lane * V, gm);
+#pragma unroll
+  for (int i = 0; i < V; ++i) pg[i] = pb[i] = 0.f;
+  for (long row = wglob; row < M; row += nwaves) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float d[V], xh[V], g[V];
+    ldv<V>(dy + row * D + lane * V, d);
+    ldv<V>(x + row * D + lane * V, xh);
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      xh[i] = (xh[i] - mean) * rstd;
+      g[i] = d[i] * gm[i];
+      pg[i] += d[i] * xh[i];
+      pb[i] += d[i];
+      sg += g[i];
+      sgx += g[i] * xh[i];
+    }
+    sg = wave_sum(sg) * (1.f / D);
+    sgx = wave_sum(sgx) * (1.f / D);
+    float o[V];
+    if (dres) ldv<V>(dres + row * D + lane * V, o);
+    else {
+#pragma unroll
+      for (int i = 0; i < V; ++i) o[i] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] += rstd * (g[i] - sg - xh[i] * sgx);
+    stv<V>(dx + row * D + lane * V, o);
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    red[wv][lane * V + i] = pg[i];
+    red[wv][D + lane * V + i] = pb[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += 256)
+    ws[(long)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+// ---------------------------------------------------------------- generic kernels (any D <= 1024)
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int dtx,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, void* __restrict__ y,
@@ -91,7 +239,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
       }
     }
   }
-  // combine the 4 waves' dgamma/dbeta partials in LDS -> one partial row per workgroup
   __shared__ float red[4][2 * 64 * MAXJ];
   const int wv = threadIdx.x >> 6;
 #pragma unroll
@@ -111,20 +258,58 @@ int ln_bwd_blocks(long M) {
   long b = (M + 15) / 16;     // ~4 rows per wave
   return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
 }
+
+bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; }
+
+template <int V>
+bool ln_fwd_fast(const void* x, int dtx, const float* gamma, const float* beta, void* y, int dty, float* mean,
+                 float* rstd, long M, int D, float eps, hipStream_t s) {
+  if (D != 64 * V || dtx != CFM_F32 || !aligned16(x) || !aligned16(y) || !aligned16(gamma) || !aligned16(beta))
+    return false;
+  dim3 g((unsigned)((M + 3) / 4));
+  if (dty == CFM_BF16)
+    hipLaunchKernelGGL((ln_fwd_vec<V, bf16>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (bf16*)y, mean, rstd, M,
+                       eps);
+  else
+    hipLaunchKernelGGL((ln_fwd_vec<V, float>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (float*)y, mean, rstd,
+                       M, eps);
+  return true;
+}
+
+template <int V>
+bool ln_bwd_fast(const void* dy, int dtdy, const void* x, int dtx, const float* gamma, const float* mean,
+                 const float* rstd, const void* dres, int dtres, void* dx, int dtdx, float* ws, long M, int D, int nb,
+                 hipStream_t s) {
+  if (D != 64 * V || dtx != CFM_F32 || dtdx != CFM_F32 || (dres && dtres != CFM_F32)) return false;
+  if (!aligned16(dy) || !aligned16(x) || !aligned16(dres) || !aligned16(dx) || !aligned16(gamma)) return false;
+  if (dtdy == CFM_BF16)
+    hipLaunchKernelGGL((ln_bwd_vec<V, bf16>), dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const float*)x, gamma, mean,
+                       rstd, (const float*)dres, (float*)dx, ws, M);
+  else
+    hipLaunchKernelGGL((ln_bwd_vec<V, float>), dim3(nb), dim3(256), 0, s, (const float*)dy, (const float*)x, gamma,
+                       mean, rstd, (const float*)dres, (float*)dx, ws, M);
+  return true;
+}
 }  // namespace
 
-CFM_EXPORT int cfm_layernorm_fwd(const void* x, int dtx, const float* gamma, const float* beta, void* y,
-                                 int dty, float* mean, float* rstd, long M, int D, float eps, void* stream) {
+CFM_EXPORT int cfm_layernorm_fwd(const void* x, int dtx, const float* gamma, const float* beta, void* y, int dty,
+                                 float* mean, float* rstd, long M, int D, float eps, void* stream) {
   CFM_REQUIRE(x && gamma && beta && y && mean && rstd, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(D > 0 && D <= 64 * MAXJ && M >= 0, CFM_ERR_SHAPE, "D must be in (0, 1024]");
   if (M == 0) return CFM_OK;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, cfm::as_stream(stream), x,
-                     dtx, gamma, beta, y, dty, mean, rstd, M, D, eps);
+  hipStream_t s = cfm::as_stream(stream);
+  const bool fast = ln_fwd_fast<2>(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s) ||
+                    ln_fwd_fast<4>(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s) ||
+                    ln_fwd_fast<8>(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s) ||
+                    ln_fwd_fast<16>(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s);
+  if (!fast)
+    hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, dtx, gamma, beta, y, dty,
+                       mean, rstd, M, D, eps);
   return cfm::check_launch("cfm_layernorm_fwd");
 }
 
 CFM_EXPORT size_t cfm_layernorm_ws_bytes(long M, int D) {
-  return (size_t)ln_bwd_blocks(M) * 2 * D * sizeof(float);
+  return (size_t)ln_bwd_blocks(M) * 2 * D * sizeof(float) + 2 * D * sizeof(float);
 }
 
 CFM_EXPORT int cfm_layernorm_bwd(const void* dy, int dtdy, const void* x, int dtx, const float* gamma,
@@ -135,9 +320,18 @@ CFM_EXPORT int cfm_layernorm_bwd(const void* dy, int dtdy, const void* x, int dt
   CFM_REQUIRE(D > 0 && D <= 64 * MAXJ && M >= 0, CFM_ERR_SHAPE, "D must be in (0, 1024]");
   hipStream_t s = cfm::as_stream(stream);
   const int nb = ln_bwd_blocks(M);
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nb), dim3(256), 0, s, dy, dtdy, x, dtx, gamma, mean, rstd, dres,
-                     dtres, dx, dtdx, ws, M, D);
-  if (dgamma) cfm::colreduce(ws, nb, D, dgamma, 0, s, 2L * D);
-  if (dbeta) cfm::colreduce(ws + D, nb, D, dbeta, 0, s, 2L * D);
+  const bool fast = ln_bwd_fast<2>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s) ||
+                    ln_bwd_fast<4>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s) ||
+                    ln_bwd_fast<8>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s) ||
+                    ln_bwd_fast<16>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s);
+  if (!fast)
+    hipLaunchKernelGGL(ln_bwd_kernel, dim3(nb), dim3(256), 0, s, dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres,
+                       dx, dtdx, ws, M, D);
+  if (dgamma && dbeta && dbeta == dgamma + D) {
+    cfm::colreduce(ws, nb, 2L * D, dgamma, 0, s);               // one pass for [dgamma | dbeta]
+  } else {
+    if (dgamma) cfm::colreduce(ws, nb, D, dgamma, 0, s, 2L * D);
+    if (dbeta) cfm::colreduce(ws + D, nb, D, dbeta, 0, s, 2L * D);
+  }
   return cfm::check_launch("cfm_layernorm_bwd");
 }

@@ -126,8 +126,8 @@ def layernorm_fwd(x, gamma, beta, eps=1e-5, out_dtype=None):
 def layernorm_bwd(dy, x, gamma, mean, rstd, dres=None, dx_dtype=torch.float32):
     M, D = x.shape
     dx = torch.empty(M, D, device=x.device, dtype=dx_dtype)
-    dgamma = torch.empty(D, device=x.device, dtype=torch.float32)
-    dbeta = torch.empty(D, device=x.device, dtype=torch.float32)
+    gb = torch.empty(2, D, device=x.device, dtype=torch.float32)   # adjacent: one reduction pass
+    dgamma, dbeta = gb[0], gb[1]
     ws = workspace(L.size_call("cfm_layernorm_ws_bytes", M, D), x.device)
     L.call("cfm_layernorm_bwd", L.ptr(dy), L.dt(dy), L.ptr(x), L.dt(x), L.ptr(gamma), L.ptr(mean), L.ptr(rstd),
            L.ptr(dres), L.dt(dres), L.ptr(dx), L.dt(dx), L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws), M, D, L.stream())
