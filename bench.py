@@ -162,7 +162,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-optimizer", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--gemm-mode", type=int, default=None, help="cfm_gemm_set_mode value (A/B tuning)")
     args = ap.parse_args()
+    if args.gemm_mode is not None:
+        from nn_conformer_for_speech_recognition_amd import _lib
+        _lib.call("cfm_gemm_set_mode", args.gemm_mode)
 
     rank, world, local = cdist.init_from_env()
     torch.cuda.set_device(local)

@@ -1,0 +1,58 @@
+"""A/B timing of GEMM kernel variants (cfm_gemm_set_mode values) on the encoder's shapes,
+interleaved per shape so clock drift hits every variant alike.
+    python benchmarks/gemm_ab.py --modes 1,2,18 [--epi plain|silu]"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nn_conformer_for_speech_recognition_amd import _lib, ops  # noqa: E402
+
+
+def timeit(fn, n=30, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n
+
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--modes", default="1,2")
+ap.add_argument("--epi", default="plain")
+a = ap.parse_args()
+modes = [int(m) for m in a.modes.split(",")]
+M = 32 * 373
+bf = torch.bfloat16
+shapes = [("ffn_up", 2048, 512), ("ffn_down", 512, 2048), ("qkv", 1536, 512), ("out/pw2", 512, 512), ("pw1", 1024, 512)]
+print(f"epilogue={a.epi}; columns: mode -> us (TF/s)")
+for name, N, K in shapes:
+    x = torch.randn(M, K, device="cuda", dtype=bf)
+    w = torch.randn(N, K, device="cuda", dtype=bf) * 0.05
+    b = torch.randn(N, device="cuda")
+    y = torch.empty(M, N, device="cuda", dtype=bf)
+    pre = torch.empty(M, N, device="cuda", dtype=bf)
+    dy = torch.randn(M, N, device="cuda", dtype=bf)
+    dx = torch.empty(M, K, device="cuda", dtype=bf)
+    fl = 2.0 * M * N * K
+    cases = {
+        "fwd": (lambda: ops.linear(x, w, b, out=y)) if a.epi == "plain" else
+               (lambda: ops.linear(x, w, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=1, out=y)),
+        "dgrad": lambda: ops.linear_dgrad(dy, w, out=dx),
+        "wgrad": lambda: ops.linear_wgrad(dy, x),
+    }
+    for cname, fn in cases.items():
+        row = []
+        for m in modes:
+            _lib.call("cfm_gemm_set_mode", m)
+            t = timeit(fn)
+            row.append(f"{m}: {t*1e3:6.1f} ({fl/t/1e9:4.0f})")
+        print(f"  {name:9s} {cname:5s} N={N:5d} K={K:5d} | " + " | ".join(row))
+_lib.call("cfm_gemm_set_mode", 3)

@@ -30,9 +30,19 @@ def timeit(fn, n=20, warm=3):
 
 
 def bench_gemm():
+    from nn_conformer_for_speech_recognition_amd import _lib
+    _bench_gemm("warm-up pass (clocks ramp)")
+    for mode, tag in ((0, "register-staged 128x128"), (1, "register-staged, 256x128 when wide"),
+                      (2, "LDS-DMA pipeline"), (6, "LDS-DMA pipeline, 256x128 forced")):
+        _lib.call("cfm_gemm_set_mode", mode)
+        _bench_gemm(f"mode {mode}: {tag}")
+    _lib.call("cfm_gemm_set_mode", 3)
+
+
+def _bench_gemm(tag):
     M = 32 * 373
     bf = torch.bfloat16
-    print("GEMM (bf16 operands):")
+    print(f"GEMM (bf16 operands, {tag}):")
     for (name, N, K) in [("ffn_up", 2048, 512), ("ffn_down", 512, 2048), ("qkv", 1536, 512), ("out/pw2", 512, 512),
                          ("pw1", 1024, 512)]:
         x = torch.randn(M, K, device=DEV, dtype=bf)

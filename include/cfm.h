@@ -87,6 +87,11 @@ typedef struct cfm_gemm_desc {
                               second pass reduces into C (deterministic, no pre-initialisation) */
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
+/* kernel-selection switch for A/B measurements: bit 0 = 256-row register-staged tiles allowed,
+   bit 1 = LDS-DMA pipelined kernel allowed, bit 3 = timing experiment (pipelined kernel skips its
+   stores), bits 4-5 = pipelined variant (0 auto, 1 256x128/BK64, 2 256x128/BK32 two per CU,
+   3 128x128/BK64); default 3. */
+int cfm_gemm_set_mode(int mode);
 
 /* out[n] (+)= sum_m x[m*ld + n]  — bias gradients (sum over tokens).  ws: >= 4*N*256 bytes. */
 int cfm_colsum(const void* x, int dtype_x, long M, int N, long ld, float* out, int accumulate,

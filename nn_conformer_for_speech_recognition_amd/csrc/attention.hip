@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dot_kernel(const bf16* __restric
 
 // ------------------------------------------------------------------------------------ dQ
 // grid (ceil(T/128), H, B); wave = 32 queries.  dqkv q-part written (bf16), scaled by 1/sqrt(dk).
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnM p, const bf16* __restrict__ dout,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(AttnM p, const bf16* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ Dg,
                                                           bf16* __restrict__ dqkv) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];

@@ -60,20 +60,83 @@ __device__ __forceinline__ float silu_grad_f(float x) {
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
 
-// ----------------------------------------------------------------------------- dropout RNG
-// Counter-based: keep(seed, idx) is a pure function, so backward regenerates the mask.
-__device__ __forceinline__ uint32_t cfm_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = idx * 0x9E3779B97F4A7C15ull + seed;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+// 8 consecutive elements (16-B aligned) of a bf16 or f32 array, as f32
+__device__ __forceinline__ void ld8_dyn(const void* p, int dt, long idx, float (&o)[8]) {
+  if (dt == CFM_BF16) {
+    const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p) + idx);
+    const bf16x8 b = __builtin_bit_cast(bf16x8, u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (float)b[e];
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + idx);
+    const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + idx + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = c.x; o[5] = c.y; o[6] = c.z; o[7] = c.w;
+  }
 }
-// returns scale (1/(1-p)) if kept, 0 if dropped
+__device__ __forceinline__ void st8_dyn(void* p, int dt, long idx, const float (&v)[8]) {
+  if (dt == CFM_BF16) {
+    bf16x8 b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = (bf16)v[e];
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p) + idx) = __builtin_bit_cast(uint4, b);
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + idx) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + idx + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+// ----------------------------------------------------------------------------- dropout RNG
+// Counter-based dropout: element idx of a call keyed by `seed` draws 16 uniform bits; elements
+// 2j and 2j+1 share one 32-bit hash of j (lowbias32 mixer, two 32-bit multiplies), so the mask
+// costs a few VALU ops per element and is regenerated bit-identically in the backward kernels.
+__device__ __forceinline__ uint32_t cfm_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t drop_key(uint64_t seed, uint32_t jhi) {
+  return cfm_mix32(jhi ^ (uint32_t)seed ^ cfm_mix32((uint32_t)(seed >> 32) + 0x9E3779B9u));
+}
+__device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t idx) {
+  const uint64_t j = idx >> 1;
+  const uint32_t h = cfm_mix32((uint32_t)j ^ drop_key(seed, (uint32_t)(j >> 32)));
+  return (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
+}
+// dropped iff the 16 bits fall below round(p * 65536); kept elements scale by the exact inverse
+// keep probability
+__device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+__device__ __forceinline__ float drop_keep_scale(uint32_t thr) { return 65536.f / (float)(65536u - thr); }
+// returns the keep scale if kept, 0 if dropped
 __device__ __forceinline__ float dropout_scale(float p, uint64_t seed, uint64_t idx) {
   if (p <= 0.f) return 1.f;
-  float u = (float)(cfm_hash(seed, idx) >> 8) * (1.0f / 16777216.0f);
-  return u >= p ? 1.f / (1.f - p) : 0.f;
+  const uint32_t thr = drop_thr(p);
+  return drop_bits(seed, idx) >= thr ? drop_keep_scale(thr) : 0.f;
+}
+// the same mask for the 8 consecutive elements base .. base+7 (5 hashes instead of 8 x 2)
+__device__ __forceinline__ void dropout_scale8(float p, uint64_t seed, uint64_t base, float (&s)[8]) {
+  const uint32_t thr = drop_thr(p);
+  const float keep = drop_keep_scale(thr);
+  const uint64_t j0 = base >> 1;
+  const uint32_t lo0 = (uint32_t)j0;
+  if (lo0 <= 0xFFFFFFFBu) {
+    const uint32_t key = drop_key(seed, (uint32_t)(j0 >> 32));
+    uint32_t h[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) h[q] = cfm_mix32((lo0 + q) ^ key);
+    const int odd = (int)(base & 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int q = (odd + e) >> 1;
+      const uint32_t b = ((odd + e) & 1) ? (h[q] >> 16) : (h[q] & 0xFFFFu);
+      s[e] = b >= thr ? keep : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = drop_bits(seed, base + e) >= thr ? keep : 0.f;
+  }
 }
 
 // ----------------------------------------------------------------------------- reductions

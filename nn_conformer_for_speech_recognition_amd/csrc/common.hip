@@ -43,6 +43,18 @@ __global__ void scale_dropout_kernel(const void* x, int dtx, void* y, int dty, l
     st_dyn(y, dty, i, v);
   }
 }
+// 8 elements per thread (n % 8 == 0, 16-B aligned x / y)
+__global__ void scale_dropout8_kernel(const void* x, int dtx, void* y, int dty, long n8, float scale,
+                                      float p, uint64_t seed, uint64_t off) {
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (long)gridDim.x * blockDim.x) {
+    float v[8], s[8];
+    ld8_dyn(x, dtx, q * 8, v);
+    if (p > 0.f) dropout_scale8(p, seed, off + (uint64_t)(q * 8), s);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= p > 0.f ? scale * s[e] : scale;
+    st8_dyn(y, dty, q * 8, v);
+  }
+}
 }  // namespace
 
 static int grid_for(long n, int per_thread) {
@@ -74,8 +86,12 @@ CFM_EXPORT int cfm_scale_dropout(const void* x, int dtx, void* y, int dty, long 
                                  float p, uint64_t seed, uint64_t off, void* stream) {
   CFM_REQUIRE(x && y && n >= 0, CFM_ERR_ARG, "bad args");
   if (n == 0) return CFM_OK;
-  hipLaunchKernelGGL(scale_dropout_kernel, dim3(grid_for(n, 1)), dim3(256), 0, cfm::as_stream(stream), x,
-                     dtx, y, dty, n, scale, p, seed, off);
+  if (n % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0)
+    hipLaunchKernelGGL(scale_dropout8_kernel, dim3(grid_for(n / 8, 1)), dim3(256), 0, cfm::as_stream(stream), x,
+                       dtx, y, dty, n / 8, scale, p, seed, off);
+  else
+    hipLaunchKernelGGL(scale_dropout_kernel, dim3(grid_for(n, 1)), dim3(256), 0, cfm::as_stream(stream), x,
+                       dtx, y, dty, n, scale, p, seed, off);
   return cfm::check_launch("cfm_scale_dropout");
 }
 

@@ -36,6 +36,7 @@ struct GemmP {
   // output row remap for the conv2 data-grad parity classes: row m = (b, i, j) of the class
   // -> dh1 row (b, 2i+pf, 2j+pt)
   int cmap, cm_F1c, cm_T1c, cm_pf, cm_pt, cm_F1, cm_T1;
+  int dbg;     // timing experiments only (cfm_gemm_set_mode bit 3): skip the epilogue's stores
 };
 
 __device__ __forceinline__ long out_row(const GemmP& p, int m) {
@@ -175,16 +176,17 @@ constexpr int F_STRIDE = 128 + 4;
 constexpr int TILE32 = BK32 * F_STRIDE;
 
 // Read one 32x32x16 operand fragment (8 bf16, natural k order) from a staged tile.
-template <bool KMAJOR>
+// MNS: row stride of the MN-major image (rows + 32 elements: 64 mod 256 bytes -> conflict-free tr16)
+template <bool KMAJOR, int MNS = MN_STRIDE>
 __device__ __forceinline__ bf16x8 frag16(const bf16* tile, int row0, int kk, int lane) {
   if constexpr (KMAJOR) {
     const bf16* p = tile + (row0 + (lane & 31)) * KM_STRIDE + kk + 8 * (lane >> 5);
     return *reinterpret_cast<const bf16x8*>(p);
   } else {
     const int h = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
-    const bf16* base = tile + (kk + 8 * h + q) * MN_STRIDE + row0 + 16 * g1 + 4 * p4;
+    const bf16* base = tile + (kk + 8 * h + q) * MNS + row0 + 16 * g1 + 4 * p4;
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 4 * MN_STRIDE));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 4 * MNS));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, v);
@@ -218,30 +220,6 @@ __device__ __forceinline__ void epilogue_store(const GemmP& p, int z, int m, int
 
 constexpr int EP_STRIDE = 128 + 4;   // f32 staging row stride: rows r and r+4 land 16 banks apart
 static_assert(128 * EP_STRIDE * 4 <= 4 * TILE16 * 2, "epilogue staging fits in the K-loop LDS");
-
-__device__ __forceinline__ void ld8_dyn(const void* p, int dt, long idx, float (&o)[8]) {
-  if (dt == CFM_BF16) {
-    const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p) + idx);
-    const bf16x8 b = __builtin_bit_cast(bf16x8, u);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = (float)b[e];
-  } else {
-    const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + idx);
-    const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + idx + 4);
-    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = c.x; o[5] = c.y; o[6] = c.z; o[7] = c.w;
-  }
-}
-__device__ __forceinline__ void st8_dyn(void* p, int dt, long idx, const float (&v)[8]) {
-  if (dt == CFM_BF16) {
-    bf16x8 b;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) b[e] = (bf16)v[e];
-    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p) + idx) = __builtin_bit_cast(uint4, b);
-  } else {
-    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + idx) = make_float4(v[0], v[1], v[2], v[3]);
-    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + idx + 4) = make_float4(v[4], v[5], v[6], v[7]);
-  }
-}
 
 // the epilogue of cfm_gemm_desc on 8 consecutive columns (vectorised when legal)
 __device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int m, int n, float (&v)[8]) {
@@ -279,8 +257,10 @@ __device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int m, in
   }
   if (p.drop_p > 0.f) {
     const uint64_t base = p.doff + (uint64_t)((long)z * p.M * p.N + (long)m * p.N + n);
+    float ds[8];
+    dropout_scale8(p.drop_p, p.seed, base, ds);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] *= dropout_scale(p.drop_p, p.seed, base + e);
+    for (int e = 0; e < 8; ++e) v[e] *= ds[e];
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
@@ -294,14 +274,34 @@ __device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int m, in
 }
 
 // ---------------------------------------------------------------- bf16 kernel
-template <bool AK, bool BKM, class OA, class OB>
-__global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[4 * TILE16];   // [buf][A,B] 80 KiB
+// BMt x 128 output tile, BMt*2 threads (BMt/64 x 2 waves of 64x64): BMt = 128 (80 KiB LDS, 2
+// workgroups/CU) for narrow or split-K shapes, BMt = 256 (112 KiB, 1 workgroup/CU of 8 waves: 1.5x
+// the FLOP per staged byte) for the wide token-major GEMMs.
+template <int BMt>
+struct Geo16 {
+  static constexpr int NTt = BMt * 2;
+  static constexpr int NVA = BMt * BK16 / 8 / NTt;      // A vectors per thread (4)
+  static constexpr int NVB = BN * BK16 / 8 / NTt;       // B vectors per thread (4 or 2)
+  static constexpr int MNSA = BMt + 32;                  // MN-major A row stride
+  static constexpr int TILEA = (BMt * KM_STRIDE > BK16 * MNSA) ? BMt * KM_STRIDE : BK16 * MNSA;
+  static constexpr int TILEB = TILE16;
+  static constexpr int LDS = 2 * (TILEA + TILEB);        // elements
+};
+
+template <int BMt>
+__device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2], float* st, int z, int m0, int n0,
+                                              int wm, int wn, int lane, int tid);
+
+template <int BMt, bool AK, bool BKM, class OA, class OB>
+__global__ __launch_bounds__(BMt * 2) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
+  typedef Geo16<BMt> G;
+  constexpr int NTt = G::NTt, NVA = G::NVA, NVB = G::NVB, TILEA = G::TILEA;
+  __shared__ __attribute__((aligned(16))) bf16 lds[G::LDS];   // [buf][A,B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   int tm, tn;
   xcd_tile(tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * BMt, n0 = tn * BN;
   const int z = blockIdx.z / p.split_k, ks = blockIdx.z % p.split_k;
   oa.batch(z);
   ob.batch(z);
@@ -315,27 +315,36 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
 
-  uint4 ra[NV16], rb[NV16];
+  constexpr int AV = BMt / 8;     // MN-major A: vectors per k-row
+  uint4 ra[NVA], rb[NVB];
   auto gload = [&](int kt) {
     const int k0 = kbeg + kt * BK16;
 #pragma unroll
-    for (int i = 0; i < NV16; ++i) {
-      const int v = tid + NT * i;
+    for (int i = 0; i < NVA; ++i) {
+      const int v = tid + NTt * i;
       if constexpr (AK) ra[i] = oa.load(m0 + v / KV16, k0 + (v % KV16) * 8, p.M, kend);
-      else ra[i] = oa.load(k0 + (v >> 4), m0 + (v & 15) * 8, kend, p.M);
+      else ra[i] = oa.load(k0 + v / AV, m0 + (v % AV) * 8, kend, p.M);
+    }
+#pragma unroll
+    for (int i = 0; i < NVB; ++i) {
+      const int v = tid + NTt * i;
       if constexpr (BKM) rb[i] = ob.load(n0 + v / KV16, k0 + (v % KV16) * 8, p.N, kend);
       else rb[i] = ob.load(k0 + (v >> 4), n0 + (v & 15) * 8, kend, p.N);
     }
   };
   auto sstore = [&](int buf) {
-    bf16* ta = lds + buf * 2 * TILE16;
-    bf16* tb = ta + TILE16;
+    bf16* ta = lds + buf * (TILEA + TILE16);
+    bf16* tb = ta + TILEA;
 #pragma unroll
-    for (int i = 0; i < NV16; ++i) {
-      const int v = tid + NT * i;
-      bf16* da = AK ? ta + (v / KV16) * KM_STRIDE + (v % KV16) * 8 : ta + (v >> 4) * MN_STRIDE + (v & 15) * 8;
-      bf16* db = BKM ? tb + (v / KV16) * KM_STRIDE + (v % KV16) * 8 : tb + (v >> 4) * MN_STRIDE + (v & 15) * 8;
+    for (int i = 0; i < NVA; ++i) {
+      const int v = tid + NTt * i;
+      bf16* da = AK ? ta + (v / KV16) * KM_STRIDE + (v % KV16) * 8 : ta + (v / AV) * G::MNSA + (v % AV) * 8;
       *reinterpret_cast<uint4*>(da) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NVB; ++i) {
+      const int v = tid + NTt * i;
+      bf16* db = BKM ? tb + (v / KV16) * KM_STRIDE + (v % KV16) * 8 : tb + (v >> 4) * MN_STRIDE + (v & 15) * 8;
       *reinterpret_cast<uint4*>(db) = rb[i];
     }
   };
@@ -348,13 +357,13 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const bf16* ta = lds + cur * 2 * TILE16;
-    const bf16* tb = ta + TILE16;
+    const bf16* ta = lds + cur * (TILEA + TILE16);
+    const bf16* tb = ta + TILEA;
 #pragma unroll
     for (int kk = 0; kk < BK16; kk += 16) {
       bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = frag16<AK>(ta, wm * 64 + i * 32, kk, lane);
+      for (int i = 0; i < 2; ++i) af[i] = frag16<AK, G::MNSA>(ta, wm * 64 + i * 32, kk, lane);
 #pragma unroll
       for (int j = 0; j < 2; ++j) bfr[j] = frag16<BKM>(tb, wn * 64 + j * 32, kk, lane);
 #pragma unroll
@@ -367,6 +376,15 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
     __syncthreads();
   }
 
+  tile_epilogue<BMt>(p, acc, reinterpret_cast<float*>(lds), z, m0, n0, wm, wn, lane, tid);
+}
+
+// Epilogue of one BMt x 128 tile (4-wave rows x 2-wave columns of 64x64 accumulators).  The
+// caller guarantees every wave is done reading the staging LDS (`st`, >= 128 x EP_STRIDE floats).
+template <int BMt>
+__device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2], float* st, int z, int m0, int n0,
+                                              int wm, int wn, int lane, int tid) {
+  constexpr int NTt = BMt * 2;
   if (p.split_k > 1 && !p.slab) {
     // split-K partials: atomics straight from the accumulators (32 consecutive columns per
     // half-wave = two 128-B segments per instruction, the fast atomic shape)
@@ -382,28 +400,214 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
         }
     return;
   }
-  // epilogue: stage the 128x128 f32 tile in LDS (the staging buffers are free now), then every
-  // thread finishes 8 consecutive columns of a row -> 16-B / 32-B vector stores.
-  float* st = reinterpret_cast<float*>(lds);
+  // stage 128-row halves of the f32 tile in LDS, then every thread finishes 8 consecutive
+  // columns of a row -> 16-B / 32-B vector stores.
+#pragma unroll
+  for (int hf = 0; hf < BMt / 128; ++hf) {
+    if ((wm >> 1) == hf) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = (wm & 1) * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const int col = wn * 64 + j * 32 + (lane & 31);
+            st[row * EP_STRIDE + col] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int it = 0; it < 128 * 16 / NTt; ++it) {
+      const int row = it * (NTt / 16) + (tid >> 4), c8 = (tid & 15) * 8;
+      const float4 lo = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8);
+      const float4 hi = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8 + 4);
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      epilogue_store8(p, z, m0 + 128 * hf + row, n0 + c8, v);
+    }
+    if (hf + 1 < BMt / 128) __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- bf16 pipelined kernel
+// The fast path for plain strided bf16 operands.  Staging is LDS-DMA (buffer_load_dwordx4 ... lds:
+// no VGPR round trip, no per-element predicates) into a PS-deep ring of LDS stages: two K tiles
+// are in flight while the waves compute on a third, with one raw s_barrier and a counted
+// vmcnt per K tile (a __syncthreads would drain the DMA queue every step).
+//
+// LDS-DMA writes a wave's 64 x 16 B contiguously, so bank-conflict-free images come from
+// permuting the *source* chunks:
+//   K-major [R][64] image (128-B rows, read by ds_read_b128 along k):
+//       chunk c of row r lives at slot c ^ ((r >> 1) & 7)
+//   MN-major [64][R] image (R*2-B k-rows, read by ds_read_b64_tr_b16):
+//       chunk c of k-row k lives at slot c ^ (4 * (k & 3))
+// Rows past M/N are clamped to the last valid row (their outputs are never stored); k-rows past K
+// of an MN-major operand read as zero through the buffer resource's range check.
+struct PipeOp {
+  const bf16* base;
+  long ld, bstride;
+  int lim;          // valid rows (K-major) / columns (MN-major) of the M or N dimension
+  unsigned bytes;   // extent of one batch for the range check
+};
+
+// BMt x 128 tile, BKt-deep K steps, NST-stage ring; the f32 epilogue staging aliases the ring
+template <int BMt, int BKt, int NST>
+struct PipeGeo {
+  static constexpr int NTt = BMt * 2, NW = NTt / 64;
+  static constexpr int ABYTES = BMt * BKt * 2, BBYTES = BN * BKt * 2;
+  static constexpr int STAGE = ABYTES + BBYTES;
+  static constexpr int RING = NST * STAGE, EPI = 128 * EP_STRIDE * 4;
+  static constexpr int LDS = RING > EPI ? RING : EPI;
+  static constexpr int AI = ABYTES / 1024 / NW, BI = BBYTES / 1024 / NW;   // DMA per wave per stage
+  static_assert(AI * NW * 1024 == ABYTES && BI * NW * 1024 == BBYTES, "whole wave-instructions per stage");
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pipe_rsrc(const PipeOp& o, int z) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(o.base + (long)z * o.bstride), (short)0, (int)o.bytes,
+                                           0x00020000);
+}
+
+// one wave-instruction of LDS-DMA: lane l's 16 B from rsrc + voff land at lds_base + 16 l
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 16, voff, 0, 0, 0);
+}
+
+// K-major [R][BKt] image: BKt*2-B rows, RPB rows per 256-B bank row, CPR 16-B chunks per row;
+// chunk c of row r sits in slot c ^ ((r / RPB) % CPR): 16 consecutive rows read at one k hit 16
+// distinct 16-B bank groups (conflict-free ds_read_b128)
+template <int BKt>
+struct KmSw {
+  static constexpr int RB = BKt * 2, CPR = BKt / 8, RPB = 256 / RB;
+  __device__ static __forceinline__ int slot(int r, int c) { return c ^ ((r / RPB) & (CPR - 1)); }
+};
+
+// byte offset (in the operand) of the 16-B chunk that lands in LDS slot `lc` of an R-row image
+template <bool KM, int R, int BKt>
+__device__ __forceinline__ unsigned pipe_src(const PipeOp& o, int lc, int row0, int k0) {
+  if constexpr (KM) {
+    typedef KmSw<BKt> S;
+    const int r = lc / S::CPR, c = S::slot(r, lc % S::CPR);
+    const int row = row0 + r < o.lim ? row0 + r : o.lim - 1;
+    return (unsigned)(((long)row * o.ld + k0 + 8 * c) * 2);
+  } else {
+    constexpr int CPR = R / 8;
+    const int k = lc / CPR, c = (lc % CPR) ^ (4 * (k & 3));
+    const int col = row0 + 8 * c < o.lim - 8 ? row0 + 8 * c : o.lim - 8;
+    return (unsigned)(((long)(k0 + k) * o.ld + col) * 2);
+  }
+}
+
+// one 32x32x16 operand fragment from a swizzled stage image
+template <bool KM, int R, int BKt>
+__device__ __forceinline__ bf16x8 pipe_frag(const char* img, int row0, int kk, int lane) {
+  if constexpr (KM) {
+    typedef KmSw<BKt> S;
+    const int r = row0 + (lane & 31), c = (kk >> 3) + (lane >> 5);
+    return *reinterpret_cast<const bf16x8*>(img + r * S::RB + 16 * S::slot(r, c));
+  } else {
+    const int h = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+    const int col = row0 + 16 * g1 + 4 * p4, k = kk + 8 * h + q;   // k & 3 == q for both halves
+    const int off = 16 * ((col >> 3) ^ (4 * q)) + (col & 7) * 2;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + k * (R * 2) + off));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + (k + 4) * (R * 2) + off));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// wait until at most `younger` stages (of PER DMA instructions each) are still in flight
+template <int PER>
+__device__ __forceinline__ void wait_stages(int younger) {
+  if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+  else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM>
+__global__ __launch_bounds__(BMt * 2) __attribute__((amdgpu_waves_per_eu(OCC * BMt / 128)))
+void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
+  typedef PipeGeo<BMt, BKt, NST> G;
+  static_assert(NST >= 3 && NST <= 4, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char lds[G::LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  int tm, tn;
+  xcd_tile(tm, tn);
+  const int m0 = tm * BMt, n0 = tn * BN;
+  const int z = blockIdx.z / p.split_k, ks = blockIdx.z % p.split_k;
+  const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, z), rb = pipe_rsrc(ob, z);
+  const int kbeg = ks * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg + BKt - 1) / BKt : 0;
+
+  // per-lane source offsets of stage 0; later stages add k0 * (row stride) (MN-major) or k0 * 2
+  unsigned offa[G::AI], offb[G::BI];
+#pragma unroll
+  for (int i = 0; i < G::AI; ++i) offa[i] = pipe_src<AK, BMt, BKt>(oa, (i * G::NW + wid) * 64 + lane, m0, kbeg);
+#pragma unroll
+  for (int i = 0; i < G::BI; ++i) offb[i] = pipe_src<BKM, BN, BKt>(ob, (i * G::NW + wid) * 64 + lane, n0, kbeg);
+  const unsigned stepa = AK ? BKt * 2 : (unsigned)(BKt * oa.ld * 2);
+  const unsigned stepb = BKM ? BKt * 2 : (unsigned)(BKt * ob.ld * 2);
+
+  auto issue = [&](int kt) {
+    char* sa = lds + (kt % NST) * G::STAGE;
+    char* sb = sa + G::ABYTES;
+#pragma unroll
+    for (int i = 0; i < G::AI; ++i)
+      dma16(ra, sa + (i * G::NW + wid) * 1024, offa[i] + kt * stepa);
+#pragma unroll
+    for (int i = 0; i < G::BI; ++i)
+      dma16(rb, sb + (i * G::NW + wid) * 1024, offb[i] + kt * stepb);
+  };
+
+  f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = wn * 64 + j * 32 + (lane & 31);
-        st[row * EP_STRIDE + col] = acc[i][j][r];
-      }
-  __syncthreads();
-#pragma unroll 2
-  for (int it = 0; it < 8; ++it) {
-    const int row = it * 16 + (tid >> 4), c8 = (tid & 15) * 8;
-    const float4 lo = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8);
-    const float4 hi = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8 + 4);
-    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    epilogue_store8(p, z, m0 + row, n0 + c8, v);
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) issue(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt has landed once only the younger issued stages are outstanding
+    const int younger = min(NST - 2, nk - 1 - kt);
+    wait_stages<G::AI + G::BI>(younger);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NST - 1 < nk) issue(kt + NST - 1);   // refills the stage every wave finished reading at kt-1
+    const char* sa = lds + (kt % NST) * G::STAGE;
+    const char* sb = sa + G::ABYTES;
+#pragma unroll
+    for (int kk = 0; kk < BKt; kk += 16) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = pipe_frag<AK, BMt, BKt>(sa, wm * 64 + i * 32, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = pipe_frag<BKM, BN, BKt>(sb, wn * 64 + j * 32, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
   }
+  if (p.dbg) {       // timing experiment: keep the accumulators live, store nothing
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+    if (t == -1234.5f) reinterpret_cast<float*>(p.C)[tid] = t;
+    return;
+  }
+  __syncthreads();   // every wave done with the ring (no DMA outstanding) -> reuse it for the epilogue
+  tile_epilogue<BMt>(p, acc, reinterpret_cast<float*>(lds), z, m0, n0, wm, wn, lane, tid);
 }
 
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
@@ -533,6 +737,10 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, int split, 
   }
 }
 
+// kernel-selection switch (cfm_gemm_set_mode) for A/B measurements:
+// bit 0 = 256-row register-staged tiles allowed, bit 1 = LDS-DMA pipelined kernel allowed
+int g_gemm_mode = 3;
+
 int vec_epilogue_ok(const GemmP& p) {
   auto al = [](const void* q) { return q == nullptr || (uintptr_t)q % 16 == 0; };
   return (p.ldc % 8 == 0) && (p.sc % 8 == 0) && al(p.C) && al(p.pre) && al(p.bias) &&
@@ -546,18 +754,82 @@ int split_k_for(const GemmP& p, int bk) {
 template <bool AK, bool BKM, class OA, class OB>
 int launch_typed(int /*dtype: implied by the loaders' element type*/, GemmP p, OA oa, OB ob, int batch,
                  hipStream_t s) {
-  dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
-  if (grid.y > 65535 || grid.z > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
   p.vec_c = vec_epilogue_ok(p);
   typedef decltype(oa.load(0, 0, 0, 0)) V;
-  if constexpr (std::is_same<V, uint4>::value)
-    hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OA, OB>), grid, dim3(NT), 0, s, p, oa, ob);
-  else
+  if constexpr (std::is_same<V, uint4>::value) {
+    // 256-row tiles when the grid still fills the chip (>= ~2 tiles per CU) without split-K
+    const bool wide = p.split_k == 1 && (long)cdiv(p.M, 256) * cdiv(p.N, BN) * batch >= 512 && (g_gemm_mode & 1);
+    if (wide) {
+      dim3 grid(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k);
+      if (grid.y > 65535 || grid.z > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
+      hipLaunchKernelGGL((gemm_bf16_kernel<256, AK, BKM, OA, OB>), grid, dim3(512), 0, s, p, oa, ob);
+    } else {
+      dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
+      if (grid.y > 65535 || grid.z > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
+      hipLaunchKernelGGL((gemm_bf16_kernel<128, AK, BKM, OA, OB>), grid, dim3(256), 0, s, p, oa, ob);
+    }
+  } else {
+    dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
+    if (grid.y > 65535 || grid.z > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, OA, OB>), grid, dim3(NT), 0, s, p, oa, ob);
+  }
+  return CFM_OK;
+}
+
+// The LDS-DMA kernel takes plain strided bf16 operands whose 16-B chunks never straddle the
+// reduction edge: K-major operands need K % 64 == 0, MN-major ones M (N) % 8 == 0, and every
+// batch must fit the 32-bit range of a buffer resource.
+bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
+  if (!va || !vb || p.cmap) return false;
+  if (p.k_per_split % BK16) return false;
+  auto fits = [](long bytes) { return bytes > 0 && bytes < (1L << 31); };
+  const long ea = d.a_kmajor ? (long)d.M * d.lda : (long)d.K * d.lda;
+  const long eb = d.b_kmajor ? (long)d.N * d.ldb : (long)d.K * d.ldb;
+  if (!fits(ea * 2) || !fits(eb * 2)) return false;
+  if (d.a_kmajor ? d.K % BK16 != 0 : d.M % 8 != 0) return false;
+  if (d.b_kmajor ? d.K % BK16 != 0 : d.N % 8 != 0) return false;
+  return true;
+}
+
+// pipelined-kernel variants (cfm_gemm_set_mode bits 4-6 force one for A/B measurements):
+//   V256: 256x128 tile, BK 64, 3-stage ring (144 KiB: one workgroup of 8 waves per CU)
+//   V256S: 256x128 tile, BK 32, 3-stage ring (72 KiB: two workgroups per CU, one's epilogue
+//          overlapping the other's main loop)
+//   V128: 128x128 tile, BK 64, 3-stage ring (96 KiB, 4 waves)
+template <bool AK, bool BKM>
+void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
+  const int sel = (g_gemm_mode >> 4) & 3;   // 0 auto, 1 V256, 2 V256S, 3 V128
+  // auto: short reductions (K <= 512: the epilogue is a large share of the tile's time) run two
+  // workgroups per CU so one's epilogue hides under the other's MFMAs; long ones keep BK 64
+  const int v = sel ? sel : (p.k_per_split <= 512 ? 2 : 1);
+  const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k), g128(cdiv(p.N, BN), cdiv(p.M, 128), batch * p.split_k);
+  if (v == 1) hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob);
+  else if (v == 2) hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob);
+  else hipLaunchKernelGGL((gemm_pipe_kernel<128, 64, 3, 1, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob);
+}
+
+int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
+  p.vec_c = vec_epilogue_ok(p);
+  p.dbg = (g_gemm_mode & 8) ? 1 : 0;
+  if (cdiv(p.M, 128) > 65535 || (long)d.batch * p.split_k > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
+  const long ea = d.a_kmajor ? (long)d.M * d.lda : (long)d.K * d.lda;
+  const long eb = d.b_kmajor ? (long)d.N * d.ldb : (long)d.K * d.ldb;
+  const PipeOp oa{(const bf16*)d.A, d.lda, d.stride_a, d.M, (unsigned)(ea * 2)};
+  const PipeOp ob{(const bf16*)d.B, d.ldb, d.stride_b, d.N, (unsigned)(eb * 2)};
+  const bool ak = d.a_kmajor != 0, bkm = d.b_kmajor != 0;
+  if (ak && bkm) launch_pipe_t<true, true>(p, oa, ob, d.batch, s);
+  else if (ak) launch_pipe_t<true, false>(p, oa, ob, d.batch, s);
+  else if (bkm) launch_pipe_t<false, true>(p, oa, ob, d.batch, s);
+  else launch_pipe_t<false, false>(p, oa, ob, d.batch, s);
   return CFM_OK;
 }
 
 }  // namespace
+
+CFM_EXPORT int cfm_gemm_set_mode(int mode) {
+  g_gemm_mode = mode;
+  return CFM_OK;
+}
 
 CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   CFM_REQUIRE(d != nullptr, CFM_ERR_ARG, "null descriptor");
@@ -603,7 +875,9 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
     CFM_REQUIRE(d->N % 4 == 0 && d->ldc % 4 == 0, CFM_ERR_SHAPE, "slab split-K needs N % 4 == 0");
     p.slab = d->workspace;
   }
-  if (bf) go(bf16{}); else go(float{});
+  if (bf && (g_gemm_mode & 2) && pipe_ok(*d, p, va, vb)) rc = launch_pipe(*d, p, s);
+  else if (bf) go(bf16{});
+  else go(float{});
   if (rc != CFM_OK) return rc;
   if (p.slab) {
     const long n4 = (long)d->batch * d->M * d->N / 4;

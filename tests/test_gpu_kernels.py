@@ -39,6 +39,56 @@ def test_gemm_layouts(dtype, ak, bk, M, N, K):
     assert _rel(C, ref) < tol
 
 
+@pytest.fixture
+def gemm_mode():
+    from nn_conformer_for_speech_recognition_amd import _lib
+    yield lambda m: _lib.call("cfm_gemm_set_mode", m)
+    _lib.call("cfm_gemm_set_mode", 3)
+
+
+@pytest.mark.parametrize("mode", [1, 18, 34, 50])   # register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(1000, 512, 512), (264, 136, 192), (520, 264, 1000), (8, 8, 64)])
+def test_gemm_kernel_variants(gemm_mode, mode, ak, bk, M, N, K):
+    """Every bf16 kernel variant (incl. the LDS-DMA pipeline's clamped M/N edges and zero-filled
+    MN-major K tail) against an fp32 reference, bias + SiLU epilogue included."""
+    gemm_mode(mode)
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K + mode)
+    A = torch.randn(M, K, generator=g).bfloat16().float()
+    B = torch.randn(N, K, generator=g).bfloat16().float()
+    bias = torch.randn(N, generator=g)
+    z = A @ B.T + bias
+    Ad = (A if ak else A.T.contiguous()).to(DEV, torch.bfloat16)
+    Bd = (B if bk else B.T.contiguous()).to(DEV, torch.bfloat16)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(Ad, Bd, C, M, N, K, a_kmajor=ak, b_kmajor=bk, bias=bias.to(DEV), act=ops.ACT_SILU, pre=pre)
+    torch.cuda.synchronize()
+    assert _rel(pre, z) < 1e-5
+    assert _rel(C.float(), torch.nn.functional.silu(z)) < 1e-2
+
+
+@pytest.mark.parametrize("mode", [1, 18, 34])
+def test_gemm_kernel_variants_splitk_batched(gemm_mode, mode):
+    gemm_mode(mode)
+    g = torch.Generator().manual_seed(17)
+    M, N, K = 256, 192, 5000
+    dy = torch.randn(K, M, generator=g).bfloat16().float()     # tokens x out  (MN-major operands)
+    x = torch.randn(K, N, generator=g).bfloat16().float()
+    for split in (1, 4, 8):
+        dw = ops.linear_wgrad(dy.to(DEV, torch.bfloat16), x.to(DEV, torch.bfloat16), split_k=split)
+        assert _rel(dw, dy.T @ x) < 1e-5
+    # batched K-major x K-major with a batch stride (the attention-free batched form)
+    Z, M2, N2, K2 = 3, 300, 136, 128
+    A = torch.randn(Z, M2, K2, generator=g).bfloat16().float()
+    B = torch.randn(Z, N2, K2, generator=g).bfloat16().float()
+    C = torch.empty(Z, M2, N2, device=DEV)
+    ops.gemm(A.to(DEV, torch.bfloat16), B.to(DEV, torch.bfloat16), C, M2, N2, K2, batch=Z,
+             stride_a=M2 * K2, stride_b=N2 * K2, stride_c=M2 * N2)
+    torch.cuda.synchronize()
+    assert _rel(C, A @ B.transpose(1, 2)) < 1e-5
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_epilogues(dtype):
     g = torch.Generator().manual_seed(5)
