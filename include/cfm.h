@@ -43,6 +43,18 @@ const char* cfm_get_last_error(void);
 /* y[i] = (dy)x[i] for n elements (dtype conversion; fp32 master weights -> bf16 compute copies). */
 int cfm_cast(const void* x, int dtype_x, void* y, int dtype_y, long n, void* stream);
 
+/* Many casts in one launch (the per-step bf16 shadow of every weight matrix): `tasks` is a
+   DEVICE array of ntasks cfm_cast_task; task t owns blocks [blk0, blk0 + ceil(n / 2048)) of a grid of
+   `nblocks` blocks (blk0 ascending, tasks back to back).  Replaces one cfm_cast launch per weight. */
+typedef struct {
+  const void* src;
+  void* dst;
+  long n;
+  long blk0;
+} cfm_cast_task;
+int cfm_cast_batch(const cfm_cast_task* tasks, int ntasks, long nblocks, int dtype_x, int dtype_y,
+                   void* stream);
+
 /* ---------------------------------------------------------------- SpecAugment
  * Replaces ASRNN.SpecAugment / time_warping / frequency_masking / time_masking
  * (lib/standard/asrnn.py:91-192).  The random draws stay on the host (python `random`, the

@@ -96,7 +96,11 @@ _REL_PNAMES = ["self_attn.linear_pos.weight", "self_attn.pos_bias_u", "self_attn
 
 class _Cfg:
     __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
-                 "bn_rm", "bn_rv", "bn_mom", "pe")
+                 "bn_rm", "bn_rv", "bn_mom", "pe", "shadow")
+
+
+# the 2-D (and pointwise-conv) weight matrices of _PNAMES: cast to the compute dtype once per step
+_WIDX = (2, 4, 8, 10, 14, 20, 24, 26)
 
 
 def _w(t, cd):
@@ -204,8 +208,11 @@ class _ConformerLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, lens, cfg, *params):
-        P = params[:len(_PNAMES)]
+        P = list(params[:len(_PNAMES)])
         R = params[len(_PNAMES):]
+        if cfg.shadow is not None:       # compute-dtype copies refreshed by Conformer (one launch)
+            for i, t in cfg.shadow.items():
+                P[i] = t
         s = cfg.seed
         x0 = x
         x1, sv1 = _ffn_fwd(x0, P, 0, cfg, s)
@@ -279,9 +286,11 @@ class ConformerLayer(nn.Module):
             ps += [sd[n] for n in _REL_PNAMES]
         return ps
 
-    def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None):
-        """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device."""
+    def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None, shadow=None):
+        """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device; shadow: optional
+        {param index: compute-dtype copy} of this layer's weight matrices (see Conformer)."""
         cfg = _Cfg()
+        cfg.shadow = shadow
         cfg.B, cfg.T, cfg.d, cfg.H, cfg.ffn, cfg.K = B, T, self.d, self.H, self.ffn, self.K
         cfg.p = float(self.dropout) if self.training else 0.0
         cfg.cd = compute_dtype
@@ -322,6 +331,7 @@ class Conformer(nn.Module):
         self.compute_dtype = compute_dtype
         self._pe_cache = {}
         self._step = 0
+        self._shadow = None
 
     def _pe(self, T, device):
         key = (T, str(device))
@@ -329,13 +339,29 @@ class Conformer(nn.Module):
             self._pe_cache[key] = rel_pos_table(T, self.input_dim, device)
         return self._pe_cache[key]
 
+    def _shadows(self, device):
+        """Compute-dtype copies of every layer's weight matrices, refreshed by ONE cfm_cast_batch
+        launch per forward (instead of one cast per matrix per layer)."""
+        if self.compute_dtype == torch.float32:
+            return [None] * len(self.conformer_layers)
+        srcs = [layer.params()[i] for layer in self.conformer_layers for i in _WIDX]
+        key = (str(device), tuple(t.data_ptr() for t in srcs))
+        if self._shadow is None or self._shadow[0] != key:
+            dsts = [torch.empty(t.shape, device=device, dtype=self.compute_dtype) for t in srcs]
+            per = [dict(zip(_WIDX, dsts[j * len(_WIDX):(j + 1) * len(_WIDX)]))
+                   for j in range(len(self.conformer_layers))]
+            self._shadow = (key, ops.CastBatch(srcs, dsts), per)
+        self._shadow[1].refresh()
+        return self._shadow[2]
+
     def forward_tokens(self, x, lens_i32, B, T, seed=None):
         if seed is None:
             seed = (self._step * 1000003 + 12345) & 0x7FFFFFFF
             self._step += 1
         pe = self._pe(T, x.device) if self.pos_enc == "rel" else None
+        shadows = self._shadows(x.device)
         for i, layer in enumerate(self.conformer_layers):
-            x = layer.forward_tokens(x, lens_i32, B, T, self.compute_dtype, seed + 100 * i, pe)
+            x = layer.forward_tokens(x, lens_i32, B, T, self.compute_dtype, seed + 100 * i, pe, shadows[i])
         return x
 
     def forward(self, input, lengths):

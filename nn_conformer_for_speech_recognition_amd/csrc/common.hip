@@ -1,6 +1,8 @@
 // common.hip — error plumbing, version, dtype casts and small elementwise kernels.
 #include "cfm_common.h"
 
+#include <type_traits>
+
 namespace cfm {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
@@ -80,6 +82,44 @@ CFM_EXPORT int cfm_cast(const void* x, int dtx, void* y, int dty, long n, void* 
   else
     return cfm::fail(CFM_ERR_DTYPE, "cfm_cast: dtype");
   return cfm::check_launch("cfm_cast");
+}
+
+namespace {
+constexpr int CAST_BLK = 2048;   // elements per block (256 threads x 8)
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void cast_batch_kernel(const cfm_cast_task* __restrict__ tasks, int ntasks) {
+  // the task owning this block: last t with blk0 <= blockIdx.x (binary search, wave-uniform)
+  int lo = 0, hi = ntasks - 1;
+  const long b = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tasks[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const cfm_cast_task t = tasks[lo];
+  const long e0 = (b - t.blk0) * CAST_BLK + threadIdx.x * 8;
+  const TI* x = reinterpret_cast<const TI*>(t.src);
+  TO* y = reinterpret_cast<TO*>(t.dst);
+  if (e0 + 8 <= t.n && ((uintptr_t)(x + e0) % 16 == 0) && ((uintptr_t)(y + e0) % 16 == 0)) {
+    float v[8];
+    ld8_dyn(x, std::is_same<TI, bf16>::value ? CFM_BF16 : CFM_F32, e0, v);
+    st8_dyn(y, std::is_same<TO, bf16>::value ? CFM_BF16 : CFM_F32, e0, v);
+  } else {
+    for (long e = e0; e < e0 + 8 && e < t.n; ++e) y[e] = from_f32<TO>(to_f32(x[e]));
+  }
+}
+}  // namespace
+
+CFM_EXPORT int cfm_cast_batch(const cfm_cast_task* tasks, int ntasks, long nblocks, int dtx, int dty,
+                              void* stream) {
+  CFM_REQUIRE(tasks && ntasks > 0 && nblocks > 0 && nblocks < (1L << 31), CFM_ERR_ARG, "bad task table");
+  hipStream_t s = cfm::as_stream(stream);
+  if (dtx == CFM_F32 && dty == CFM_BF16)
+    hipLaunchKernelGGL((cast_batch_kernel<float, bf16>), dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks);
+  else if (dtx == CFM_BF16 && dty == CFM_F32)
+    hipLaunchKernelGGL((cast_batch_kernel<bf16, float>), dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks);
+  else
+    return cfm::fail(CFM_ERR_DTYPE, "cfm_cast_batch: f32 <-> bf16 only");
+  return cfm::check_launch("cfm_cast_batch");
 }
 
 CFM_EXPORT int cfm_scale_dropout(const void* x, int dtx, void* y, int dty, long n, float scale,

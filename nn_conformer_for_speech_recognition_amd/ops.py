@@ -108,6 +108,38 @@ def cast(x, dtype):
     return y
 
 
+_CAST_BLK = 2048
+
+
+class CastBatch:
+    """One launch that casts a fixed list of tensors into fixed destination tensors (cfm_cast_batch).
+    The device task table is built once; call refresh() to re-run the casts (e.g. the bf16 shadow
+    of every weight matrix, once per step)."""
+
+    def __init__(self, srcs, dsts):
+        import numpy as np
+        if not srcs or len(srcs) != len(dsts):
+            raise L.CfmError("CastBatch: need matching non-empty source / destination lists")
+        dtx, dty = {L.dt(t) for t in srcs}, {L.dt(t) for t in dsts}
+        if len(dtx) != 1 or len(dty) != 1:
+            raise L.CfmError("CastBatch: one source dtype and one destination dtype per batch")
+        self.dtx, self.dty = dtx.pop(), dty.pop()
+        rec = np.zeros((len(srcs), 4), dtype=np.int64)
+        blk = 0
+        for i, (s, d) in enumerate(zip(srcs, dsts)):
+            if s.numel() != d.numel() or not s.is_contiguous() or not d.is_contiguous():
+                raise L.CfmError("CastBatch: contiguous tensors of equal size required")
+            rec[i] = (L.ptr(s), L.ptr(d), s.numel(), blk)
+            blk += (s.numel() + _CAST_BLK - 1) // _CAST_BLK
+        self.nblocks = blk
+        self.table = torch.from_numpy(rec.view(np.uint8).reshape(-1).copy()).to(srcs[0].device)
+        self.n = len(srcs)
+        self._keep = (list(srcs), list(dsts))
+
+    def refresh(self):
+        L.call("cfm_cast_batch", L.ptr(self.table), self.n, self.nblocks, self.dtx, self.dty, L.stream())
+
+
 def cast_into(x, y):
     L.call("cfm_cast", L.ptr(x), L.dt(x), L.ptr(y), L.dt(y), x.numel(), L.stream())
     return y
