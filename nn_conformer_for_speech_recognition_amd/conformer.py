@@ -103,6 +103,45 @@ class _Cfg:
 _WIDX = (2, 4, 8, 10, 14, 20, 24, 26)
 
 
+_SIDE_STREAMS = {}
+
+
+class _Side:
+    """Weight-gradient work of one layer's backward (wgrad GEMMs + bias column sums) on a second
+    HIP stream, so it overlaps the data-gradient chain on the main stream.  Inputs are fenced with
+    an event and record_stream()'d on the side stream; join() makes the main stream wait for every
+    side launch before the layer's gradients are handed back to autograd."""
+
+    def __init__(self, device):
+        self.main = torch.cuda.current_stream(device)
+        key = str(device)
+        if key not in _SIDE_STREAMS:
+            _SIDE_STREAMS[key] = torch.cuda.Stream(device)
+        self.side = _SIDE_STREAMS[key]
+        self.out = []
+
+    def run(self, fn, *inputs):
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            r = fn()
+        for t in inputs:
+            t.record_stream(self.side)
+        self.out.append(r)
+        return r
+
+    def join(self):
+        self.main.wait_stream(self.side)
+        for r in self.out:
+            for t in (r if isinstance(r, tuple) else (r,)):
+                t.record_stream(self.main)
+        self.out = []
+
+
+def _wgrad_bias(side, dy, x):
+    """(dW, db) = (dyᵀ·x, Σ_rows dy) on the side stream."""
+    return side.run(lambda: (ops.linear_wgrad(dy, x), ops.colsum(dy)), dy, x)
+
+
 def _w(t, cd):
     """Compute-dtype view of a weight (2-D)."""
     return t if t.dtype == cd else ops.cast(t, cd)
@@ -118,15 +157,13 @@ def _ffn_fwd(x, P, o, cfg, seed):
     return y, (xn, mu, rs, pre, h, w1, w2)
 
 
-def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads):
+def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads, side):
     xn, mu, rs, pre, h, w1, w2 = sv
     cd = cfg.cd
     g2 = ops.scale_dropout(g, 0.5, cfg.p, seed + 1, 0, out_dtype=cd)
-    grads[o + 4] = ops.linear_wgrad(g2, h)
-    grads[o + 5] = ops.colsum(g2)
+    grads[o + 4], grads[o + 5] = _wgrad_bias(side, g2, h)
     da = ops.linear_dgrad(g2, w2, pre=pre, act_grad=True, drop_p=cfg.p, seed=seed)
-    grads[o + 2] = ops.linear_wgrad(da, xn)
-    grads[o + 3] = ops.colsum(da)
+    grads[o + 2], grads[o + 3] = _wgrad_bias(side, da, xn)
     dxn = ops.linear_dgrad(da, w1)
     dx, grads[o], grads[o + 1] = ops.layernorm_bwd(dxn, x, P[o], mu, rs, dres=g)
     return dx
@@ -149,21 +186,19 @@ def _mha_fwd(x, P, R, cfg, seed, lens):
     return y, (xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv)
 
 
-def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads):
+def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side):
     xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv = sv
     cd = cfg.cd
     B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
     g4 = ops.scale_dropout(g, 1.0, cfg.p, seed + 1, 0, out_dtype=cd)
-    grads[10] = ops.linear_wgrad(g4, o)
-    grads[11] = ops.colsum(g4)
+    grads[10], grads[11] = _wgrad_bias(side, g4, o)
     do = ops.linear_dgrad(g4, wout)
     dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
     if cfg.rel:
         rgrads[0] = ops.linear_wgrad(_w(dpos, cd), _w(cfg.pe, cd))
         rgrads[1] = dpu.view(H, d // H)
         rgrads[2] = dpv.view(H, d // H)
-    grads[8] = ops.linear_wgrad(dqkv, xn)
-    grads[9] = ops.colsum(dqkv)
+    grads[8], grads[9] = _wgrad_bias(side, dqkv, xn)
     dxn = ops.linear_dgrad(dqkv, win)
     dx, grads[6], grads[7] = ops.layernorm_bwd(dxn, x, P[6], mu, rs, dres=g)
     return dx
@@ -184,20 +219,20 @@ def _conv_fwd(x, P, cfg, seed):
     return y, (xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw)
 
 
-def _conv_bwd(g, x, sv, P, cfg, seed, grads):
+def _conv_bwd(g, x, sv, P, cfg, seed, grads, side):
     xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw = sv
     cd = cfg.cd
     B, T, d, K = cfg.B, cfg.T, cfg.d, cfg.K
     g3 = ops.scale_dropout(g, 1.0, cfg.p, seed, 0, out_dtype=cd)
-    grads[20] = ops.linear_wgrad(g3, z).view(d, d, 1)
-    grads[21] = ops.colsum(g3)
+    dw, grads[21] = _wgrad_bias(side, g3, z)
+    grads[20] = dw.view(d, d, 1)
     dz = ops.linear_dgrad(g3, wp2)
     ws = ops.convmod_ws(B, T, d, K, x.device)
     dy, grads[18], grads[19] = ops.bn_silu_bwd(dz, yv, P[18], P[19], bmean, binv, cfg.training, ws)
     da, dwdw, grads[17] = ops.glu_dwconv_bwd(dy, a, wdw, B, T, d, K, ws, cd)
     grads[16] = dwdw.view(d, 1, K)
-    grads[14] = ops.linear_wgrad(da, xn).view(2 * d, d, 1)
-    grads[15] = ops.colsum(da)
+    dw, grads[15] = _wgrad_bias(side, da, xn)
+    grads[14] = dw.view(2 * d, d, 1)
     dxn = ops.linear_dgrad(da, wp1)
     dx, grads[12], grads[13] = ops.layernorm_bwd(dxn, x, P[12], mu, rs, dres=g)
     return dx
@@ -246,15 +281,17 @@ class _ConformerLayerFn(torch.autograd.Function):
         rgrads = [None] * len(R)
         s = cfg.seed
         gout = gout.contiguous()
+        side = _Side(gout.device)
         g, grads[28], grads[29] = ops.layernorm_bwd(gout, x4, P[28], mu5, rs5)
-        g = _ffn_bwd(g, x3, sv4, P, 22, cfg, s + 30, grads)
+        g = _ffn_bwd(g, x3, sv4, P, 22, cfg, s + 30, grads, side)
         if cfg.conv_first:
-            g = _mha_bwd(g, c1, sva, P, R, cfg, s + 20, lens, grads, rgrads)
-            g = _conv_bwd(g, c0, svc, P, cfg, s + 10, grads)
+            g = _mha_bwd(g, c1, sva, P, R, cfg, s + 20, lens, grads, rgrads, side)
+            g = _conv_bwd(g, c0, svc, P, cfg, s + 10, grads, side)
         else:
-            g = _conv_bwd(g, c1, svc, P, cfg, s + 10, grads)
-            g = _mha_bwd(g, c0, sva, P, R, cfg, s + 20, lens, grads, rgrads)
-        g = _ffn_bwd(g, x0, sv1, P, 0, cfg, s, grads)
+            g = _conv_bwd(g, c1, svc, P, cfg, s + 10, grads, side)
+            g = _mha_bwd(g, c0, sva, P, R, cfg, s + 20, lens, grads, rgrads, side)
+        g = _ffn_bwd(g, x0, sv1, P, 0, cfg, s, grads, side)
+        side.join()
         ctx.sv = None
         return (g, None, None, *grads, *rgrads)
 
