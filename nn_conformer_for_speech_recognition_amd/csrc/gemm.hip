@@ -170,6 +170,23 @@ __device__ __forceinline__ void xcd_tile(int& tm, int& tn) {
   tn = id % gx;
 }
 
+// The same over the whole 3-D grid (z = batch x split-K slice, slowest): each XCD gets a contiguous
+// run of (slice, tile) pairs, i.e. whole K slices -- the 4-8 tiles that re-read one slice's
+// operand panels then do so from that XCD's L2 instead of every XCD fetching every panel.
+__device__ __forceinline__ void xcd_tile3(int& tm, int& tn, int& zz) {
+  const int gx = gridDim.x, gxy = gx * gridDim.y, nwg = gxy * gridDim.z;
+  const int L = (blockIdx.z * gridDim.y + blockIdx.y) * gx + blockIdx.x;
+  int id = L;
+  if (nwg > 8) {
+    const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+  }
+  zz = id / gxy;
+  const int t = id % gxy;
+  tm = t / gx;
+  tn = t % gx;
+}
+
 // fp32 LDS geometry: both operands stored [BK][128+4] (k-rows)
 constexpr int BK32 = 16;
 constexpr int F_STRIDE = 128 + 4;
@@ -193,16 +210,17 @@ __device__ __forceinline__ bf16x8 frag16(const bf16* tile, int row0, int kk, int
   }
 }
 
-__device__ __forceinline__ void epilogue_store(const GemmP& p, int z, int m, int n, float acc) {
+// zs: the launch's batch x split-K slice index (selects the split-K slab)
+__device__ __forceinline__ void epilogue_store(const GemmP& p, int z, int zs, int m, int n, float acc) {
   if (m >= p.M || n >= p.N) return;
   const long cidx = (long)z * p.sc + out_row(p, m) * p.ldc + n;
   float v = acc * p.alpha;
   if (p.split_k > 1) {
     if (p.slab) {
-      p.slab[(long)blockIdx.z * p.M * p.N + (long)m * p.N + n] = v;
+      p.slab[(long)zs * p.M * p.N + (long)m * p.N + n] = v;
       return;
     }
-    if (p.bias && blockIdx.z % p.split_k == 0) v += p.bias[n];
+    if (p.bias && zs % p.split_k == 0) v += p.bias[n];
     atomicAdd(reinterpret_cast<float*>(p.C) + cidx, v);
     return;
   }
@@ -222,10 +240,10 @@ constexpr int EP_STRIDE = 128 + 4;   // f32 staging row stride: rows r and r+4 l
 static_assert(128 * EP_STRIDE * 4 <= 4 * TILE16 * 2, "epilogue staging fits in the K-loop LDS");
 
 // the epilogue of cfm_gemm_desc on 8 consecutive columns (vectorised when legal)
-__device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int m, int n, float (&v)[8]) {
+__device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int zs, int m, int n, float (&v)[8]) {
   if (m >= p.M || n >= p.N) return;
   if (p.split_k > 1 && p.slab && n + 8 <= p.N && (p.N & 3) == 0) {
-    float* dst = p.slab + (long)blockIdx.z * p.M * p.N + (long)m * p.N + n;
+    float* dst = p.slab + (long)zs * p.M * p.N + (long)m * p.N + n;
     *reinterpret_cast<float4*>(dst) = make_float4(v[0] * p.alpha, v[1] * p.alpha, v[2] * p.alpha, v[3] * p.alpha);
     *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4] * p.alpha, v[5] * p.alpha, v[6] * p.alpha, v[7] * p.alpha);
     return;
@@ -233,7 +251,7 @@ __device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int m, in
   if (!p.vec_c || n + 8 > p.N || p.split_k > 1) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      if (n + e < p.N) epilogue_store(p, z, m, n + e, v[e]);
+      if (n + e < p.N) epilogue_store(p, z, zs, m, n + e, v[e]);
     return;
   }
   const long cidx = (long)z * p.sc + out_row(p, m) * p.ldc + n;
@@ -289,8 +307,8 @@ struct Geo16 {
 };
 
 template <int BMt>
-__device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2], float* st, int z, int m0, int n0,
-                                              int wm, int wn, int lane, int tid);
+__device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2], float* st, int z, int zs, int m0,
+                                              int n0, int wm, int wn, int lane, int tid);
 
 template <int BMt, bool AK, bool BKM, class OA, class OB>
 __global__ __launch_bounds__(BMt * 2) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
@@ -376,14 +394,14 @@ __global__ __launch_bounds__(BMt * 2) void gemm_bf16_kernel(GemmP p, OA oa, OB o
     __syncthreads();
   }
 
-  tile_epilogue<BMt>(p, acc, reinterpret_cast<float*>(lds), z, m0, n0, wm, wn, lane, tid);
+  tile_epilogue<BMt>(p, acc, reinterpret_cast<float*>(lds), z, blockIdx.z, m0, n0, wm, wn, lane, tid);
 }
 
 // Epilogue of one BMt x 128 tile (4-wave rows x 2-wave columns of 64x64 accumulators).  The
 // caller guarantees every wave is done reading the staging LDS (`st`, >= 128 x EP_STRIDE floats).
 template <int BMt>
-__device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2], float* st, int z, int m0, int n0,
-                                              int wm, int wn, int lane, int tid) {
+__device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2], float* st, int z, int zs, int m0,
+                                              int n0, int wm, int wn, int lane, int tid) {
   constexpr int NTt = BMt * 2;
   if (p.split_k > 1 && !p.slab) {
     // split-K partials: atomics straight from the accumulators (32 consecutive columns per
@@ -396,7 +414,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           const int n = n0 + wn * 64 + j * 32 + (lane & 31);
-          epilogue_store(p, z, m, n, acc[i][j][r]);
+          epilogue_store(p, z, zs, m, n, acc[i][j][r]);
         }
     return;
   }
@@ -423,7 +441,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2
       const float4 lo = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8);
       const float4 hi = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8 + 4);
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      epilogue_store8(p, z, m0 + 128 * hf + row, n0 + c8, v);
+      epilogue_store8(p, z, zs, m0 + 128 * hf + row, n0 + c8, v);
     }
     if (hf + 1 < BMt / 128) __syncthreads();
   }
@@ -534,10 +552,10 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
   __shared__ __attribute__((aligned(1024))) char lds[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  int tm, tn;
-  xcd_tile(tm, tn);
+  int tm, tn, zz;
+  xcd_tile3(tm, tn, zz);
   const int m0 = tm * BMt, n0 = tn * BN;
-  const int z = blockIdx.z / p.split_k, ks = blockIdx.z % p.split_k;
+  const int z = zz / p.split_k, ks = zz % p.split_k;
   const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, z), rb = pipe_rsrc(ob, z);
   const int kbeg = ks * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
@@ -607,7 +625,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
     return;
   }
   __syncthreads();   // every wave done with the ring (no DMA outstanding) -> reuse it for the epilogue
-  tile_epilogue<BMt>(p, acc, reinterpret_cast<float*>(lds), z, m0, n0, wm, wn, lane, tid);
+  tile_epilogue<BMt>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane, tid);
 }
 
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
@@ -701,7 +719,7 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p, OA oa, OB ob) {
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int n = n0 + wn * 64 + j * 32 + (lane & 31);
-        epilogue_store(p, z, m, n, acc[i][j][r]);
+        epilogue_store(p, z, blockIdx.z, m, n, acc[i][j][r]);
       }
 }
 
