@@ -27,6 +27,7 @@ def timeit(fn, n=30, warm=5):
 ap = argparse.ArgumentParser()
 ap.add_argument("--modes", default="1,2")
 ap.add_argument("--epi", default="plain")
+ap.add_argument("--torch", action="store_true", help="also time torch (hipBLASLt) as a ceiling reference")
 a = ap.parse_args()
 modes = [int(m) for m in a.modes.split(",")]
 M = 32 * 373
@@ -48,8 +49,13 @@ for name, N, K in shapes:
         "dgrad": lambda: ops.linear_dgrad(dy, w, out=dx),
         "wgrad": lambda: ops.linear_wgrad(dy, x),
     }
+    ref = {"fwd": lambda: torch.nn.functional.linear(x, w, b.to(bf)), "dgrad": lambda: dy @ w,
+           "wgrad": lambda: dy.t() @ x}
     for cname, fn in cases.items():
         row = []
+        if a.torch:
+            t = timeit(ref[cname])
+            row.append(f"hipBLASLt: {t*1e3:6.1f} ({fl/t/1e9:4.0f})")
         for m in modes:
             _lib.call("cfm_gemm_set_mode", m)
             t = timeit(fn)

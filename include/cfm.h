@@ -40,6 +40,15 @@ extern "C" {
 int cfm_version(void);
 const char* cfm_get_last_error(void);
 
+/* Graph-safe dropout streams.  Binds a DEVICE uint64 step counter for this process (nullptr
+   unbinds).  While bound, every dropout-capable kernel (GEMM epilogue, scale_dropout, attention)
+   reads the counter when it RUNS and uses seed + counter * 0x9E3779B97F4A7C15 instead of the
+   seed passed at launch, so a training step captured once into a HIP graph draws fresh masks on
+   every replay after the caller increments the counter on the stream.  Backward kernels see the
+   same counter value as their forward within a step, so masks regenerate bit-identically.
+   Replaces the per-call torch RNG state of nn.Dropout (asrnn.py:31, torchaudio Conformer). */
+int cfm_rng_bind(const uint64_t* counter);
+
 /* y[i] = (dy)x[i] for n elements (dtype conversion; fp32 master weights -> bf16 compute copies). */
 int cfm_cast(const void* x, int dtype_x, void* y, int dtype_y, long n, void* stream);
 
@@ -217,6 +226,41 @@ long cfm_adafactor_rowmean_tasks(int nb, int R);
 int cfm_adafactor_step(const void* dev_table, int n, long nrow_tasks, long ncols, long nblocks,
                        long nrowmean_tasks, float* rowmean, float* sumsq, float lr, float beta1,
                        float beta2t, float eps1, float clip, void* stream);
+
+/* ---------------------------------------------------------------- CTC head (runner.py:35,142-143)
+ * Replaces torch.nn.CTCLoss(blank=hp.blank_idx, zero_infinity=True) on
+ * log_softmax(final_fc(...)) (asrnn.py:45,256): log-softmax, alpha/beta recursions and the
+ * gradient w.r.t. the logits, without host synchronisation (graph-capturable).
+ * logits fp32, row (b, t) at logits + b*sb + t*st, classes contiguous (sb/st cover both the
+ * reference's time-major (T, B, V) and batch-major layouts).  Feeding log-probabilities instead
+ * of logits gives torch's result too (log_softmax is idempotent; the gradient is then exactly
+ * torch's grad w.r.t. log_probs).  targets int32: utterance b at targets + tgt_off[b] (tgt_off
+ * != NULL: torch's concatenated 1-D form) or targets + b*ldt (padded (B, ldt)); Smax >= every
+ * target length.  in_len / tgt_len int32 on the device.
+ * fwd: nll[b] = -log p(target_b | x_b), 0 where infinite and zero_infinity (torch semantics);
+ *      ws: cfm_ctc_ws_bytes(B, T, Smax) bytes, read again by the backward.
+ * bwd: grad[b, t, v] = (softmax - posterior) * grad_out[b * grad_out_stride] * r_b with
+ *      r_b = 1 / (B * max(L_b, 1)) for reduction 1 (mean), 1 for 0 (none) / 2 (sum); zero for
+ *      t >= in_len[b] and for zeroed infinite losses.  Output layout gsb/gst, dtype_grad f32|bf16. */
+size_t cfm_ctc_ws_bytes(int B, int T, int Smax);
+int cfm_ctc_loss_fwd(const float* logits, long sb, long st, const int32_t* targets, int ldt,
+                     const int32_t* tgt_off, const int32_t* in_len, const int32_t* tgt_len, int B,
+                     int T, int V, int Smax, int blank, int zero_infinity, float* nll, float* ws,
+                     void* stream);
+int cfm_ctc_loss_bwd(const float* logits, long sb, long st, const int32_t* targets, int ldt,
+                     const int32_t* tgt_off, const int32_t* in_len, const int32_t* tgt_len, int B,
+                     int T, int V, int Smax, int blank, int zero_infinity, const float* ws,
+                     const float* grad_out, int grad_out_stride, int reduction, void* grad_logits,
+                     int dtype_grad, long gsb, long gst, void* stream);
+
+/* Greedy decode: ASRNN.predict (asrnn.py:48-58, torch.argmax over classes: first maximum,
+ * NaN wins) -> ids (B, T) int64; optionally (out, out_len != NULL) the Vocab.decode id filter
+ * (myvocab.py:211-231): frames t < lens[b] (lens NULL: all T), ids equal to `blank` or `pad`
+ * dropped (pad < 0: none), repeats collapsed first if `collapse` (the reference does not);
+ * out (B, T) int32 padded with -1, out_len (B) int32. */
+int cfm_ctc_greedy_decode(const float* logits, long sb, long st, const int32_t* lens, int B, int T,
+                          int V, int blank, int pad, int collapse, int64_t* ids, int32_t* out,
+                          int32_t* out_len, void* stream);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,7 @@ class GemmDesc(ctypes.Structure):
 _SIGS = {
     "cfm_version": (c_int, []),
     "cfm_get_last_error": (ctypes.c_char_p, []),
+    "cfm_rng_bind": (c_int, [c_void_p]),
     "cfm_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_void_p]),
     "cfm_cast_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
     "cfm_specaug_apply": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p]),
@@ -95,6 +96,14 @@ _SIGS = {
                                    c_void_p]),
     "cfm_conv2_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_void_p]),
+    "cfm_ctc_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "cfm_ctc_loss_fwd": (c_int, [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                 c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "cfm_ctc_loss_bwd": (c_int, [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                 c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_long,
+                                 c_long, c_void_p]),
+    "cfm_ctc_greedy_decode": (c_int, [c_void_p, c_long, c_long, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_void_p, c_void_p, c_void_p, c_void_p]),
     "cfm_conv1_bwd_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "cfm_conv1_bwd_weight": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                      c_void_p, c_void_p]),

@@ -42,6 +42,7 @@ struct AttnM {
   float scale;
   float drop_p; uint64_t seed;
   bool vec;    // 16-B vector loads legal
+  const uint64_t* salt;   // bound dropout step counter or nullptr
 };
 
 __device__ __forceinline__ uint64_t didx(const AttnM& p, int b, int h, int i, int j) {
@@ -135,6 +136,7 @@ __device__ void store_transposed(float* stage, const f32x16& a0, const f32x16& a
 
 // ------------------------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnM p, bf16* __restrict__ o, float* __restrict__ lse) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];   // [buf][K,V][64][72]  36 KiB
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -259,6 +261,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dot_kernel(const bf16* __restric
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(AttnM p, const bf16* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ Dg,
                                                           bf16* __restrict__ dqkv) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -338,6 +341,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnM p, const bf16* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ Dg, bf16* __restrict__ dqkv) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];   // [buf][Q, dO][64][72]
   __shared__ float sLD[2][2][TILE];                                        // [buf][lse2, D][64]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
@@ -458,7 +462,7 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
-          ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0)};
+          ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), cfm::g_rng_salt};
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (bf16*)o, lse);
   return cfm::check_launch("cfm_attn_fwd");
 }
@@ -480,7 +484,8 @@ CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, co
     return cfm::attn_simt_bwd_launch(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B,
                                      T, H, dk, dtype, drop_p, seed, ws, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
-          ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0)};
+          ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0),
+          cfm::g_rng_salt};
   const long nrow = (long)B * H * T;
   (void)nrow;
   CFM_REQUIRE(H * dk <= 1024, CFM_ERR_UNSUPPORTED, "H*dk must be <= 1024");

@@ -22,6 +22,7 @@ struct AttnP {
   const float* pu; const float* pv;
   float scale;
   float drop_p; uint64_t seed;
+  const uint64_t* salt;      // bound dropout step counter or nullptr
 };
 
 __device__ __forceinline__ float qkv_at(const AttnP& p, int b, int t, int which, int h, int d) {
@@ -48,6 +49,7 @@ __device__ __forceinline__ float score(const AttnP& p, int b, int h, int i, int 
 
 // grid (ceil(T/4), H, B), 256 threads: one wave per query
 __global__ __launch_bounds__(256) void attn_simt_fwd(AttnP p, void* __restrict__ o, float* __restrict__ lse) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   __shared__ float sq[4][2][64];
   __shared__ float sp[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -89,6 +91,7 @@ __global__ __launch_bounds__(256) void attn_simt_bwd_dq(AttnP p, const void* __r
                                                         const void* __restrict__ dout, const float* __restrict__ lse,
                                                         void* __restrict__ dqkv, float* __restrict__ ws_ds,
                                                         float* __restrict__ dpu, float* __restrict__ dpv) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   __shared__ float sq[4][2][64];
   __shared__ float sdo[4][64];
   __shared__ float sds[4][64];
@@ -149,6 +152,7 @@ __global__ __launch_bounds__(256) void attn_simt_bwd_dq(AttnP p, const void* __r
 __global__ __launch_bounds__(256) void attn_simt_bwd_dkdv(AttnP p, const void* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           void* __restrict__ dqkv, const float* __restrict__ ws_ds) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   __shared__ float sk[4][64];
   __shared__ float sw[4][2][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -198,6 +202,7 @@ __global__ __launch_bounds__(256) void attn_simt_bwd_dkdv(AttnP p, const void* _
 // dpos[r][h][d] = sum_{b,i} dS[b,h,i,j=r-(T-1)+i] * (q_i+v)[d].  grid (ceil((2T-1)/4), H)
 __global__ __launch_bounds__(256) void attn_simt_bwd_dpos(AttnP p, const float* __restrict__ ws_ds,
                                                           float* __restrict__ dpos) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = blockIdx.x * 4 + wv, h = blockIdx.y;
   if (r >= 2 * p.T - 1 || lane >= p.dk) return;
@@ -219,7 +224,7 @@ namespace cfm {
 int attn_simt_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len, const void* pos, const float* pu,
                          const float* pv, int B, int T, int H, int dk, int dtype, float drop_p, uint64_t seed,
                          hipStream_t s) {
-  AttnP p{qkv, dtype, B, T, H, dk, 3 * H * dk, len, pos, pu, pv, 1.f / sqrtf((float)dk), drop_p, seed};
+  AttnP p{qkv, dtype, B, T, H, dk, 3 * H * dk, len, pos, pu, pv, 1.f / sqrtf((float)dk), drop_p, seed, cfm::g_rng_salt};
   hipLaunchKernelGGL(attn_simt_fwd, dim3(cdiv(T, 4), H, B), dim3(256), 0, s, p, o, lse);
   return check_launch("cfm_attn_fwd(simt)");
 }
@@ -230,7 +235,7 @@ int attn_simt_bwd_launch(const void* qkv, const void* o, const void* dout, const
                          const void* pos, const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu,
                          float* dpv, int B, int T, int H, int dk, int dtype, float drop_p, uint64_t seed,
                          float* ws, hipStream_t s) {
-  AttnP p{qkv, dtype, B, T, H, dk, 3 * H * dk, len, pos, pu, pv, 1.f / sqrtf((float)dk), drop_p, seed};
+  AttnP p{qkv, dtype, B, T, H, dk, 3 * H * dk, len, pos, pu, pv, 1.f / sqrtf((float)dk), drop_p, seed, cfm::g_rng_salt};
   if (pos) {
     (void)hipMemsetAsync(dpu, 0, sizeof(float) * H * dk, s);
     (void)hipMemsetAsync(dpv, 0, sizeof(float) * H * dk, s);

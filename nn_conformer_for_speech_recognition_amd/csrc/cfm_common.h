@@ -28,6 +28,9 @@ int check_launch(const char* what);
 // out[n] (+)= sum_p part[p*ldp + n]  (deterministic, block = 16 waves x 64 columns; ldp 0 -> N)
 void colreduce(const float* part, int nparts, long N, float* out, int accumulate, hipStream_t s, long ldp = 0);
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+// device step counter bound by cfm_rng_bind (nullptr: seeds are used as passed); read by every
+// dropout kernel at run time so one captured HIP graph replays with fresh masks each step
+extern const uint64_t* g_rng_salt;
 }  // namespace cfm
 
 #define CFM_EXPORT extern "C" __attribute__((visibility("default")))
@@ -109,6 +112,10 @@ __device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t idx) {
 // keep probability
 __device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
 __device__ __forceinline__ float drop_keep_scale(uint32_t thr) { return 65536.f / (float)(65536u - thr); }
+// the seed a kernel actually uses: the caller's seed offset by the bound device step counter
+__device__ __forceinline__ uint64_t salted_seed(uint64_t seed, const uint64_t* salt) {
+  return salt ? seed + salt[0] * 0x9E3779B97F4A7C15ull : seed;
+}
 // returns the keep scale if kept, 0 if dropped
 __device__ __forceinline__ float dropout_scale(float p, uint64_t seed, uint64_t idx) {
   if (p <= 0.f) return 1.f;

@@ -17,7 +17,16 @@ int check_launch(const char* what) {
 }
 }  // namespace cfm
 
+namespace cfm {
+const uint64_t* g_rng_salt = nullptr;
+}
+
 CFM_EXPORT int cfm_version(void) { return 1; }
+
+CFM_EXPORT int cfm_rng_bind(const uint64_t* counter) {
+  cfm::g_rng_salt = counter;
+  return CFM_OK;
+}
 CFM_EXPORT const char* cfm_get_last_error(void) { return cfm::g_last_error.c_str(); }
 
 namespace {
@@ -36,7 +45,8 @@ __global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long n
 }
 
 __global__ void scale_dropout_kernel(const void* x, int dtx, void* y, int dty, long n, float scale,
-                                     float p, uint64_t seed, uint64_t off) {
+                                     float p, uint64_t seed, uint64_t off, const uint64_t* salt) {
+  if (p > 0.f) seed = salted_seed(seed, salt);
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
   for (; i < n; i += stride) {
@@ -47,7 +57,8 @@ __global__ void scale_dropout_kernel(const void* x, int dtx, void* y, int dty, l
 }
 // 8 elements per thread (n % 8 == 0, 16-B aligned x / y)
 __global__ void scale_dropout8_kernel(const void* x, int dtx, void* y, int dty, long n8, float scale,
-                                      float p, uint64_t seed, uint64_t off) {
+                                      float p, uint64_t seed, uint64_t off, const uint64_t* salt) {
+  if (p > 0.f) seed = salted_seed(seed, salt);
   for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (long)gridDim.x * blockDim.x) {
     float v[8], s[8];
     ld8_dyn(x, dtx, q * 8, v);
@@ -128,10 +139,10 @@ CFM_EXPORT int cfm_scale_dropout(const void* x, int dtx, void* y, int dty, long 
   if (n == 0) return CFM_OK;
   if (n % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0)
     hipLaunchKernelGGL(scale_dropout8_kernel, dim3(grid_for(n / 8, 1)), dim3(256), 0, cfm::as_stream(stream), x,
-                       dtx, y, dty, n / 8, scale, p, seed, off);
+                       dtx, y, dty, n / 8, scale, p, seed, off, cfm::g_rng_salt);
   else
     hipLaunchKernelGGL(scale_dropout_kernel, dim3(grid_for(n, 1)), dim3(256), 0, cfm::as_stream(stream), x,
-                       dtx, y, dty, n, scale, p, seed, off);
+                       dtx, y, dty, n, scale, p, seed, off, cfm::g_rng_salt);
   return cfm::check_launch("cfm_scale_dropout");
 }
 

@@ -1,0 +1,362 @@
+// ctc.hip — CTC head of the training step and the greedy decoder, on the device.
+//
+//   cfm_ctc_loss_fwd / cfm_ctc_loss_bwd replace torch.nn.CTCLoss(blank, zero_infinity=True)
+//   applied to log_softmax(logits) (runner.py:35,142-143; asrnn.py:45,256): log-softmax,
+//   alpha/beta recursions and the gradient w.r.t. the LOGITS (softmax - posterior, i.e. the CTC
+//   gradient already pushed through log_softmax) with no host synchronisation, so the whole
+//   training step can be captured in one HIP graph.
+//   cfm_ctc_greedy_decode replaces ASRNN.predict (asrnn.py:48-58: argmax over the vocabulary)
+//   plus the id filtering of Vocab.decode (myvocab.py:211-231: drop <pad>/<blank>, no repeat
+//   collapse unless asked).
+//
+// Kernels (B utterances, T frames, V classes, L_b target labels, S_b = 2 L_b + 1 states):
+//   ctc_prep     one wave per frame row: lse = logsumexp(logits row); lpe[b,t,s] = logit of the
+//                s-th extended label (blank, l1, blank, l2, ...) - lse          HBM: one row read
+//   ctc_alphabeta one workgroup per (utterance, direction); states across threads, the time loop
+//                sequential with one barrier per frame; lpe rows are prefetched 16 frames ahead
+//                into registers (coalesced, latency hidden behind the recursion)
+//   ctc_grad     one workgroup per frame row: grad[v] = (exp(logit - lse) - sum_{s: l'(s)=v}
+//                exp(alpha + beta + nll - lpe)) * scale; duplicate labels are summed in label order
+//                (deterministic, no atomics)
+#include "cfm_common.h"
+
+#include <math.h>
+
+namespace {
+
+constexpr float NEG_INF = -INFINITY;
+constexpr int AB_THREADS = 256;
+constexpr int PF = 16;   // frames of lpe prefetched per chunk
+
+__device__ __forceinline__ float lse2(float a, float b) {
+  const float m = fmaxf(a, b);
+  if (m == NEG_INF) return NEG_INF;
+  return m + logf(expf(a - m) + expf(b - m));
+}
+__device__ __forceinline__ float lse3(float a, float b, float c) {
+  const float m = fmaxf(fmaxf(a, b), c);
+  if (m == NEG_INF) return NEG_INF;
+  return m + logf(expf(a - m) + expf(b - m) + expf(c - m));
+}
+
+// extended label of state s
+__device__ __forceinline__ int ext_label(const int32_t* tg, int s, int blank) { return (s & 1) ? tg[s >> 1] : blank; }
+
+struct CtcP {
+  const float* logits; long sb, st;   // row (b, t) at logits + b*sb + t*st (batch- or time-major)
+  const int32_t* tgt; int ldt;        // targets: utterance b at tgt + (off ? off[b] : b*ldt)
+  const int32_t* off;
+  const int32_t* in_len; const int32_t* tgt_len;
+  int B, T, V, Smax, S;               // S = 2*Smax + 1 (state stride of the work arrays)
+  int blank;
+  float* lse;                         // (B, T)
+  float* lpe;                         // (B, T, S)
+  float* alpha;                       // (B, T, S)
+  float* beta;                        // (B, T, S)
+  float* nll_raw;                     // (B) -log p, may be +inf
+};
+
+__device__ __forceinline__ const int32_t* tgt_of(const CtcP& p, int b) {
+  return p.tgt + (p.off ? (long)p.off[b] : (long)b * p.ldt);
+}
+
+// ---------------------------------------------------------------------------------- prep
+__global__ __launch_bounds__(256) void ctc_prep(CtcP p) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)p.B * p.T) return;
+  const int b = (int)(row / p.T), t = (int)(row % p.T);
+  if (t >= p.in_len[b]) return;
+  const float* x = p.logits + b * p.sb + t * p.st;
+  float m = NEG_INF;
+  const bool v4 = (p.V % 4 == 0) && (p.sb % 4 == 0) && (p.st % 4 == 0) && ((uintptr_t)p.logits % 16 == 0);
+  if (v4) {
+    for (int v = lane * 4; v < p.V; v += 256) {
+      const float4 q = *reinterpret_cast<const float4*>(x + v);
+      m = fmaxf(m, fmaxf(fmaxf(q.x, q.y), fmaxf(q.z, q.w)));
+    }
+  } else {
+    for (int v = lane; v < p.V; v += 64) m = fmaxf(m, x[v]);
+  }
+  m = wave_max(m);
+  float s = 0.f;
+  if (v4) {
+    for (int v = lane * 4; v < p.V; v += 256) {
+      const float4 q = *reinterpret_cast<const float4*>(x + v);
+      s += expf(q.x - m) + expf(q.y - m) + expf(q.z - m) + expf(q.w - m);
+    }
+  } else {
+    for (int v = lane; v < p.V; v += 64) s += expf(x[v] - m);
+  }
+  s = wave_sum(s);
+  const float l = m + logf(s);
+  if (lane == 0) p.lse[row] = l;
+  const int Sb = 2 * p.tgt_len[b] + 1;
+  const int32_t* tg = tgt_of(p, b);
+  float* dst = p.lpe + row * p.S;
+  for (int st = lane; st < Sb; st += 64) dst[st] = x[ext_label(tg, st, p.blank)] - l;
+}
+
+// ---------------------------------------------------------------------------------- alpha / beta
+// blockIdx.x = utterance, blockIdx.y = 0 (alpha, forward in time) / 1 (beta, backward in time).
+// Thread `tid` owns states tid + 256 j, j < SPT.
+template <int SPT>
+__global__ __launch_bounds__(AB_THREADS) void ctc_alphabeta(CtcP p) {
+  extern __shared__ float sh[];        // [2][S]
+  const int b = blockIdx.x, dir = blockIdx.y, tid = threadIdx.x;
+  const int Tb = p.in_len[b], L = p.tgt_len[b], Sb = 2 * L + 1;
+  const int32_t* tg = tgt_of(p, b);
+  float* out = (dir == 0 ? p.alpha : p.beta) + (long)b * p.T * p.S;
+  const float* lp = p.lpe + (long)b * p.T * p.S;
+  if (Tb <= 0) {
+    if (dir == 0 && tid == 0) p.nll_raw[b] = L == 0 ? 0.f : INFINITY;
+    return;
+  }
+  // per-state transition flags: alpha may skip from s-2 (beta: from s+2) when the labels differ
+  bool skip[SPT];
+  int sidx[SPT];
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = tid + AB_THREADS * j;
+    sidx[j] = s;
+    if (dir == 0) skip[j] = s < Sb && s >= 2 && (s & 1) && ext_label(tg, s, p.blank) != ext_label(tg, s - 2, p.blank);
+    else skip[j] = s + 2 < Sb && (s & 1) && ext_label(tg, s, p.blank) != ext_label(tg, s + 2, p.blank);
+  }
+  // frame order: step i handles t = i (alpha) or Tb-1-i (beta)
+  auto frame = [&](int i) { return dir == 0 ? i : Tb - 1 - i; };
+  float cur[SPT][PF], nxt[SPT][PF];
+  auto fetch = [&](float (&r)[SPT][PF], int i0) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int i = i0 + q;
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+        r[j][q] = (i < Tb && sidx[j] < Sb) ? lp[(long)frame(i) * p.S + sidx[j]] : NEG_INF;
+    }
+  };
+  fetch(cur, 0);
+  for (int i0 = 0; i0 < Tb; i0 += PF) {
+    if (i0 + PF < Tb) fetch(nxt, i0 + PF);
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int i = i0 + q;
+      if (i >= Tb) break;
+      const int t = frame(i);
+      float* wr = sh + (i & 1) * p.S;
+      const float* rd = sh + ((i + 1) & 1) * p.S;
+#pragma unroll
+      for (int j = 0; j < SPT; ++j) {
+        const int s = sidx[j];
+        if (s >= Sb) continue;
+        float v;
+        if (i == 0) {
+          v = dir == 0 ? (s <= 1 ? cur[j][q] : NEG_INF) : (s >= Sb - 2 ? cur[j][q] : NEG_INF);
+        } else if (dir == 0) {
+          const float a0 = rd[s], a1 = s >= 1 ? rd[s - 1] : NEG_INF, a2 = skip[j] ? rd[s - 2] : NEG_INF;
+          v = lse3(a0, a1, a2) + cur[j][q];
+        } else {
+          const float a0 = rd[s], a1 = s + 1 < Sb ? rd[s + 1] : NEG_INF, a2 = skip[j] ? rd[s + 2] : NEG_INF;
+          v = lse3(a0, a1, a2) + cur[j][q];
+        }
+        wr[s] = v;
+        out[(long)t * p.S + s] = v;
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+#pragma unroll
+      for (int j = 0; j < SPT; ++j) cur[j][q] = nxt[j][q];
+  }
+  if (dir == 0 && tid == 0) {
+    const float* last = sh + ((Tb - 1) & 1) * p.S;
+    const float l1 = last[Sb - 1], l2 = Sb >= 2 ? last[Sb - 2] : NEG_INF;
+    p.nll_raw[b] = -lse2(l1, l2);
+  }
+}
+
+// nll (B): -log p, or 0 where infinite and zero_infinity
+__global__ void ctc_finish(const float* nll_raw, int B, int zero_inf, float* nll) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) {
+    const float v = nll_raw[b];
+    nll[b] = (zero_inf && isinf(v)) ? 0.f : v;
+  }
+}
+
+// ---------------------------------------------------------------------------------- gradient
+// one workgroup (256 threads) per frame row; corr[V] in dynamic LDS
+template <typename TG>
+__global__ __launch_bounds__(256) void ctc_grad(CtcP p, const float* grad_out, int go_stride, int reduction,
+                                                int zero_inf, TG* __restrict__ g, long gsb, long gst) {
+  extern __shared__ float corr[];
+  const long row = blockIdx.x;
+  const int b = (int)(row / p.T), t = (int)(row % p.T);
+  TG* dst = g + b * gsb + t * gst;
+  const int Tb = p.in_len[b], L = p.tgt_len[b];
+  const float nll = p.nll_raw[b];
+  if (t >= Tb || (zero_inf && isinf(nll))) {   // as torch: padded frames and zeroed infinite losses
+    for (int v = threadIdx.x; v < p.V; v += 256) dst[v] = from_f32<TG>(0.f);
+    return;
+  }
+  float scale = grad_out[go_stride * b];
+  if (reduction == 1) scale /= (float)p.B * (float)(L > 0 ? L : 1);
+  for (int v = threadIdx.x; v < p.V; v += 256) corr[v] = 0.f;
+  const long base = row * p.S;
+  const int32_t* tg = tgt_of(p, b);
+  __syncthreads();
+  // blank: sum over the even states in state order (one wave, fixed-order tree)
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+    for (int u = threadIdx.x; u <= L; u += 64) {
+      const int st = 2 * u;
+      s += expf(p.alpha[base + st] + p.beta[base + st] + nll - p.lpe[base + st]);
+    }
+    s = wave_sum(s);
+    if (threadIdx.x == 0) corr[p.blank] = s;
+  }
+  // labels: the first occurrence of each label sums all its occurrences in label order
+  for (int u = threadIdx.x - 64; u >= 0 && u < L; u += 192) {
+    const int c = tg[u];
+    bool first = true;
+    for (int w = 0; w < u; ++w) first = first && tg[w] != c;
+    if (!first) continue;
+    float s = 0.f;
+    for (int w = u; w < L; ++w)
+      if (tg[w] == c) {
+        const int st = 2 * w + 1;
+        s += expf(p.alpha[base + st] + p.beta[base + st] + nll - p.lpe[base + st]);
+      }
+    corr[c] = s;
+  }
+  __syncthreads();
+  const float* x = p.logits + b * p.sb + t * p.st;
+  const float l = p.lse[row];
+  for (int v = threadIdx.x; v < p.V; v += 256) dst[v] = from_f32<TG>((expf(x[v] - l) - corr[v]) * scale);
+}
+
+// ---------------------------------------------------------------------------------- greedy decode
+// one wave per frame row: argmax (first maximum, as torch.argmax) -> ids (B, T) int64
+__global__ __launch_bounds__(256) void greedy_argmax(const float* __restrict__ x, long sb, long st, int B, int T,
+                                                     int V, int64_t* __restrict__ ids) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)B * T) return;
+  const float* r = x + (row / T) * sb + (row % T) * st;
+  float m = NEG_INF;
+  int mi = 0x7fffffff;
+  for (int v = lane; v < V; v += 64) {
+    const float q = r[v];
+    if (q > m || (q == m && v < mi) || (isnan(q) && !isnan(m))) { m = q; mi = v; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64);
+    const int oi = __shfl_xor(mi, o, 64);
+    const bool take = (isnan(om) && !isnan(m)) || om > m || (om == m && oi < mi);
+    if (take) { m = om; mi = oi; }
+  }
+  if (lane == 0) ids[row] = mi == 0x7fffffff ? 0 : mi;
+}
+
+// one thread per utterance: compact the ids of frames < len dropping `blank` and `pad`
+// (pad < 0: none), optionally collapsing repeats first (standard CTC greedy)
+__global__ void greedy_compact(const int64_t* __restrict__ ids, const int32_t* __restrict__ lens, int B, int T,
+                               int blank, int pad, int collapse, int32_t* __restrict__ out, int32_t* __restrict__ out_len) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int Tb = lens ? min(lens[b], T) : T;
+  int n = 0;
+  long prev = -1;
+  for (int t = 0; t < Tb; ++t) {
+    const long c = ids[(long)b * T + t];
+    const bool rep = collapse && c == prev;
+    prev = c;
+    if (rep || c == blank || c == pad) continue;
+    out[(long)b * T + n++] = (int32_t)c;
+  }
+  for (int t = n; t < T; ++t) out[(long)b * T + t] = -1;
+  out_len[b] = n;
+}
+
+CtcP make_p(const float* logits, long sb, long st, const int32_t* targets, int ldt, const int32_t* off,
+            const int32_t* in_len, const int32_t* tgt_len, int B, int T, int V, int Smax, int blank, float* ws) {
+  CtcP p;
+  p.logits = logits; p.sb = sb; p.st = st; p.tgt = targets; p.ldt = ldt; p.off = off;
+  p.in_len = in_len; p.tgt_len = tgt_len;
+  p.B = B; p.T = T; p.V = V; p.Smax = Smax; p.S = 2 * Smax + 1; p.blank = blank;
+  const long bt = (long)B * T, bts = bt * p.S;
+  p.lse = ws;
+  p.lpe = ws + bt;
+  p.alpha = p.lpe + bts;
+  p.beta = p.alpha + bts;
+  p.nll_raw = p.beta + bts;
+  return p;
+}
+
+}  // namespace
+
+CFM_EXPORT size_t cfm_ctc_ws_bytes(int B, int T, int Smax) {
+  const long bt = (long)B * T;
+  return sizeof(float) * (size_t)(bt + 3 * bt * (2L * Smax + 1) + B);
+}
+
+CFM_EXPORT int cfm_ctc_loss_fwd(const float* logits, long sb, long st, const int32_t* targets, int ldt,
+                                const int32_t* tgt_off, const int32_t* in_len, const int32_t* tgt_len, int B, int T,
+                                int V, int Smax, int blank, int zero_infinity, float* nll, float* ws, void* stream) {
+  CFM_REQUIRE(logits && targets && in_len && tgt_len && nll && ws, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(B > 0 && T > 0 && V > 0 && Smax >= 0 && (tgt_off || ldt >= Smax), CFM_ERR_SHAPE, "bad shape");
+  CFM_REQUIRE(blank >= 0 && blank < V, CFM_ERR_ARG, "blank out of range");
+  const int S = 2 * Smax + 1;
+  CFM_REQUIRE(S <= 4 * AB_THREADS, CFM_ERR_UNSUPPORTED, "target length must be <= 511");
+  CFM_REQUIRE(2L * S * sizeof(float) <= 64 * 1024, CFM_ERR_UNSUPPORTED, "state count");
+  hipStream_t s = cfm::as_stream(stream);
+  CtcP p = make_p(logits, sb, st, targets, ldt, tgt_off, in_len, tgt_len, B, T, V, Smax, blank, ws);
+  hipLaunchKernelGGL(ctc_prep, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s, p);
+  const size_t sh = 2 * S * sizeof(float);
+  if (S <= AB_THREADS)
+    hipLaunchKernelGGL(ctc_alphabeta<1>, dim3(B, 2), dim3(AB_THREADS), sh, s, p);
+  else if (S <= 2 * AB_THREADS)
+    hipLaunchKernelGGL(ctc_alphabeta<2>, dim3(B, 2), dim3(AB_THREADS), sh, s, p);
+  else
+    hipLaunchKernelGGL(ctc_alphabeta<4>, dim3(B, 2), dim3(AB_THREADS), sh, s, p);
+  hipLaunchKernelGGL(ctc_finish, dim3(cdiv(B, 256)), dim3(256), 0, s, p.nll_raw, B, zero_infinity, nll);
+  return cfm::check_launch("cfm_ctc_loss_fwd");
+}
+
+CFM_EXPORT int cfm_ctc_loss_bwd(const float* logits, long sb, long st, const int32_t* targets, int ldt,
+                                const int32_t* tgt_off, const int32_t* in_len, const int32_t* tgt_len, int B, int T,
+                                int V, int Smax, int blank, int zero_infinity, const float* ws, const float* grad_out,
+                                int grad_out_stride, int reduction, void* grad_logits, int dtype_grad, long gsb,
+                                long gst, void* stream) {
+  CFM_REQUIRE(logits && targets && in_len && tgt_len && ws && grad_out && grad_logits, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(B > 0 && T > 0 && V > 0, CFM_ERR_SHAPE, "bad shape");
+  CFM_REQUIRE(reduction >= 0 && reduction <= 2, CFM_ERR_ARG, "reduction: 0 none / 1 mean / 2 sum");
+  CFM_REQUIRE((size_t)V * sizeof(float) <= 64 * 1024, CFM_ERR_UNSUPPORTED, "V too large for the LDS row");
+  hipStream_t s = cfm::as_stream(stream);
+  CtcP p = make_p(logits, sb, st, targets, ldt, tgt_off, in_len, tgt_len, B, T, V, Smax, blank, const_cast<float*>(ws));
+  const size_t sh = (size_t)V * sizeof(float);
+  const dim3 grid((unsigned)((long)B * T));
+  if (dtype_grad == CFM_BF16)
+    hipLaunchKernelGGL(ctc_grad<bf16>, grid, dim3(256), sh, s, p, grad_out, grad_out_stride, reduction,
+                       zero_infinity, (bf16*)grad_logits, gsb, gst);
+  else if (dtype_grad == CFM_F32)
+    hipLaunchKernelGGL(ctc_grad<float>, grid, dim3(256), sh, s, p, grad_out, grad_out_stride, reduction,
+                       zero_infinity, (float*)grad_logits, gsb, gst);
+  else
+    return cfm::fail(CFM_ERR_DTYPE, "cfm_ctc_loss_bwd: grad dtype");
+  return cfm::check_launch("cfm_ctc_loss_bwd");
+}
+
+CFM_EXPORT int cfm_ctc_greedy_decode(const float* logits, long sb, long st, const int32_t* lens, int B, int T, int V,
+                                     int blank, int pad, int collapse, int64_t* ids, int32_t* out, int32_t* out_len,
+                                     void* stream) {
+  CFM_REQUIRE(logits && ids && B > 0 && T > 0 && V > 0, CFM_ERR_ARG, "bad args");
+  hipStream_t s = cfm::as_stream(stream);
+  hipLaunchKernelGGL(greedy_argmax, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s, logits, sb, st, B, T,
+                     V, ids);
+  if (out && out_len)
+    hipLaunchKernelGGL(greedy_compact, dim3(cdiv(B, 64)), dim3(64), 0, s, ids, lens, B, T, blank, pad, collapse, out,
+                       out_len);
+  return cfm::check_launch("cfm_ctc_greedy_decode");
+}

@@ -28,6 +28,7 @@ struct GemmP {
   int act, act_grad;
   void* pre; int dtpre;
   float drop_p; uint64_t seed, doff;
+  const uint64_t* salt;   // bound dropout step counter (cfm_rng_bind) or nullptr
   float out_scale;
   const void* res; long ldr; int dtr;
   int split_k, k_per_split;
@@ -313,6 +314,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2
 template <int BMt, bool AK, bool BKM, class OA, class OB>
 __global__ __launch_bounds__(BMt * 2) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
   typedef Geo16<BMt> G;
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   constexpr int NTt = G::NTt, NVA = G::NVA, NVB = G::NVB, TILEA = G::TILEA;
   __shared__ __attribute__((aligned(16))) bf16 lds[G::LDS];   // [buf][A,B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -548,6 +550,7 @@ template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM>
 __global__ __launch_bounds__(BMt * 2) __attribute__((amdgpu_waves_per_eu(OCC * BMt / 128)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
   typedef PipeGeo<BMt, BKt, NST> G;
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   static_assert(NST >= 3 && NST <= 4, "ring depth");
   __shared__ __attribute__((aligned(1024))) char lds[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -631,6 +634,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
 template <bool AK, bool BKM, class OA, class OB>
 __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p, OA oa, OB ob) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   __shared__ __attribute__((aligned(16))) float lds[4 * TILE32];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -869,7 +873,7 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   p.sc = d->stride_c;
   p.alpha = d->alpha; p.bias = d->bias; p.act = d->act; p.act_grad = d->act_grad;
   p.pre = d->pre; p.dtpre = d->dtype_pre;
-  p.drop_p = d->drop_p; p.seed = d->drop_seed; p.doff = d->drop_offset;
+  p.drop_p = d->drop_p; p.seed = d->drop_seed; p.doff = d->drop_offset; p.salt = cfm::g_rng_salt;
   p.out_scale = d->out_scale; p.res = d->residual; p.ldr = d->ldr; p.dtr = d->dtype_r;
   p.split_k = split;
   const bool bf = d->dtype_ab == CFM_BF16;

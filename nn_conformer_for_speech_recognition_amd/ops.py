@@ -318,3 +318,51 @@ def conv2_bwd_weight(dh2, h1):
     dw2r = torch.empty(C2, 9 * C1, device=h1.device, dtype=torch.float32)
     L.call("cfm_conv2_bwd_weight", L.ptr(dh2), L.ptr(h1), L.ptr(dw2r), L.dt(h1), B, F1, T1, C1, C2, L.stream())
     return dw2r
+
+
+# ----------------------------------------------------------------------------- CTC head
+def _rows(x, batch_first):
+    """(B, T, sb, st) of a (B, T, V) / (T, B, V) tensor with contiguous classes."""
+    if x.stride(-1) != 1:
+        raise L.CfmError("CTC: the class dimension must be contiguous")
+    if batch_first:
+        return x.shape[0], x.shape[1], x.stride(0), x.stride(1)
+    return x.shape[1], x.shape[0], x.stride(1), x.stride(0)
+
+
+def ctc_loss_fwd(x, targets_i32, ldt, tgt_off, in_len_i32, tgt_len_i32, smax, blank, zero_infinity, batch_first):
+    """nll (B,) fp32 (0 where infinite and zero_infinity) + the workspace the backward needs."""
+    B, T, sb, st = _rows(x, batch_first)
+    V = x.shape[-1]
+    ws = workspace(L.size_call("cfm_ctc_ws_bytes", B, T, smax), x.device)
+    nll = torch.empty(B, device=x.device, dtype=torch.float32)
+    L.call("cfm_ctc_loss_fwd", L.ptr(x), sb, st, L.ptr(targets_i32), ldt, L.ptr(tgt_off), L.ptr(in_len_i32),
+           L.ptr(tgt_len_i32), B, T, V, smax, blank, int(bool(zero_infinity)), L.ptr(nll), L.ptr(ws), L.stream())
+    return nll, ws
+
+
+def ctc_loss_bwd(x, targets_i32, ldt, tgt_off, in_len_i32, tgt_len_i32, smax, blank, zero_infinity, batch_first, ws,
+                 grad_out, reduction, grad_dtype=torch.float32):
+    """d loss / d logits (softmax - posterior, scaled) in x's layout, dtype grad_dtype."""
+    B, T, sb, st = _rows(x, batch_first)
+    V = x.shape[-1]
+    g = torch.empty(x.shape, device=x.device, dtype=grad_dtype)
+    _, _, gsb, gst = _rows(g, batch_first)
+    go = grad_out.float().contiguous()
+    L.call("cfm_ctc_loss_bwd", L.ptr(x), sb, st, L.ptr(targets_i32), ldt, L.ptr(tgt_off), L.ptr(in_len_i32),
+           L.ptr(tgt_len_i32), B, T, V, smax, blank, int(bool(zero_infinity)), L.ptr(ws), L.ptr(go),
+           1 if go.numel() > 1 else 0, {"none": 0, "mean": 1, "sum": 2}[reduction], L.ptr(g), L.dt(g), gsb, gst,
+           L.stream())
+    return g
+
+
+def ctc_greedy_decode(x, lengths_i32=None, blank=0, pad=-1, collapse=False, batch_first=True, compact=True):
+    """argmax ids (B, T) int64 (torch.argmax semantics) and, if compact, the per-utterance id lists
+    with `blank` / `pad` removed (and repeats collapsed if asked): (B, T) int32 padded with -1 + lengths."""
+    B, T, sb, st = _rows(x, batch_first)
+    ids = torch.empty(B, T, device=x.device, dtype=torch.int64)
+    out = torch.empty(B, T, device=x.device, dtype=torch.int32) if compact else None
+    out_len = torch.empty(B, device=x.device, dtype=torch.int32) if compact else None
+    L.call("cfm_ctc_greedy_decode", L.ptr(x), sb, st, L.ptr(lengths_i32), B, T, x.shape[-1], int(blank), int(pad),
+           int(bool(collapse)), L.ptr(ids), L.ptr(out), L.ptr(out_len), L.stream())
+    return ids, out, out_len
