@@ -4,9 +4,10 @@
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 
 One step = one utterance batch through the hot path, forward + backward:
-SpecAugment (optional, --specaug) -> ConvSubSampling -> frame projection -> 17 Conformer-L layers
--> CTC head (Linear d->V) -> log_softmax + CTC loss -> full backward -> (N>1) RCCL gradient
-all-reduce -> optimizer step.  Inputs are synthetic 80-bin log-mel batches already resident in HBM
+ConvSubSampling -> frame projection -> 17 Conformer-L layers -> fused CTC head (Linear d->V +
+log_softmax + CTC loss, ctc.hip) -> full backward -> (N>1) RCCL gradient all-reduce -> Adafactor
+step.  Forward + backward are captured once into a HIP graph and replayed (--eager: launched from
+Python every step); dropout masks still change every step (device step counter, cfm_rng_bind).  Inputs are synthetic 80-bin log-mel batches already resident in HBM
 (SURVEY.md §8d), weights random-init.  Weak scaling: B=32 utterances per GPU.
 
 Prints ONE JSON line (rank 0) with the contract fields plus `roofline` (dominant kernel, measured
@@ -27,8 +28,10 @@ import torch.nn.functional as F
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+from nn_conformer_for_speech_recognition_amd import _lib  # noqa: E402
 from nn_conformer_for_speech_recognition_amd import dist as cdist  # noqa: E402
 from nn_conformer_for_speech_recognition_amd import ops  # noqa: E402
+from nn_conformer_for_speech_recognition_amd.ctc import ctc_head_loss  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.conformer import Conformer  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.frontend import linear  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.lib.convsubsampling import ConvSubSampling  # noqa: E402
@@ -77,40 +80,57 @@ class EncoderCTC(torch.nn.Module):
         self.ctc_fc = torch.nn.Linear(d, V)
         self.dropout = dropout
 
-    def forward(self, x, lens_i32, seed):
+    def forward(self, x, lens_i32, targets_i32, tgt_lens_i32, seed):
+        """-> (CTC loss (mean, zero_infinity), logits (B, T2, V)).  The head is the fused
+        Linear + log_softmax + CTC node (ctc.hip); dropout seeds are offset on the device by the
+        bound step counter, so one captured graph replays with fresh masks."""
         B = x.shape[0]
         h2 = self.conv_sub_sampling.forward_frames(x, self.cd)
         p = self.dropout if self.training else 0.0
         h = linear(h2.view(B * self.T2, -1), self.standard_linear.weight, self.standard_linear.bias, cd=self.cd,
                    drop_p=p, seed=seed)
         y = self.conformers.forward_tokens(h, lens_i32, B, self.T2, seed=seed + 7)
-        logits = linear(y, self.ctc_fc.weight, self.ctc_fc.bias, cd=self.cd, out_dtype=torch.float32)
-        return logits.view(B, self.T2, -1)
+        return ctc_head_loss(y, self.ctc_fc.weight, self.ctc_fc.bias, targets_i32, lens_i32, tgt_lens_i32, B,
+                             self.T2, blank=0, reduction="mean", zero_infinity=True, compute_dtype=self.cd)
 
 
 class KernelProbe:
-    """HIP-event timing of one kernel family on the stream it is launched on (torch's current
-    stream, which every libcfm op uses).  Installed as ops.PROBE while the timed region runs."""
+    """Timing of one kernel family, installed as ops.PROBE.  Each matching launch gets a probe slot
+    (cfm_gemm_desc.probe): the kernel itself records its first workgroup's start and its last
+    workgroup's end (s_memrealtime) — the interval rocprofv3 reports as the kernel's duration —
+    and one-lane kernels on the same stream reset the slot before and accumulate it after the
+    launch.  Works eagerly and inside a captured HIP graph (every replay accumulates)."""
 
-    def __init__(self, match):
+    MAX_SLOTS = 512
+
+    def __init__(self, match, device):
         self.match = match
-        self.pairs = []
         self.active = False
+        self.slots = torch.zeros(self.MAX_SLOTS, 4, dtype=torch.int64, device=device)
+        self.used = 0
+        self.khz = _lib.load().cfm_wallclock_khz()
 
-    def __call__(self, kind, shape, launch):
-        if not (self.active and self.match(kind, shape)):
+    def __call__(self, kind, shape, desc, launch):
+        if not (self.active and self.match(kind, shape, desc)) or self.khz <= 0:
             return launch()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
+        slot = self.used % self.MAX_SLOTS
+        self.used += 1
+        ptr = _lib.ptr(self.slots[slot])
+        _lib.call("cfm_probe_slot", ptr, 0, _lib.stream())
+        desc.probe = ptr
         r = launch()
-        e.record()
-        self.pairs.append((s, e, shape))
+        desc.probe = None
+        _lib.call("cfm_probe_slot", ptr, 1, _lib.stream())
         return r
+
+    def reset(self):
+        self.slots.zero_()
 
     def mean_ms(self):
         torch.cuda.synchronize()
-        t = [s.elapsed_time(e) for s, e, _ in self.pairs]
-        return sum(t) / len(t) if t else float("nan"), len(t)
+        tot = self.slots[:, 2].double().sum().item()
+        n = int(self.slots[:, 3].sum().item())
+        return (tot / self.khz / n) if n else float("nan"), n
 
 
 def cpu_baseline(cfg, threads, steps=2):
@@ -163,9 +183,9 @@ def main():
     ap.add_argument("--no-optimizer", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--gemm-mode", type=int, default=None, help="cfm_gemm_set_mode value (A/B tuning)")
+    ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no HIP graph)")
     args = ap.parse_args()
     if args.gemm_mode is not None:
-        from nn_conformer_for_speech_recognition_amd import _lib
         _lib.call("cfm_gemm_set_mode", args.gemm_mode)
 
     rank, world, local = cdist.init_from_env()
@@ -192,32 +212,73 @@ def main():
     lens_i32 = torch.full((B,), T2, dtype=torch.int32, device=dev)
     U = T2 // 4
     targets = torch.randint(1, V, (B, U), generator=g).to(dev)
-    in_lens = torch.full((B,), T2, dtype=torch.long)
-    tgt_lens = torch.full((B,), U, dtype=torch.long)
 
-    def step(i):
-        opt.zero_grad(set_to_none=True)     # autograd hands our fp32 grads over without an extra add
-        logits = model(x, lens_i32, seed=1000 * i + 17 * rank)
-        lp = F.log_softmax(logits, -1).transpose(0, 1)
-        loss = F.ctc_loss(lp, targets, in_lens, tgt_lens, blank=0, reduction="mean", zero_infinity=True)
+    rng = torch.zeros(1, dtype=torch.int64, device=dev)     # device dropout step counter
+    _lib.call("cfm_rng_bind", _lib.ptr(rng))
+    tgt_i32 = targets.to(torch.int32).contiguous()
+    tlen_i32 = torch.full((B,), U, dtype=torch.int32, device=dev)
+    seed0 = 17 * rank + 1
+
+    def fwd_bwd():
+        rng.add_(1)
+        loss, _ = model(x, lens_i32, tgt_i32, tlen_i32, seed=seed0)
         loss.backward()
+        return loss
+
+    def post():
         reducer.allreduce()
         if not args.no_optimizer:
             opt.step()
-        return loss
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
 
     # dominant kernel: the FFN up-projection GEMM (M=B*T2, N=ffn, K=d, bf16, SiLU epilogue)
     M_ffn = B * T2
-    probe = KernelProbe(lambda kind, shape: kind == "gemm" and shape == (M_ffn, ffn, d))
+    # (the FFN down-projection's data-gradient GEMM has the same (M, N, K): match the forward's
+    # bias + SiLU epilogue on K-major operands, not the shape alone)
+    probe = KernelProbe(lambda kind, shape, dsc: kind == "gemm" and shape == (M_ffn, ffn, d) and dsc.act == 1
+                        and not dsc.act_grad and dsc.a_kmajor and dsc.b_kmajor, dev)
     ops.PROBE = probe
+    graph = None
+    if args.eager:
+        def step(i):
+            opt.zero_grad(set_to_none=True)
+            loss = fwd_bwd()
+            post()
+            return loss
+        for i in range(args.warmup):
+            step(i)
+        torch.cuda.synchronize()
+    else:
+        # warm up on a side stream (allocator + autotuned state settle), then capture ONE training
+        # step's forward + backward into a HIP graph; all-reduce + optimizer stay eager (few launches)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for i in range(max(args.warmup, 1)):
+                opt.zero_grad(set_to_none=True)
+                fwd_bwd()
+                post()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        opt.zero_grad(set_to_none=True)
+        graph = torch.cuda.CUDAGraph()
+        probe.active = True          # the probe's slot kernels become nodes of the graph
+        with torch.cuda.graph(graph):
+            static_loss = fwd_bwd()
+        probe.active = False
+
+        def step(i):
+            graph.replay()
+            post()
+            return static_loss
+        step(0)                      # one replay outside the timed region
+        torch.cuda.synchronize()
+        probe.reset()
+
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    probe.active = True
+    if graph is None:
+        probe.active = True
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(args.warmup + i)
@@ -237,6 +298,10 @@ def main():
     value = frames_total / elapsed
 
     gemm_ms, n_launch = probe.mean_ms()
+    if os.environ.get("BENCH_PROBE_DUMP"):
+        torch.save(probe.slots.cpu(), os.environ["BENCH_PROBE_DUMP"])
+    timing = ("in-kernel s_memrealtime first-start / last-end of every matching launch in the timed "
+              "region" + (" (graph replays)" if graph is not None else ""))
     gemm_flops = 2.0 * M_ffn * ffn * d
     achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
     _, fpf = algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, model.F2)
@@ -250,7 +315,7 @@ def main():
                    "model": name, "layers": L, "d_model": d, "heads": H, "ffn": ffn, "conv_kernel": K,
                    "global_batch": B * world, "seq_len": T_in, "enc_frames": T2, "frontend": "frame",
                    "dropout": args.dropout, "optimizer": None if args.no_optimizer else "adafactor",
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "launch": "eager" if args.eager else "hip-graph (fwd+bwd)"},
         "per_gpu_value": round(value / world, 1),
         "step_algorithmic_tflops": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
@@ -259,6 +324,7 @@ def main():
                      "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
                      "avg_launch_ms": round(gemm_ms, 4), "launches_timed": n_launch,
+                     "timing": timing,
                      "flops_per_launch": gemm_flops},
     }
     pmc = os.path.join(REPO, "profiles", "r01", "gemm_ffn_up_pmc.json")

@@ -49,6 +49,14 @@ const char* cfm_get_last_error(void);
    Replaces the per-call torch RNG state of nn.Dropout (asrnn.py:31, torchaudio Conformer). */
 int cfm_rng_bind(const uint64_t* counter);
 
+/* Measurement probes (bench.py roofline timing, also inside a captured HIP graph where HIP events
+   cannot be read back on ROCm).  A probe slot is 4 x u64 {start, end, total, count}: mode 0
+   resets start = ~0, end = 0 (before the probed launch, which records its first-start / last-end
+   into start / end, see cfm_gemm_desc.probe); mode 1 adds end - start to total and 1 to count
+   (after it).  Ticks of the constant-rate GPU wall clock at cfm_wallclock_khz() kHz. */
+int cfm_probe_slot(unsigned long long* slot, int mode, void* stream);
+int cfm_wallclock_khz(void);
+
 /* y[i] = (dy)x[i] for n elements (dtype conversion; fp32 master weights -> bf16 compute copies). */
 int cfm_cast(const void* x, int dtype_x, void* y, int dtype_y, long n, void* stream);
 
@@ -106,6 +114,9 @@ typedef struct cfm_gemm_desc {
   float* workspace;        /* split_k > 1: NULL -> partial sums are atomically added into a
                               pre-initialised C; else >= split_k*batch*M*N floats of slabs that a
                               second pass reduces into C (deterministic, no pre-initialisation) */
+  unsigned long long* probe; /* optional timing slot (measurement only): the launch atomically
+                              min-records its first workgroup's start and max-records its last
+                              workgroup's end (s_memrealtime ticks) into probe[0] / probe[1] */
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 /* kernel-selection switch for A/B measurements: bit 0 = 256-row register-staged tiles allowed,

@@ -39,6 +39,7 @@ class GemmDesc(ctypes.Structure):
         ("residual", c_void_p), ("ldr", c_long), ("dtype_r", c_int),
         ("split_k", c_int),
         ("workspace", c_void_p),
+        ("probe", c_void_p),
     ]
 
 
@@ -47,6 +48,8 @@ _SIGS = {
     "cfm_version": (c_int, []),
     "cfm_get_last_error": (ctypes.c_char_p, []),
     "cfm_rng_bind": (c_int, [c_void_p]),
+    "cfm_probe_slot": (c_int, [c_void_p, c_int, c_void_p]),
+    "cfm_wallclock_khz": (c_int, []),
     "cfm_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_void_p]),
     "cfm_cast_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
     "cfm_specaug_apply": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p]),

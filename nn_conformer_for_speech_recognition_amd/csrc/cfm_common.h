@@ -116,6 +116,16 @@ __device__ __forceinline__ float drop_keep_scale(uint32_t thr) { return 65536.f 
 __device__ __forceinline__ uint64_t salted_seed(uint64_t seed, const uint64_t* salt) {
   return salt ? seed + salt[0] * 0x9E3779B97F4A7C15ull : seed;
 }
+// timing probe of a launch (cfm_gemm_desc.probe): first workgroup start / last workgroup end
+__device__ __forceinline__ void probe_begin(unsigned long long* slot) {
+  if (slot && threadIdx.x == 0) atomicMin(slot, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void probe_end(unsigned long long* slot) {
+  if (slot) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(slot + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+}
 // returns the keep scale if kept, 0 if dropped
 __device__ __forceinline__ float dropout_scale(float p, uint64_t seed, uint64_t idx) {
   if (p <= 0.f) return 1.f;

@@ -236,3 +236,32 @@ CFM_EXPORT int cfm_colsum(const void* x, int dtx, long M, int N, long ld, float*
   cfm::colreduce(ws, nblk, N, out, accumulate, s);
   return cfm::check_launch("cfm_colsum");
 }
+
+// --------------------------------------------------------------------------- probes
+// A probed kernel records its own first-workgroup start and last-workgroup end (s_memrealtime) in
+// slot[0] / slot[1]; these one-lane kernels reset the slot before it and accumulate the interval
+// after it, on the same stream (so they work as nodes of a captured HIP graph too).
+namespace {
+__global__ void probe_slot_kernel(unsigned long long* s, int mode) {
+  if (mode == 0) {
+    s[0] = ~0ull;
+    s[1] = 0ull;
+  } else {
+    if (s[1] > s[0]) s[2] += s[1] - s[0];
+    s[3] += 1;
+  }
+}
+}  // namespace
+
+CFM_EXPORT int cfm_probe_slot(unsigned long long* slot, int mode, void* stream) {
+  CFM_REQUIRE(slot && (mode == 0 || mode == 1), CFM_ERR_ARG, "bad args");
+  hipLaunchKernelGGL(probe_slot_kernel, dim3(1), dim3(1), 0, cfm::as_stream(stream), slot, mode);
+  return cfm::check_launch("cfm_probe_slot");
+}
+
+CFM_EXPORT int cfm_wallclock_khz(void) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return 0;
+  return khz;
+}

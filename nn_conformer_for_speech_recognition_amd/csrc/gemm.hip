@@ -38,6 +38,7 @@ struct GemmP {
   // -> dh1 row (b, 2i+pf, 2j+pt)
   int cmap, cm_F1c, cm_T1c, cm_pf, cm_pt, cm_F1, cm_T1;
   int dbg;     // timing experiments only (cfm_gemm_set_mode bit 3): skip the epilogue's stores
+  unsigned long long* probe;   // optional timing slot (cfm_gemm_desc.probe)
 };
 
 __device__ __forceinline__ long out_row(const GemmP& p, int m) {
@@ -314,6 +315,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2
 template <int BMt, bool AK, bool BKM, class OA, class OB>
 __global__ __launch_bounds__(BMt * 2) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
   typedef Geo16<BMt> G;
+  probe_begin(p.probe);
   if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   constexpr int NTt = G::NTt, NVA = G::NVA, NVB = G::NVB, TILEA = G::TILEA;
   __shared__ __attribute__((aligned(16))) bf16 lds[G::LDS];   // [buf][A,B]
@@ -397,6 +399,7 @@ __global__ __launch_bounds__(BMt * 2) void gemm_bf16_kernel(GemmP p, OA oa, OB o
   }
 
   tile_epilogue<BMt>(p, acc, reinterpret_cast<float*>(lds), z, blockIdx.z, m0, n0, wm, wn, lane, tid);
+  probe_end(p.probe);
 }
 
 // Epilogue of one BMt x 128 tile (4-wave rows x 2-wave columns of 64x64 accumulators).  The
@@ -550,6 +553,7 @@ template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM>
 __global__ __launch_bounds__(BMt * 2) __attribute__((amdgpu_waves_per_eu(OCC * BMt / 128)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
   typedef PipeGeo<BMt, BKt, NST> G;
+  probe_begin(p.probe);
   if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   static_assert(NST >= 3 && NST <= 4, "ring depth");
   __shared__ __attribute__((aligned(1024))) char lds[G::LDS];
@@ -629,6 +633,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
   }
   __syncthreads();   // every wave done with the ring (no DMA outstanding) -> reuse it for the epilogue
   tile_epilogue<BMt>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane, tid);
+  probe_end(p.probe);
 }
 
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
@@ -876,6 +881,7 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   p.drop_p = d->drop_p; p.seed = d->drop_seed; p.doff = d->drop_offset; p.salt = cfm::g_rng_salt;
   p.out_scale = d->out_scale; p.res = d->residual; p.ldr = d->ldr; p.dtr = d->dtype_r;
   p.split_k = split;
+  p.probe = d->probe;
   const bool bf = d->dtype_ab == CFM_BF16;
   p.k_per_split = split_k_for(p, bf ? BK16 : BK32);
   const int vlen = bf ? 8 : 4;

@@ -34,13 +34,13 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         ldr=ldr if ldr is not None else N, dtype_r=L.dt(residual) if residual is not None else F32,
         split_k=int(split_k), workspace=L.ptr(workspace))
     if PROBE is not None:
-        PROBE("gemm", (M, N, K), lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
+        PROBE("gemm", (M, N, K), d, lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
     else:
         L.call("cfm_gemm", L.ctypes.byref(d), L.stream())
     return C
 
 
-PROBE = None   # optional timing hook (bench.py KernelProbe): PROBE(kind, shape, launch)
+PROBE = None   # optional timing hook (bench.py KernelProbe): PROBE(kind, shape, desc, launch)
 
 
 def linear(x, w, bias=None, out_dtype=None, act=ACT_NONE, pre=None, drop_p=0.0, seed=0, offset=0,

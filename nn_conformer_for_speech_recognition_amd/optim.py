@@ -35,6 +35,7 @@ class Adafactor(torch.optim.Optimizer):
         super().__init__(params, defaults)
         self._step = 0
         self._dev = {}
+        self._tables = {}
 
     @staticmethod
     def _geom(p):
@@ -104,7 +105,16 @@ class Adafactor(torch.optim.Optimizer):
                 raise L.CfmError("libcfm Adafactor: all parameters of a group must share the step count")
             step = steps[0]
             dev = ps[0].device
-            table = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev, non_blocking=False)
+            # the device table only changes when a parameter / gradient / state buffer moves (e.g.
+            # never, once gradients live in a captured graph's pool): reuse it, no per-step H2D copy
+            raw = bytes(host)
+            tkey = (id(group), dev)
+            cached = self._tables.get(tkey)
+            if cached is not None and cached[0] == raw:
+                table = cached[1]
+            else:
+                table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev, non_blocking=False)
+                self._tables[tkey] = (raw, table)
             key = (id(group), dev)
             buf = self._dev.get(key)
             if buf is None or buf[0].numel() < max(rm_off, 1) or buf[1].numel() < n:
