@@ -226,17 +226,23 @@ int cfm_conv1_bwd_weight(const void* dh1, int dtype_h, const float* x, float* dw
  * buffer of cfm_adafactor_table_bytes(n)), copies it to the device, and calls
  * cfm_adafactor_step with the prefix totals (factored rows, factored columns, elementwise
  * blocks = sum of cfm_adafactor_blocks(numel)).  col == NULL marks an unfactored (1-D) tensor,
- * whose full second moment lives in `row`.  rowmean: >= sum(nb) floats; sumsq: n floats. */
+ * whose full second moment lives in `row`.  rowmean: >= sum(nb) floats. */
 size_t cfm_adafactor_table_bytes(int n_params);
 int cfm_adafactor_fill_table(void* host_table, int i, float* p, const float* g, float* m, float* row,
                              float* col, long numel, int nb, int R, int C, long row_task_off,
-                             long col_off, long blk_off, long rm_off, long rm_task_off);
+                             long col_off, long blk_off, long rm_off, long rm_task_off,
+                             long colpart_task_off, long part_off);
 int cfm_adafactor_blocks(long numel);
 long cfm_adafactor_row_tasks(int nb, int R, int C);
 long cfm_adafactor_rowmean_tasks(int nb, int R);
+long cfm_adafactor_colpart_tasks(int nb, int R, int C);
+long cfm_adafactor_part_floats(int nb, int R, int C);
+/* part: >= sum of cfm_adafactor_part_floats floats (column partials of wide matrices);
+   partial: >= nblocks floats (per-block u^2 sums; RMS summed in block order, deterministic). */
 int cfm_adafactor_step(const void* dev_table, int n, long nrow_tasks, long ncols, long nblocks,
-                       long nrowmean_tasks, float* rowmean, float* sumsq, float lr, float beta1,
-                       float beta2t, float eps1, float clip, void* stream);
+                       long nrowmean_tasks, long ncolpart_tasks, float* rowmean, float* part,
+                       float* partial, float lr, float beta1, float beta2t, float eps1, float clip,
+                       void* stream);
 
 /* ---------------------------------------------------------------- CTC head (runner.py:35,142-143)
  * Replaces torch.nn.CTCLoss(blank=hp.blank_idx, zero_infinity=True) on

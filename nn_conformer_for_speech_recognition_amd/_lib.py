@@ -72,12 +72,15 @@ _SIGS = {
                                 c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p]),
     "cfm_adafactor_table_bytes": (c_size_t, [c_int]),
     "cfm_adafactor_fill_table": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
-                                         c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long]),
+                                         c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long, c_long,
+                                         c_long]),
+    "cfm_adafactor_colpart_tasks": (c_long, [c_int, c_int, c_int]),
+    "cfm_adafactor_part_floats": (c_long, [c_int, c_int, c_int]),
     "cfm_adafactor_blocks": (c_int, [c_long]),
     "cfm_adafactor_row_tasks": (c_long, [c_int, c_int, c_int]),
     "cfm_adafactor_rowmean_tasks": (c_long, [c_int, c_int]),
-    "cfm_adafactor_step": (c_int, [c_void_p, c_int, c_long, c_long, c_long, c_long, c_void_p, c_void_p, c_float,
-                                   c_float, c_float, c_float, c_float, c_void_p]),
+    "cfm_adafactor_step": (c_int, [c_void_p, c_int, c_long, c_long, c_long, c_long, c_long, c_void_p, c_void_p,
+                                   c_void_p, c_float, c_float, c_float, c_float, c_float, c_void_p]),
     "cfm_silu_bwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_long, c_void_p]),
     "cfm_bn_ws_bytes": (c_size_t, [c_int]),
     "cfm_bn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_int, c_void_p,

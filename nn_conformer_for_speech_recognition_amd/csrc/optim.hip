@@ -6,8 +6,10 @@
 // for ndim >= 2 (row/col EMAs of g^2+eps1), full EMA otherwise; update u = g * rsqrt(row_r /
 // mean(row)) * rsqrt(col_c) (or g * rsqrt(v)), clipped by max(1, RMS(u)/clip), scaled by lr,
 // first moment m = b1*m + (1-b1)*u, p -= m.  All parameters are handled by five launches over a
-// device-side parameter table (no per-tensor launches): row stats, column stats, row-stat means,
-// u^2 sums (one atomic per workgroup per tensor), apply.  Work items are "tasks" whose shape
+// device-side parameter table (no per-tensor launches): one pass over g for the row statistics
+// and column partial sums of wide matrices (64 <= C <= 2560), row stats of narrow ones, column
+// finish (partials in fixed order), row-stat means, u^2 block partials, apply (each block sums its
+// tensor's partials in block order: deterministic, no atomics).  float4 paths where aligned.  Work items are "tasks" whose shape
 // adapts to the tensor: a wide row (C >= 64) is one wave, narrow rows (e.g. the 3x3 taps of the
 // conv2 weight, nb = 65536) are packed 64 per wave (one per lane).  HBM-bound.
 #include "cfm_common.h"
@@ -16,15 +18,21 @@ namespace {
 
 constexpr int EB = 256;          // threads per block
 constexpr int CHUNK = 4096;      // elements per block in the elementwise passes
+constexpr int RB = 32;           // rows per column-partial task (wide factored tensors)
+constexpr int KMAX = 40;         // 64-column groups a lane keeps in registers: wide means 64 <= C <= 2560
 
 struct AdaP {
   float* p; const float* g; float* m; float* row; float* col;   // col == nullptr: unfactored (row = v)
   long numel; int nb, R, C, factored;
   long row_toff, col_off, blk_off, rm_off, rm_toff;              // prefix offsets (tasks / elements)
+  long cp_toff, part_off;                                        // column-partial tasks / partial floats
 };
 
+__host__ __device__ __forceinline__ bool is_wide(int C) { return C >= 64 && C <= 64 * KMAX; }
+
 __device__ __forceinline__ long off_of(const AdaP& q, int which) {
-  return which == 0 ? q.row_toff : which == 1 ? q.col_off : which == 2 ? q.blk_off : q.rm_toff;
+  return which == 0 ? q.row_toff : which == 1 ? q.col_off : which == 2 ? q.blk_off : which == 3 ? q.rm_toff
+                                                                                                  : q.cp_toff;
 }
 __device__ __forceinline__ int find_param(const AdaP* t, int n, long idx, int which) {
   int lo = 0, hi = n - 1;
@@ -39,42 +47,92 @@ __device__ __forceinline__ void row_update(const AdaP& q, long lr, float s, floa
   q.row[lr] = b2t * q.row[lr] + (1.f - b2t) * (s / q.C);
 }
 
-// row tasks: wide rows -> one wave per row; narrow rows -> 64 rows per wave (lane = row)
+// Wide factored tensors (64 <= C <= 2560), one pass over g: task (b, rb) covers rows
+// rb*RB .. rb*RB+RB-1 of matrix b.  Row statistics are finished here (wave reduction per row);
+// column sums of the block go to part[b][rb][c] (finished by ada_cols, fixed order).
+__global__ __launch_bounds__(EB) void ada_colpart(const AdaP* __restrict__ t, int n, long ntasks, float b2t,
+                                                  float eps1, float* __restrict__ part) {
+  __shared__ float red[4][64 * KMAX];
+  const long task = blockIdx.x;
+  if (task >= ntasks) return;
+  const AdaP& q = t[find_param(t, n, task, 4)];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nrb = (q.R + RB - 1) / RB;
+  const long lt = task - q.cp_toff;
+  const int b = (int)(lt / nrb), rb = (int)(lt % nrb);
+  const int r0 = rb * RB, r1 = min(q.R, r0 + RB);
+  const int nk = (q.C + 63) / 64;
+  float cacc[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) cacc[k] = 0.f;
+  for (int r = r0 + wv; r < r1; r += 4) {
+    const float* g = q.g + ((long)b * q.R + r) * q.C;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int c = lane + 64 * k;
+      if (k < nk && c < q.C) {
+        const float v = g[c];
+        const float e = v * v + eps1;
+        s += e;
+        cacc[k] += e;
+      }
+    }
+    s = wave_sum(s);
+    if (lane == 0) row_update(q, (long)b * q.R + r, s, b2t);
+  }
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (k < nk) red[wv][lane + 64 * k] = cacc[k];
+  __syncthreads();
+  float* dst = part + q.part_off + ((long)b * nrb + rb) * q.C;
+  for (int c = threadIdx.x; c < q.C; c += EB) dst[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+// row tasks of NARROW factored tensors: 64 rows per wave (lane = row)
 __global__ void ada_rows(const AdaP* __restrict__ t, int n, long ntasks, float b2t, float eps1) {
   const int lane = threadIdx.x & 63;
   const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (task >= ntasks) return;
   const AdaP& q = t[find_param(t, n, task, 0)];
   const long lt = task - q.row_toff;
-  if (q.C >= 64) {
+  if (is_wide(q.C)) {      // (wide rows are done by ada_colpart; kept for a wide tensor with no tasks)
     const float* g = q.g + lt * q.C;
     float s = 0.f;
     for (int c = lane; c < q.C; c += 64) s += g[c] * g[c] + eps1;
     s = wave_sum(s);
     if (lane == 0) row_update(q, lt, s, b2t);
-  } else {
-    const long lr = lt * 64 + lane;
-    if (lr < (long)q.nb * q.R) {
-      const float* g = q.g + lr * q.C;
-      float s = 0.f;
-      for (int c = 0; c < q.C; ++c) s += g[c] * g[c] + eps1;
-      row_update(q, lr, s, b2t);
-    }
+    return;
+  }
+  const long lr = lt * 64 + lane;
+  if (lr < (long)q.nb * q.R) {
+    const float* g = q.g + lr * q.C;
+    float s = 0.f;
+    for (int c = 0; c < q.C; ++c) s += g[c] * g[c] + eps1;
+    row_update(q, lr, s, b2t);
   }
 }
 
 // one thread per factored column: col = b2t*col + (1-b2t)*mean_r(g^2 + eps1)
-__global__ void ada_cols(const AdaP* __restrict__ t, int n, long ncols, float b2t, float eps1) {
+// wide: sum of the ada_colpart partials in row-block order; narrow: direct sum over the R rows
+__global__ void ada_cols(const AdaP* __restrict__ t, int n, long ncols, float b2t, float eps1,
+                         const float* __restrict__ part) {
   const long cidx = (long)blockIdx.x * EB + threadIdx.x;
   if (cidx >= ncols) return;
   const AdaP& q = t[find_param(t, n, cidx, 1)];
   const long lc = cidx - q.col_off;     // = b*C + j
   const int b = (int)(lc / q.C), j = (int)(lc % q.C);
-  const float* g = q.g + (long)b * q.R * q.C + j;
   float s = 0.f;
-  for (int r = 0; r < q.R; ++r) {
-    const float v = g[(long)r * q.C];
-    s += v * v + eps1;
+  if (is_wide(q.C)) {
+    const int nrb = (q.R + RB - 1) / RB;
+    const float* pp = part + q.part_off + (long)b * nrb * q.C + j;
+    for (int k = 0; k < nrb; ++k) s += pp[(long)k * q.C];
+  } else {
+    const float* g = q.g + (long)b * q.R * q.C + j;
+    for (int r = 0; r < q.R; ++r) {
+      const float v = g[(long)r * q.C];
+      s += v * v + eps1;
+    }
   }
   q.col[lc] = b2t * q.col[lc] + (1.f - b2t) * (s / q.R);
 }
@@ -102,61 +160,119 @@ __global__ void ada_rowmean(const AdaP* __restrict__ t, int n, long ntasks, floa
   }
 }
 
-__device__ __forceinline__ float ada_u(const AdaP& q, const float* rowmean, long i, float b2t, float eps1,
-                                       bool update_v) {
-  const float g = q.g[i];
-  if (!q.factored) {
-    float v = q.row[i];
-    if (update_v) {
-      v = b2t * v + (1.f - b2t) * (g * g + eps1);
-      q.row[i] = v;
-    }
-    return g * rsqrtf(v);
+// The update direction of 4 consecutive elements i..i+3 (same row: C % 4 == 0, i % 4 == 0) or of
+// one element (n4 == 1).  32-bit index arithmetic (numel < 2^31, checked on the host).
+template <int W>
+__device__ __forceinline__ void ada_u(const AdaP& q, const float* rowmean, unsigned i, float b2t, float eps1,
+                                      bool update_v, float (&u)[W]) {
+  float g[W];
+  if constexpr (W == 4) {
+    const float4 v = *reinterpret_cast<const float4*>(q.g + i);
+    g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
+  } else {
+    g[0] = q.g[i];
   }
-  const long rc = (long)q.R * q.C;
-  const int b = (int)(i / rc);
-  const long w = i % rc;
-  const int r = (int)(w / q.C), c = (int)(w % q.C);
+  if (!q.factored) {
+#pragma unroll
+    for (int e = 0; e < W; ++e) {
+      float v = q.row[i + e];
+      if (update_v) {
+        v = b2t * v + (1.f - b2t) * (g[e] * g[e] + eps1);
+        q.row[i + e] = v;
+      }
+      u[e] = g[e] * rsqrtf(v);
+    }
+    return;
+  }
+  const unsigned rc = (unsigned)q.R * (unsigned)q.C;
+  const unsigned b = i / rc, w = i - b * rc;
+  const unsigned r = w / (unsigned)q.C, c = w - r * (unsigned)q.C;
   const float rf = rsqrtf(q.row[(long)b * q.R + r] / rowmean[q.rm_off + b]);
-  const float cf = rsqrtf(q.col[(long)b * q.C + c]);
-  return g * rf * cf;
+  const float* cp = q.col + (long)b * q.C + c;
+#pragma unroll
+  for (int e = 0; e < W; ++e) u[e] = g[e] * rf * rsqrtf(cp[e]);
 }
 
-// per-block sum of u^2 -> one atomic per block into sumsq[param]
-__global__ void ada_sumsq(const AdaP* __restrict__ t, int n, const float* __restrict__ rowmean, float b2t,
-                          float eps1, float* __restrict__ sumsq) {
+__device__ __forceinline__ bool vec4_ok(const AdaP& q) {
+  return (q.numel % 4 == 0) && (!q.factored || q.C % 4 == 0) && ((uintptr_t)q.g % 16 == 0) &&
+         ((uintptr_t)q.p % 16 == 0) && (!q.m || (uintptr_t)q.m % 16 == 0) &&
+         (q.factored || (uintptr_t)q.row % 16 == 0);
+}
+
+// per-block sum of u^2 -> partial[blk] (summed in block order by ada_apply: deterministic)
+__global__ __launch_bounds__(EB) void ada_sumsq(const AdaP* __restrict__ t, int n, const float* __restrict__ rowmean,
+                                                float b2t, float eps1, float* __restrict__ partial) {
   __shared__ float red[EB / 64];
   const int pi = find_param(t, n, blockIdx.x, 2);
   const AdaP& q = t[pi];
   const long start = (long)(blockIdx.x - q.blk_off) * CHUNK;
   const long end = min(q.numel, start + CHUNK);
   float s = 0.f;
-  for (long i = start + threadIdx.x; i < end; i += EB) {
-    const float u = ada_u(q, rowmean, i, b2t, eps1, true);
-    s += u * u;
+  if (vec4_ok(q)) {
+    for (long i = start + 4 * threadIdx.x; i < end; i += 4 * EB) {
+      float u[4];
+      ada_u<4>(q, rowmean, (unsigned)i, b2t, eps1, true, u);
+      s += u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3];
+    }
+  } else {
+    for (long i = start + threadIdx.x; i < end; i += EB) {
+      float u[1];
+      ada_u<1>(q, rowmean, (unsigned)i, b2t, eps1, true, u);
+      s += u[0] * u[0];
+    }
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(sumsq + pi, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ void ada_apply(const AdaP* __restrict__ t, int n, const float* __restrict__ rowmean, float b2t, float eps1,
-                          const float* __restrict__ sumsq, float lr, float beta1, float clip) {
+__global__ __launch_bounds__(EB) void ada_apply(const AdaP* __restrict__ t, int n, const float* __restrict__ rowmean,
+                                                float b2t, float eps1, const float* __restrict__ partial, float lr,
+                                                float beta1, float clip) {
+  __shared__ float red[EB / 64];
   const int pi = find_param(t, n, blockIdx.x, 2);
   const AdaP& q = t[pi];
+  // RMS(u) of the whole tensor: its blocks' partials in block order
+  const int nblk = (int)((q.numel + CHUNK - 1) / CHUNK);
+  float ps = 0.f;
+  for (int k = threadIdx.x; k < nblk; k += EB) ps += partial[q.blk_off + k];
+  ps = wave_sum(ps);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ps;
+  __syncthreads();
+  const float sumsq = red[0] + red[1] + red[2] + red[3];
   const long start = (long)(blockIdx.x - q.blk_off) * CHUNK;
   const long end = min(q.numel, start + CHUNK);
-  const float rms = sqrtf(sumsq[pi] / (float)q.numel);
+  const float rms = sqrtf(sumsq / (float)q.numel);
   const float scale = lr / fmaxf(rms / clip, 1.f);
-  for (long i = start + threadIdx.x; i < end; i += EB) {
-    const float u = ada_u(q, rowmean, i, b2t, eps1, false) * scale;
-    float upd = u;
-    if (q.m) {
-      upd = beta1 * q.m[i] + (1.f - beta1) * u;
-      q.m[i] = upd;
+  if (vec4_ok(q)) {
+    for (long i = start + 4 * threadIdx.x; i < end; i += 4 * EB) {
+      float u[4];
+      ada_u<4>(q, rowmean, (unsigned)i, b2t, eps1, false, u);
+      float4 upd = make_float4(u[0] * scale, u[1] * scale, u[2] * scale, u[3] * scale);
+      if (q.m) {
+        const float4 m = *reinterpret_cast<const float4*>(q.m + i);
+        upd.x = beta1 * m.x + (1.f - beta1) * upd.x;
+        upd.y = beta1 * m.y + (1.f - beta1) * upd.y;
+        upd.z = beta1 * m.z + (1.f - beta1) * upd.z;
+        upd.w = beta1 * m.w + (1.f - beta1) * upd.w;
+        *reinterpret_cast<float4*>(q.m + i) = upd;
+      }
+      float4 p = *reinterpret_cast<const float4*>(q.p + i);
+      p.x -= upd.x; p.y -= upd.y; p.z -= upd.z; p.w -= upd.w;
+      *reinterpret_cast<float4*>(q.p + i) = p;
     }
-    q.p[i] -= upd;
+  } else {
+    for (long i = start + threadIdx.x; i < end; i += EB) {
+      float u[1];
+      ada_u<1>(q, rowmean, (unsigned)i, b2t, eps1, false, u);
+      float upd = u[0] * scale;
+      if (q.m) {
+        upd = beta1 * q.m[i] + (1.f - beta1) * upd;
+        q.m[i] = upd;
+      }
+      q.p[i] -= upd;
+    }
   }
 }
 
@@ -166,37 +282,46 @@ CFM_EXPORT size_t cfm_adafactor_table_bytes(int n_params) { return (size_t)n_par
 
 CFM_EXPORT int cfm_adafactor_fill_table(void* host_table, int i, float* p, const float* g, float* m, float* row,
                                         float* col, long numel, int nb, int R, int C, long row_toff, long col_off,
-                                        long blk_off, long rm_off, long rm_toff) {
+                                        long blk_off, long rm_off, long rm_toff, long cp_toff, long part_off) {
   CFM_REQUIRE(host_table && p && g && row, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(numel < (1L << 31), CFM_ERR_SHAPE, "tensor too large (2^31 elements)");
   AdaP* t = reinterpret_cast<AdaP*>(host_table) + i;
   t->p = p; t->g = g; t->m = m; t->row = row; t->col = col;
   t->numel = numel; t->nb = nb; t->R = R; t->C = C; t->factored = col != nullptr;
   t->row_toff = row_toff; t->col_off = col_off; t->blk_off = blk_off; t->rm_off = rm_off; t->rm_toff = rm_toff;
+  t->cp_toff = cp_toff; t->part_off = part_off;
   return CFM_OK;
 }
 
 CFM_EXPORT int cfm_adafactor_blocks(long numel) { return (int)((numel + CHUNK - 1) / CHUNK); }
 
-// number of row tasks / row-mean tasks a factored tensor contributes (see ada_rows / ada_rowmean)
-CFM_EXPORT long cfm_adafactor_row_tasks(int nb, int R, int C) { return C >= 64 ? (long)nb * R : ((long)nb * R + 63) / 64; }
+// number of row tasks / row-mean tasks / column-partial tasks / partial floats a factored tensor
+// contributes (see ada_rows / ada_rowmean / ada_colpart)
+CFM_EXPORT long cfm_adafactor_row_tasks(int nb, int R, int C) { return is_wide(C) ? 0 : ((long)nb * R + 63) / 64; }
+CFM_EXPORT long cfm_adafactor_colpart_tasks(int nb, int R, int C) { return is_wide(C) ? (long)nb * ((R + RB - 1) / RB) : 0; }
+CFM_EXPORT long cfm_adafactor_part_floats(int nb, int R, int C) {
+  return is_wide(C) ? (long)nb * ((R + RB - 1) / RB) * C : 0;
+}
 CFM_EXPORT long cfm_adafactor_rowmean_tasks(int nb, int R) { return R >= 64 ? (long)nb : ((long)nb + 63) / 64; }
 
 CFM_EXPORT int cfm_adafactor_step(const void* dev_table, int n, long nrow_tasks, long ncols, long nblocks,
-                                  long nrm_tasks, float* rowmean, float* sumsq, float lr, float beta1, float beta2t,
-                                  float eps1, float clip, void* stream) {
-  CFM_REQUIRE(dev_table && rowmean && sumsq && n > 0, CFM_ERR_ARG, "bad args");
+                                  long nrm_tasks, long ncp_tasks, float* rowmean, float* part, float* partial,
+                                  float lr, float beta1, float beta2t, float eps1, float clip, void* stream) {
+  CFM_REQUIRE(dev_table && rowmean && partial && n > 0 && (ncp_tasks == 0 || part), CFM_ERR_ARG, "bad args");
   const AdaP* t = reinterpret_cast<const AdaP*>(dev_table);
   hipStream_t s = cfm::as_stream(stream);
-  (void)hipMemsetAsync(sumsq, 0, sizeof(float) * n, s);
+  if (ncp_tasks > 0)
+    hipLaunchKernelGGL(ada_colpart, dim3((unsigned)ncp_tasks), dim3(EB), 0, s, t, n, ncp_tasks, beta2t, eps1, part);
   if (nrow_tasks > 0)
     hipLaunchKernelGGL(ada_rows, dim3((unsigned)((nrow_tasks + 3) / 4)), dim3(256), 0, s, t, n, nrow_tasks, beta2t,
                        eps1);
   if (ncols > 0)
-    hipLaunchKernelGGL(ada_cols, dim3((unsigned)((ncols + EB - 1) / EB)), dim3(EB), 0, s, t, n, ncols, beta2t, eps1);
+    hipLaunchKernelGGL(ada_cols, dim3((unsigned)((ncols + EB - 1) / EB)), dim3(EB), 0, s, t, n, ncols, beta2t, eps1,
+                       part);
   if (nrm_tasks > 0)
     hipLaunchKernelGGL(ada_rowmean, dim3((unsigned)((nrm_tasks + 3) / 4)), dim3(256), 0, s, t, n, nrm_tasks, rowmean);
-  hipLaunchKernelGGL(ada_sumsq, dim3((unsigned)nblocks), dim3(EB), 0, s, t, n, rowmean, beta2t, eps1, sumsq);
-  hipLaunchKernelGGL(ada_apply, dim3((unsigned)nblocks), dim3(EB), 0, s, t, n, rowmean, beta2t, eps1, sumsq, lr,
+  hipLaunchKernelGGL(ada_sumsq, dim3((unsigned)nblocks), dim3(EB), 0, s, t, n, rowmean, beta2t, eps1, partial);
+  hipLaunchKernelGGL(ada_apply, dim3((unsigned)nblocks), dim3(EB), 0, s, t, n, rowmean, beta2t, eps1, partial, lr,
                      beta1, clip);
   return cfm::check_launch("cfm_adafactor_step");
 }

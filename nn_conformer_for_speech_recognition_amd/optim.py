@@ -82,7 +82,7 @@ class Adafactor(torch.optim.Optimizer):
                     p.grad = p.grad.contiguous()
             n = len(ps)
             host = (ctypes.c_char * L.size_call("cfm_adafactor_table_bytes", n))()
-            row_off = col_off = blk_off = rm_off = rm_toff = 0
+            row_off = col_off = blk_off = rm_off = rm_toff = cp_off = part_off = 0
             steps = []
             for i, p in enumerate(ps):
                 st = self._ensure_state(p, group)
@@ -94,9 +94,11 @@ class Adafactor(torch.optim.Optimizer):
                 col = st["exp_avg_sq_col"] if factored else None
                 L.call("cfm_adafactor_fill_table", ctypes.cast(host, ctypes.c_void_p), i, L.ptr(p), L.ptr(p.grad),
                        L.ptr(m), L.ptr(row), L.ptr(col), p.numel(), nb, R, C, row_off, col_off, blk_off, rm_off,
-                       rm_toff)
+                       rm_toff, cp_off, part_off)
                 if factored:
                     row_off += lib.cfm_adafactor_row_tasks(nb, R, C)
+                    cp_off += lib.cfm_adafactor_colpart_tasks(nb, R, C)
+                    part_off += lib.cfm_adafactor_part_floats(nb, R, C)
                     col_off += nb * C
                     rm_off += nb
                     rm_toff += lib.cfm_adafactor_rowmean_tasks(nb, R)
@@ -117,13 +119,15 @@ class Adafactor(torch.optim.Optimizer):
                 self._tables[tkey] = (raw, table)
             key = (id(group), dev)
             buf = self._dev.get(key)
-            if buf is None or buf[0].numel() < max(rm_off, 1) or buf[1].numel() < n:
-                buf = (torch.empty(max(rm_off, 1), device=dev), torch.empty(n, device=dev))
+            if (buf is None or buf[0].numel() < max(rm_off, 1) or buf[1].numel() < max(part_off, 1)
+                    or buf[2].numel() < blk_off):
+                buf = (torch.empty(max(rm_off, 1), device=dev), torch.empty(max(part_off, 1), device=dev),
+                       torch.empty(max(blk_off, 1), device=dev))
                 self._dev[key] = buf
             b2t = 1.0 - math.pow(step, group["decay_rate"])
             beta1 = group["beta1"] if group["beta1"] is not None else 0.0
-            L.call("cfm_adafactor_step", L.ptr(table), n, row_off, col_off, blk_off, rm_toff, L.ptr(buf[0]),
-                   L.ptr(buf[1]),
+            L.call("cfm_adafactor_step", L.ptr(table), n, row_off, col_off, blk_off, rm_toff, cp_off, L.ptr(buf[0]),
+                   L.ptr(buf[1]), L.ptr(buf[2]),
                    float(self._lr(group, step)), float(beta1), float(b2t), float(group["eps"][0]),
                    float(group["clip_threshold"]), L.stream())
             self._keep = table      # keep the table alive until the stream has consumed it
