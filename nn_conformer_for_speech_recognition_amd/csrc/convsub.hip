@@ -6,7 +6,9 @@
 // second convolution (implicit GEMM in gemm.hip) reads 16-byte channel chunks.
 // Forward: one workgroup per (b, f1, 32-frame tile); the 7 x 69 input patch sits in LDS (all
 // lanes read the same pixel: LDS broadcast), each thread owns up to 2 channels with their 49
-// taps in registers; stores are 1 KiB-coalesced channel rows.
+// taps in registers; stores are 1 KiB-coalesced channel rows.  (VALU-bound: 49 FMAs per output;
+// an MFMA im2col form is the next step.)  The weight-gradient stages the block's [32][C1] dh1 rows
+// (one contiguous run in NHWC) in LDS with 16-byte loads and keeps the 7x7 input window in registers.
 // Weight-gradient: a persistent grid sweeps (b, f1) rows; each thread accumulates 49 tap sums +
 // the bias sum for its channels in registers; per-workgroup partials are reduced by a second
 // kernel (deterministic).
@@ -17,6 +19,9 @@ constexpr int KK = 7, ST = 2, TW = 32;   // kernel, stride, output frames per wo
 constexpr int PW = (TW - 1) * ST + KK;   // 69 input columns per patch
 constexpr int CMAX = 512;                // channels supported (2 per thread)
 
+// the 7x7 input window of output frame tt slides by 2 columns per frame: keep it in registers
+// (fully unrolled frame loop -> the shifts are register renames) so each frame costs 14 LDS
+// broadcast reads for 98 FMAs instead of 49
 template <typename TO>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bias, TO* __restrict__ h1, int F,
@@ -62,6 +67,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const TI* __restrict__
                                                           int B, int F, int T, int C1, int F1, int T1,
                                                           float* __restrict__ ws) {
   __shared__ float patch[KK][PW + 1];
+  __shared__ __attribute__((aligned(16))) TI stage[TW * CMAX];   // the block's [nt][C1] dh1 rows
   const int tid = threadIdx.x;
   float acc[2][KK * KK + 1];
 #pragma unroll
@@ -82,19 +88,44 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const TI* __restrict__
       const int tc = ST * t10 + cc;
       patch[r][cc] = (tc < T) ? xb[(long)(ST * f1 + r) * T + tc] : 0.f;
     }
-    __syncthreads();
     const int nt = min(TW, T1 - t10);
-    for (int tt = 0; tt < nt; ++tt) {
-      const TI* row = dh1 + (((long)b * F1 + f1) * T1 + t10 + tt) * C1;
-      const float g0 = tid < C1 ? to_f32(row[tid]) : 0.f;
-      const float g1 = tid + 256 < C1 ? to_f32(row[tid + 256]) : 0.f;
+    {
+      const TI* src = dh1 + (((long)b * F1 + f1) * T1 + t10) * C1;
+      const long n = (long)nt * C1;
+      constexpr int V = 16 / sizeof(TI);
+      if ((C1 % V) == 0 && ((uintptr_t)src % 16) == 0) {
+        for (long i = (long)tid * V; i < n; i += 256 * V)
+          *reinterpret_cast<uint4*>(stage + i) = *reinterpret_cast<const uint4*>(src + i);
+      } else {
+        for (long i = tid; i < n; i += 256) stage[i] = src[i];
+      }
+    }
+    __syncthreads();
+    float win[KK][KK];
+#pragma unroll
+    for (int r = 0; r < KK; ++r)
+#pragma unroll
+      for (int q = 0; q < KK; ++q) win[r][q] = patch[r][q];
+#pragma unroll
+    for (int tt = 0; tt < TW; ++tt) {
+      if (tt >= nt) break;
+      if (tt > 0) {
+#pragma unroll
+        for (int r = 0; r < KK; ++r) {
+#pragma unroll
+          for (int q = 0; q < KK - ST; ++q) win[r][q] = win[r][q + ST];
+          win[r][KK - 2] = patch[r][ST * tt + KK - 2];
+          win[r][KK - 1] = patch[r][ST * tt + KK - 1];
+        }
+      }
+      const float g0 = 2 * tid < C1 ? to_f32(stage[tt * C1 + 2 * tid]) : 0.f;
+      const float g1 = 2 * tid + 1 < C1 ? to_f32(stage[tt * C1 + 2 * tid + 1]) : 0.f;
 #pragma unroll
       for (int kh = 0; kh < KK; ++kh)
 #pragma unroll
         for (int kw = 0; kw < KK; ++kw) {
-          const float v = patch[kh][ST * tt + kw];
-          acc[0][kh * KK + kw] += g0 * v;
-          acc[1][kh * KK + kw] += g1 * v;
+          acc[0][kh * KK + kw] += g0 * win[kh][kw];
+          acc[1][kh * KK + kw] += g1 * win[kh][kw];
         }
       acc[0][KK * KK] += g0;
       acc[1][KK * KK] += g1;
@@ -103,7 +134,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const TI* __restrict__
   float* out = ws + (long)blockIdx.x * C1 * (KK * KK + 1);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int c = tid + 256 * q;
+    const int c = 2 * tid + q;
     if (c < C1)
 #pragma unroll
       for (int k = 0; k <= KK * KK; ++k) out[(long)c * (KK * KK + 1) + k] = acc[q][k];
@@ -122,7 +153,7 @@ __global__ void conv1_wgrad_reduce(const float* __restrict__ ws, int nblk, int C
   else if (db) db[c] = (float)s;
 }
 
-constexpr int WGRAD_BLOCKS = 1024;
+constexpr int WGRAD_BLOCKS = 512;   // 2 workgroups per CU (174 VGPRs)
 }  // namespace
 
 CFM_EXPORT int cfm_conv1_fwd(const float* x, const float* w1, const float* b1, void* h1, int dtype_h, int B, int F,
