@@ -742,26 +742,28 @@ GemmP plain_params(int M, int N, int K, void* C, long ldc, int dtc) {
 }
 
 // C[z][m][n] = sum_s slab[z*split + s][m][n] + bias[n]   (fp32 C, 4 columns per thread)
-__global__ void splitk_reduce_kernel(const float* __restrict__ slab, int split, int batch, int M, int N,
-                                     float* __restrict__ C, long ldc, long sc, const float* __restrict__ bias) {
-  const long per = (long)M * N;
-  const long n4 = (long)batch * per / 4;
-  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long)gridDim.x * blockDim.x) {
-    const long i = q * 4;
-    const int z = (int)(i / per);
-    const long w = i % per;
-    const int m = (int)(w / N), n = (int)(w % N);
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < split; ++k) {
-      const float4 a = *reinterpret_cast<const float4*>(slab + ((long)z * split + k) * per + w);
-      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
-    }
-    if (bias) {
-      s.x += bias[n]; s.y += bias[n + 1]; s.z += bias[n + 2]; s.w += bias[n + 3];
-    }
-    float* dst = C + (long)z * sc + (long)m * ldc + n;
-    dst[0] = s.x; dst[1] = s.y; dst[2] = s.z; dst[3] = s.w;
+// grid (ceil(M*N/4 / 256), batch): 32-bit index math (M*N < 2^31), the split slabs summed in order
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int split, int M, int N,
+                                                            float* __restrict__ C, long ldc, long sc,
+                                                            const float* __restrict__ bias) {
+  const unsigned per = (unsigned)M * (unsigned)N;
+  const unsigned q = blockIdx.x * 256u + threadIdx.x;
+  if (q * 4u >= per) return;
+  const unsigned w = q * 4u;
+  const int z = blockIdx.y;
+  const unsigned m = w / (unsigned)N, n = w - m * (unsigned)N;
+  const float* src = slab + ((long)z * split) * per + w;
+  float4 s = *reinterpret_cast<const float4*>(src);
+  for (int k = 1; k < split; ++k) {
+    const float4 a = *reinterpret_cast<const float4*>(src + (long)k * per);
+    s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
   }
+  if (bias) {
+    s.x += bias[n]; s.y += bias[n + 1]; s.z += bias[n + 2]; s.w += bias[n + 3];
+  }
+  float* dst = C + (long)z * sc + (long)m * ldc + n;
+  if (((uintptr_t)dst & 15) == 0) *reinterpret_cast<float4*>(dst) = s;
+  else { dst[0] = s.x; dst[1] = s.y; dst[2] = s.z; dst[3] = s.w; }
 }
 
 // kernel-selection switch (cfm_gemm_set_mode) for A/B measurements:
@@ -908,11 +910,10 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   else go(float{});
   if (rc != CFM_OK) return rc;
   if (p.slab) {
-    const long n4 = (long)d->batch * d->M * d->N / 4;
-    long blocks = (n4 + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p.slab, split, d->batch, d->M,
-                       d->N, (float*)d->C, d->ldc, d->stride_c, d->bias);
+    CFM_REQUIRE((long)d->M * d->N < (1L << 31) && d->batch <= 65535, CFM_ERR_SHAPE, "split-K slab too large");
+    const long n4 = (long)d->M * d->N / 4;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n4 + 255) / 256), d->batch), dim3(256), 0, s, p.slab,
+                       split, d->M, d->N, (float*)d->C, d->ldc, d->stride_c, d->bias);
   }
   return cfm::check_launch("cfm_gemm");
 }
