@@ -63,13 +63,14 @@ def bench_attn():
     B, T, H, dk = 32, 373, 8, 64
     qkv = torch.randn(B * T, 3 * H * dk, device=DEV, dtype=torch.bfloat16)
     lens = torch.full((B,), T, dtype=torch.int32, device=DEV)
-    o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk)
     fl = 4.0 * B * H * T * T * dk
-    t = timeit(lambda: ops.attn_fwd(qkv, lens, B, T, H, dk))
-    do = torch.randn_like(o)
-    t2 = timeit(lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk))
-    print(f"attention B={B} T={T} H={H} dk={dk}: fwd {t*1e3:.1f}us {fl/t/1e9:.0f} TF | bwd {t2*1e3:.1f}us "
-          f"{2.5*fl/t2/1e9:.0f} TF")
+    for p in (0.0, 0.1):
+        o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=p, seed=3)
+        t = timeit(lambda: ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=p, seed=3))
+        do = torch.randn_like(o)
+        t2 = timeit(lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=p, seed=3))
+        print(f"attention B={B} T={T} H={H} dk={dk} p={p}: fwd {t*1e3:.1f}us {fl/t/1e9:.0f} TF | bwd "
+              f"{t2*1e3:.1f}us {2.5*fl/t2/1e9:.0f} TF")
 
 
 def bench_ln():

@@ -137,6 +137,8 @@ __device__ void store_transposed(float* stage, const f32x16& a0, const f32x16& a
 // ------------------------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnM p, bf16* __restrict__ o, float* __restrict__ lse) {
   if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];   // [buf][K,V][64][72]  36 KiB
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -203,8 +205,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnM p, bf16* __restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int k0 = kt * TILE + acc_row(r, hh);
-        s0[r] *= dropout_scale(p.drop_p, p.seed, didx(p, b, h, qi, k0));
-        s1[r] *= dropout_scale(p.drop_p, p.seed, didx(p, b, h, qi, k0 + 32));
+        s0[r] *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0));
+        s1[r] *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0 + 32));
       }
     }
     // O^T[d][q] += sum_key V[key][d] P^T[key][q]
@@ -262,6 +264,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
                                                           const float* __restrict__ lse, const float* __restrict__ Dg,
                                                           bf16* __restrict__ dqkv) {
   if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -308,8 +312,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       float p1 = (k0 + 32 < len && qvalid) ? exp2f(s1[r] * c - L2) : 0.f;
       float g0 = d0[r], g1 = d1[r];
       if (p.drop_p > 0.f) {
-        g0 *= dropout_scale(p.drop_p, p.seed, didx(p, b, h, qi, k0));
-        g1 *= dropout_scale(p.drop_p, p.seed, didx(p, b, h, qi, k0 + 32));
+        g0 *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0));
+        g1 *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0 + 32));
       }
       s0[r] = p0 * (g0 - Dq);
       s1[r] = p1 * (g1 - Dq);
@@ -342,6 +346,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnM p, const bf16*
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ Dg, bf16* __restrict__ dqkv) {
   if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE * KS];   // [buf][Q, dO][64][72]
   __shared__ float sLD[2][2][TILE];                                        // [buf][lse2, D][64]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
@@ -415,8 +421,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnM p, const bf16*
       const float pb = kvalid ? exp2f(s1[r] * c - sLD[cur][0][qb]) : 0.f;
       float ma = 1.f, mb = 1.f;
       if (p.drop_p > 0.f) {
-        ma = dropout_scale(p.drop_p, p.seed, didx(p, b, h, qia, kj));
-        mb = dropout_scale(p.drop_p, p.seed, didx(p, b, h, qib, kj));
+        ma = dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qia, kj));
+        mb = dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qib, kj));
       }
       pd0[r] = pa * ma;
       pd1[r] = pb * mb;
@@ -458,6 +464,7 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   CFM_REQUIRE(!pos || (pos_u && pos_v), CFM_ERR_ARG, "rel-pos needs pos_u and pos_v");
   CFM_REQUIRE(dtype == CFM_BF16 || dtype == CFM_F32, CFM_ERR_DTYPE, "dtype");
   CFM_REQUIRE(pos || dtype == CFM_F32 || dk <= DKP, CFM_ERR_UNSUPPORTED, "bf16 head dim must be <= 64");
+  CFM_REQUIRE((double)B * H * T * T < 8589934592.0, CFM_ERR_SHAPE, "attention dropout index space (2^33)");
   hipStream_t s = cfm::as_stream(stream);
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, s);

@@ -132,6 +132,13 @@ __device__ __forceinline__ float dropout_scale(float p, uint64_t seed, uint64_t 
   const uint32_t thr = drop_thr(p);
   return drop_bits(seed, idx) >= thr ? drop_keep_scale(thr) : 0.f;
 }
+// dropout_scale with the per-seed key hoisted (valid for idx < 2^33, where drop_key's high word is 0):
+// bit-identical masks at one mix per element (attention kernels: key = drop_key(seed, 0))
+__device__ __forceinline__ float dropout_keyed(uint32_t thr, float keep, uint32_t key, uint64_t idx) {
+  const uint32_t h = cfm_mix32((uint32_t)(idx >> 1) ^ key);
+  const uint32_t bits = (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
+  return bits >= thr ? keep : 0.f;
+}
 // the same mask for the 8 consecutive elements base .. base+7 (5 hashes instead of 8 x 2)
 __device__ __forceinline__ void dropout_scale8(float p, uint64_t seed, uint64_t base, float (&s)[8]) {
   const uint32_t thr = drop_thr(p);

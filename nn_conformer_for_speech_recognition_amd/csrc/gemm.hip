@@ -825,15 +825,21 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 //   V256S: 256x128 tile, BK 32, 3-stage ring (72 KiB: two workgroups per CU, one's epilogue
 //          overlapping the other's main loop)
 //   V128: 128x128 tile, BK 64, 3-stage ring (96 KiB, 4 waves)
+//   V128S: 128x128 tile, BK 32, 3-stage ring (68 KiB incl. the aliased epilogue staging: two
+//          workgroups of 4 waves per CU) -- narrow outputs (N = 512) fill the chip
 template <bool AK, bool BKM>
 void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
-  const int sel = (g_gemm_mode >> 4) & 3;   // 0 auto, 1 V256, 2 V256S, 3 V128
-  // auto: short reductions (K <= 512: the epilogue is a large share of the tile's time) run two
-  // workgroups per CU so one's epilogue hides under the other's MFMAs; long ones keep BK 64
-  const int v = sel ? sel : (p.k_per_split <= 512 ? 2 : 1);
+  const int sel = (g_gemm_mode >> 4) & 7;   // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k), g128(cdiv(p.N, BN), cdiv(p.M, 128), batch * p.split_k);
+  int v = sel;
+  if (!v) {
+    // auto: short reductions (K <= 512: the epilogue is a large share of the tile's time) run two
+    // 256-row workgroups per CU so one's epilogue hides under the other's MFMAs; long ones keep BK 64
+    v = p.k_per_split <= 512 ? 2 : 1;      // (V128S measured no faster for N = 512 outputs)
+  }
   if (v == 1) hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob);
   else if (v == 2) hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob);
+  else if (v == 4) hipLaunchKernelGGL((gemm_pipe_kernel<128, 32, 3, 2, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob);
   else hipLaunchKernelGGL((gemm_pipe_kernel<128, 64, 3, 1, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob);
 }
 
