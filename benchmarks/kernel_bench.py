@@ -64,12 +64,14 @@ def bench_attn():
     qkv = torch.randn(B * T, 3 * H * dk, device=DEV, dtype=torch.bfloat16)
     lens = torch.full((B,), T, dtype=torch.int32, device=DEV)
     fl = 4.0 * B * H * T * T * dk
-    for p in (0.0, 0.1):
+    from nn_conformer_for_speech_recognition_amd import _lib
+    for mode, p in ((1, 0.0), (0, 0.0), (0, 0.1), (2, 0.0), (4, 0.0), (4, 0.1)):
+        _lib.call("cfm_attn_set_mode", mode)
         o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=p, seed=3)
         t = timeit(lambda: ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=p, seed=3))
         do = torch.randn_like(o)
         t2 = timeit(lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=p, seed=3))
-        print(f"attention B={B} T={T} H={H} dk={dk} p={p}: fwd {t*1e3:.1f}us {fl/t/1e9:.0f} TF | bwd "
+        print(f"attention mode={mode} B={B} T={T} H={H} dk={dk} p={p}: fwd {t*1e3:.1f}us {fl/t/1e9:.0f} TF | bwd "
               f"{t2*1e3:.1f}us {2.5*fl/t2/1e9:.0f} TF")
 
 

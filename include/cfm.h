@@ -192,6 +192,9 @@ int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dtype_a, const float*
  * qkv: (B*T, 3*H*dk) rows [q | k | v]; o: (B*T, H*dk); lse: (B*H*T) fp32 log-sum-exp per query
  * (saved for backward); lengths: (B) int32 valid keys.  pos (rel only): (2T-1, H*dk) projected
  * table; pos_u / pos_v: (H*dk) fp32.  dtype: CFM_BF16 (MFMA) or CFM_F32. */
+/* A/B switch (measurement only): bit 0 forces the tiled attention kernels instead of the
+   whole-head ones (T <= 384: one workgroup per (b, h) with K/V staged once in LDS). */
+int cfm_attn_set_mode(int mode);
 int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
                  const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
                  float drop_p, uint64_t seed, void* stream);

@@ -55,6 +55,7 @@ _SIGS = {
     "cfm_specaug_apply": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p]),
     "cfm_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "cfm_gemm_set_mode": (c_int, [c_int]),
+    "cfm_attn_set_mode": (c_int, [c_int]),
     "cfm_colsum": (c_int, [c_void_p, c_int, c_long, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p]),
     "cfm_layernorm_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                   c_long, c_int, c_float, c_void_p]),

@@ -42,6 +42,7 @@ struct AttnM {
   float scale;
   float drop_p; uint64_t seed;
   bool vec;    // 16-B vector loads legal
+  int dbg;     // timing experiments (cfm_attn_set_mode bits 1-2)
   const uint64_t* salt;   // bound dropout step counter or nullptr
 };
 
@@ -232,6 +233,323 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnM p, bf16* __restrict
   store_transposed(stage, o0, o1, inv, o + (long)b * p.T * p.HD + h * p.dk, p.HD, q0, min(32, p.T - q0), p.dk,
                    lane);
   if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
+}
+
+// ------------------------------------------------------------------------------------ whole-head kernels
+// T <= HEAD_TMAX: ONE workgroup per (b, h) stages the head's whole K and V in LDS once (16-byte
+// loads, eight in flight per thread), then every wave runs its 32-query block over the staged keys
+// with no further barriers.  B*H workgroups (256 at Conformer-L B=32: one per CU) instead of
+// ceil(T/128)*B*H workgroups that each re-stream K/V tile by tile behind a barrier per tile.
+constexpr int HEAD_TMAX = 384;      // 12 waves of 32 queries; K+V images 2 * 384 * 144 B = 108 KiB
+
+// 2^x for softmax arguments <= 0: the bare v_exp_f32 (results below 2^-126 flush to 0)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// stage rows [0, nrows) of two head slices (dk <= 64 columns at base0 / base1, row stride ld) into
+// LDS images [nrows][KS]; rows >= T read as zero
+__device__ __forceinline__ void head_stage(const AttnM& p, const bf16* base0, const bf16* base1, long ld0, long ld1,
+                                           int nrows, bf16* img0, bf16* img1, int tid, int nthreads) {
+  const int nch = nrows * 8;                      // 16-B chunks per image
+  if (p.vec && p.dk == 64) {
+    // rows >= T clamp to row T-1 (finite data; those keys are masked by len <= T)
+    for (int i0 = 0; i0 < 2 * nch; i0 += 8 * nthreads) {
+      uint4 r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = min(i0 + u * nthreads + tid, 2 * nch - 1);
+        const int which = i >= nch, j = i - which * nch;
+        const int row = min(j >> 3, p.T - 1);
+        r[u] = *reinterpret_cast<const uint4*>((which ? base1 + (long)row * ld1 : base0 + (long)row * ld0) + (j & 7) * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * nthreads + tid;
+        if (i < 2 * nch) {
+          const int which = i >= nch, j = i - which * nch;
+          *reinterpret_cast<uint4*>((which ? img1 : img0) + (j >> 3) * KS + (j & 7) * 8) = r[u];
+        }
+      }
+    }
+    return;
+  }
+  for (int i0 = 0; i0 < 2 * nch; i0 += 8 * nthreads) {
+    uint4 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * nthreads + tid;
+      const int which = i >= nch, j = i - which * nch;
+      r[u] = i < 2 * nch ? ld8(which ? base1 : base0, which ? ld1 : ld0, j >> 3, p.T, (j & 7) * 8, p.dk, p.vec)
+                         : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * nthreads + tid;
+      if (i < 2 * nch) {
+        const int which = i >= nch, j = i - which * nch;
+        *reinterpret_cast<uint4*>((which ? img1 : img0) + (j >> 3) * KS + (j & 7) * 8) = r[u];
+      }
+    }
+  }
+}
+
+// forward: grid (B*H), block 64 * ceil(T/32); dynamic LDS head_lds_bytes(T)
+__global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(AttnM p, bf16* __restrict__ o,
+                                                                            float* __restrict__ lse) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int len = p.len[b];
+  const int nkt = (len + TILE - 1) / TILE, Tp = nkt * TILE;
+  bf16* sKall = hsm;
+  bf16* sVall = hsm + (long)Tp * KS;
+  const bf16* kvbase = p.qkv + (long)b * p.T * p.D3;
+  head_stage(p, kvbase + p.HD + h * p.dk, kvbase + 2 * p.HD + h * p.dk, p.D3, p.D3, Tp, sKall, sVall, tid,
+             blockDim.x);
+  const int q0 = wv * 32;
+  bf16x8 qf[4];
+  load_bfrags(p, kvbase + h * p.dk, p.D3, q0 + (lane & 31), p.T, qf, lane);
+  __syncthreads();
+  if (p.dbg & 2) {   // timing experiment: staging only
+    if (tid == 0 && hsm[5] == (bf16)-12345.f) lse[0] = 1.f;
+    return;
+  }
+  f32x16 o0 = (f32x16){0}, o1 = (f32x16){0};
+  float m = -INFINITY, l = 0.f;
+  const float c = p.scale * LOG2E;
+  const int qi = q0 + (lane & 31);
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* sK = sKall + kt * TILE * KS;
+    const bf16* sV = sVall + kt * TILE * KS;
+    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k0 = kt * TILE + acc_row(r, hh);
+      s0[r] = (k0 < len) ? s0[r] * c : -INFINITY;
+      s1[r] = (k0 + 32 < len) ? s1[r] * c : -INFINITY;
+      mloc = fmaxf(mloc, fmaxf(s0[r], s1[r]));
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float mn = fmaxf(m, mloc);
+    const float alpha = fast_exp2(m - mn);
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = fast_exp2(s0[r] - mn);
+      s1[r] = fast_exp2(s1[r] - mn);
+      ls += s0[r] + s1[r];
+    }
+    ls += __shfl_xor(ls, 32, 64);
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      o0[r] *= alpha;
+      o1[r] *= alpha;
+    }
+    if (p.drop_p > 0.f) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k0 = kt * TILE + acc_row(r, hh);
+        s0[r] *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0));
+        s1[r] *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0 + 32));
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 0, lane), pf, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 32, lane), pf, o1, 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();     // every wave is done with K/V: the images become the epilogue staging
+  float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
+  const float inv = 1.f / l;
+  if (p.dbg & 4) {   // timing experiment: no epilogue stores
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t += o0[r] + o1[r];
+    if (t == -1234.5f) lse[0] = t;
+    return;
+  }
+  if (q0 < p.T)
+    store_transposed(stage, o0, o1, inv, o + (long)b * p.T * p.HD + h * p.dk, p.HD, q0, min(32, p.T - q0), p.dk,
+                     lane);
+  if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
+}
+
+// dQ: grid (B*H), block 64 * ceil(T/32); K and V staged whole
+__global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(AttnM p, const bf16* __restrict__ dout,
+                                                                               const float* __restrict__ lse,
+                                                                               const float* __restrict__ Dg,
+                                                                               bf16* __restrict__ dqkv) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int len = p.len[b];
+  const int nkt = (len + TILE - 1) / TILE, Tp = nkt * TILE;
+  bf16* sKall = hsm;
+  bf16* sVall = hsm + (long)Tp * KS;
+  const bf16* kvbase = p.qkv + (long)b * p.T * p.D3;
+  head_stage(p, kvbase + p.HD + h * p.dk, kvbase + 2 * p.HD + h * p.dk, p.D3, p.D3, Tp, sKall, sVall, tid,
+             blockDim.x);
+  const int q0 = wv * 32;
+  const int qi = q0 + (lane & 31);
+  bf16x8 qf[4], gf[4];
+  load_bfrags(p, kvbase + h * p.dk, p.D3, qi, p.T, qf, lane);
+  load_bfrags(p, dout + (long)b * p.T * p.HD + h * p.dk, p.HD, qi, p.T, gf, lane);
+  const bool qvalid = qi < p.T;
+  const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : 0.f;
+  const float Dq = qvalid ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
+  const float c = p.scale * LOG2E;
+  __syncthreads();
+  f32x16 a0 = (f32x16){0}, a1 = (f32x16){0};
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* sK = sKall + kt * TILE * KS;
+    const bf16* sV = sVall + kt * TILE * KS;
+    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0}, d0 = (f32x16){0}, d1 = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
+      d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 0, 16 * s, lane), gf[s], d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32, 16 * s, lane), gf[s], d1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k0 = kt * TILE + acc_row(r, hh);
+      float p0 = (k0 < len && qvalid) ? fast_exp2(s0[r] * c - L2) : 0.f;
+      float p1 = (k0 + 32 < len && qvalid) ? fast_exp2(s1[r] * c - L2) : 0.f;
+      float g0 = d0[r], g1 = d1[r];
+      if (p.drop_p > 0.f) {
+        g0 *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0));
+        g1 *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0 + 32));
+      }
+      s0[r] = p0 * (g0 - Dq);
+      s1[r] = p1 * (g1 - Dq);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 0, lane), pf, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 32, lane), pf, a1, 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();
+  float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
+  if (q0 < p.T)
+    store_transposed(stage, a0, a1, p.scale, dqkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, q0, min(32, p.T - q0),
+                     p.dk, lane);
+}
+
+// dK, dV: grid (B*H), 4 waves (one per SIMD: the kernel keeps ~400 registers live); the head's whole
+// Q and dO (and lse, D) are staged once; wave w handles key blocks w, w+4, ... over all query tiles
+constexpr int DKDV_WAVES = 4;
+__global__ __launch_bounds__(64 * DKDV_WAVES) void attn_bwd_dkdv_head_kernel(AttnM p, const bf16* __restrict__ dout,
+                                                                             const float* __restrict__ lse,
+                                                                             const float* __restrict__ Dg,
+                                                                             bf16* __restrict__ dqkv) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int len = p.len[b];
+  const int nqt = (p.T + TILE - 1) / TILE, Tq = nqt * TILE;
+  bf16* sQall = hsm;
+  bf16* sGall = hsm + (long)Tq * KS;
+  float* sL = reinterpret_cast<float*>(sGall + (long)Tq * KS);      // [Tq] lse * log2(e) (+inf past T)
+  float* sD = sL + Tq;                                              // [Tq] D
+  float* stage = sD + Tq + wv * 32 * 65;
+  const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
+  head_stage(p, qbase, dout + (long)b * p.T * p.HD + h * p.dk, p.D3, p.HD, Tq, sQall, sGall, tid, blockDim.x);
+  for (int i = tid; i < Tq; i += blockDim.x) {
+    sL[i] = i < p.T ? lse[((long)b * p.H + h) * p.T + i] * LOG2E : INFINITY;
+    sD[i] = i < p.T ? Dg[((long)b * p.H + h) * p.T + i] : 0.f;
+  }
+  __syncthreads();
+  const float c = p.scale * LOG2E;
+  const int nkb = (p.T + 31) / 32;
+  bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
+  for (int kb = wv; kb < nkb; kb += DKDV_WAVES) {
+    const int k0w = kb * 32;
+    const int kj = k0w + (lane & 31);
+    const bool kvalid = kj < len;
+    bf16x8 kf[4], vf[4];
+    load_bfrags(p, qbase + p.HD, p.D3, kj, p.T, kf, lane);
+    load_bfrags(p, qbase + 2 * p.HD, p.D3, kj, p.T, vf, lane);
+    f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
+    const int nq = k0w < len ? nqt : 0;      // key blocks past len: zero gradients
+    for (int qt = 0; qt < nq; ++qt) {
+      const bf16* sQ = sQall + qt * TILE * KS;
+      const bf16* sG = sGall + qt * TILE * KS;
+      const float* tL = sL + qt * TILE;
+      const float* tD = sD + qt * TILE;
+      f32x16 s0 = (f32x16){0}, s1 = (f32x16){0}, g0 = (f32x16){0}, g1 = (f32x16){0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQ, 0, 16 * s, lane), kf[s], s0, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQ, 32, 16 * s, lane), kf[s], s1, 0, 0, 0);
+        g0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sG, 0, 16 * s, lane), vf[s], g0, 0, 0, 0);
+        g1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sG, 32, 16 * s, lane), vf[s], g1, 0, 0, 0);
+      }
+      f32x16 pd0, pd1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qa = acc_row(r, hh), qb = 32 + qa;
+        const int qia = qt * TILE + qa, qib = qt * TILE + qb;
+        const float pa = kvalid ? fast_exp2(s0[r] * c - tL[qa]) : 0.f;   // lse = +inf for q >= T
+        const float pb = kvalid ? fast_exp2(s1[r] * c - tL[qb]) : 0.f;
+        float ma = 1.f, mb = 1.f;
+        if (p.drop_p > 0.f) {
+          ma = dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qia, kj));
+          mb = dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qib, kj));
+        }
+        pd0[r] = pa * ma;
+        pd1[r] = pb * mb;
+        s0[r] = pa * (g0[r] * ma - tD[qa]);
+        s1[r] = pb * (g1[r] * mb - tD[qb]);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pf = acc2frag(t == 0 ? pd0 : pd1, s);
+          const bf16x8 sf = acc2frag(t == 0 ? s0 : s1, s);
+          dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s, 0, lane), pf, dv0, 0, 0, 0);
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s, 32, lane), pf, dv1, 0, 0, 0);
+          dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQ, 32 * t + 16 * s, 0, lane), sf, dk0, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQ, 32 * t + 16 * s, 32, lane), sf, dk1, 0, 0, 0);
+        }
+      }
+    }
+    const int nvalid = min(32, p.T - k0w);
+    store_transposed(stage, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
+    store_transposed(stage, dv0, dv1, 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
+  }
+}
+
+size_t dkdv_head_lds_bytes(int T) {
+  const size_t rows = (size_t)cdiv(T, TILE) * TILE;
+  return 2 * rows * KS * sizeof(bf16) + 2 * rows * sizeof(float) + (size_t)DKDV_WAVES * 32 * 65 * sizeof(float);
 }
 
 // ------------------------------------------------------------------------------------ D = rowsum(dO*O)
@@ -454,6 +772,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnM p, const bf16*
 
 bool use_mfma(int dtype, const void* pos, int dk) { return dtype == CFM_BF16 && pos == nullptr && dk <= DKP; }
 
+// whole-head kernels: T <= HEAD_TMAX; cfm_attn_set_mode bit 0 forces the tiled kernels (A/B)
+int g_attn_mode = 0;
+bool use_head(int T) { return T <= HEAD_TMAX && (g_attn_mode & 1) == 0; }
+size_t head_lds_bytes(int T) {
+  const size_t rows = (size_t)cdiv(T, TILE) * TILE;
+  const size_t img = 2 * rows * KS * sizeof(bf16);
+  const size_t stage = (size_t)cdiv(T, 32) * 32 * 65 * sizeof(float);
+  return img > stage ? img : stage;
+}
+
 }  // namespace
 
 CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
@@ -469,7 +797,14 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
-          ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), cfm::g_rng_salt};
+          ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 6,
+          cfm::g_rng_salt};
+  if (use_head(T)) {
+    // LDS sized for the full padded length (lengths are device data; len <= T)
+    hipLaunchKernelGGL(attn_fwd_head_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), head_lds_bytes(T), s, p, (bf16*)o,
+                       lse);
+    return cfm::check_launch("cfm_attn_fwd");
+  }
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (bf16*)o, lse);
   return cfm::check_launch("cfm_attn_fwd");
 }
@@ -492,15 +827,28 @@ CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, co
                                      T, H, dk, dtype, drop_p, seed, ws, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0),
-          cfm::g_rng_salt};
+          g_attn_mode & 6, cfm::g_rng_salt};
   const long nrow = (long)B * H * T;
   (void)nrow;
   CFM_REQUIRE(H * dk <= 1024, CFM_ERR_UNSUPPORTED, "H*dk must be <= 1024");
   hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s,
                      (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse,
-                     ws, (bf16*)dqkv);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse, ws,
-                     (bf16*)dqkv);
+  if (use_head(T))
+    hipLaunchKernelGGL(attn_bwd_dkdv_head_kernel, dim3(B * H), dim3(64 * DKDV_WAVES), dkdv_head_lds_bytes(T), s, p,
+                       (const bf16*)dout, lse, ws, (bf16*)dqkv);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse,
+                       ws, (bf16*)dqkv);
+  if (use_head(T))
+    hipLaunchKernelGGL(attn_bwd_dq_head_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), head_lds_bytes(T), s, p,
+                       (const bf16*)dout, lse, ws, (bf16*)dqkv);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse, ws,
+                       (bf16*)dqkv);
   return cfm::check_launch("cfm_attn_bwd");
+}
+
+CFM_EXPORT int cfm_attn_set_mode(int mode) {
+  g_attn_mode = mode;
+  return CFM_OK;
 }
