@@ -88,10 +88,28 @@ def bench_ln():
           f"{M*D*14/t2/1e6:.0f} GB/s")
 
 
+def bench_conv():
+    B, T, C, K = 32, 373, 512, 31
+    a = torch.randn(B * T, 2 * C, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(C, K, device=DEV) * 0.1
+    bias = torch.randn(C, device=DEV)
+    ws = ops.convmod_ws(B, T, C, K, a.device)
+    t = timeit(lambda: ops.glu_dwconv_fwd(a, w, bias, B, T, C, K, ws))
+    dy = torch.randn(B * T, C, device=DEV)
+    t2 = timeit(lambda: ops.glu_dwconv_bwd(dy, a, w, B, T, C, K, ws, torch.bfloat16))
+    nb = B * T * C
+    print(f"glu_dwconv B={B} T={T} C={C} K={K}: fwd {t*1e3:.1f}us {nb*(4+4)/t/1e6:.0f} GB/s | bwd {t2*1e3:.1f}us "
+          f"{nb*(4+4+4)/t2/1e6:.0f} GB/s")
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
     a = ap.parse_args()
-    for name, fn in (("gemm", bench_gemm), ("attn", bench_attn), ("ln", bench_ln)):
+    for name, fn in (("gemm", bench_gemm), ("attn", bench_attn), ("ln", bench_ln), ("conv", bench_conv)):
         if a.only in (None, name):
             fn()
+
+
+
+

@@ -25,7 +25,7 @@ __device__ __forceinline__ float glu_at(const void* a, int dta, long row, int C,
 
 // grid: (ceil(C/CT), ceil(T/TT), B), block 256 = 4 waves; lane = channel, wave strides time.
 // part: [2][nparts][C] (sum, sumsq) with part index b*gridDim.y + blockIdx.y.
-template <int KT>
+template <int KT, typename TA>
 __global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const void* __restrict__ a, int dta,
                                                              const float* __restrict__ w,
                                                              const float* __restrict__ bias, float* __restrict__ y,
@@ -37,30 +37,76 @@ __global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const void* __restr
   const int t0 = blockIdx.y * TT, b = blockIdx.z;
   const int pad = (K - 1) / 2;
   const int rows = TT + K - 1;
-  for (int r = wv; r < rows; r += 4) {
-    const int t = t0 - pad + r;
-    float v = 0.f;
-    if (c < C && t >= 0 && t < T) v = glu_at(a, dta, (long)b * T + t, C, c);
-    sg[r * CT + lane] = v;
+  if constexpr (KT > 0) {
+    // every load of the wave's rows in flight before the first use (latency, not bandwidth, bound)
+    // unconditional loads at clamped addresses (a select around each load makes hipcc branch and
+    // wait vmcnt(0) per element); out-of-range rows are zeroed after the fact
+    constexpr int NR = (TT + KT - 1 + 3) / 4;
+    const TA* ap = reinterpret_cast<const TA*>(a) + (c < C ? c : C - 1);
+    float xv[NR], gv[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int t = min(max(t0 - pad + wv + 4 * i, 0), T - 1);
+      const long row = (long)b * T + t;
+      xv[i] = to_f32(ap[row * 2 * C]);
+      gv[i] = to_f32(ap[row * 2 * C + C]);
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = wv + 4 * i, t = t0 - pad + r;
+      const bool ok = c < C && t >= 0 && t < T;
+      if (r < rows) sg[r * CT + lane] = ok ? xv[i] * sigmoid_f(gv[i]) : 0.f;
+    }
+  } else {
+    for (int r = wv; r < rows; r += 4) {
+      const int t = t0 - pad + r;
+      float v = 0.f;
+      if (c < C && t >= 0 && t < T) v = glu_at(a, dta, (long)b * T + t, C, c);
+      sg[r * CT + lane] = v;
+    }
   }
   __syncthreads();
   constexpr int KR = KT > 0 ? KT : KMAX;
   float wr[KR];
+  const int cw = c < C ? c : C - 1;
 #pragma unroll
-  for (int k = 0; k < KR; ++k) wr[k] = (c < C && k < K) ? w[c * K + k] : 0.f;
-  const float bb = c < C ? bias[c] : 0.f;
+  for (int k = 0; k < KR; ++k) wr[k] = w[cw * K + (k < K ? k : 0)];
+#pragma unroll
+  for (int k = 0; k < KR; ++k) wr[k] = (c < C && k < K) ? wr[k] : 0.f;
+  const float bb = c < C ? bias[cw] : 0.f;
   float s1 = 0.f, s2 = 0.f;
-  for (int tt = wv; tt < TT; tt += 4) {
-    const int t = t0 + tt;
-    if (t >= T) break;
-    float acc = bb;
+  if constexpr (KT > 0) {
+    // wave w: frames 16w .. 16w+15 with the 16+K-1 GLU values they touch held in registers
+    constexpr int FB = TT / 4, WN = FB + KT - 1;
+    const int tb = wv * FB;
+    float win[WN];
 #pragma unroll
-    for (int k = 0; k < KR; ++k)
-      if (KT > 0 || k < K) acc += wr[k] * sg[(tt + k) * CT + lane];
-    if (c < C) {
-      y[((long)b * T + t) * C + c] = acc;
-      s1 += acc;
-      s2 += acc * acc;
+    for (int j = 0; j < WN; ++j) win[j] = sg[(tb + j) * CT + lane];
+#pragma unroll
+    for (int f = 0; f < FB; ++f) {
+      const int t = t0 + tb + f;
+      float acc = bb;
+#pragma unroll
+      for (int k = 0; k < KT; ++k) acc += wr[k] * win[f + k];
+      if (c < C && t < T) {
+        y[((long)b * T + t) * C + c] = acc;
+        s1 += acc;
+        s2 += acc * acc;
+      }
+    }
+  } else {
+    for (int tt = wv; tt < TT; tt += 4) {
+      const int t = t0 + tt;
+      if (t >= T) break;
+      float acc = bb;
+#pragma unroll
+      for (int k = 0; k < KR; ++k)
+        if (k < K) acc += wr[k] * sg[(tt + k) * CT + lane];
+      if (c < C) {
+        y[((long)b * T + t) * C + c] = acc;
+        s1 += acc;
+        s2 += acc * acc;
+      }
     }
   }
   __syncthreads();
@@ -189,7 +235,7 @@ __global__ void bn_bwd_apply_kernel(const void* __restrict__ dz, int dtdz, const
 
 // backward of y = dwconv(GLU(a)).  grid (ceil(C/CT), ceil(T/TT), B)
 // part: [nparts][K+1][C] per-block partial dw (K taps) and db (tap K).
-template <int KT>
+template <int KT, typename TA>
 __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const float* __restrict__ dy,
                                                              const void* __restrict__ a, int dta,
                                                              const float* __restrict__ w, void* __restrict__ da,
@@ -204,46 +250,119 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const float* __rest
   const int rows = TT + K - 1;
   float* sdy = sm;
   float* sg = sm + rows * CT;
-  for (int r = wv; r < rows; r += 4) {
-    const int t = t0 - pad + r;
-    float vd = 0.f, vg = 0.f;
-    if (c < C && t >= 0 && t < T) {
+  if constexpr (KT > 0) {
+    constexpr int NR = (TT + KT - 1 + 3) / 4;
+    const int cc = c < C ? c : C - 1;
+    const TA* ap = reinterpret_cast<const TA*>(a) + cc;
+    float dv[NR], xv[NR], gv[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int t = min(max(t0 - pad + wv + 4 * i, 0), T - 1);
       const long row = (long)b * T + t;
-      vd = dy[row * C + c];
-      vg = glu_at(a, dta, row, C, c);
+      dv[i] = dy[row * C + cc];
+      xv[i] = to_f32(ap[row * 2 * C]);
+      gv[i] = to_f32(ap[row * 2 * C + C]);
     }
-    sdy[r * CT + lane] = vd;
-    sg[r * CT + lane] = vg;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = wv + 4 * i, t = t0 - pad + r;
+      const bool ok = c < C && t >= 0 && t < T;
+      if (r < rows) {
+        sdy[r * CT + lane] = ok ? dv[i] : 0.f;
+        sg[r * CT + lane] = ok ? xv[i] * sigmoid_f(gv[i]) : 0.f;
+      }
+    }
+  } else {
+    for (int r = wv; r < rows; r += 4) {
+      const int t = t0 - pad + r;
+      float vd = 0.f, vg = 0.f;
+      if (c < C && t >= 0 && t < T) {
+        const long row = (long)b * T + t;
+        vd = dy[row * C + c];
+        vg = glu_at(a, dta, row, C, c);
+      }
+      sdy[r * CT + lane] = vd;
+      sg[r * CT + lane] = vg;
+    }
   }
   __syncthreads();
   constexpr int KR = KT > 0 ? KT : KMAX;
   float wr[KR], dw[KR];
+  const int cw = c < C ? c : C - 1;
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
-    wr[k] = (c < C && k < K) ? w[c * K + k] : 0.f;
+    wr[k] = w[cw * K + (k < K ? k : 0)];
     dw[k] = 0.f;
   }
+#pragma unroll
+  for (int k = 0; k < KR; ++k) wr[k] = (c < C && k < K) ? wr[k] : 0.f;
   float db = 0.f;
-  for (int tt = wv; tt < TT; tt += 4) {
-    const int t = t0 + tt;
-    if (t >= T) break;
-    // y[t] = sum_k w[k] g[t+k-pad]  =>  dg[t] = sum_k w[k] dy[t-k+pad];  sdy[r] = dy[t0-pad+r]
-    float dg = 0.f;
+  // y[t] = sum_k w[k] g[t+k-pad]  =>  dg[t] = sum_k w[k] dy[t-k+pad];  sdy[r] = dy[t0-pad+r]
+  // dw[k] += dy[t] * g[t+k-pad]  (sg[r] = g[t0-pad+r] -> r = tt + k)
+  auto emit = [&](int t, float dg) {
+    const long row = (long)b * T + t;
+    const float x = to_f32(reinterpret_cast<const TA*>(a)[row * 2 * C + c]);
+    const float s = sigmoid_f(to_f32(reinterpret_cast<const TA*>(a)[row * 2 * C + C + c]));
+    st_dyn(da, dtda, row * 2 * C + c, dg * s);
+    st_dyn(da, dtda, row * 2 * C + C + c, dg * x * s * (1.f - s));
+  };
+  if constexpr (KT > 0) {
+    // wave w: frames 16w .. 16w+15; the dy and GLU values they touch (16+K-1 each) in registers
+    constexpr int FB = TT / 4, WN = FB + KT - 1;
+    const int tb = wv * FB;
+    float wd[WN], wg[WN];
 #pragma unroll
-    for (int k = 0; k < KR; ++k)
-      if (KT > 0 || k < K) dg += wr[k] * sdy[(tt - k + 2 * pad) * CT + lane];
-    // dw[k] += dy[t] * g[t+k-pad]  (sg[r] = g[t0-pad+r] -> r = tt + k)
-    const float dyt = sdy[(tt + pad) * CT + lane];
+    for (int j = 0; j < WN; ++j) {
+      wd[j] = sdy[(tb + j) * CT + lane];     // dy rows tb .. tb+WN-1  (frame f, tap k: row tb+f-k+2pad)
+      wg[j] = sg[(tb + j) * CT + lane];      // g rows tb .. tb+WN-1   (frame f, tap k: row tb+f+k)
+    }
+    // the GLU inputs of the wave's frames, loaded unconditionally (clamped) ahead of the math
+    const int cc2 = c < C ? c : C - 1;
+    float xa[FB], ga[FB];
 #pragma unroll
-    for (int k = 0; k < KR; ++k)
-      if (KT > 0 || k < K) dw[k] += dyt * sg[(tt + k) * CT + lane];
-    db += dyt;
-    if (c < C) {
-      const long row = (long)b * T + t;
-      const float x = ld_dyn(a, dta, row * 2 * C + c);
-      const float s = sigmoid_f(ld_dyn(a, dta, row * 2 * C + C + c));
-      st_dyn(da, dtda, row * 2 * C + c, dg * s);
-      st_dyn(da, dtda, row * 2 * C + C + c, dg * x * s * (1.f - s));
+    for (int f = 0; f < FB; ++f) {
+      const long row = (long)b * T + min(t0 + tb + f, T - 1);
+      xa[f] = to_f32(reinterpret_cast<const TA*>(a)[row * 2 * C + cc2]);
+      ga[f] = to_f32(reinterpret_cast<const TA*>(a)[row * 2 * C + C + cc2]);
+    }
+#pragma unroll
+    for (int f = 0; f < FB; ++f) {
+      const int t = t0 + tb + f;
+      float dg = 0.f;
+#pragma unroll
+      for (int k = 0; k < KT; ++k) dg += wr[k] * wd[f - k + 2 * ((KT - 1) / 2)];
+      const float dyt = wd[f + (KT - 1) / 2];
+#pragma unroll
+      for (int k = 0; k < KT; ++k) dw[k] += dyt * wg[f + k];
+      db += dyt;
+      if (c < C && t < T) {
+        const long row = (long)b * T + t;
+        const float sg1 = sigmoid_f(ga[f]);
+        if constexpr (sizeof(TA) == 2) {
+          if (dtda == CFM_BF16) {
+            reinterpret_cast<bf16*>(da)[row * 2 * C + c] = (bf16)(dg * sg1);
+            reinterpret_cast<bf16*>(da)[row * 2 * C + C + c] = (bf16)(dg * xa[f] * sg1 * (1.f - sg1));
+            continue;
+          }
+        }
+        st_dyn(da, dtda, row * 2 * C + c, dg * sg1);
+        st_dyn(da, dtda, row * 2 * C + C + c, dg * xa[f] * sg1 * (1.f - sg1));
+      }
+    }
+  } else {
+    for (int tt = wv; tt < TT; tt += 4) {
+      const int t = t0 + tt;
+      if (t >= T) break;
+      float dg = 0.f;
+#pragma unroll
+      for (int k = 0; k < KR; ++k)
+        if (k < K) dg += wr[k] * sdy[(tt - k + 2 * pad) * CT + lane];
+      const float dyt = sdy[(tt + pad) * CT + lane];
+#pragma unroll
+      for (int k = 0; k < KR; ++k)
+        if (k < K) dw[k] += dyt * sg[(tt + k) * CT + lane];
+      db += dyt;
+      if (c < C) emit(t, dg);
     }
   }
   __syncthreads();
@@ -330,10 +449,13 @@ CFM_EXPORT int cfm_glu_dwconv_fwd(const void* a, int dta, const float* w, const 
   const size_t lds = (size_t)(TT + K - 1) * CT * sizeof(float);
   hipStream_t s = cfm::as_stream(stream);
   switch (K) {
-#define X(k) case k: hipLaunchKernelGGL(glu_dwconv_fwd_kernel<k>, grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws); break;
+#define X(k) case k: if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_fwd_kernel<k, bf16>), grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws); \
+                    else hipLaunchKernelGGL((glu_dwconv_fwd_kernel<k, float>), grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws); break;
     CFM_K_CASES(X)
 #undef X
-    default: hipLaunchKernelGGL(glu_dwconv_fwd_kernel<0>, grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws);
+    default:
+      if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_fwd_kernel<0, bf16>), grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws);
+      else hipLaunchKernelGGL((glu_dwconv_fwd_kernel<0, float>), grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws);
   }
   return cfm::check_launch("cfm_glu_dwconv_fwd");
 }
@@ -411,10 +533,13 @@ CFM_EXPORT int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dta, const
   if (red > lds) lds = red;
   hipStream_t s = cfm::as_stream(stream);
   switch (K) {
-#define X(k) case k: hipLaunchKernelGGL(glu_dwconv_bwd_kernel<k>, grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws); break;
+#define X(k) case k: if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_bwd_kernel<k, bf16>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws); \
+                    else hipLaunchKernelGGL((glu_dwconv_bwd_kernel<k, float>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws); break;
     CFM_K_CASES(X)
 #undef X
-    default: hipLaunchKernelGGL(glu_dwconv_bwd_kernel<0>, grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws);
+    default:
+      if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_bwd_kernel<0, bf16>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws);
+      else hipLaunchKernelGGL((glu_dwconv_bwd_kernel<0, float>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws);
   }
   const long np = conv_nparts(B, T);
   float* sums = ws + np * (long)C * (K + 1);
