@@ -6,7 +6,7 @@ TAG=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
 O=$R/gpurun_out/$TAG; mkdir -p $O
 cd $R
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1 || { echo "pytest failed rc=$?"; tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed rc=$?"; tail -30 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $O/smoke.log; exit 1; }
 timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
