@@ -42,14 +42,16 @@ for name, N, K in shapes:
     pre = torch.empty(M, N, device="cuda", dtype=bf)
     dy = torch.randn(M, N, device="cuda", dtype=bf)
     dx = torch.empty(M, K, device="cuda", dtype=bf)
+    wt = w.t().contiguous()
     fl = 2.0 * M * N * K
     cases = {
         "fwd": (lambda: ops.linear(x, w, b, out=y)) if a.epi == "plain" else
                (lambda: ops.linear(x, w, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=1, out=y)),
         "dgrad": lambda: ops.linear_dgrad(dy, w, out=dx),
+        "dgradT": lambda: ops.linear(dy, wt, out=dx),
         "wgrad": lambda: ops.linear_wgrad(dy, x),
     }
-    ref = {"fwd": lambda: torch.nn.functional.linear(x, w, b.to(bf)), "dgrad": lambda: dy @ w,
+    ref = {"fwd": lambda: torch.nn.functional.linear(x, w, b.to(bf)), "dgrad": lambda: dy @ w, "dgradT": lambda: dy @ w,
            "wgrad": lambda: dy.t() @ x}
     for cname, fn in cases.items():
         row = []

@@ -9,7 +9,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 nlast = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 filt = sys.argv[3] if len(sys.argv) > 3 else ""
 ks = sorted(rows, key=lambda r: int(r["Start_Timestamp"]))
-marks = [int(r["Start_Timestamp"]) for r in ks if "conv1_fwd_kernel" in r["Kernel_Name"]]
+marks = [int(r["Start_Timestamp"]) for r in ks if "conv1_fwd" in r["Kernel_Name"]]
 lo = marks[max(0, len(marks) - 1 - nlast)]
 hi = marks[-1]
 agg = defaultdict(list)

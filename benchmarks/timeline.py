@@ -9,7 +9,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 nlast = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Queue_Id", r.get("Stream_Id", "?")),
               r["Kernel_Name"]) for r in rows))
-marks = [s for s, e, q, n in ks if "conv1_fwd_kernel" in n]
+marks = [s for s, e, q, n in ks if "conv1_fwd" in n]
 for i in range(max(0, len(marks) - 1 - nlast), len(marks) - 1):
     a, b = marks[i], marks[i + 1]
     seg = [(s, e, q, n) for s, e, q, n in ks if a <= s < b]

@@ -72,6 +72,20 @@ typedef struct {
 int cfm_cast_batch(const cfm_cast_task* tasks, int ntasks, long nblocks, int dtype_x, int dtype_y,
                    void* stream);
 
+/* Transposed casts in one launch: dst (cols x rows) = (dy) src (rows x cols)^T, row-major both.
+   Task t owns blocks [blk0, blk0 + ceil(rows/64) * ceil(cols/64)) (64 x 64 tiles).  Used for the
+   per-step K-major bf16 copies W^T of the weight matrices, so the data-gradient GEMMs dX = dY W
+   read both operands K-major (replaces the MN-major B path of those GEMMs; no reference
+   counterpart -- autograd's mm backward, torch/csrc/autograd/FunctionsManual.cpp mm_mat1_backward). */
+typedef struct {
+  const void* src;
+  void* dst;
+  long rows, cols;
+  long blk0;
+} cfm_castT_task;
+int cfm_cast_transpose_batch(const cfm_castT_task* tasks, int ntasks, long nblocks, int dtype_x, int dtype_y,
+                             void* stream);
+
 /* ---------------------------------------------------------------- SpecAugment
  * Replaces ASRNN.SpecAugment / time_warping / frequency_masking / time_masking
  * (lib/standard/asrnn.py:91-192).  The random draws stay on the host (python `random`, the

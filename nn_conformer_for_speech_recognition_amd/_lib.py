@@ -52,6 +52,7 @@ _SIGS = {
     "cfm_wallclock_khz": (c_int, []),
     "cfm_cast": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_void_p]),
     "cfm_cast_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
+    "cfm_cast_transpose_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
     "cfm_specaug_apply": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p]),
     "cfm_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "cfm_gemm_set_mode": (c_int, [c_int]),

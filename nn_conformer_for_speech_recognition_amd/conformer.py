@@ -96,7 +96,7 @@ _REL_PNAMES = ["self_attn.linear_pos.weight", "self_attn.pos_bias_u", "self_attn
 
 class _Cfg:
     __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
-                 "bn_rm", "bn_rv", "bn_mom", "pe", "shadow")
+                 "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t")
 
 
 # the 2-D (and pointwise-conv) weight matrices of _PNAMES: cast to the compute dtype once per step
@@ -108,9 +108,11 @@ _SIDE_STREAMS = {}
 
 class _Side:
     """Weight-gradient work of one layer's backward (wgrad GEMMs + bias column sums) on a second
-    HIP stream, so it overlaps the data-gradient chain on the main stream.  Inputs are fenced with
-    an event and record_stream()'d on the side stream; join() makes the main stream wait for every
-    side launch before the layer's gradients are handed back to autograd."""
+    HIP stream, so it overlaps the data-gradient chain on the main stream.  No record_stream():
+    outputs are allocated on the main stream before the side launches, inputs are kept referenced
+    until join(), and join() makes the main stream wait for every side launch -- so every block the
+    side stream touched is only freed / reused in main-stream order after that wait (also under
+    HIP-graph capture, where cross-stream record_stream bookkeeping is fragile)."""
 
     def __init__(self, device):
         self.main = torch.cuda.current_stream(device)
@@ -118,33 +120,36 @@ class _Side:
         if key not in _SIDE_STREAMS:
             _SIDE_STREAMS[key] = torch.cuda.Stream(device)
         self.side = _SIDE_STREAMS[key]
-        self.out = []
+        self.keep = []
 
     def run(self, fn, *inputs):
         self.side.wait_stream(self.main)
         with torch.cuda.stream(self.side):
             r = fn()
-        for t in inputs:
-            t.record_stream(self.side)
-        self.out.append(r)
+        self.keep.extend(inputs)
         return r
 
     def join(self):
         self.main.wait_stream(self.side)
-        for r in self.out:
-            for t in (r if isinstance(r, tuple) else (r,)):
-                t.record_stream(self.main)
-        self.out = []
+        self.keep = []
 
 
 def _wgrad_bias(side, dy, x):
-    """(dW, db) = (dyᵀ·x, Σ_rows dy) on the side stream."""
-    return side.run(lambda: (ops.linear_wgrad(dy, x), ops.colsum(dy)), dy, x)
+    """(dW, db) = (dyᵀ·x, Σ_rows dy) on the side stream (outputs allocated on the main stream)."""
+    dw = torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=torch.float32)
+    db = torch.empty(dy.shape[1], device=dy.device, dtype=torch.float32)
+    side.run(lambda: (ops.linear_wgrad(dy, x, out=dw), ops.colsum(dy, out=db)), dy, x, dw, db)
+    return dw, db
 
 
 def _w(t, cd):
     """Compute-dtype view of a weight (2-D)."""
     return t if t.dtype == cd else ops.cast(t, cd)
+
+
+def _wt(cfg, i):
+    """K-major (transposed) compute-dtype copy of weight matrix i, if the shadows carry one."""
+    return cfg.shadow_t.get(i) if cfg.shadow_t else None
 
 
 def _ffn_fwd(x, P, o, cfg, seed):
@@ -162,9 +167,9 @@ def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads, side):
     cd = cfg.cd
     g2 = ops.scale_dropout(g, 0.5, cfg.p, seed + 1, 0, out_dtype=cd)
     grads[o + 4], grads[o + 5] = _wgrad_bias(side, g2, h)
-    da = ops.linear_dgrad(g2, w2, pre=pre, act_grad=True, drop_p=cfg.p, seed=seed)
+    da = ops.linear_dgrad(g2, w2, pre=pre, act_grad=True, drop_p=cfg.p, seed=seed, wt=_wt(cfg, o + 4))
     grads[o + 2], grads[o + 3] = _wgrad_bias(side, da, xn)
-    dxn = ops.linear_dgrad(da, w1)
+    dxn = ops.linear_dgrad(da, w1, wt=_wt(cfg, o + 2))
     dx, grads[o], grads[o + 1] = ops.layernorm_bwd(dxn, x, P[o], mu, rs, dres=g)
     return dx
 
@@ -192,14 +197,14 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side):
     B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
     g4 = ops.scale_dropout(g, 1.0, cfg.p, seed + 1, 0, out_dtype=cd)
     grads[10], grads[11] = _wgrad_bias(side, g4, o)
-    do = ops.linear_dgrad(g4, wout)
+    do = ops.linear_dgrad(g4, wout, wt=_wt(cfg, 10))
     dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
     if cfg.rel:
         rgrads[0] = ops.linear_wgrad(_w(dpos, cd), _w(cfg.pe, cd))
         rgrads[1] = dpu.view(H, d // H)
         rgrads[2] = dpv.view(H, d // H)
     grads[8], grads[9] = _wgrad_bias(side, dqkv, xn)
-    dxn = ops.linear_dgrad(dqkv, win)
+    dxn = ops.linear_dgrad(dqkv, win, wt=_wt(cfg, 8))
     dx, grads[6], grads[7] = ops.layernorm_bwd(dxn, x, P[6], mu, rs, dres=g)
     return dx
 
@@ -226,14 +231,14 @@ def _conv_bwd(g, x, sv, P, cfg, seed, grads, side):
     g3 = ops.scale_dropout(g, 1.0, cfg.p, seed, 0, out_dtype=cd)
     dw, grads[21] = _wgrad_bias(side, g3, z)
     grads[20] = dw.view(d, d, 1)
-    dz = ops.linear_dgrad(g3, wp2)
+    dz = ops.linear_dgrad(g3, wp2, wt=_wt(cfg, 20))
     ws = ops.convmod_ws(B, T, d, K, x.device)
     dy, grads[18], grads[19] = ops.bn_silu_bwd(dz, yv, P[18], P[19], bmean, binv, cfg.training, ws)
     da, dwdw, grads[17] = ops.glu_dwconv_bwd(dy, a, wdw, B, T, d, K, ws, cd)
     grads[16] = dwdw.view(d, 1, K)
     dw, grads[15] = _wgrad_bias(side, da, xn)
     grads[14] = dw.view(2 * d, d, 1)
-    dxn = ops.linear_dgrad(da, wp1)
+    dxn = ops.linear_dgrad(da, wp1, wt=_wt(cfg, 14))
     dx, grads[12], grads[13] = ops.layernorm_bwd(dxn, x, P[12], mu, rs, dres=g)
     return dx
 
@@ -246,8 +251,11 @@ class _ConformerLayerFn(torch.autograd.Function):
         P = list(params[:len(_PNAMES)])
         R = params[len(_PNAMES):]
         if cfg.shadow is not None:       # compute-dtype copies refreshed by Conformer (one launch)
-            for i, t in cfg.shadow.items():
+            for i, t in cfg.shadow[0].items():
                 P[i] = t
+            cfg.shadow_t = cfg.shadow[1]
+        else:
+            cfg.shadow_t = None
         s = cfg.seed
         x0 = x
         x1, sv1 = _ffn_fwd(x0, P, 0, cfg, s)
@@ -325,7 +333,8 @@ class ConformerLayer(nn.Module):
 
     def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None, shadow=None):
         """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device; shadow: optional
-        {param index: compute-dtype copy} of this layer's weight matrices (see Conformer)."""
+        ({param index: compute-dtype copy}, {param index: its transposed K-major copy}) of this
+        layer's weight matrices (see Conformer._shadows)."""
         cfg = _Cfg()
         cfg.shadow = shadow
         cfg.B, cfg.T, cfg.d, cfg.H, cfg.ffn, cfg.K = B, T, self.d, self.H, self.ffn, self.K
@@ -384,12 +393,17 @@ class Conformer(nn.Module):
         srcs = [layer.params()[i] for layer in self.conformer_layers for i in _WIDX]
         key = (str(device), tuple(t.data_ptr() for t in srcs))
         if self._shadow is None or self._shadow[0] != key:
+            n = len(_WIDX)
             dsts = [torch.empty(t.shape, device=device, dtype=self.compute_dtype) for t in srcs]
-            per = [dict(zip(_WIDX, dsts[j * len(_WIDX):(j + 1) * len(_WIDX)]))
+            # K-major copies Wᵀ (K, N) for the data-gradient GEMMs (pointwise convs viewed 2-D)
+            srcs2 = [t.detach().view(t.shape[0], -1) for t in srcs]   # detached: no autograd view nodes kept alive
+            dsts_t = [torch.empty(t.shape[1], t.shape[0], device=device, dtype=self.compute_dtype) for t in srcs2]
+            per = [(dict(zip(_WIDX, dsts[j * n:(j + 1) * n])), dict(zip(_WIDX, dsts_t[j * n:(j + 1) * n])))
                    for j in range(len(self.conformer_layers))]
-            self._shadow = (key, ops.CastBatch(srcs, dsts), per)
+            self._shadow = (key, ops.CastBatch(srcs, dsts), ops.CastTBatch(srcs2, dsts_t), per)
         self._shadow[1].refresh()
-        return self._shadow[2]
+        self._shadow[2].refresh()
+        return self._shadow[3]
 
     def forward_tokens(self, x, lens_i32, B, T, seed=None):
         if seed is None:

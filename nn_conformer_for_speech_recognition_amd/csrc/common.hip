@@ -133,6 +133,59 @@ CFM_EXPORT int cfm_cast_batch(const cfm_cast_task* tasks, int ntasks, long nbloc
   return cfm::check_launch("cfm_cast_batch");
 }
 
+namespace {
+// one 64 x 64 tile of one task per block: coalesced fp32 row reads -> LDS -> transposed 16-B stores
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void cast_t_batch_kernel(const cfm_castT_task* __restrict__ tasks, int ntasks) {
+  __shared__ float tile[64][65];
+  int lo = 0, hi = ntasks - 1;
+  const long b = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tasks[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const cfm_castT_task t = tasks[lo];
+  const int tcols = (t.cols + 63) / 64;
+  const int tb = (int)(b - t.blk0), r0 = (tb / tcols) * 64, c0 = (tb % tcols) * 64;
+  const TI* x = reinterpret_cast<const TI*>(t.src);
+  TO* y = reinterpret_cast<TO*>(t.dst);
+  const int tid = threadIdx.x, rr = tid >> 2, cq = (tid & 3) * 16;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int r = r0 + rr, c = c0 + cq + e;
+    tile[rr][cq + e] = (r < t.rows && c < t.cols) ? to_f32(x[(long)r * t.cols + c]) : 0.f;
+  }
+  __syncthreads();
+  // output row = source column c0 + rr, output columns = source rows r0 + cq .. + 16
+  const int orow = c0 + rr;
+  if (orow >= t.cols) return;
+  TO* dst = y + (long)orow * t.rows + r0 + cq;
+  float v0[8], v1[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { v0[e] = tile[cq + e][rr]; v1[e] = tile[cq + 8 + e][rr]; }
+  constexpr int DT = std::is_same<TO, bf16>::value ? CFM_BF16 : CFM_F32;
+  if (r0 + cq + 16 <= t.rows && ((uintptr_t)dst % 16) == 0) {
+    st8_dyn(dst, DT, 0, v0);
+    st8_dyn(dst + 8, DT, 0, v1);
+  } else {
+    for (int e = 0; e < 16 && r0 + cq + e < t.rows; ++e) dst[e] = from_f32<TO>(e < 8 ? v0[e] : v1[e - 8]);
+  }
+}
+}  // namespace
+
+CFM_EXPORT int cfm_cast_transpose_batch(const cfm_castT_task* tasks, int ntasks, long nblocks, int dtx, int dty,
+                                        void* stream) {
+  CFM_REQUIRE(tasks && ntasks > 0 && nblocks > 0 && nblocks < (1L << 31), CFM_ERR_ARG, "bad task table");
+  hipStream_t s = cfm::as_stream(stream);
+  if (dtx == CFM_F32 && dty == CFM_BF16)
+    hipLaunchKernelGGL((cast_t_batch_kernel<float, bf16>), dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks);
+  else if (dtx == CFM_F32 && dty == CFM_F32)
+    hipLaunchKernelGGL((cast_t_batch_kernel<float, float>), dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks);
+  else
+    return cfm::fail(CFM_ERR_DTYPE, "cfm_cast_transpose_batch: f32 -> bf16 / f32 only");
+  return cfm::check_launch("cfm_cast_transpose_batch");
+}
+
 CFM_EXPORT int cfm_scale_dropout(const void* x, int dtx, void* y, int dty, long n, float scale,
                                  float p, uint64_t seed, uint64_t off, void* stream) {
   CFM_REQUIRE(x && y && n >= 0, CFM_ERR_ARG, "bad args");

@@ -54,13 +54,20 @@ def linear(x, w, bias=None, out_dtype=None, act=ACT_NONE, pre=None, drop_p=0.0, 
                 out_scale=out_scale, residual=residual)
 
 
-def linear_dgrad(dy, w, out_dtype=None, pre=None, act_grad=False, drop_p=0.0, seed=0, offset=0, out=None):
+def linear_dgrad(dy, w, out_dtype=None, pre=None, act_grad=False, drop_p=0.0, seed=0, offset=0, out=None,
+                 wt=None):
     """dx = dy·w for dy (M, N), w (N, K); optional silu'/dropout-mask epilogue (backward of the
-    producing GEMM's epilogue)."""
+    producing GEMM's epilogue).  wt: optional (K, N) row-major copy of wᵀ (CastTBatch) -- then both
+    operands are read K-major, the faster GEMM path."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dy.device, dtype=out_dtype or dy.dtype)
+    if wt is not None:
+        if tuple(wt.shape) != (K, N) or not wt.is_contiguous() or wt.dtype != dy.dtype:
+            raise L.CfmError(f"linear_dgrad: wt must be a contiguous ({K}, {N}) {dy.dtype} copy of w^T")
+        return gemm(dy, wt, out, M, K, N, a_kmajor=True, b_kmajor=True, lda=N, ldb=N, act_grad=act_grad, pre=pre,
+                    drop_p=drop_p, seed=seed, offset=offset)
     return gemm(dy, w, out, M, K, N, a_kmajor=True, b_kmajor=False, lda=N, ldb=K, act_grad=act_grad, pre=pre,
                 drop_p=drop_p, seed=seed, offset=offset)
 
@@ -138,6 +145,35 @@ class CastBatch:
 
     def refresh(self):
         L.call("cfm_cast_batch", L.ptr(self.table), self.n, self.nblocks, self.dtx, self.dty, L.stream())
+
+
+class CastTBatch:
+    """One launch that writes transposed compute-dtype copies dst = srcᵀ of a fixed list of 2-D
+    tensors (cfm_cast_transpose_batch): the K-major weight copies of the data-gradient GEMMs."""
+
+    def __init__(self, srcs, dsts):
+        import numpy as np
+        if not srcs or len(srcs) != len(dsts):
+            raise L.CfmError("CastTBatch: need matching non-empty source / destination lists")
+        dtx, dty = {L.dt(t) for t in srcs}, {L.dt(t) for t in dsts}
+        if len(dtx) != 1 or len(dty) != 1:
+            raise L.CfmError("CastTBatch: one source dtype and one destination dtype per batch")
+        self.dtx, self.dty = dtx.pop(), dty.pop()
+        rec = np.zeros((len(srcs), 5), dtype=np.int64)
+        blk = 0
+        for i, (s, d) in enumerate(zip(srcs, dsts)):
+            if s.dim() != 2 or tuple(d.shape) != (s.shape[1], s.shape[0]) or not s.is_contiguous() \
+                    or not d.is_contiguous():
+                raise L.CfmError("CastTBatch: contiguous 2-D source and its transposed-shape destination required")
+            rec[i] = (L.ptr(s), L.ptr(d), s.shape[0], s.shape[1], blk)
+            blk += ((s.shape[0] + 63) // 64) * ((s.shape[1] + 63) // 64)
+        self.nblocks = blk
+        self.table = torch.from_numpy(rec.view(np.uint8).reshape(-1).copy()).to(srcs[0].device)
+        self.n = len(srcs)
+        self._keep = (list(srcs), list(dsts))
+
+    def refresh(self):
+        L.call("cfm_cast_transpose_batch", L.ptr(self.table), self.n, self.nblocks, self.dtx, self.dty, L.stream())
 
 
 def cast_into(x, y):

@@ -120,6 +120,38 @@ def test_gemm_epilogues(dtype):
     assert _rel(dz, zr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("rows,cols", [(2048, 512), (512, 1536), (100, 70), (1, 64)])
+def test_cast_transpose_batch(rows, cols):
+    g = torch.Generator().manual_seed(rows + cols)
+    srcs = [torch.randn(rows, cols, generator=g).to(DEV), torch.randn(cols, rows + 3, generator=g).to(DEV)]
+    dsts = [torch.empty(t.shape[1], t.shape[0], device=DEV, dtype=torch.bfloat16) for t in srcs]
+    ops.CastTBatch(srcs, dsts).refresh()
+    torch.cuda.synchronize()
+    for s_, d_ in zip(srcs, dsts):
+        assert torch.equal(d_, s_.t().to(torch.bfloat16))   # a cast + transpose: bit-exact
+
+
+def test_linear_dgrad_transposed_weight():
+    """dX via the K-major W^T copy equals dX via the MN-major W path (same products, bf16)."""
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 1000, 2048, 512
+    dy = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(DEV)
+    pre = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w16 = W.to(torch.bfloat16)
+    wt = torch.empty(K, N, device=DEV, dtype=torch.bfloat16)
+    ops.CastTBatch([W], [wt]).refresh()
+    a = ops.linear_dgrad(dy, w16, out_dtype=torch.float32)
+    b = ops.linear_dgrad(dy, w16, out_dtype=torch.float32, wt=wt)
+    ref = dy.float() @ w16.float()
+    assert _rel(a, ref) < 1e-5 and _rel(b, ref) < 1e-5
+    a = ops.linear_dgrad(dy[:, :K], w16[:K, :K].contiguous(), pre=pre, act_grad=True, drop_p=0.1, seed=4)
+    b = ops.linear_dgrad(dy[:, :K], w16[:K, :K].contiguous(), pre=pre, act_grad=True, drop_p=0.1, seed=4,
+                         wt=w16[:K, :K].t().contiguous())
+    assert _rel(a.float(), b.float()) < 1e-2
+    assert torch.equal(a == 0, b == 0)   # identical dropout masks
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_wgrad_splitk(dtype):
     g = torch.Generator().manual_seed(9)
@@ -210,3 +242,30 @@ def test_specaug_large_bit_exact():
     random.seed(42)
     y = psa.spec_augment(x.to(DEV), tau, hp, intended=True)
     np.testing.assert_array_equal(y.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("B,F,T", [(2, 80, 201), (1, 9, 7), (3, 16, 100)])
+def test_conv1_mfma_fwd_and_wgrad(B, F, T):
+    """conv1 (1 -> 512 ch, 7x7, stride 2) on the matrix cores (bf16 NHWC output, x as hi+lo bf16):
+    forward within bf16 output rounding of the fp32 conv, weight/bias gradients of a bf16 dh1
+    within 1e-4 of the fp32 reduction of the same dh1."""
+    g = torch.Generator().manual_seed(B * 1000 + T)
+    x = torch.rand(B, F, T, generator=g)
+    w = torch.randn(512, 49, generator=g) * 0.2
+    b = torch.randn(512, generator=g)
+    h1 = ops.conv1_fwd(x.to(DEV), w.to(DEV), b.to(DEV), torch.bfloat16)
+    ref = torch.nn.functional.conv2d(x.unsqueeze(1), w.view(512, 1, 7, 7), b, stride=2)   # (B, 512, F1, T1)
+    ref = ref.permute(0, 2, 3, 1)
+    assert h1.shape == ref.shape
+    assert _rel(h1.float(), ref) < 4e-3
+    w16 = w.to(torch.bfloat16).float()
+    ref16 = torch.nn.functional.conv2d(x.unsqueeze(1), w16.view(512, 1, 7, 7), b, stride=2).permute(0, 2, 3, 1)
+    assert (h1.float().cpu() - ref16).abs().max().item() <= 1e-2 * ref16.abs().max().item()
+    dh1 = torch.randn(ref.shape, generator=g).to(torch.bfloat16)
+    dw, db = ops.conv1_bwd_weight(dh1.to(DEV), x.to(DEV), 512)
+    xr = x.unsqueeze(1).double().requires_grad_()
+    wr = w.view(512, 1, 7, 7).double().requires_grad_()
+    br = b.double().requires_grad_()
+    torch.nn.functional.conv2d(xr, wr, br, stride=2).backward(dh1.double().permute(0, 3, 1, 2))
+    assert _rel(dw, wr.grad.view(512, 49)) < 1e-4
+    assert _rel(db, br.grad) < 1e-5
