@@ -72,14 +72,16 @@ typedef struct {
 int cfm_cast_batch(const cfm_cast_task* tasks, int ntasks, long nblocks, int dtype_x, int dtype_y,
                    void* stream);
 
-/* Transposed casts in one launch: dst (cols x rows) = (dy) src (rows x cols)^T, row-major both.
+/* Transposed casts in one launch: dst (cols x rows) = (dy) src (rows x cols)^T, row-major both,
+   and (when dst_n != NULL) the plain copy dst_n (rows x cols) = (dy) src from the same read.
    Task t owns blocks [blk0, blk0 + ceil(rows/64) * ceil(cols/64)) (64 x 64 tiles).  Used for the
    per-step K-major bf16 copies W^T of the weight matrices, so the data-gradient GEMMs dX = dY W
    read both operands K-major (replaces the MN-major B path of those GEMMs; no reference
    counterpart -- autograd's mm backward, torch/csrc/autograd/FunctionsManual.cpp mm_mat1_backward). */
 typedef struct {
-  const void* src;
-  void* dst;
+  const void* src;   /* fp32 */
+  void* dst;         /* transposed copy */
+  void* dst_n;       /* optional row-major copy (NULL: none) */
   long rows, cols;
   long blk0;
 } cfm_castT_task;

@@ -386,8 +386,8 @@ class Conformer(nn.Module):
         return self._pe_cache[key]
 
     def _shadows(self, device):
-        """Compute-dtype copies of every layer's weight matrices, refreshed by ONE cfm_cast_batch
-        launch per forward (instead of one cast per matrix per layer)."""
+        """Compute-dtype copies of every layer's weight matrices and their transposes, refreshed by
+        ONE cfm_cast_transpose_batch launch per forward (instead of one cast per matrix per layer)."""
         if self.compute_dtype == torch.float32:
             return [None] * len(self.conformer_layers)
         srcs = [layer.params()[i] for layer in self.conformer_layers for i in _WIDX]
@@ -400,10 +400,9 @@ class Conformer(nn.Module):
             dsts_t = [torch.empty(t.shape[1], t.shape[0], device=device, dtype=self.compute_dtype) for t in srcs2]
             per = [(dict(zip(_WIDX, dsts[j * n:(j + 1) * n])), dict(zip(_WIDX, dsts_t[j * n:(j + 1) * n])))
                    for j in range(len(self.conformer_layers))]
-            self._shadow = (key, ops.CastBatch(srcs, dsts), ops.CastTBatch(srcs2, dsts_t), per)
+            self._shadow = (key, ops.CastTBatch(srcs2, dsts_t, dsts), per)   # one launch, one read
         self._shadow[1].refresh()
-        self._shadow[2].refresh()
-        return self._shadow[3]
+        return self._shadow[2]
 
     def forward_tokens(self, x, lens_i32, B, T, seed=None):
         if seed is None:

@@ -547,6 +547,90 @@ __global__ __launch_bounds__(64 * DKDV_WAVES) void attn_bwd_dkdv_head_kernel(Att
   }
 }
 
+// dK, dV, one wave per 32-key block: grid (B*H), block 64 * ceil(T/32) (three waves per SIMD at
+// T = 373); the head's whole Q and dO (and lse, D) are staged once and every wave sweeps 32-query
+// steps over them with no further barriers.  Per step 16 MFMAs (S, dP, dV^T += dO^T P, dK^T +=
+// Q^T dS) on ~150 live registers: P / dS are formed in place in the S / dP accumulators.
+__global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel(AttnM p, const bf16* __restrict__ dout,
+                                                                                 const float* __restrict__ lse,
+                                                                                 const float* __restrict__ Dg,
+                                                                                 bf16* __restrict__ dqkv) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
+  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const int len = p.len[b];
+  const int nq = (p.T + 31) / 32, Tq = nq * 32;
+  bf16* sQall = hsm;
+  bf16* sGall = hsm + (long)Tq * KS;
+  float* sL = reinterpret_cast<float*>(sGall + (long)Tq * KS);      // [Tq] lse * log2(e) (+inf past T)
+  float* sD = sL + Tq;                                              // [Tq] D
+  const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
+  head_stage(p, qbase, dout + (long)b * p.T * p.HD + h * p.dk, p.D3, p.HD, Tq, sQall, sGall, tid, blockDim.x);
+  for (int i = tid; i < Tq; i += blockDim.x) {
+    sL[i] = i < p.T ? lse[((long)b * p.H + h) * p.T + i] * LOG2E : INFINITY;
+    sD[i] = i < p.T ? Dg[((long)b * p.H + h) * p.T + i] : 0.f;
+  }
+  const int k0w = wv * 32;
+  const int kj = k0w + (lane & 31);
+  const bool kvalid = kj < len;
+  bf16x8 kf[4], vf[4];
+  load_bfrags(p, qbase + p.HD, p.D3, kj, p.T, kf, lane);
+  load_bfrags(p, qbase + 2 * p.HD, p.D3, kj, p.T, vf, lane);
+  __syncthreads();
+  const float c = p.scale * LOG2E;
+  f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
+  const int nqs = k0w < len ? nq : 0;      // key blocks past len: zero gradients
+  const uint64_t dbase = (((uint64_t)b * p.H + h) * p.T) * p.T + kj;
+  for (int qt = 0; qt < nqs; ++qt) {
+    const int q0 = qt * 32;
+    f32x16 sa = (f32x16){0}, ga = (f32x16){0};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, q0, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
+      ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sGall, q0, 16 * s4, lane), vf[s4], ga, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the next phase's LDS reads from being hoisted (VGPR cap)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = q0 + acc_row(r, hh);
+      const float pa = kvalid ? fast_exp2(sa[r] * c - sL[q]) : 0.f;   // lse = +inf for q >= T
+      float ma = 1.f;
+      if (p.drop_p > 0.f) ma = dropout_keyed(dthr, dkeep, dkey, dbase + (uint64_t)q * p.T);
+      sa[r] = pa * ma;                       // P (dropped)
+      ga[r] = pa * (ga[r] * ma - sD[q]);     // dS
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = acc2frag(sa, s2);
+      const bf16x8 sf = acc2frag(ga, s2);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 0, lane), pf, dv0, 0, 0, 0);
+      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 32, lane), pf, dv1, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 0, lane), sf, dk0, 0, 0, 0);
+      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 32, lane), sf, dk1, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();     // every wave is done with Q / dO: the images become the epilogue staging
+  float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
+  if (k0w < p.T) {
+    bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
+    const int nvalid = min(32, p.T - k0w);
+    store_transposed(stage, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
+    store_transposed(stage, dv0, dv1, 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
+  }
+}
+
+size_t dkdv_wave_lds_bytes(int T) {
+  const size_t rows = (size_t)cdiv(T, 32) * 32;
+  const size_t img = 2 * rows * KS * sizeof(bf16) + 2 * rows * sizeof(float);
+  const size_t stage = rows * 65 * sizeof(float);
+  return img > stage ? img : stage;
+}
+
 size_t dkdv_head_lds_bytes(int T) {
   const size_t rows = (size_t)cdiv(T, TILE) * TILE;
   return 2 * rows * KS * sizeof(bf16) + 2 * rows * sizeof(float) + (size_t)DKDV_WAVES * 32 * 65 * sizeof(float);
@@ -772,7 +856,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnM p, const bf16*
 
 bool use_mfma(int dtype, const void* pos, int dk) { return dtype == CFM_BF16 && pos == nullptr && dk <= DKP; }
 
-// whole-head kernels: T <= HEAD_TMAX; cfm_attn_set_mode bit 0 forces the tiled kernels (A/B)
+// whole-head kernels: T <= HEAD_TMAX; cfm_attn_set_mode bit 0 forces the tiled kernels, bit 3 selects
+// the wave-per-key-block dK/dV kernel (A/B)
 int g_attn_mode = 0;
 bool use_head(int T) { return T <= HEAD_TMAX && (g_attn_mode & 1) == 0; }
 size_t head_lds_bytes(int T) {
@@ -833,7 +918,10 @@ CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, co
   CFM_REQUIRE(H * dk <= 1024, CFM_ERR_UNSUPPORTED, "H*dk must be <= 1024");
   hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s,
                      (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
-  if (use_head(T))
+  if (use_head(T) && (g_attn_mode & 8) != 0)
+    hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), dkdv_wave_lds_bytes(T), s, p,
+                       (const bf16*)dout, lse, ws, (bf16*)dqkv);
+  else if (use_head(T))
     hipLaunchKernelGGL(attn_bwd_dkdv_head_kernel, dim3(B * H), dim3(64 * DKDV_WAVES), dkdv_head_lds_bytes(T), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);
   else

@@ -134,8 +134,9 @@ CFM_EXPORT int cfm_cast_batch(const cfm_cast_task* tasks, int ntasks, long nbloc
 }
 
 namespace {
-// one 64 x 64 tile of one task per block: coalesced fp32 row reads -> LDS -> transposed 16-B stores
-template <typename TI, typename TO>
+// one 64 x 64 tile of one task per block: float4 row reads (16 lanes per 256-B row) -> optional
+// row-major copy (8-B stores) + LDS -> transposed copy (2 x 16-B stores per thread)
+template <typename TO>
 __global__ __launch_bounds__(256) void cast_t_batch_kernel(const cfm_castT_task* __restrict__ tasks, int ntasks) {
   __shared__ float tile[64][65];
   int lo = 0, hi = ntasks - 1;
@@ -147,23 +148,50 @@ __global__ __launch_bounds__(256) void cast_t_batch_kernel(const cfm_castT_task*
   const cfm_castT_task t = tasks[lo];
   const int tcols = (t.cols + 63) / 64;
   const int tb = (int)(b - t.blk0), r0 = (tb / tcols) * 64, c0 = (tb % tcols) * 64;
-  const TI* x = reinterpret_cast<const TI*>(t.src);
-  TO* y = reinterpret_cast<TO*>(t.dst);
-  const int tid = threadIdx.x, rr = tid >> 2, cq = (tid & 3) * 16;
+  const float* x = reinterpret_cast<const float*>(t.src);
+  TO* yn = reinterpret_cast<TO*>(t.dst_n);
+  const int tid = threadIdx.x;
+  constexpr int DT = std::is_same<TO, bf16>::value ? CFM_BF16 : CFM_F32;
+  {
+    const int c4 = (tid & 15) * 4, c = c0 + c4;
+    const bool vec = (t.cols % 4) == 0 && c + 4 <= t.cols;
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int r = r0 + rr, c = c0 + cq + e;
-    tile[rr][cq + e] = (r < t.rows && c < t.cols) ? to_f32(x[(long)r * t.cols + c]) : 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const int rr = (tid >> 4) + 16 * i, r = r0 + rr;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (r < t.rows) {
+        if (vec) {
+          const float4 q = *reinterpret_cast<const float4*>(x + (long)r * t.cols + c);
+          v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = c + e < t.cols ? x[(long)r * t.cols + c + e] : 0.f;
+        }
+        if (yn) {
+          TO* d = yn + (long)r * t.cols + c;
+          if (vec && DT == CFM_BF16) {
+            bf16x4 w4 = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+            *reinterpret_cast<bf16x4*>(d) = w4;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (c + e < t.cols) d[e] = from_f32<TO>(v[e]);
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tile[rr][c4 + e] = v[e];
+    }
   }
   __syncthreads();
   // output row = source column c0 + rr, output columns = source rows r0 + cq .. + 16
+  const int rr = tid >> 2, cq = (tid & 3) * 16;
   const int orow = c0 + rr;
-  if (orow >= t.cols) return;
-  TO* dst = y + (long)orow * t.rows + r0 + cq;
+  if (orow >= t.cols || r0 + cq >= t.rows) return;
+  TO* dst = reinterpret_cast<TO*>(t.dst) + (long)orow * t.rows + r0 + cq;
   float v0[8], v1[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { v0[e] = tile[cq + e][rr]; v1[e] = tile[cq + 8 + e][rr]; }
-  constexpr int DT = std::is_same<TO, bf16>::value ? CFM_BF16 : CFM_F32;
   if (r0 + cq + 16 <= t.rows && ((uintptr_t)dst % 16) == 0) {
     st8_dyn(dst, DT, 0, v0);
     st8_dyn(dst + 8, DT, 0, v1);
@@ -178,9 +206,9 @@ CFM_EXPORT int cfm_cast_transpose_batch(const cfm_castT_task* tasks, int ntasks,
   CFM_REQUIRE(tasks && ntasks > 0 && nblocks > 0 && nblocks < (1L << 31), CFM_ERR_ARG, "bad task table");
   hipStream_t s = cfm::as_stream(stream);
   if (dtx == CFM_F32 && dty == CFM_BF16)
-    hipLaunchKernelGGL((cast_t_batch_kernel<float, bf16>), dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks);
+    hipLaunchKernelGGL((cast_t_batch_kernel<bf16>), dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks);
   else if (dtx == CFM_F32 && dty == CFM_F32)
-    hipLaunchKernelGGL((cast_t_batch_kernel<float, float>), dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks);
+    hipLaunchKernelGGL((cast_t_batch_kernel<float>), dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks);
   else
     return cfm::fail(CFM_ERR_DTYPE, "cfm_cast_transpose_batch: f32 -> bf16 / f32 only");
   return cfm::check_launch("cfm_cast_transpose_batch");

@@ -452,6 +452,56 @@ __device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2
   }
 }
 
+// Epilogue of one tile held as WM x WN waves of FM x FN 32x32 accumulators (wave band = FM*32
+// rows).  Rows are staged through LDS in chunks of CHB bands (<= 128 rows), then every thread
+// finishes 8 consecutive columns of a row (16-B / 32-B vector stores).  The caller guarantees every
+// wave is done reading the staging LDS (`st`, >= 128 x EP_STRIDE floats).
+template <int FM, int FN, int WM, int WN, int NTt>
+__device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM][FN], float* st, int z, int zs,
+                                                int m0, int n0, int wm, int wn, int lane, int tid) {
+  constexpr int BAND = FM * 32, CHB = (128 / BAND) >= 1 && WM % (128 / BAND) == 0 ? 128 / BAND : 1;
+  constexpr int RC = CHB * BAND;
+  static_assert(WN * FN * 32 == BN, "tile width");
+  if (p.split_k > 1 && !p.slab) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * BAND + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int n = n0 + wn * FN * 32 + j * 32 + (lane & 31);
+          epilogue_store(p, z, zs, m, n, acc[i][j][r]);
+        }
+    return;
+  }
+#pragma unroll
+  for (int hf = 0; hf < WM / CHB; ++hf) {
+    if (wm / CHB == hf) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = (wm % CHB) * BAND + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const int col = wn * FN * 32 + j * 32 + (lane & 31);
+            st[row * EP_STRIDE + col] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int it = 0; it < RC * 16 / NTt; ++it) {
+      const int row = it * (NTt / 16) + (tid >> 4), c8 = (tid & 15) * 8;
+      const float4 lo = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8);
+      const float4 hi = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8 + 4);
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      epilogue_store8(p, z, zs, m0 + RC * hf + row, n0 + c8, v);
+    }
+    if (hf + 1 < WM / CHB) __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- bf16 pipelined kernel
 // The fast path for plain strided bf16 operands.  Staging is LDS-DMA (buffer_load_dwordx4 ... lds:
 // no VGPR round trip, no per-element predicates) into a PS-deep ring of LDS stages: two K tiles
@@ -473,10 +523,10 @@ struct PipeOp {
   unsigned bytes;   // extent of one batch for the range check
 };
 
-// BMt x 128 tile, BKt-deep K steps, NST-stage ring; the f32 epilogue staging aliases the ring
-template <int BMt, int BKt, int NST>
+// BMt x 128 tile, BKt-deep K steps, NST-stage ring, NWV waves; the f32 epilogue staging aliases the ring
+template <int BMt, int BKt, int NST, int NWV>
 struct PipeGeo {
-  static constexpr int NTt = BMt * 2, NW = NTt / 64;
+  static constexpr int NTt = NWV * 64, NW = NWV;
   static constexpr int ABYTES = BMt * BKt * 2, BBYTES = BN * BKt * 2;
   static constexpr int STAGE = ABYTES + BBYTES;
   static constexpr int RING = NST * STAGE, EPI = 128 * EP_STRIDE * 4;
@@ -549,16 +599,21 @@ __device__ __forceinline__ void wait_stages(int younger) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM>
-__global__ __launch_bounds__(BMt * 2) __attribute__((amdgpu_waves_per_eu(OCC * BMt / 128)))
+// NWV waves as WM x WN, each owning FM x FN 32x32 accumulators: (BMt, NWV, WN) = (256, 8, 2) ->
+// 64x64 per wave; (192, 8, 4) -> 96x32 per wave (192-row tiles: 63 x N/128 tiles of the encoder's
+// M = 11,936 fill the 256 CUs in whole rounds); (128, 4, 2) -> 64x64.
+template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2>
+__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(OCC * NWV / 4)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
-  typedef PipeGeo<BMt, BKt, NST> G;
+  typedef PipeGeo<BMt, BKt, NST, NWV> G;
+  constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BN / WN / 32;
+  static_assert(WM * FM * 32 == BMt && WN * FN * 32 == BN, "wave tiling");
   probe_begin(p.probe);
   if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
   static_assert(NST >= 3 && NST <= 4, "ring depth");
   __shared__ __attribute__((aligned(1024))) char lds[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   int tm, tn, zz;
   xcd_tile3(tm, tn, zz);
   const int m0 = tm * BMt, n0 = tn * BN;
@@ -588,11 +643,11 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
       dma16(rb, sb + (i * G::NW + wid) * 1024, offb[i] + kt * stepb);
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x16){0};
 
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s)
@@ -608,31 +663,31 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
     const char* sb = sa + G::ABYTES;
 #pragma unroll
     for (int kk = 0; kk < BKt; kk += 16) {
-      bf16x8 af[2], bfr[2];
+      bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = pipe_frag<AK, BMt, BKt>(sa, wm * 64 + i * 32, kk, lane);
+      for (int i = 0; i < FM; ++i) af[i] = pipe_frag<AK, BMt, BKt>(sa, wm * FM * 32 + i * 32, kk, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = pipe_frag<BKM, BN, BKt>(sb, wn * 64 + j * 32, kk, lane);
+      for (int j = 0; j < FN; ++j) bfr[j] = pipe_frag<BKM, BN, BKt>(sb, wn * FN * 32 + j * 32, kk, lane);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
   if (p.dbg) {       // timing experiment: keep the accumulators live, store nothing
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) t += acc[i][j][r];
     if (t == -1234.5f) reinterpret_cast<float*>(p.C)[tid] = t;
     return;
   }
   __syncthreads();   // every wave done with the ring (no DMA outstanding) -> reuse it for the epilogue
-  tile_epilogue<BMt>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane, tid);
+  tile_epilogue_g<FM, FN, WM, WN, G::NTt>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane, tid);
   probe_end(p.probe);
 }
 
@@ -829,9 +884,19 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 //          workgroups of 4 waves per CU) -- narrow outputs (N = 512) fill the chip
 template <bool AK, bool BKM>
 void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
-  const int sel = (g_gemm_mode >> 4) & 7;   // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S
+  const int sel = (g_gemm_mode >> 4) & 7;   // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S, 5 V192
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k), g128(cdiv(p.N, BN), cdiv(p.M, 128), batch * p.split_k);
   int v = sel;
+  if constexpr (AK) {
+    // auto: outputs <= 512 columns (the encoder's d-wide outputs) take the 192-row tiles: 63 x 4 = 252
+    // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
+    if (v == 5 || (v == 0 && p.N <= 512 && p.split_k == 1 && p.M >= 4096)) {
+      const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
+      hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob);
+      return;
+    }
+  }
+  if (v == 5) v = 0;
   if (!v) {
     // auto: short reductions (K <= 512: the epilogue is a large share of the tile's time) run two
     // 256-row workgroups per CU so one's epilogue hides under the other's MFMAs; long ones keep BK 64

@@ -149,9 +149,10 @@ class CastBatch:
 
 class CastTBatch:
     """One launch that writes transposed compute-dtype copies dst = srcᵀ of a fixed list of 2-D
-    tensors (cfm_cast_transpose_batch): the K-major weight copies of the data-gradient GEMMs."""
+    fp32 tensors (cfm_cast_transpose_batch): the K-major weight copies of the data-gradient GEMMs;
+    with dsts_n also the plain copies dsts_n = src from the same read (the per-step bf16 shadow)."""
 
-    def __init__(self, srcs, dsts):
+    def __init__(self, srcs, dsts, dsts_n=None):
         import numpy as np
         if not srcs or len(srcs) != len(dsts):
             raise L.CfmError("CastTBatch: need matching non-empty source / destination lists")
@@ -159,18 +160,28 @@ class CastTBatch:
         if len(dtx) != 1 or len(dty) != 1:
             raise L.CfmError("CastTBatch: one source dtype and one destination dtype per batch")
         self.dtx, self.dty = dtx.pop(), dty.pop()
-        rec = np.zeros((len(srcs), 5), dtype=np.int64)
+        if self.dtx != L.F32:
+            raise L.CfmError("CastTBatch: fp32 sources only")
+        if dsts_n is not None and (len(dsts_n) != len(srcs) or {L.dt(t) for t in dsts_n} != {self.dty}):
+            raise L.CfmError("CastTBatch: dsts_n must match srcs in count and dsts in dtype")
+        rec = np.zeros((len(srcs), 6), dtype=np.int64)
         blk = 0
         for i, (s, d) in enumerate(zip(srcs, dsts)):
             if s.dim() != 2 or tuple(d.shape) != (s.shape[1], s.shape[0]) or not s.is_contiguous() \
                     or not d.is_contiguous():
                 raise L.CfmError("CastTBatch: contiguous 2-D source and its transposed-shape destination required")
-            rec[i] = (L.ptr(s), L.ptr(d), s.shape[0], s.shape[1], blk)
+            pn = 0
+            if dsts_n is not None:
+                dn = dsts_n[i]
+                if dn.numel() != s.numel() or not dn.is_contiguous():
+                    raise L.CfmError("CastTBatch: contiguous plain destination of the source's size required")
+                pn = L.ptr(dn)
+            rec[i] = (L.ptr(s), L.ptr(d), pn, s.shape[0], s.shape[1], blk)
             blk += ((s.shape[0] + 63) // 64) * ((s.shape[1] + 63) // 64)
         self.nblocks = blk
         self.table = torch.from_numpy(rec.view(np.uint8).reshape(-1).copy()).to(srcs[0].device)
         self.n = len(srcs)
-        self._keep = (list(srcs), list(dsts))
+        self._keep = (list(srcs), list(dsts), list(dsts_n or []))
 
     def refresh(self):
         L.call("cfm_cast_transpose_batch", L.ptr(self.table), self.n, self.nblocks, self.dtx, self.dty, L.stream())

@@ -46,7 +46,7 @@ def gemm_mode():
     _lib.call("cfm_gemm_set_mode", 3)
 
 
-@pytest.mark.parametrize("mode", [1, 18, 34, 50])   # register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128
+@pytest.mark.parametrize("mode", [1, 18, 34, 50, 82])   # register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128 / 192x128 (AK only)
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(1000, 512, 512), (264, 136, 192), (520, 264, 1000), (8, 8, 64)])
 def test_gemm_kernel_variants(gemm_mode, mode, ak, bk, M, N, K):
@@ -68,7 +68,7 @@ def test_gemm_kernel_variants(gemm_mode, mode, ak, bk, M, N, K):
     assert _rel(C.float(), torch.nn.functional.silu(z)) < 1e-2
 
 
-@pytest.mark.parametrize("mode", [1, 18, 34])
+@pytest.mark.parametrize("mode", [1, 18, 34, 82])
 def test_gemm_kernel_variants_splitk_batched(gemm_mode, mode):
     gemm_mode(mode)
     g = torch.Generator().manual_seed(17)
@@ -125,10 +125,17 @@ def test_cast_transpose_batch(rows, cols):
     g = torch.Generator().manual_seed(rows + cols)
     srcs = [torch.randn(rows, cols, generator=g).to(DEV), torch.randn(cols, rows + 3, generator=g).to(DEV)]
     dsts = [torch.empty(t.shape[1], t.shape[0], device=DEV, dtype=torch.bfloat16) for t in srcs]
+    plain = [torch.empty(t.shape, device=DEV, dtype=torch.bfloat16) for t in srcs]
     ops.CastTBatch(srcs, dsts).refresh()
     torch.cuda.synchronize()
     for s_, d_ in zip(srcs, dsts):
         assert torch.equal(d_, s_.t().to(torch.bfloat16))   # a cast + transpose: bit-exact
+    dsts2 = [torch.empty_like(d_) for d_ in dsts]
+    ops.CastTBatch(srcs, dsts2, plain).refresh()
+    torch.cuda.synchronize()
+    for s_, d_, p_ in zip(srcs, dsts2, plain):
+        assert torch.equal(d_, s_.t().to(torch.bfloat16))
+        assert torch.equal(p_, s_.to(torch.bfloat16))
 
 
 def test_linear_dgrad_transposed_weight():
