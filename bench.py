@@ -266,9 +266,14 @@ def main():
             static_loss = fwd_bwd()
         probe.active = False
 
+        host_t = []
+
         def step(i):
+            t_a = time.perf_counter()
             graph.replay()
+            t_b = time.perf_counter()
             post()
+            host_t.append((t_b - t_a, time.perf_counter() - t_b))
             return static_loss
         step(0)                      # one replay outside the timed region
         torch.cuda.synchronize()
@@ -294,6 +299,9 @@ def main():
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = tt.item()
     ms_step = 1000.0 * elapsed / args.steps
+    if graph is not None and os.environ.get("BENCH_HOST_TIMING"):
+        print("host ms per step (replay, post):", [(round(1e3 * a, 2), round(1e3 * b, 2)) for a, b in host_t],
+              file=sys.stderr)
     frames_total = B * T_in * world * args.steps
     value = frames_total / elapsed
 

@@ -233,6 +233,11 @@ int cfm_conv2_fwd(const void* h1, const void* w2r, const float* b2, void* h2, in
 /* grads: dh1 from dh2 (transposed conv), dw2r (=), db2 via cfm_colsum; dw1 (=) and db1 (=). */
 int cfm_conv2_bwd_data(const void* dh2, const void* w2r, void* dh1, int dtype, int B, int F1,
                        int T1, int C1, int C2, void* stream);
+/* The same on the LDS-DMA GEMM pipeline: `ws` (cfm_conv2_bwd_data_ws_bytes) receives the per-parity-
+   class K-major packing of w2r; NULL ws (or fp32) falls back to cfm_conv2_bwd_data. */
+size_t cfm_conv2_bwd_data_ws_bytes(int C1, int C2);
+int cfm_conv2_bwd_data_ws(const void* dh2, const void* w2r, void* dh1, int dtype, int B, int F1,
+                          int T1, int C1, int C2, void* ws, void* stream);
 int cfm_conv2_bwd_weight(const void* dh2, const void* h1, float* dw2r, int dtype, int B, int F1,
                          int T1, int C1, int C2, void* stream);
 size_t cfm_conv1_bwd_ws_bytes(int B, int F, int T, int C1);

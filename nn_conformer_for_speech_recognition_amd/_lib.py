@@ -102,6 +102,9 @@ _SIGS = {
                               c_int, c_void_p]),
     "cfm_conv2_bwd_data": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                    c_void_p]),
+    "cfm_conv2_bwd_data_ws_bytes": (c_size_t, [c_int, c_int]),
+    "cfm_conv2_bwd_data_ws": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_void_p, c_void_p]),
     "cfm_conv2_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_void_p]),
     "cfm_ctc_ws_bytes": (c_size_t, [c_int, c_int, c_int]),

@@ -56,12 +56,14 @@ __device__ __forceinline__ void st_dyn(void* p, int dtype, long idx, float v) {
   else ((float*)p)[idx] = v;
 }
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+// sigmoid via the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division (~10 VALU ops):
+// these run per element in GEMM epilogues.  exp(-x) = inf gives rcp = 0 (silu(-inf side) = -0).
+__device__ __forceinline__ float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
 __device__ __forceinline__ float silu_grad_f(float x) {
-  float s = 1.f / (1.f + __expf(-x));
+  const float s = sigmoid_f(x);
   return s * (1.f + x * (1.f - s));
 }
-__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
 
 // 8 consecutive elements (16-B aligned) of a bf16 or f32 array, as f32
 __device__ __forceinline__ void ld8_dyn(const void* p, int dt, long idx, float (&o)[8]) {

@@ -523,6 +523,15 @@ struct PipeOp {
   unsigned bytes;   // extent of one batch for the range check
 };
 
+// Gathered K-major A operand of the conv2 data-gradient (one stride-2 parity class): GEMM row
+// m = (b, i, j) of the class, k = (tap ti, c2) reads dh2[b, t2 = j - dj[ti], f2 = i - di[ti], c2]
+// (dh2 rows (b, t2, f2) of C2 channels); rows whose (t2, f2) fall outside the map read zero via an
+// out-of-range buffer offset.  Each BKt-deep K tile lies inside one tap (C2 % BKt == 0).
+struct GatherA {
+  int F2, T2, C2, F1c, T1c;
+  int di[4], dj[4];
+};
+
 // BMt x 128 tile, BKt-deep K steps, NST-stage ring, NWV waves; the f32 epilogue staging aliases the ring
 template <int BMt, int BKt, int NST, int NWV>
 struct PipeGeo {
@@ -602,9 +611,9 @@ __device__ __forceinline__ void wait_stages(int younger) {
 // NWV waves as WM x WN, each owning FM x FN 32x32 accumulators: (BMt, NWV, WN) = (256, 8, 2) ->
 // 64x64 per wave; (192, 8, 4) -> 96x32 per wave (192-row tiles: 63 x N/128 tiles of the encoder's
 // M = 11,936 fill the 256 CUs in whole rounds); (128, 4, 2) -> 64x64.
-template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2>
+template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2, bool GA = false>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(OCC * NWV / 4)))
-void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
+void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   typedef PipeGeo<BMt, BKt, NST, NWV> G;
   constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BN / WN / 32;
   static_assert(WM * FM * 32 == BMt && WN * FN * 32 == BN, "wave tiling");
@@ -625,8 +634,26 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
 
   // per-lane source offsets of stage 0; later stages add k0 * (row stride) (MN-major) or k0 * 2
   unsigned offa[G::AI], offb[G::BI];
+  int gi[GA ? G::AI : 1], gj[GA ? G::AI : 1];   // gathered rows: class coordinates (i, j); gi < 0: past M
+  if constexpr (GA) {
+    static_assert(AK, "gathered A is K-major");
+    typedef KmSw<BKt> S;
 #pragma unroll
-  for (int i = 0; i < G::AI; ++i) offa[i] = pipe_src<AK, BMt, BKt>(oa, (i * G::NW + wid) * 64 + lane, m0, kbeg);
+    for (int i = 0; i < G::AI; ++i) {
+      const int lc = (i * G::NW + wid) * 64 + lane;
+      const int r = lc / S::CPR, c = S::slot(r, lc % S::CPR), m = m0 + r;
+      if (m < p.M) {
+        const int j = m % ga.T1c, q = m / ga.T1c, ii = q % ga.F1c, b = q / ga.F1c;
+        gi[i] = ii; gj[i] = j;
+        offa[i] = (unsigned)(((((long)b * ga.T2 + j) * ga.F2 + ii) * ga.C2 + 8 * c) * 2);
+      } else {
+        gi[i] = -1000; gj[i] = -1000; offa[i] = 0;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < G::AI; ++i) offa[i] = pipe_src<AK, BMt, BKt>(oa, (i * G::NW + wid) * 64 + lane, m0, kbeg);
+  }
 #pragma unroll
   for (int i = 0; i < G::BI; ++i) offb[i] = pipe_src<BKM, BN, BKt>(ob, (i * G::NW + wid) * 64 + lane, n0, kbeg);
   const unsigned stepa = AK ? BKt * 2 : (unsigned)(BKt * oa.ld * 2);
@@ -635,9 +662,21 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob) {
   auto issue = [&](int kt) {
     char* sa = lds + (kt % NST) * G::STAGE;
     char* sb = sa + G::ABYTES;
+    if constexpr (GA) {
+      const int k0 = kbeg + kt * BKt, ti = k0 / ga.C2, c20 = k0 - ti * ga.C2;
+      const int di = ga.di[ti], dj = ga.dj[ti];
+      const unsigned back = (unsigned)(((dj * ga.F2 + di) * ga.C2 - c20) * 2);
 #pragma unroll
-    for (int i = 0; i < G::AI; ++i)
-      dma16(ra, sa + (i * G::NW + wid) * 1024, offa[i] + kt * stepa);
+      for (int i = 0; i < G::AI; ++i) {
+        const int f2 = gi[i] - di, t2 = gj[i] - dj;
+        const bool ok = f2 >= 0 && t2 >= 0 && f2 < ga.F2 && t2 < ga.T2;
+        dma16(ra, sa + (i * G::NW + wid) * 1024, ok ? offa[i] - back : 0xFFFFFF00u);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < G::AI; ++i)
+        dma16(ra, sa + (i * G::NW + wid) * 1024, offa[i] + kt * stepa);
+    }
 #pragma unroll
     for (int i = 0; i < G::BI; ++i)
       dma16(rb, sb + (i * G::NW + wid) * 1024, offb[i] + kt * stepb);
@@ -884,7 +923,7 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 //          workgroups of 4 waves per CU) -- narrow outputs (N = 512) fill the chip
 template <bool AK, bool BKM>
 void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
-  const int sel = (g_gemm_mode >> 4) & 7;   // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S, 5 V192
+  const int sel = (g_gemm_mode >> 4) & 7;   // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S, 5 V192, 6 V192S
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k), g128(cdiv(p.N, BN), cdiv(p.M, 128), batch * p.split_k);
   int v = sel;
   if constexpr (AK) {
@@ -892,20 +931,25 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
     // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
     if (v == 5 || (v == 0 && p.N <= 512 && p.split_k == 1 && p.M >= 4096)) {
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
-      hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob);
+      hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob, GatherA{});
+      return;
+    }
+    if (v == 6) {   // 192 x 128 tiles, 4 waves of 96x64, BK 32: two workgroups per CU
+      const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
+      hipLaunchKernelGGL((gemm_pipe_kernel<192, 32, 3, 2, AK, BKM, 4, 2>), g192, dim3(256), 0, s, p, oa, ob, GatherA{});
       return;
     }
   }
-  if (v == 5) v = 0;
+  if (v == 5 || v == 6) v = 0;
   if (!v) {
     // auto: short reductions (K <= 512: the epilogue is a large share of the tile's time) run two
     // 256-row workgroups per CU so one's epilogue hides under the other's MFMAs; long ones keep BK 64
     v = p.k_per_split <= 512 ? 2 : 1;      // (V128S measured no faster for N = 512 outputs)
   }
-  if (v == 1) hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob);
-  else if (v == 2) hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob);
-  else if (v == 4) hipLaunchKernelGGL((gemm_pipe_kernel<128, 32, 3, 2, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob);
-  else hipLaunchKernelGGL((gemm_pipe_kernel<128, 64, 3, 1, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob);
+  if (v == 1) hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob, GatherA{});
+  else if (v == 2) hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob, GatherA{});
+  else if (v == 4) hipLaunchKernelGGL((gemm_pipe_kernel<128, 32, 3, 2, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob, GatherA{});
+  else hipLaunchKernelGGL((gemm_pipe_kernel<128, 64, 3, 1, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob, GatherA{});
 }
 
 int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
@@ -1039,6 +1083,87 @@ CFM_EXPORT int cfm_conv2_bwd_weight(const void* dh2, const void* h1, float* dw2r
                                     Conv2WgradB<float>{(const float*)h1, g}, 1, s);
   if (rc != CFM_OK) return rc;
   return cfm::check_launch("cfm_conv2_bwd_weight");
+}
+
+namespace {
+// Per-class K-major data-gradient weights: wt[koff(class) + c1 * K_class + ti * C2 + c2] =
+// w2r[c2][kh_ti][kw_ti][c1] for the class's taps (classes (pf, pt) in order (0,0) (0,1) (1,0) (1,1):
+// 4, 2, 2, 1 taps -> 9 * C1 * C2 elements in all)
+__global__ __launch_bounds__(256) void conv2_dgrad_pack(const bf16* __restrict__ w2r, bf16* __restrict__ wt, int C1,
+                                                        int C2) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long per = (long)C1 * C2;
+  if (e >= 9 * per) return;
+  // which class / tap of the class does slab e / per belong to
+  const int slab = (int)(e / per);        // 0..8: class (0,0) taps 0-3, (0,1) 4-5, (1,0) 6-7, (1,1) 8
+  const int cls = slab < 4 ? 0 : (slab < 6 ? 1 : (slab < 8 ? 2 : 3));
+  const int first = cls == 0 ? 0 : (cls == 1 ? 4 : (cls == 2 ? 6 : 8));
+  const int ntaps = cls == 0 ? 4 : (cls == 3 ? 1 : 2);
+  const int pf = cls >> 1, pt = cls & 1;
+  const long r = e - (long)first * per;   // offset inside the class block (C1 x ntaps*C2)
+  const int K = ntaps * C2;
+  const int c1 = (int)(r / K), k = (int)(r % K), ti = k / C2, c2 = k % C2;
+  // taps of the class in (kh, kw) order, kh = pf (+2), kw = pt (+2)
+  const int nkw = pt == 0 ? 2 : 1;
+  const int kh = pf + 2 * (ti / nkw), kw = pt + 2 * (ti % nkw);
+  wt[e] = w2r[((long)c2 * 9 + kh * 3 + kw) * C1 + c1];
+}
+}  // namespace
+
+CFM_EXPORT int cfm_conv2_bwd_data(const void* dh2, const void* w2r, void* dh1, int dtype, int B, int F1, int T1,
+                                  int C1, int C2, void* stream);
+
+CFM_EXPORT size_t cfm_conv2_bwd_data_ws_bytes(int C1, int C2) { return (size_t)9 * C1 * C2 * sizeof(bf16); }
+
+// conv2 data-gradient on the LDS-DMA pipeline (bf16): per parity class, A rows gathered straight from
+// dh2 by the DMA (GatherA), B = the class's packed K-major weights (from `ws`, written by
+// conv2_dgrad_pack on the same stream), output rows scattered to the class's dh1 pixels (cmap).
+// Falls back to the register-staged gather kernel when ws is NULL or the shape does not qualify.
+CFM_EXPORT int cfm_conv2_bwd_data_ws(const void* dh2, const void* w2r, void* dh1, int dtype, int B, int F1, int T1,
+                                     int C1, int C2, void* ws, void* stream) {
+  CFM_REQUIRE(dh2 && w2r && dh1, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(C1 % 8 == 0 && C2 % 8 == 0, CFM_ERR_SHAPE, "conv2: C1 and C2 must be multiples of 8");
+  const Conv2Geo g = conv2_geo(B, F1, T1, C1, C2);
+  const long dh2_bytes = (long)B * g.T2 * g.F2 * C2 * 2;
+  const bool fast = ws && dtype == CFM_BF16 && C2 % 32 == 0 && C1 % 8 == 0 && (g_gemm_mode & 2) &&
+                    dh2_bytes < (1L << 31) - 4096 && ((uintptr_t)dh2 % 16) == 0 && ((uintptr_t)dh1 % 16) == 0;
+  if (!fast) return cfm_conv2_bwd_data(dh2, w2r, dh1, dtype, B, F1, T1, C1, C2, stream);
+  hipStream_t s = cfm::as_stream(stream);
+  bf16* wt = (bf16*)ws;
+  const long per = (long)C1 * C2;
+  hipLaunchKernelGGL(conv2_dgrad_pack, dim3((unsigned)cdiv(9 * per, 256)), dim3(256), 0, s, (const bf16*)w2r, wt, C1,
+                     C2);
+  long koff = 0;
+  for (int pf = 0; pf < 2; ++pf)
+    for (int pt = 0; pt < 2; ++pt) {
+      GatherA ga{};
+      ga.F2 = g.F2; ga.T2 = g.T2; ga.C2 = C2;
+      ga.F1c = (F1 - pf + 1) / 2;
+      ga.T1c = (T1 - pt + 1) / 2;
+      int nt = 0;
+      for (int kh = pf; kh < 3; kh += 2)
+        for (int kw = pt; kw < 3; kw += 2) {
+          ga.di[nt] = (kh - pf) / 2;
+          ga.dj[nt] = (kw - pt) / 2;
+          ++nt;
+        }
+      const int K = nt * C2;
+      const bf16* wc = wt + koff;
+      koff += (long)nt * per;
+      if (ga.F1c <= 0 || ga.T1c <= 0) continue;
+      GemmP p = plain_params(B * ga.F1c * ga.T1c, C1, K, dh1, C1, dtype);
+      p.cmap = 1; p.cm_F1c = ga.F1c; p.cm_T1c = ga.T1c; p.cm_pf = pf; p.cm_pt = pt; p.cm_F1 = F1; p.cm_T1 = T1;
+      p.split_k = 1;
+      p.k_per_split = K;
+      p.vec_c = vec_epilogue_ok(p);
+      const PipeOp oa{(const bf16*)dh2, C2, 0, p.M, (unsigned)dh2_bytes};
+      const PipeOp ob{wc, K, 0, C1, (unsigned)(per * nt * 2)};
+      const dim3 grid(cdiv(C1, BN), cdiv(p.M, 256), 1);
+      CFM_REQUIRE(grid.y <= 65535, CFM_ERR_SHAPE, "conv2 dgrad: grid too large");
+      hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, true, true, 8, 2, true>), grid, dim3(512), 0, s, p, oa, ob,
+                         ga);
+    }
+  return cfm::check_launch("cfm_conv2_bwd_data_ws");
 }
 
 CFM_EXPORT int cfm_conv2_bwd_data(const void* dh2, const void* w2r, void* dh1, int dtype, int B, int F1, int T1,

@@ -355,6 +355,11 @@ def conv2_bwd_data(dh2, w2r, F1, T1):
     B, T2, F2, C2 = dh2.shape
     C1 = w2r.shape[1] // 9
     dh1 = torch.empty(B, F1, T1, C1, device=dh2.device, dtype=dh2.dtype)
+    if dh2.dtype == torch.bfloat16:     # LDS-DMA pipeline: gathered dh2 rows, packed K-major weights in ws
+        ws = workspace(L.size_call("cfm_conv2_bwd_data_ws_bytes", C1, C2), dh2.device)
+        L.call("cfm_conv2_bwd_data_ws", L.ptr(dh2), L.ptr(w2r), L.ptr(dh1), L.dt(dh2), B, F1, T1, C1, C2, L.ptr(ws),
+               L.stream())
+        return dh1
     L.call("cfm_conv2_bwd_data", L.ptr(dh2), L.ptr(w2r), L.ptr(dh1), L.dt(dh2), B, F1, T1, C1, C2, L.stream())
     return dh1
 

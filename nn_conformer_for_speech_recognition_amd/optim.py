@@ -36,6 +36,7 @@ class Adafactor(torch.optim.Optimizer):
         self._step = 0
         self._dev = {}
         self._tables = {}
+        self._fast = {}
 
     @staticmethod
     def _geom(p):
@@ -66,10 +67,47 @@ class Adafactor(torch.optim.Optimizer):
             lr = min(min_step, 1.0 / math.sqrt(step))
         return lr
 
+    def _build_table(self, group, ps, dev):
+        """Host-side task table of one group (one ctypes fill per parameter) -> device copy."""
+        lib = L.load()
+        n = len(ps)
+        host = (ctypes.c_char * L.size_call("cfm_adafactor_table_bytes", n))()
+        row_off = col_off = blk_off = rm_off = rm_toff = cp_off = part_off = 0
+        steps = []
+        for i, p in enumerate(ps):
+            st = self._ensure_state(p, group)
+            st["step"] += 1
+            steps.append(st["step"])
+            factored, nb, R, C = self._geom(p)
+            m = st.get("exp_avg")
+            row = st["exp_avg_sq_row"] if factored else st["exp_avg_sq"]
+            col = st["exp_avg_sq_col"] if factored else None
+            L.call("cfm_adafactor_fill_table", ctypes.cast(host, ctypes.c_void_p), i, L.ptr(p), L.ptr(p.grad),
+                   L.ptr(m), L.ptr(row), L.ptr(col), p.numel(), nb, R, C, row_off, col_off, blk_off, rm_off,
+                   rm_toff, cp_off, part_off)
+            if factored:
+                row_off += lib.cfm_adafactor_row_tasks(nb, R, C)
+                cp_off += lib.cfm_adafactor_colpart_tasks(nb, R, C)
+                part_off += lib.cfm_adafactor_part_floats(nb, R, C)
+                col_off += nb * C
+                rm_off += nb
+                rm_toff += lib.cfm_adafactor_rowmean_tasks(nb, R)
+            blk_off += lib.cfm_adafactor_blocks(p.numel())
+        if len(set(steps)) != 1:
+            raise L.CfmError("libcfm Adafactor: all parameters of a group must share the step count")
+        raw = bytes(host)
+        tkey = (id(group), dev)
+        cached = self._tables.get(tkey)
+        if cached is not None and cached[0] == raw:
+            table = cached[1]
+        else:
+            table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev, non_blocking=False)
+            self._tables[tkey] = (raw, table)
+        return table, steps[0], (row_off, col_off, blk_off, rm_off, rm_toff, cp_off, part_off)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        lib = L.load()
         self._step += 1
         for group in self.param_groups:
             ps = [p for p in group["params"] if p.grad is not None]
@@ -81,42 +119,27 @@ class Adafactor(torch.optim.Optimizer):
                 if not p.grad.is_contiguous():
                     p.grad = p.grad.contiguous()
             n = len(ps)
-            host = (ctypes.c_char * L.size_call("cfm_adafactor_table_bytes", n))()
-            row_off = col_off = blk_off = rm_off = rm_toff = cp_off = part_off = 0
-            steps = []
-            for i, p in enumerate(ps):
-                st = self._ensure_state(p, group)
-                st["step"] += 1
-                steps.append(st["step"])
-                factored, nb, R, C = self._geom(p)
-                m = st.get("exp_avg")
-                row = st["exp_avg_sq_row"] if factored else st["exp_avg_sq"]
-                col = st["exp_avg_sq_col"] if factored else None
-                L.call("cfm_adafactor_fill_table", ctypes.cast(host, ctypes.c_void_p), i, L.ptr(p), L.ptr(p.grad),
-                       L.ptr(m), L.ptr(row), L.ptr(col), p.numel(), nb, R, C, row_off, col_off, blk_off, rm_off,
-                       rm_toff, cp_off, part_off)
-                if factored:
-                    row_off += lib.cfm_adafactor_row_tasks(nb, R, C)
-                    cp_off += lib.cfm_adafactor_colpart_tasks(nb, R, C)
-                    part_off += lib.cfm_adafactor_part_floats(nb, R, C)
-                    col_off += nb * C
-                    rm_off += nb
-                    rm_toff += lib.cfm_adafactor_rowmean_tasks(nb, R)
-                blk_off += lib.cfm_adafactor_blocks(p.numel())
-            if len(set(steps)) != 1:
-                raise L.CfmError("libcfm Adafactor: all parameters of a group must share the step count")
-            step = steps[0]
             dev = ps[0].device
-            # the device table only changes when a parameter / gradient / state buffer moves (e.g.
-            # never, once gradients live in a captured graph's pool): reuse it, no per-step H2D copy
-            raw = bytes(host)
-            tkey = (id(group), dev)
-            cached = self._tables.get(tkey)
-            if cached is not None and cached[0] == raw:
-                table = cached[1]
+            # fast path: same parameter / gradient buffers as the cached table (every step of a
+            # training loop whose gradients live in a captured graph's pool, or are re-used in
+            # place): no per-parameter ctypes table build on the host, only the step counters
+            ptrkey = tuple((p.data_ptr(), p.grad.data_ptr()) for p in ps)
+            fast = self._fast.get((id(group), dev))
+            if fast is not None and fast[0] == ptrkey:
+                table, offs = fast[1], fast[2]
+                steps = set()
+                for p in ps:
+                    st = self.state[p]
+                    st["step"] += 1
+                    steps.add(st["step"])
+                if len(steps) != 1:
+                    raise L.CfmError("libcfm Adafactor: all parameters of a group must share the step count")
+                step = steps.pop()
+                row_off, col_off, blk_off, rm_off, rm_toff, cp_off, part_off = offs
             else:
-                table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev, non_blocking=False)
-                self._tables[tkey] = (raw, table)
+                table, step, offs = self._build_table(group, ps, dev)
+                row_off, col_off, blk_off, rm_off, rm_toff, cp_off, part_off = offs
+                self._fast[(id(group), dev)] = (ptrkey, table, offs)
             key = (id(group), dev)
             buf = self._dev.get(key)
             if (buf is None or buf[0].numel() < max(rm_off, 1) or buf[1].numel() < max(part_off, 1)

@@ -46,7 +46,7 @@ def gemm_mode():
     _lib.call("cfm_gemm_set_mode", 3)
 
 
-@pytest.mark.parametrize("mode", [1, 18, 34, 50, 82])   # register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128 / 192x128 (AK only)
+@pytest.mark.parametrize("mode", [1, 18, 34, 50, 82, 98])   # register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128 / 192x128 BK64, BK32 (AK only)
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(1000, 512, 512), (264, 136, 192), (520, 264, 1000), (8, 8, 64)])
 def test_gemm_kernel_variants(gemm_mode, mode, ak, bk, M, N, K):
@@ -276,3 +276,24 @@ def test_conv1_mfma_fwd_and_wgrad(B, F, T):
     torch.nn.functional.conv2d(xr, wr, br, stride=2).backward(dh1.double().permute(0, 3, 1, 2))
     assert _rel(dw, wr.grad.view(512, 49)) < 1e-4
     assert _rel(db, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("B,F1,T1,C1,C2", [(2, 37, 100, 512, 128), (1, 9, 11, 64, 32), (2, 10, 8, 128, 64)])
+def test_conv2_bwd_data_pipeline(gemm_mode, B, F1, T1, C1, C2):
+    """conv2 data-gradient on the LDS-DMA pipeline (gathered dh2 rows, packed per-class weights)
+    against the transposed convolution in fp64, and against the register-staged gather path."""
+    g = torch.Generator().manual_seed(F1 * T1 + C1)
+    F2, T2 = (F1 - 3) // 2 + 1, (T1 - 3) // 2 + 1
+    W = (torch.randn(C2, C1, 3, 3, generator=g) * 0.05).to(torch.bfloat16)
+    dh2 = torch.randn(B, T2, F2, C2, generator=g).to(torch.bfloat16)
+    w2r = W.permute(0, 2, 3, 1).reshape(C2, 9 * C1).contiguous()
+    ref = torch.nn.functional.conv_transpose2d(dh2.double().permute(0, 3, 2, 1), W.double(), stride=2,
+                                               output_padding=(F1 - (2 * F2 + 1), T1 - (2 * T2 + 1)))
+    ref = ref.permute(0, 2, 3, 1)          # (B, F1, T1, C1)
+    fast = ops.conv2_bwd_data(dh2.to(DEV), w2r.to(DEV), F1, T1)
+    gemm_mode(1)                           # no LDS-DMA pipeline: the register-staged gather kernel
+    slow = ops.conv2_bwd_data(dh2.to(DEV), w2r.to(DEV), F1, T1)
+    torch.cuda.synchronize()
+    assert fast.shape == ref.shape
+    assert _rel(fast.float(), ref) < 1e-2
+    assert _rel(fast.float(), slow.float()) < 1e-2
