@@ -523,13 +523,18 @@ struct PipeOp {
   unsigned bytes;   // extent of one batch for the range check
 };
 
-// Gathered K-major A operand of the conv2 data-gradient (one stride-2 parity class): GEMM row
-// m = (b, i, j) of the class, k = (tap ti, c2) reads dh2[b, t2 = j - dj[ti], f2 = i - di[ti], c2]
-// (dh2 rows (b, t2, f2) of C2 channels); rows whose (t2, f2) fall outside the map read zero via an
-// out-of-range buffer offset.  Each BKt-deep K tile lies inside one tap (C2 % BKt == 0).
+// Gathered K-major A operand (implicit-GEMM convolutions): GEMM row m decomposes as
+// j = m % Jn, i = (m / Jn) % In, b = m / (Jn * In); its source row (of Cr channels) for tap ti is
+// b * sB + i * sI + j * sJ + dR[ti], valid iff 0 <= i - di[ti] < Ilim and 0 <= j - dj[ti] < Jlim
+// (invalid rows read zero through an out-of-range buffer offset).  k = (ti, c) with Ck channels per
+// tap, so each BKt-deep K tile lies inside one tap (Ck % BKt == 0).
+//   conv2 forward:        rows (b, t2, f2) of h1 taps: i = t2, j = f2, row = (b F1 + 2 f2 + kh) T1 + 2 t2 + kw
+//   conv2 data-gradient:  rows (b, i, j) of a parity class, source dh2 (b, t2 = j - dj, f2 = i - di)
 struct GatherA {
-  int F2, T2, C2, F1c, T1c;
-  int di[4], dj[4];
+  int Jn, In;
+  long sB;
+  int sI, sJ, Cr, Ck, Ilim, Jlim;
+  int di[9], dj[9], dR[9];
 };
 
 // BMt x 128 tile, BKt-deep K steps, NST-stage ring, NWV waves; the f32 epilogue staging aliases the ring
@@ -643,9 +648,9 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
       const int lc = (i * G::NW + wid) * 64 + lane;
       const int r = lc / S::CPR, c = S::slot(r, lc % S::CPR), m = m0 + r;
       if (m < p.M) {
-        const int j = m % ga.T1c, q = m / ga.T1c, ii = q % ga.F1c, b = q / ga.F1c;
+        const int j = m % ga.Jn, q = m / ga.Jn, ii = q % ga.In, b = q / ga.In;
         gi[i] = ii; gj[i] = j;
-        offa[i] = (unsigned)(((((long)b * ga.T2 + j) * ga.F2 + ii) * ga.C2 + 8 * c) * 2);
+        offa[i] = (unsigned)((((long)b * ga.sB + (long)ii * ga.sI + (long)j * ga.sJ) * ga.Cr + 8 * c) * 2);
       } else {
         gi[i] = -1000; gj[i] = -1000; offa[i] = 0;
       }
@@ -663,14 +668,14 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     char* sa = lds + (kt % NST) * G::STAGE;
     char* sb = sa + G::ABYTES;
     if constexpr (GA) {
-      const int k0 = kbeg + kt * BKt, ti = k0 / ga.C2, c20 = k0 - ti * ga.C2;
+      const int k0 = kbeg + kt * BKt, ti = k0 / ga.Ck, c0 = k0 - ti * ga.Ck;
       const int di = ga.di[ti], dj = ga.dj[ti];
-      const unsigned back = (unsigned)(((dj * ga.F2 + di) * ga.C2 - c20) * 2);
+      const unsigned shift = (unsigned)((ga.dR[ti] * ga.Cr + c0) * 2);   // mod 2^32: negative row shifts wrap
 #pragma unroll
       for (int i = 0; i < G::AI; ++i) {
-        const int f2 = gi[i] - di, t2 = gj[i] - dj;
-        const bool ok = f2 >= 0 && t2 >= 0 && f2 < ga.F2 && t2 < ga.T2;
-        dma16(ra, sa + (i * G::NW + wid) * 1024, ok ? offa[i] - back : 0xFFFFFF00u);
+        const int ii = gi[i] - di, jj = gj[i] - dj;
+        const bool ok = ii >= 0 && jj >= 0 && ii < ga.Ilim && jj < ga.Jlim;
+        dma16(ra, sa + (i * G::NW + wid) * 1024, ok ? offa[i] + shift : 0xFFFFFF00u);
       }
     } else {
 #pragma unroll
@@ -1048,6 +1053,26 @@ CFM_EXPORT int cfm_conv2_fwd(const void* h1, const void* w2r, const float* b2, v
   GemmP p = plain_params(B * g.T2 * g.F2, C2, 9 * C1, h2, C2, dtype_h2);
   p.bias = b2;
   hipStream_t s = cfm::as_stream(stream);
+  const long h1_bytes = (long)B * F1 * T1 * C1 * 2;
+  if (dtype == CFM_BF16 && (g_gemm_mode & 2) && C1 % 64 == 0 && h1_bytes < (1L << 31) - 4096 &&
+      cdiv(p.M, 256) <= 65535) {
+    // LDS-DMA pipeline with h1 rows gathered per tap: rows m = (b, t2, f2), tap (kh, kw) reads h1 row
+    // (b F1 + 2 f2 + kh) T1 + 2 t2 + kw -- every tap in range (no padding)
+    GatherA ga{};
+    ga.Jn = g.F2; ga.In = g.T2;
+    ga.sB = (long)F1 * T1; ga.sI = 2; ga.sJ = 2 * T1; ga.Cr = C1; ga.Ck = C1;
+    ga.Ilim = 0x7FFFFFFF; ga.Jlim = 0x7FFFFFFF;
+    for (int kh = 0; kh < 3; ++kh)
+      for (int kw = 0; kw < 3; ++kw) ga.dR[kh * 3 + kw] = kh * T1 + kw;
+    p.split_k = 1;
+    p.k_per_split = 9 * C1;
+    p.vec_c = vec_epilogue_ok(p);
+    const PipeOp oa{(const bf16*)h1, C1, 0, p.M, (unsigned)h1_bytes};
+    const PipeOp ob{(const bf16*)w2r, 9L * C1, 0, C2, (unsigned)((long)C2 * 9 * C1 * 2)};
+    hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, true, true, 8, 2, true>), dim3(cdiv(C2, BN), cdiv(p.M, 256), 1),
+                       dim3(512), 0, s, p, oa, ob, ga);
+    return cfm::check_launch("cfm_conv2_fwd");
+  }
   int rc;
   if (dtype == CFM_BF16)
     rc = launch_typed<true, true>(dtype, p, Conv2FwdA<bf16>{(const bf16*)h1, g},
@@ -1137,22 +1162,24 @@ CFM_EXPORT int cfm_conv2_bwd_data_ws(const void* dh2, const void* w2r, void* dh1
   for (int pf = 0; pf < 2; ++pf)
     for (int pt = 0; pt < 2; ++pt) {
       GatherA ga{};
-      ga.F2 = g.F2; ga.T2 = g.T2; ga.C2 = C2;
-      ga.F1c = (F1 - pf + 1) / 2;
-      ga.T1c = (T1 - pt + 1) / 2;
+      const int F1c = (F1 - pf + 1) / 2, T1c = (T1 - pt + 1) / 2;
+      // rows (b, i, j) of the class; source dh2 rows (b, t2, f2) = b T2 F2 + t2 F2 + f2 with f2 = i - di, t2 = j - dj
+      ga.Jn = T1c; ga.In = F1c;
+      ga.sB = (long)g.T2 * g.F2; ga.sI = 1; ga.sJ = g.F2; ga.Cr = C2; ga.Ck = C2; ga.Ilim = g.F2; ga.Jlim = g.T2;
       int nt = 0;
       for (int kh = pf; kh < 3; kh += 2)
         for (int kw = pt; kw < 3; kw += 2) {
           ga.di[nt] = (kh - pf) / 2;
           ga.dj[nt] = (kw - pt) / 2;
+          ga.dR[nt] = -(ga.dj[nt] * g.F2 + ga.di[nt]);
           ++nt;
         }
       const int K = nt * C2;
       const bf16* wc = wt + koff;
       koff += (long)nt * per;
-      if (ga.F1c <= 0 || ga.T1c <= 0) continue;
-      GemmP p = plain_params(B * ga.F1c * ga.T1c, C1, K, dh1, C1, dtype);
-      p.cmap = 1; p.cm_F1c = ga.F1c; p.cm_T1c = ga.T1c; p.cm_pf = pf; p.cm_pt = pt; p.cm_F1 = F1; p.cm_T1 = T1;
+      if (F1c <= 0 || T1c <= 0) continue;
+      GemmP p = plain_params(B * F1c * T1c, C1, K, dh1, C1, dtype);
+      p.cmap = 1; p.cm_F1c = F1c; p.cm_T1c = T1c; p.cm_pf = pf; p.cm_pt = pt; p.cm_F1 = F1; p.cm_T1 = T1;
       p.split_k = 1;
       p.k_per_split = K;
       p.vec_c = vec_epilogue_ok(p);

@@ -297,3 +297,23 @@ def test_conv2_bwd_data_pipeline(gemm_mode, B, F1, T1, C1, C2):
     assert fast.shape == ref.shape
     assert _rel(fast.float(), ref) < 1e-2
     assert _rel(fast.float(), slow.float()) < 1e-2
+
+
+@pytest.mark.parametrize("B,F1,T1,C1,C2", [(2, 37, 100, 512, 128), (1, 9, 11, 64, 32), (2, 10, 8, 128, 64)])
+def test_conv2_fwd_pipeline(gemm_mode, B, F1, T1, C1, C2):
+    """conv2 forward (3x3, stride 2) as the LDS-DMA implicit GEMM with h1 rows gathered per tap,
+    against conv2d in fp64 and against the register-staged implicit GEMM."""
+    g = torch.Generator().manual_seed(F1 + T1 * C2)
+    W = (torch.randn(C2, C1, 3, 3, generator=g) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(C2, generator=g)
+    h1 = torch.randn(B, F1, T1, C1, generator=g).to(torch.bfloat16)
+    w2r = W.permute(0, 2, 3, 1).reshape(C2, 9 * C1).contiguous()
+    ref = torch.nn.functional.conv2d(h1.double().permute(0, 3, 1, 2), W.double(), bias.double(), stride=2)
+    ref = ref.permute(0, 3, 2, 1)         # (B, T2, F2, C2)
+    fast = ops.conv2_fwd(h1.to(DEV), w2r.to(DEV), bias.to(DEV), torch.float32)
+    gemm_mode(1)
+    slow = ops.conv2_fwd(h1.to(DEV), w2r.to(DEV), bias.to(DEV), torch.float32)
+    torch.cuda.synchronize()
+    assert fast.shape == ref.shape
+    assert _rel(fast, ref) < 1e-5
+    assert _rel(fast, slow) < 1e-5
