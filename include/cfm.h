@@ -142,6 +142,10 @@ int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 int cfm_gemm_set_mode(int mode);
 
 /* out[n] (+)= sum_m x[m*ld + n]  — bias gradients (sum over tokens).  ws: >= 4*N*256 bytes. */
+/* out[n] (+)= sum_p part[p * ldp + n] for n < N: the deterministic second level of every partial-row
+   reduction (LayerNorm dgamma|dbeta partials left by cfm_layernorm_bwd with NULL dgamma/dbeta, so the
+   weight-gradient reduction can run on another stream). */
+int cfm_colreduce(const float* part, int nparts, long N, long ldp, float* out, int accumulate, void* stream);
 int cfm_colsum(const void* x, int dtype_x, long M, int N, long ld, float* out, int accumulate,
                float* ws, void* stream);
 
@@ -200,6 +204,9 @@ int cfm_bn_bwd(const void* dz, int dtype_dz, const float* y, const float* gamma,
 int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dtype_a, const float* w_dw, void* da,
                        int dtype_da, float* dw, float* db, int B, int T, int C, int K, float* ws,
                        void* stream);
+/* With dw == NULL, cfm_glu_dwconv_bwd leaves the depthwise weight/bias partial sums in ws; this
+   reduces them (deterministically) into dw (C x K) and db (C) -- on any stream ordered after it. */
+int cfm_glu_dwconv_bwd_wgrad(float* ws, int B, int T, int C, int K, float* dw, float* db, void* stream);
 
 /* ---------------------------------------------------------------- Attention
  * nn.MultiheadAttention(need_weights=False, key_padding_mask) core (torchaudio ConformerLayer

@@ -57,6 +57,7 @@ _SIGS = {
     "cfm_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "cfm_gemm_set_mode": (c_int, [c_int]),
     "cfm_attn_set_mode": (c_int, [c_int]),
+    "cfm_colreduce": (c_int, [c_void_p, c_int, c_long, c_long, c_void_p, c_int, c_void_p]),
     "cfm_colsum": (c_int, [c_void_p, c_int, c_long, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p]),
     "cfm_layernorm_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                   c_long, c_int, c_float, c_void_p]),
@@ -89,6 +90,7 @@ _SIGS = {
                            c_void_p, c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_void_p]),
     "cfm_bn_bwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                            c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p]),
+    "cfm_glu_dwconv_bwd_wgrad": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "cfm_glu_dwconv_bwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                    c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "cfm_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,

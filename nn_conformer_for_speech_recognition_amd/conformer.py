@@ -170,7 +170,7 @@ def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads, side):
     da = ops.linear_dgrad(g2, w2, pre=pre, act_grad=True, drop_p=cfg.p, seed=seed, wt=_wt(cfg, o + 4))
     grads[o + 2], grads[o + 3] = _wgrad_bias(side, da, xn)
     dxn = ops.linear_dgrad(da, w1, wt=_wt(cfg, o + 2))
-    dx, grads[o], grads[o + 1] = ops.layernorm_bwd(dxn, x, P[o], mu, rs, dres=g)
+    dx, grads[o], grads[o + 1] = ops.layernorm_bwd(dxn, x, P[o], mu, rs, dres=g, side=side)
     return dx
 
 
@@ -205,7 +205,7 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side):
         rgrads[2] = dpv.view(H, d // H)
     grads[8], grads[9] = _wgrad_bias(side, dqkv, xn)
     dxn = ops.linear_dgrad(dqkv, win, wt=_wt(cfg, 8))
-    dx, grads[6], grads[7] = ops.layernorm_bwd(dxn, x, P[6], mu, rs, dres=g)
+    dx, grads[6], grads[7] = ops.layernorm_bwd(dxn, x, P[6], mu, rs, dres=g, side=side)
     return dx
 
 
@@ -234,12 +234,12 @@ def _conv_bwd(g, x, sv, P, cfg, seed, grads, side):
     dz = ops.linear_dgrad(g3, wp2, wt=_wt(cfg, 20))
     ws = ops.convmod_ws(B, T, d, K, x.device)
     dy, grads[18], grads[19] = ops.bn_silu_bwd(dz, yv, P[18], P[19], bmean, binv, cfg.training, ws)
-    da, dwdw, grads[17] = ops.glu_dwconv_bwd(dy, a, wdw, B, T, d, K, ws, cd)
+    da, dwdw, grads[17] = ops.glu_dwconv_bwd(dy, a, wdw, B, T, d, K, ws, cd, side=side)
     grads[16] = dwdw.view(d, 1, K)
     dw, grads[15] = _wgrad_bias(side, da, xn)
     grads[14] = dw.view(2 * d, d, 1)
     dxn = ops.linear_dgrad(da, wp1, wt=_wt(cfg, 14))
-    dx, grads[12], grads[13] = ops.layernorm_bwd(dxn, x, P[12], mu, rs, dres=g)
+    dx, grads[12], grads[13] = ops.layernorm_bwd(dxn, x, P[12], mu, rs, dres=g, side=side)
     return dx
 
 
@@ -290,7 +290,7 @@ class _ConformerLayerFn(torch.autograd.Function):
         s = cfg.seed
         gout = gout.contiguous()
         side = _Side(gout.device)
-        g, grads[28], grads[29] = ops.layernorm_bwd(gout, x4, P[28], mu5, rs5)
+        g, grads[28], grads[29] = ops.layernorm_bwd(gout, x4, P[28], mu5, rs5, side=side)
         g = _ffn_bwd(g, x3, sv4, P, 22, cfg, s + 30, grads, side)
         if cfg.conv_first:
             g = _mha_bwd(g, c1, sva, P, R, cfg, s + 20, lens, grads, rgrads, side)

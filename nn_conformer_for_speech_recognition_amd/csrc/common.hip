@@ -304,6 +304,13 @@ void colreduce(const float* part, int nparts, long N, float* out, int accumulate
 }
 }  // namespace cfm
 
+CFM_EXPORT int cfm_colreduce(const float* part, int nparts, long N, long ldp, float* out, int accumulate,
+                             void* stream) {
+  CFM_REQUIRE(part && out && nparts > 0 && N > 0 && ldp >= N, CFM_ERR_ARG, "bad args");
+  cfm::colreduce(part, nparts, N, out, accumulate, cfm::as_stream(stream), ldp);
+  return cfm::check_launch("cfm_colreduce");
+}
+
 CFM_EXPORT int cfm_colsum(const void* x, int dtx, long M, int N, long ld, float* out, int accumulate,
                           float* ws, void* stream) {
   CFM_REQUIRE(x && out && ws && N > 0 && M >= 0 && ld >= N, CFM_ERR_ARG, "bad args");

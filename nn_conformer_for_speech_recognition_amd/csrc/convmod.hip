@@ -524,7 +524,7 @@ CFM_EXPORT int cfm_bn_bwd(const void* dz, int dtdz, const float* y, const float*
 
 CFM_EXPORT int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dta, const float* w, void* da, int dtda,
                                   float* dw, float* db, int B, int T, int C, int K, float* ws, void* stream) {
-  CFM_REQUIRE(dy && a && w && da && dw && ws, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(dy && a && w && da && ws, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, CFM_ERR_UNSUPPORTED, "depthwise kernel must be odd and <= 63");
   CFM_REQUIRE(B > 0 && T > 0 && C > 0, CFM_ERR_SHAPE, "bad shape");
   dim3 grid(cdiv(C, CT), cdiv(T, TT), B);
@@ -541,9 +541,20 @@ CFM_EXPORT int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dta, const
       if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_bwd_kernel<0, bf16>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws);
       else hipLaunchKernelGGL((glu_dwconv_bwd_kernel<0, float>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws);
   }
+  if (!dw) return cfm::check_launch("cfm_glu_dwconv_bwd");   // weight grads later: cfm_glu_dwconv_bwd_wgrad
   const long np = conv_nparts(B, T);
   float* sums = ws + np * (long)C * (K + 1);
   cfm::colreduce(ws, (int)np, (long)C * (K + 1), sums, 0, s);
   hipLaunchKernelGGL(dwconv_scatter_kernel, dim3(cdiv((long)C * (K + 1), 256)), dim3(256), 0, s, sums, C, K, dw, db);
   return cfm::check_launch("cfm_glu_dwconv_bwd");
+}
+
+CFM_EXPORT int cfm_glu_dwconv_bwd_wgrad(float* ws, int B, int T, int C, int K, float* dw, float* db, void* stream) {
+  CFM_REQUIRE(ws && dw, CFM_ERR_ARG, "null pointer");
+  hipStream_t s = cfm::as_stream(stream);
+  const long np = conv_nparts(B, T);
+  float* sums = ws + np * (long)C * (K + 1);
+  cfm::colreduce(ws, (int)np, (long)C * (K + 1), sums, 0, s);
+  hipLaunchKernelGGL(dwconv_scatter_kernel, dim3(cdiv((long)C * (K + 1), 256)), dim3(256), 0, s, sums, C, K, dw, db);
+  return cfm::check_launch("cfm_glu_dwconv_bwd_wgrad");
 }

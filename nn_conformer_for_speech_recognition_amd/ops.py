@@ -202,14 +202,21 @@ def layernorm_fwd(x, gamma, beta, eps=1e-5, out_dtype=None):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, gamma, mean, rstd, dres=None, dx_dtype=torch.float32):
+def layernorm_bwd(dy, x, gamma, mean, rstd, dres=None, dx_dtype=torch.float32, side=None):
+    """dx (+ dres) and (dgamma, dbeta).  side: optional object with run(fn, *keep) (conformer._Side):
+    the dgamma|dbeta partial-row reduction is then launched there, off the data-gradient chain."""
     M, D = x.shape
     dx = torch.empty(M, D, device=x.device, dtype=dx_dtype)
     gb = torch.empty(2, D, device=x.device, dtype=torch.float32)   # adjacent: one reduction pass
     dgamma, dbeta = gb[0], gb[1]
     ws = workspace(L.size_call("cfm_layernorm_ws_bytes", M, D), x.device)
+    defer = side is not None
     L.call("cfm_layernorm_bwd", L.ptr(dy), L.dt(dy), L.ptr(x), L.dt(x), L.ptr(gamma), L.ptr(mean), L.ptr(rstd),
-           L.ptr(dres), L.dt(dres), L.ptr(dx), L.dt(dx), L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws), M, D, L.stream())
+           L.ptr(dres), L.dt(dres), L.ptr(dx), L.dt(dx), None if defer else L.ptr(dgamma),
+           None if defer else L.ptr(dbeta), L.ptr(ws), M, D, L.stream())
+    if defer:
+        nb = (L.size_call("cfm_layernorm_ws_bytes", M, D) // 4 - 2 * D) // (2 * D)
+        side.run(lambda: L.call("cfm_colreduce", L.ptr(ws), nb, 2 * D, 2 * D, L.ptr(gb), 0, L.stream()), ws, gb)
     return dx, dgamma, dbeta
 
 
@@ -290,12 +297,17 @@ def bn_silu_bwd(dz, y, gamma, beta, mean, invstd, training, ws):
     return dy, dgamma, dbeta
 
 
-def glu_dwconv_bwd(dy, a, w_dw, B, T, C, K, ws, da_dtype):
+def glu_dwconv_bwd(dy, a, w_dw, B, T, C, K, ws, da_dtype, side=None):
+    """side: optional conformer._Side -- the depthwise weight/bias reduction then runs there."""
     da = torch.empty(B * T, 2 * C, device=a.device, dtype=da_dtype)
     dw = torch.empty(C, K, device=a.device, dtype=torch.float32)
     db = torch.empty(C, device=a.device, dtype=torch.float32)
-    L.call("cfm_glu_dwconv_bwd", L.ptr(dy), L.ptr(a), L.dt(a), L.ptr(w_dw), L.ptr(da), L.dt(da), L.ptr(dw),
-           L.ptr(db), B, T, C, K, L.ptr(ws), L.stream())
+    defer = side is not None
+    L.call("cfm_glu_dwconv_bwd", L.ptr(dy), L.ptr(a), L.dt(a), L.ptr(w_dw), L.ptr(da), L.dt(da),
+           None if defer else L.ptr(dw), None if defer else L.ptr(db), B, T, C, K, L.ptr(ws), L.stream())
+    if defer:
+        side.run(lambda: L.call("cfm_glu_dwconv_bwd_wgrad", L.ptr(ws), B, T, C, K, L.ptr(dw), L.ptr(db), L.stream()),
+                 ws, dw, db)
     return da, dw, db
 
 
