@@ -46,8 +46,18 @@ struct AttnM {
   const uint64_t* salt;   // bound dropout step counter or nullptr
 };
 
+// attention-dropout element index: rows of an EVEN stride (T rounded up to even), so the keys 2m and
+// 2m+1 of one (query, key-pair) share one 32-bit hash (low / high 16 bits): kernels holding both keys of
+// a pair in one lane (accumulator registers r, r+1 for even r) hash once per pair (dropout_pair)
 __device__ __forceinline__ uint64_t didx(const AttnM& p, int b, int h, int i, int j) {
-  return (((uint64_t)b * p.H + h) * p.T + i) * p.T + j;
+  return (((uint64_t)b * p.H + h) * p.T + i) * (uint64_t)(p.T + (p.T & 1)) + j;
+}
+// keep-scales of elements idx (even) and idx + 1: one mix for both (== dropout_keyed of each)
+__device__ __forceinline__ void dropout_pair(uint32_t thr, float keep, uint32_t key, uint64_t idx, float& m0,
+                                             float& m1) {
+  const uint32_t h = cfm_mix32((uint32_t)(idx >> 1) ^ key);
+  m0 = (h & 0xFFFFu) >= thr ? keep : 0.f;
+  m1 = (h >> 16) >= thr ? keep : 0.f;
 }
 
 // 8 consecutive head-dim elements c..c+7 of row `row` of matrix base (row stride ld), zero-padded
@@ -356,11 +366,15 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
       o1[r] *= alpha;
     }
     if (p.drop_p > 0.f) {
+      const uint64_t rowi = didx(p, b, h, qi, kt * TILE);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int k0 = kt * TILE + acc_row(r, hh);
-        s0[r] *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0));
-        s1[r] *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0 + 32));
+      for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
+        const int k0 = acc_row(r, hh);
+        float m0, m1, m2, m3;
+        dropout_pair(dthr, dkeep, dkey, rowi + k0, m0, m1);
+        dropout_pair(dthr, dkeep, dkey, rowi + k0 + 32, m2, m3);
+        s0[r] *= m0; s0[r + 1] *= m1;
+        s1[r] *= m2; s1[r + 1] *= m3;
       }
     }
 #pragma unroll
@@ -429,18 +443,25 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
       d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 0, 16 * s, lane), gf[s], d0, 0, 0, 0);
       d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32, 16 * s, lane), gf[s], d1, 0, 0, 0);
     }
+    if (p.drop_p > 0.f) {
+      const uint64_t rowi = didx(p, b, h, qi, kt * TILE);
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
+        const int k0 = acc_row(r, hh);
+        float m0, m1, m2, m3;
+        dropout_pair(dthr, dkeep, dkey, rowi + k0, m0, m1);
+        dropout_pair(dthr, dkeep, dkey, rowi + k0 + 32, m2, m3);
+        d0[r] *= m0; d0[r + 1] *= m1;
+        d1[r] *= m2; d1[r + 1] *= m3;
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int k0 = kt * TILE + acc_row(r, hh);
-      float p0 = (k0 < len && qvalid) ? fast_exp2(s0[r] * c - L2) : 0.f;
-      float p1 = (k0 + 32 < len && qvalid) ? fast_exp2(s1[r] * c - L2) : 0.f;
-      float g0 = d0[r], g1 = d1[r];
-      if (p.drop_p > 0.f) {
-        g0 *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0));
-        g1 *= dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qi, k0 + 32));
-      }
-      s0[r] = p0 * (g0 - Dq);
-      s1[r] = p1 * (g1 - Dq);
+      const float p0 = (k0 < len && qvalid) ? fast_exp2(s0[r] * c - L2) : 0.f;
+      const float p1 = (k0 + 32 < len && qvalid) ? fast_exp2(s1[r] * c - L2) : 0.f;
+      s0[r] = p0 * (d0[r] - Dq);
+      s1[r] = p1 * (d1[r] - Dq);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -583,7 +604,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
   const float c = p.scale * LOG2E;
   f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
   const int nqs = k0w < len ? nq : 0;      // key blocks past len: zero gradients
-  const uint64_t dbase = (((uint64_t)b * p.H + h) * p.T) * p.T + kj;
+  const uint64_t dbase = didx(p, b, h, 0, kj);
   for (int qt = 0; qt < nqs; ++qt) {
     const int q0 = qt * 32;
     f32x16 sa = (f32x16){0}, ga = (f32x16){0};
@@ -598,7 +619,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
       const int q = q0 + acc_row(r, hh);
       const float pa = kvalid ? fast_exp2(sa[r] * c - sL[q]) : 0.f;   // lse = +inf for q >= T
       float ma = 1.f;
-      if (p.drop_p > 0.f) ma = dropout_keyed(dthr, dkeep, dkey, dbase + (uint64_t)q * p.T);
+      if (p.drop_p > 0.f) ma = dropout_keyed(dthr, dkeep, dkey, dbase + (uint64_t)q * (p.T + (p.T & 1)));
       sa[r] = pa * ma;                       // P (dropped)
       ga[r] = pa * (ga[r] * ma - sD[q]);     // dS
     }
@@ -877,7 +898,7 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   CFM_REQUIRE(!pos || (pos_u && pos_v), CFM_ERR_ARG, "rel-pos needs pos_u and pos_v");
   CFM_REQUIRE(dtype == CFM_BF16 || dtype == CFM_F32, CFM_ERR_DTYPE, "dtype");
   CFM_REQUIRE(pos || dtype == CFM_F32 || dk <= DKP, CFM_ERR_UNSUPPORTED, "bf16 head dim must be <= 64");
-  CFM_REQUIRE((double)B * H * T * T < 8589934592.0, CFM_ERR_SHAPE, "attention dropout index space (2^33)");
+  CFM_REQUIRE((double)B * H * T * (T + 1) < 8589934592.0, CFM_ERR_SHAPE, "attention dropout index space (2^33)");
   hipStream_t s = cfm::as_stream(stream);
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, s);

@@ -31,8 +31,10 @@ __device__ __forceinline__ float qkv_at(const AttnP& p, int b, int t, int which,
 __device__ __forceinline__ float pos_at(const AttnP& p, int r, int h, int d) {
   return ld_dyn(p.pos, p.dt, (long)r * p.H * p.dk + h * p.dk + d);
 }
+// attention-dropout element index: rows of an EVEN stride (T rounded up to even), so keys 2m and
+// 2m+1 of a row share one 32-bit hash (same convention as attention.hip's didx)
 __device__ __forceinline__ uint64_t drop_idx(const AttnP& p, int b, int h, int i, int j) {
-  return (((uint64_t)b * p.H + h) * p.T + i) * p.T + j;
+  return (((uint64_t)b * p.H + h) * p.T + i) * (uint64_t)(p.T + (p.T & 1)) + j;
 }
 
 // score for (i, j): lanes hold their own j; qa/qb are broadcast from LDS
