@@ -160,6 +160,13 @@ int cfm_layernorm_bwd(const void* dy, int dtype_dy, const void* x, int dtype_x, 
                       const float* mean, const float* rstd, const void* dres, int dtype_dres,
                       void* dx, int dtype_dx, float* dgamma, float* dbeta, float* ws, long M, int D,
                       void* stream);
+/* The same plus g2 (bf16, M x D) = dx * g2_scale * dropout(g2_p, g2_seed, element index) -- exactly
+   cfm_scale_dropout(dx, ..., offset 0) -- written by the same pass: the next module's (residual-
+   dropout) input gradient in the encoder backward.  g2 == NULL: identical to cfm_layernorm_bwd. */
+int cfm_layernorm_bwd_drop(const void* dy, int dtdy, const void* x, int dtx, const float* gamma,
+                           const float* mean, const float* rstd, const void* dres, int dtres, void* dx,
+                           int dtdx, float* dgamma, float* dbeta, float* ws, long M, int D, void* g2,
+                           float g2_scale, float g2_p, uint64_t g2_seed, void* stream);
 
 /* y = act(x*scale [dropout]) + residual, elementwise helpers used at residual joins. */
 int cfm_scale_dropout(const void* x, int dtype_x, void* y, int dtype_y, long n, float scale,

@@ -64,6 +64,9 @@ _SIGS = {
     "cfm_layernorm_ws_bytes": (c_size_t, [c_long, c_int]),
     "cfm_layernorm_bwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p]),
+    "cfm_layernorm_bwd_drop": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p,
+                                       c_float, c_float, c_u64, c_void_p]),
     "cfm_scale_dropout": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_float, c_float, c_u64, c_u64,
                                   c_void_p]),
     "cfm_convmod_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),

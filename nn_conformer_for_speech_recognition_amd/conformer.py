@@ -162,16 +162,40 @@ def _ffn_fwd(x, P, o, cfg, seed):
     return y, (xn, mu, rs, pre, h, w1, w2)
 
 
-def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads, side):
+def _in_drop(kind, cfg, seed):
+    """(scale, p, seed, dtype) of a module's residual-dropout input gradient g2 = scale * mask * g
+    (FFN: 0.5 macaron scale; the mask seeds are the forward's)."""
+    return {"ffn": (0.5, cfg.p, seed + 1), "mha": (1.0, cfg.p, seed + 1), "conv": (1.0, cfg.p, seed)}[kind] + (cfg.cd,)
+
+
+def _g2(g, g2, kind, cfg, seed):
+    if g2 is not None:
+        return g2
+    sc, p, sd, cd = _in_drop(kind, cfg, seed)
+    return ops.scale_dropout(g, sc, p, sd, 0, out_dtype=cd)
+
+
+def _ln_bwd(dxn, x, P, i, mu, rs, g, side, nxt):
+    """module-input LayerNorm backward (+ residual g); nxt: the next module's _in_drop (or None) ->
+    its g2 comes out of the same kernel.  Returns (dx, g2_next)."""
+    if nxt is None:
+        dx, gg, gb = ops.layernorm_bwd(dxn, x, P[i], mu, rs, dres=g, side=side)
+        g2n = None
+    else:
+        dx, gg, gb, g2n = ops.layernorm_bwd(dxn, x, P[i], mu, rs, dres=g, side=side, drop=nxt)
+    return dx, gg, gb, g2n
+
+
+def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads, side, g2=None, nxt=None):
     xn, mu, rs, pre, h, w1, w2 = sv
     cd = cfg.cd
-    g2 = ops.scale_dropout(g, 0.5, cfg.p, seed + 1, 0, out_dtype=cd)
+    g2 = _g2(g, g2, "ffn", cfg, seed)
     grads[o + 4], grads[o + 5] = _wgrad_bias(side, g2, h)
     da = ops.linear_dgrad(g2, w2, pre=pre, act_grad=True, drop_p=cfg.p, seed=seed, wt=_wt(cfg, o + 4))
     grads[o + 2], grads[o + 3] = _wgrad_bias(side, da, xn)
     dxn = ops.linear_dgrad(da, w1, wt=_wt(cfg, o + 2))
-    dx, grads[o], grads[o + 1] = ops.layernorm_bwd(dxn, x, P[o], mu, rs, dres=g, side=side)
-    return dx
+    dx, grads[o], grads[o + 1], g2n = _ln_bwd(dxn, x, P, o, mu, rs, g, side, nxt)
+    return dx, g2n
 
 
 def _mha_fwd(x, P, R, cfg, seed, lens):
@@ -191,11 +215,11 @@ def _mha_fwd(x, P, R, cfg, seed, lens):
     return y, (xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv)
 
 
-def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side):
+def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=None):
     xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv = sv
     cd = cfg.cd
     B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
-    g4 = ops.scale_dropout(g, 1.0, cfg.p, seed + 1, 0, out_dtype=cd)
+    g4 = _g2(g, g2, "mha", cfg, seed)
     grads[10], grads[11] = _wgrad_bias(side, g4, o)
     do = ops.linear_dgrad(g4, wout, wt=_wt(cfg, 10))
     dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
@@ -205,8 +229,8 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side):
         rgrads[2] = dpv.view(H, d // H)
     grads[8], grads[9] = _wgrad_bias(side, dqkv, xn)
     dxn = ops.linear_dgrad(dqkv, win, wt=_wt(cfg, 8))
-    dx, grads[6], grads[7] = ops.layernorm_bwd(dxn, x, P[6], mu, rs, dres=g, side=side)
-    return dx
+    dx, grads[6], grads[7], g2n = _ln_bwd(dxn, x, P, 6, mu, rs, g, side, nxt)
+    return dx, g2n
 
 
 def _conv_fwd(x, P, cfg, seed):
@@ -224,11 +248,11 @@ def _conv_fwd(x, P, cfg, seed):
     return y, (xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw)
 
 
-def _conv_bwd(g, x, sv, P, cfg, seed, grads, side):
+def _conv_bwd(g, x, sv, P, cfg, seed, grads, side, g2=None, nxt=None):
     xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw = sv
     cd = cfg.cd
     B, T, d, K = cfg.B, cfg.T, cfg.d, cfg.K
-    g3 = ops.scale_dropout(g, 1.0, cfg.p, seed, 0, out_dtype=cd)
+    g3 = _g2(g, g2, "conv", cfg, seed)
     dw, grads[21] = _wgrad_bias(side, g3, z)
     grads[20] = dw.view(d, d, 1)
     dz = ops.linear_dgrad(g3, wp2, wt=_wt(cfg, 20))
@@ -239,8 +263,8 @@ def _conv_bwd(g, x, sv, P, cfg, seed, grads, side):
     dw, grads[15] = _wgrad_bias(side, da, xn)
     grads[14] = dw.view(2 * d, d, 1)
     dxn = ops.linear_dgrad(da, wp1, wt=_wt(cfg, 14))
-    dx, grads[12], grads[13] = ops.layernorm_bwd(dxn, x, P[12], mu, rs, dres=g, side=side)
-    return dx
+    dx, grads[12], grads[13], g2n = _ln_bwd(dxn, x, P, 12, mu, rs, g, side, nxt)
+    return dx, g2n
 
 
 class _ConformerLayerFn(torch.autograd.Function):
@@ -290,15 +314,19 @@ class _ConformerLayerFn(torch.autograd.Function):
         s = cfg.seed
         gout = gout.contiguous()
         side = _Side(gout.device)
-        g, grads[28], grads[29] = ops.layernorm_bwd(gout, x4, P[28], mu5, rs5, side=side)
-        g = _ffn_bwd(g, x3, sv4, P, 22, cfg, s + 30, grads, side)
+        # each LayerNorm backward also emits the next module's dropout-scaled input gradient (g2)
+        ffn2_in = _in_drop("ffn", cfg, s + 30)
+        conv_in, mha_in, ffn1_in = _in_drop("conv", cfg, s + 10), _in_drop("mha", cfg, s + 20), _in_drop("ffn", cfg, s)
+        g, grads[28], grads[29], g2 = ops.layernorm_bwd(gout, x4, P[28], mu5, rs5, side=side, drop=ffn2_in)
         if cfg.conv_first:
-            g = _mha_bwd(g, c1, sva, P, R, cfg, s + 20, lens, grads, rgrads, side)
-            g = _conv_bwd(g, c0, svc, P, cfg, s + 10, grads, side)
+            g, g2 = _ffn_bwd(g, x3, sv4, P, 22, cfg, s + 30, grads, side, g2, mha_in)
+            g, g2 = _mha_bwd(g, c1, sva, P, R, cfg, s + 20, lens, grads, rgrads, side, g2, conv_in)
+            g, g2 = _conv_bwd(g, c0, svc, P, cfg, s + 10, grads, side, g2, ffn1_in)
         else:
-            g = _conv_bwd(g, c1, svc, P, cfg, s + 10, grads, side)
-            g = _mha_bwd(g, c0, sva, P, R, cfg, s + 20, lens, grads, rgrads, side)
-        g = _ffn_bwd(g, x0, sv1, P, 0, cfg, s, grads, side)
+            g, g2 = _ffn_bwd(g, x3, sv4, P, 22, cfg, s + 30, grads, side, g2, conv_in)
+            g, g2 = _conv_bwd(g, c1, svc, P, cfg, s + 10, grads, side, g2, mha_in)
+            g, g2 = _mha_bwd(g, c0, sva, P, R, cfg, s + 20, lens, grads, rgrads, side, g2, ffn1_in)
+        g, _ = _ffn_bwd(g, x0, sv1, P, 0, cfg, s, grads, side, g2, None)
         side.join()
         ctx.sv = None
         return (g, None, None, *grads, *rgrads)

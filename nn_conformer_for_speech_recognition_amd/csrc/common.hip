@@ -295,9 +295,38 @@ __global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict
     out[n] = acc ? out[n] + t : t;
   }
 }
+// two independent column reductions in one launch (blockIdx.y selects): BatchNorm's (sum, sumsq) /
+// (dbeta, dgamma) partial pairs
+__global__ __launch_bounds__(1024) void colreduce2_kernel(const float* __restrict__ partA, const float* __restrict__ partB,
+                                                          int nparts, long N, float* __restrict__ outA,
+                                                          float* __restrict__ outB) {
+  __shared__ float red[16][64];
+  const float* part = blockIdx.y ? partB : partA;
+  float* out = blockIdx.y ? outB : outA;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long n = (long)blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (n < N) {
+#pragma unroll 4
+    for (int p = wv; p < nparts; p += 16) s += part[(long)p * N + n];
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][lane];
+    out[n] = t;
+  }
+}
 }  // namespace
 
 namespace cfm {
+void colreduce_pair(const float* partA, const float* partB, int nparts, long N, float* outA, float* outB,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(colreduce2_kernel, dim3((unsigned)((N + 63) / 64), 2), dim3(1024), 0, s, partA, partB, nparts, N,
+                     outA, outB);
+}
 void colreduce(const float* part, int nparts, long N, float* out, int accumulate, hipStream_t s, long ldp) {
   hipLaunchKernelGGL(colreduce_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, part, nparts, N,
                      ldp > 0 ? ldp : N, out, accumulate);

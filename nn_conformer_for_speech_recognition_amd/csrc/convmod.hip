@@ -406,8 +406,7 @@ long conv_nparts(int B, int T) { return (long)B * ((T + TT - 1) / TT); }
 void bn_stats_finalize(const float* ws, int nparts, long M, int C, float* mean, float* invstd, float* rm, float* rv,
                        float mom, float eps, hipStream_t s) {
   float* sums = const_cast<float*>(ws) + 2L * nparts * C;
-  cfm::colreduce(ws, nparts, C, sums, 0, s);
-  cfm::colreduce(ws + (long)nparts * C, nparts, C, sums + C, 0, s);
+  cfm::colreduce_pair(ws, ws + (long)nparts * C, nparts, C, sums, sums + C, s);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, sums + C, M, C, mean, invstd,
                      rm, rv, mom, eps);
 }
@@ -418,8 +417,7 @@ int bn_bwd_impl(const void* dz, int dtdz, const float* y, const float* gamma, co
   const long rows_per = (M + BN_PARTS - 1) / BN_PARTS;
   hipLaunchKernelGGL(bn_bwd_rows_kernel, dim3(cdiv(C, 64), BN_PARTS), dim3(256), 0, s, dz, dtdz, y, gamma, beta, mean,
                      invstd, M, C, rows_per > 0 ? rows_per : 1, ws, act);
-  cfm::colreduce(ws, BN_PARTS, C, dbeta, 0, s);
-  cfm::colreduce(ws + (long)BN_PARTS * C, BN_PARTS, C, dgamma, 0, s);
+  cfm::colreduce_pair(ws, ws + (long)BN_PARTS * C, BN_PARTS, C, dbeta, dgamma, s);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, dz, dtdz, y, gamma, beta, mean,
                      invstd, dgamma, dbeta, training, dy, M, C, act);
   return CFM_OK;

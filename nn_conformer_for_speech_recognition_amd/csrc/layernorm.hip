@@ -106,11 +106,20 @@ __global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, c
   }
 }
 
+// optional fused second output of the vectorised backward: g2 = bf16(dx * scale * dropout(p, seed))
+struct LnDrop {
+  void* g2;
+  float scale, p;
+  uint64_t seed;
+  const uint64_t* salt;
+};
+
 template <int V, typename TDY>
 __global__ __launch_bounds__(256) void ln_bwd_vec(const TDY* __restrict__ dy, const float* __restrict__ x,
                                                   const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                   const float* __restrict__ rstd_in, const float* __restrict__ dres,
-                                                  float* __restrict__ dx, float* __restrict__ ws, long M) {
+                                                  float* __restrict__ dx, float* __restrict__ ws, long M, LnDrop dr) {
+  if (dr.g2 && dr.p > 0.f) dr.seed = salted_seed(dr.seed, dr.salt);
   constexpr int D = 64 * V;
   __shared__ float red[4][2 * D];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -146,6 +155,18 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TDY* __restrict__ dy, co
 #pragma unroll
     for (int i = 0; i < V; ++i) o[i] += rstd * (g[i] - sg - xh[i] * sgx);
     stv<V>(dx + row * D + lane * V, o);
+    if constexpr (V == 8) {
+      if (dr.g2) {   // the next module's input gradient: bf16(dx * scale * dropout mask), as cfm_scale_dropout
+        float sc[8];
+        if (dr.p > 0.f) dropout_scale8(dr.p, dr.seed, (uint64_t)(row * D + lane * V), sc);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sc[i] = dr.p > 0.f ? dr.scale * sc[i] : dr.scale;
+        float q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = o[i] * sc[i];
+        st8_dyn(dr.g2, CFM_BF16, row * D + lane * V, q);
+      }
+    }
   }
 #pragma unroll
   for (int i = 0; i < V; ++i) {
@@ -279,15 +300,16 @@ bool ln_fwd_fast(const void* x, int dtx, const float* gamma, const float* beta, 
 template <int V>
 bool ln_bwd_fast(const void* dy, int dtdy, const void* x, int dtx, const float* gamma, const float* mean,
                  const float* rstd, const void* dres, int dtres, void* dx, int dtdx, float* ws, long M, int D, int nb,
-                 hipStream_t s) {
+                 hipStream_t s, LnDrop dr) {
   if (D != 64 * V || dtx != CFM_F32 || dtdx != CFM_F32 || (dres && dtres != CFM_F32)) return false;
   if (!aligned16(dy) || !aligned16(x) || !aligned16(dres) || !aligned16(dx) || !aligned16(gamma)) return false;
+  if (dr.g2 && (V != 8 || !aligned16(dr.g2))) return false;
   if (dtdy == CFM_BF16)
     hipLaunchKernelGGL((ln_bwd_vec<V, bf16>), dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const float*)x, gamma, mean,
-                       rstd, (const float*)dres, (float*)dx, ws, M);
+                       rstd, (const float*)dres, (float*)dx, ws, M, dr);
   else
     hipLaunchKernelGGL((ln_bwd_vec<V, float>), dim3(nb), dim3(256), 0, s, (const float*)dy, (const float*)x, gamma,
-                       mean, rstd, (const float*)dres, (float*)dx, ws, M);
+                       mean, rstd, (const float*)dres, (float*)dx, ws, M, dr);
   return true;
 }
 }  // namespace
@@ -312,21 +334,37 @@ CFM_EXPORT size_t cfm_layernorm_ws_bytes(long M, int D) {
   return (size_t)ln_bwd_blocks(M) * 2 * D * sizeof(float) + 2 * D * sizeof(float);
 }
 
-CFM_EXPORT int cfm_layernorm_bwd(const void* dy, int dtdy, const void* x, int dtx, const float* gamma,
-                                 const float* mean, const float* rstd, const void* dres, int dtres, void* dx,
-                                 int dtdx, float* dgamma, float* dbeta, float* ws, long M, int D,
-                                 void* stream) {
+CFM_EXPORT int cfm_scale_dropout(const void* x, int dtx, void* y, int dty, long n, float scale, float p,
+                                 uint64_t seed, uint64_t off, void* stream);
+
+CFM_EXPORT int cfm_layernorm_bwd_drop(const void* dy, int dtdy, const void* x, int dtx, const float* gamma,
+                                      const float* mean, const float* rstd, const void* dres, int dtres, void* dx,
+                                      int dtdx, float* dgamma, float* dbeta, float* ws, long M, int D, void* g2,
+                                      float g2_scale, float g2_p, uint64_t g2_seed, void* stream) {
   CFM_REQUIRE(dy && x && gamma && mean && rstd && dx && ws, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(D > 0 && D <= 64 * MAXJ && M >= 0, CFM_ERR_SHAPE, "D must be in (0, 1024]");
   hipStream_t s = cfm::as_stream(stream);
   const int nb = ln_bwd_blocks(M);
-  const bool fast = ln_bwd_fast<2>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s) ||
-                    ln_bwd_fast<4>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s) ||
-                    ln_bwd_fast<8>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s) ||
-                    ln_bwd_fast<16>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s);
+  const LnDrop dr{g2, g2_scale, g2_p, g2_seed, cfm::g_rng_salt};
+  bool fast = ln_bwd_fast<2>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr) ||
+              ln_bwd_fast<4>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr) ||
+              ln_bwd_fast<8>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr) ||
+              ln_bwd_fast<16>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr);
+  bool g2_done = fast && g2 != nullptr;
+  if (!fast && g2) {   // no fused path for this shape: the vectorised kernel without g2, then a separate pass
+    const LnDrop none{nullptr, 0.f, 0.f, 0, nullptr};
+    fast = ln_bwd_fast<2>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none) ||
+           ln_bwd_fast<4>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none) ||
+           ln_bwd_fast<8>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none) ||
+           ln_bwd_fast<16>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none);
+  }
   if (!fast)
     hipLaunchKernelGGL(ln_bwd_kernel, dim3(nb), dim3(256), 0, s, dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres,
                        dx, dtdx, ws, M, D);
+  if (g2 && !g2_done) {
+    const int rc = cfm_scale_dropout(dx, dtdx, g2, CFM_BF16, M * D, g2_scale, g2_p, g2_seed, 0, stream);
+    if (rc != CFM_OK) return rc;
+  }
   if (dgamma && dbeta && dbeta == dgamma + D) {
     cfm::colreduce(ws, nb, 2L * D, dgamma, 0, s);               // one pass for [dgamma | dbeta]
   } else {
@@ -334,4 +372,12 @@ CFM_EXPORT int cfm_layernorm_bwd(const void* dy, int dtdy, const void* x, int dt
     if (dbeta) cfm::colreduce(ws + D, nb, D, dbeta, 0, s, 2L * D);
   }
   return cfm::check_launch("cfm_layernorm_bwd");
+}
+
+CFM_EXPORT int cfm_layernorm_bwd(const void* dy, int dtdy, const void* x, int dtx, const float* gamma,
+                                 const float* mean, const float* rstd, const void* dres, int dtres, void* dx,
+                                 int dtdx, float* dgamma, float* dbeta, float* ws, long M, int D,
+                                 void* stream) {
+  return cfm_layernorm_bwd_drop(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, dgamma, dbeta, ws, M, D,
+                                nullptr, 0.f, 0.f, 0, stream);
 }

@@ -202,21 +202,35 @@ def layernorm_fwd(x, gamma, beta, eps=1e-5, out_dtype=None):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, gamma, mean, rstd, dres=None, dx_dtype=torch.float32, side=None):
+def layernorm_bwd(dy, x, gamma, mean, rstd, dres=None, dx_dtype=torch.float32, side=None, drop=None):
     """dx (+ dres) and (dgamma, dbeta).  side: optional object with run(fn, *keep) (conformer._Side):
-    the dgamma|dbeta partial-row reduction is then launched there, off the data-gradient chain."""
+    the dgamma|dbeta partial-row reduction is then launched there, off the data-gradient chain.
+    drop: optional (scale, p, seed, dtype) -> also returns g2 = scale_dropout(dx, scale, p, seed) in
+    `dtype`, written by the same kernel (4 return values then)."""
     M, D = x.shape
     dx = torch.empty(M, D, device=x.device, dtype=dx_dtype)
     gb = torch.empty(2, D, device=x.device, dtype=torch.float32)   # adjacent: one reduction pass
     dgamma, dbeta = gb[0], gb[1]
     ws = workspace(L.size_call("cfm_layernorm_ws_bytes", M, D), x.device)
     defer = side is not None
-    L.call("cfm_layernorm_bwd", L.ptr(dy), L.dt(dy), L.ptr(x), L.dt(x), L.ptr(gamma), L.ptr(mean), L.ptr(rstd),
-           L.ptr(dres), L.dt(dres), L.ptr(dx), L.dt(dx), None if defer else L.ptr(dgamma),
-           None if defer else L.ptr(dbeta), L.ptr(ws), M, D, L.stream())
+    g2 = None
+    if drop is not None and drop[3] == torch.bfloat16:
+        scale, p, seed = float(drop[0]), float(drop[1]), int(drop[2])
+        g2 = torch.empty(M, D, device=x.device, dtype=torch.bfloat16)
+        L.call("cfm_layernorm_bwd_drop", L.ptr(dy), L.dt(dy), L.ptr(x), L.dt(x), L.ptr(gamma), L.ptr(mean),
+               L.ptr(rstd), L.ptr(dres), L.dt(dres), L.ptr(dx), L.dt(dx), None if defer else L.ptr(dgamma),
+               None if defer else L.ptr(dbeta), L.ptr(ws), M, D, L.ptr(g2), scale, p, seed, L.stream())
+    else:
+        L.call("cfm_layernorm_bwd", L.ptr(dy), L.dt(dy), L.ptr(x), L.dt(x), L.ptr(gamma), L.ptr(mean), L.ptr(rstd),
+               L.ptr(dres), L.dt(dres), L.ptr(dx), L.dt(dx), None if defer else L.ptr(dgamma),
+               None if defer else L.ptr(dbeta), L.ptr(ws), M, D, L.stream())
+        if drop is not None:
+            g2 = scale_dropout(dx, drop[0], drop[1], drop[2], 0, out_dtype=drop[3])
     if defer:
         nb = (L.size_call("cfm_layernorm_ws_bytes", M, D) // 4 - 2 * D) // (2 * D)
         side.run(lambda: L.call("cfm_colreduce", L.ptr(ws), nb, 2 * D, 2 * D, L.ptr(gb), 0, L.stream()), ws, gb)
+    if drop is not None:
+        return dx, dgamma, dbeta, g2
     return dx, dgamma, dbeta
 
 

@@ -317,3 +317,23 @@ def test_conv2_fwd_pipeline(gemm_mode, B, F1, T1, C1, C2):
     assert fast.shape == ref.shape
     assert _rel(fast, ref) < 1e-5
     assert _rel(fast, slow) < 1e-5
+
+
+@pytest.mark.parametrize("D", [512, 144])
+def test_layernorm_bwd_fused_dropout_output(D):
+    """cfm_layernorm_bwd_drop's g2 is bit-identical to cfm_scale_dropout(dx) (fused for D = 512, the
+    separate pass otherwise), dx unchanged."""
+    g = torch.Generator().manual_seed(D)
+    M = 1000
+    x = torch.randn(M, D, generator=g).to(DEV)
+    gamma = torch.randn(D, generator=g).to(DEV)
+    beta = torch.randn(D, generator=g).to(DEV)
+    _, mu, rs = ops.layernorm_fwd(x, gamma, beta, out_dtype=torch.bfloat16)
+    dy = torch.randn(M, D, generator=g).to(DEV, torch.bfloat16)
+    dres = torch.randn(M, D, generator=g).to(DEV)
+    dx0, gg0, gb0 = ops.layernorm_bwd(dy, x, gamma, mu, rs, dres=dres)
+    dx1, gg1, gb1, g2 = ops.layernorm_bwd(dy, x, gamma, mu, rs, dres=dres, drop=(0.5, 0.1, 77, torch.bfloat16))
+    ref = ops.scale_dropout(dx0, 0.5, 0.1, 77, 0, out_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1) and torch.equal(gg0, gg1) and torch.equal(gb0, gb1)
+    assert torch.equal(g2, ref)
