@@ -17,6 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("n", type=int, nargs="?", default=20)
 ap.add_argument("--mode", type=int, default=None)
 ap.add_argument("--plain", action="store_true")
+ap.add_argument("--wgrad", action="store_true", help="the FFN W1 weight-gradient GEMM (split-K 8) instead")
 a = ap.parse_args()
 if a.mode is not None:
     _lib.call("cfm_gemm_set_mode", a.mode)
@@ -27,8 +28,11 @@ w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
 b = torch.randn(N, device="cuda")
 pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+dyw = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
 for _ in range(a.n):
-    if a.plain:
+    if a.wgrad:
+        ops.linear_wgrad(dyw, x)
+    elif a.plain:
         ops.linear(x, w, b, out=y)
     else:
         ops.linear(x, w, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=1, out=y)

@@ -133,6 +133,10 @@ typedef struct cfm_gemm_desc {
   unsigned long long* probe; /* optional timing slot (measurement only): the launch atomically
                               min-records its first workgroup's start and max-records its last
                               workgroup's end (s_memrealtime ticks) into probe[0] / probe[1] */
+  float* a_colsum;         /* optional (bf16 LDS-DMA path, MN-major A, split_k > 1 with workspace, batch 1):
+                              a_colsum[m] = sum_k A(m, k) -- the bias gradient of a weight-gradient GEMM
+                              dW = dY^T X (A = dY^T) -- from the staged A tiles; workspace then needs
+                              split_k*M more floats.  NULL: off. */
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 /* kernel-selection switch for A/B measurements: bit 0 = 256-row register-staged tiles allowed,

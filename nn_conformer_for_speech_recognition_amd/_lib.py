@@ -40,6 +40,7 @@ class GemmDesc(ctypes.Structure):
         ("split_k", c_int),
         ("workspace", c_void_p),
         ("probe", c_void_p),
+        ("a_colsum", c_void_p),
     ]
 
 

@@ -39,6 +39,7 @@ struct GemmP {
   int cmap, cm_F1c, cm_T1c, cm_pf, cm_pt, cm_F1, cm_T1;
   int dbg;     // timing experiments only (cfm_gemm_set_mode bit 3): skip the epilogue's stores
   unsigned long long* probe;   // optional timing slot (cfm_gemm_desc.probe)
+  float* acs_slab;             // A column-sum partials [split][M] (cfm_gemm_desc.a_colsum) or nullptr
 };
 
 __device__ __forceinline__ long out_row(const GemmP& p, int m) {
@@ -692,6 +693,12 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x16){0};
+  // bias gradient of a weight-gradient GEMM: column sums of the staged MN-major A tile ([k][BMt],
+  // chunk c of k-row k at slot c ^ 4(k&3)); thread = one 8-column chunk x every RGth k-row
+  constexpr int ACH = BMt / 8, RG = G::NTt / ACH;
+  const bool acs = !AK && p.acs_slab != nullptr && tn == 0;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int acs_c = tid % ACH, acs_r = tid / ACH;
 
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s)
@@ -717,6 +724,30 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if constexpr (!AK) {
+      if (acs) {
+#pragma unroll
+        for (int k = acs_r; k < BKt; k += RG) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + k * (BMt * 2) + 16 * (acs_c ^ (4 * (k & 3))));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[e] += (float)v[e];
+        }
+      }
+    }
+  }
+  if constexpr (!AK) {
+    if (acs) {   // combine the RG row groups in LDS (every wave is past its last ring read after this barrier)
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[acs_r * BMt + acs_c * 8 + e] = csum[e];
+      __syncthreads();
+      if (tid < BMt && m0 + tid < p.M) {
+        float t = 0.f;
+        for (int g = 0; g < RG; ++g) t += red[g * BMt + tid];
+        p.acs_slab[(long)zz * p.M + m0 + tid] = t;
+      }
     }
   }
   if (p.dbg) {       // timing experiment: keep the accumulators live, store nothing
@@ -844,7 +875,16 @@ GemmP plain_params(int M, int N, int K, void* C, long ldc, int dtc) {
 // grid (ceil(M*N/4 / 256), batch): 32-bit index math (M*N < 2^31), the split slabs summed in order
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int split, int M, int N,
                                                             float* __restrict__ C, long ldc, long sc,
-                                                            const float* __restrict__ bias) {
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ acs_slab, float* __restrict__ acs) {
+  if (acs_slab && blockIdx.y == 0) {   // A column sums: out[m] = sum_s acs_slab[s][m] (in order)
+    const unsigned m = blockIdx.x * 256u + threadIdx.x;
+    if (m < (unsigned)M) {
+      float t = acs_slab[m];
+      for (int k = 1; k < split; ++k) t += acs_slab[(long)k * M + m];
+      acs[m] = t;
+    }
+  }
   const unsigned per = (unsigned)M * (unsigned)N;
   const unsigned q = blockIdx.x * 256u + threadIdx.x;
   if (q * 4u >= per) return;
@@ -1025,6 +1065,11 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
     CFM_REQUIRE(d->N % 4 == 0 && d->ldc % 4 == 0, CFM_ERR_SHAPE, "slab split-K needs N % 4 == 0");
     p.slab = d->workspace;
   }
+  if (d->a_colsum) {
+    CFM_REQUIRE(bf && !d->a_kmajor && p.slab && d->batch == 1 && (g_gemm_mode & 2) && pipe_ok(*d, p, va, vb),
+                CFM_ERR_UNSUPPORTED, "a_colsum needs the bf16 LDS-DMA path, MN-major A, slab split-K, batch 1");
+    p.acs_slab = p.slab + (long)split * d->M * d->N;
+  }
   if (bf && (g_gemm_mode & 2) && pipe_ok(*d, p, va, vb)) rc = launch_pipe(*d, p, s);
   else if (bf) go(bf16{});
   else go(float{});
@@ -1032,8 +1077,10 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   if (p.slab) {
     CFM_REQUIRE((long)d->M * d->N < (1L << 31) && d->batch <= 65535, CFM_ERR_SHAPE, "split-K slab too large");
     const long n4 = (long)d->M * d->N / 4;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n4 + 255) / 256), d->batch), dim3(256), 0, s, p.slab,
-                       split, d->M, d->N, (float*)d->C, d->ldc, d->stride_c, d->bias);
+    const unsigned gx = (unsigned)((n4 + 255) / 256) > (unsigned)cdiv(d->M, 256) ? (unsigned)((n4 + 255) / 256)
+                                                                                : (unsigned)cdiv(d->M, 256);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, d->batch), dim3(256), 0, s, p.slab, split, d->M, d->N,
+                       (float*)d->C, d->ldc, d->stride_c, d->bias, p.acs_slab, d->a_colsum);
   }
   return cfm::check_launch("cfm_gemm");
 }

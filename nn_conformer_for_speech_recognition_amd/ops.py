@@ -3,6 +3,8 @@ stream-ordered on torch's current HIP stream and allocates only through torch's 
 allocator (so whole steps can be captured into a HIP graph)."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -18,7 +20,8 @@ def _gemm_desc(**kw):
 
 def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, alpha=1.0,
          bias=None, act=ACT_NONE, act_grad=False, pre=None, drop_p=0.0, seed=0, offset=0, out_scale=1.0,
-         residual=None, ldr=None, split_k=1, batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None):
+         residual=None, ldr=None, split_k=1, batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None,
+         a_colsum=None):
     """C = epilogue(alpha * A·Bᵀ) — see cfm_gemm_desc in include/cfm.h."""
     if A.dtype != B.dtype:
         raise L.CfmError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
@@ -32,7 +35,7 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         drop_p=float(drop_p), drop_seed=int(seed) & (2**64 - 1), drop_offset=int(offset),
         out_scale=float(out_scale), residual=L.ptr(residual),
         ldr=ldr if ldr is not None else N, dtype_r=L.dt(residual) if residual is not None else F32,
-        split_k=int(split_k), workspace=L.ptr(workspace))
+        split_k=int(split_k), workspace=L.ptr(workspace), a_colsum=L.ptr(a_colsum))
     if PROBE is not None:
         PROBE("gemm", (M, N, K), d, lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
     else:
@@ -72,23 +75,36 @@ def linear_dgrad(dy, w, out_dtype=None, pre=None, act_grad=False, drop_p=0.0, se
                 drop_p=drop_p, seed=seed, offset=offset)
 
 
-def linear_wgrad(dy, x, out=None, split_k=None):
+# target workgroup count (in 128x128-tile units) of the split-K weight-gradient GEMMs
+_WGRAD_WGS = int(os.environ.get("CFM_WGRAD_WGS", "512"))
+
+
+def linear_wgrad(dy, x, out=None, split_k=None, bias_out=None):
     """dW = dyᵀ·x for dy (M, N), x (M, K) → (N, K) fp32 (token dim reduced; both operands stay
-    token-major in HBM and are transposed by ds_read_b64_tr_b16 on the way into the MFMAs)."""
+    token-major in HBM and are transposed by ds_read_b64_tr_b16 on the way into the MFMAs).
+    bias_out: optional (N,) fp32 <- Σ_rows dy (the bias gradient), taken from the same GEMM's staged
+    dy tiles and split-K reduction when the LDS-DMA path runs it, else by cfm_colsum."""
     M, N = dy.shape
     K = x.shape[1]
     if split_k is None:
         tiles = ((N + 127) // 128) * ((K + 127) // 128)
-        split_k = max(1, min(16, 512 // max(tiles, 1), M // 1024))
+        split_k = max(1, min(16, _WGRAD_WGS // max(tiles, 1), M // 1024))
     if out is None:
         out = torch.empty(N, K, device=dy.device, dtype=torch.float32)
     ws = None
+    fused = False
     if split_k > 1:
         if K % 4 == 0:       # deterministic slab reduction (no atomics, no zero-fill)
-            ws = torch.empty(split_k * N * K, device=dy.device, dtype=torch.float32)
+            fused = (bias_out is not None and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+                     and N % 8 == 0 and K % 8 == 0 and dy.is_contiguous() and x.is_contiguous())
+            ws = torch.empty(split_k * N * K + (split_k * N if fused else 0), device=dy.device, dtype=torch.float32)
         else:
             out.zero_()
-    return gemm(dy, x, out, N, K, M, a_kmajor=False, b_kmajor=False, lda=N, ldb=K, split_k=split_k, workspace=ws)
+    gemm(dy, x, out, N, K, M, a_kmajor=False, b_kmajor=False, lda=N, ldb=K, split_k=split_k, workspace=ws,
+         a_colsum=bias_out if fused else None)
+    if bias_out is not None and not fused:
+        colsum(dy, out=bias_out)
+    return out
 
 
 _ws_cache = {}

@@ -337,3 +337,18 @@ def test_layernorm_bwd_fused_dropout_output(D):
     torch.cuda.synchronize()
     assert torch.equal(dx0, dx1) and torch.equal(gg0, gg1) and torch.equal(gb0, gb1)
     assert torch.equal(g2, ref)
+
+
+@pytest.mark.parametrize("M,N,K,split", [(5000, 256, 144, 8), (11936, 2048, 512, None), (3000, 512, 512, 1),
+                                         (2000, 1536, 512, 4)])
+def test_wgrad_fused_bias_grad(M, N, K, split):
+    """linear_wgrad(bias_out=): the bias gradient sum_rows(dy) from the weight-gradient GEMM's staged dy
+    tiles + split-K reduction (cfm_gemm_desc.a_colsum), or cfm_colsum when split-K is off."""
+    g = torch.Generator().manual_seed(M + N)
+    dy = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    db = torch.empty(N, device=DEV)
+    dw = ops.linear_wgrad(dy, x, split_k=split, bias_out=db)
+    torch.cuda.synchronize()
+    assert _rel(db, dy.double().sum(0)) < 1e-5
+    assert _rel(dw, dy.double().t() @ x.double()) < 1e-5
