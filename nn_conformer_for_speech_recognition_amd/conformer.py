@@ -19,8 +19,6 @@ from __future__ import annotations
 
 import math
 
-import os
-
 import torch
 import torch.nn as nn
 
@@ -136,15 +134,10 @@ class _Side:
         self.keep = []
 
 
-_DIAG_SKIP_WGRAD = os.environ.get("CFM_DIAG_SKIP_WGRAD") == "1"   # timing diagnostics only: wrong grads
-
-
 def _wgrad_bias(side, dy, x):
     """(dW, db) = (dyᵀ·x, Σ_rows dy) on the side stream (outputs allocated on the main stream)."""
     dw = torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=torch.float32)
     db = torch.empty(dy.shape[1], device=dy.device, dtype=torch.float32)
-    if _DIAG_SKIP_WGRAD:
-        return dw, db
     side.run(lambda: ops.linear_wgrad(dy, x, out=dw, bias_out=db), dy, x, dw, db)
     return dw, db
 
