@@ -712,19 +712,25 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     if (kt + NST - 1 < nk) issue(kt + NST - 1);   // refills the stage every wave finished reading at kt-1
     const char* sa = lds + (kt % NST) * G::STAGE;
     const char* sb = sa + G::ABYTES;
+    // every fragment of the stage is read up front (the stage is complete after the barrier), so the
+    // LDS latency of later k-steps hides under the MFMAs of earlier ones
+    constexpr int KST = BKt / 16;
+    bf16x8 af[KST][FM], bfr[KST][FN];
 #pragma unroll
-    for (int kk = 0; kk < BKt; kk += 16) {
-      bf16x8 af[FM], bfr[FN];
+    for (int q = 0; q < KST; ++q) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = pipe_frag<AK, BMt, BKt>(sa, wm * FM * 32 + i * 32, kk, lane);
+      for (int j = 0; j < FN; ++j) bfr[q][j] = pipe_frag<BKM, BN, BKt>(sb, wn * FN * 32 + j * 32, 16 * q, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = pipe_frag<BKM, BN, BKt>(sb, wn * FN * 32 + j * 32, kk, lane);
+      for (int i = 0; i < FM; ++i) af[q][i] = pipe_frag<AK, BMt, BKt>(sa, wm * FM * 32 + i * 32, 16 * q, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (the scheduler would sink them)
+#pragma unroll
+    for (int q = 0; q < KST; ++q)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[q][i], bfr[q][j], acc[i][j], 0, 0, 0);
     if constexpr (!AK) {
       if (acs) {
 #pragma unroll
@@ -979,13 +985,18 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
       hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob, GatherA{});
       return;
     }
+    if (v == 7) {   // V192 with a 4-deep ring (160 KiB: three K tiles in flight)
+      const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
+      hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 4, 1, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob, GatherA{});
+      return;
+    }
     if (v == 6) {   // 192 x 128 tiles, 4 waves of 96x64, BK 32: two workgroups per CU
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
       hipLaunchKernelGGL((gemm_pipe_kernel<192, 32, 3, 2, AK, BKM, 4, 2>), g192, dim3(256), 0, s, p, oa, ob, GatherA{});
       return;
     }
   }
-  if (v == 5 || v == 6) v = 0;
+  if (v >= 5) v = 0;
   if (!v) {
     // auto: short reductions (K <= 512: the epilogue is a large share of the tile's time) run two
     // 256-row workgroups per CU so one's epilogue hides under the other's MFMAs; long ones keep BK 64
