@@ -137,6 +137,12 @@ typedef struct cfm_gemm_desc {
                               a_colsum[m] = sum_k A(m, k) -- the bias gradient of a weight-gradient GEMM
                               dW = dY^T X (A = dY^T) -- from the staged A tiles; workspace then needs
                               split_k*M more floats.  NULL: off. */
+  const void* rowdot_with; /* optional (bf16 C, LDS-DMA path, N % 64 == 0, batch 1, no split): per row m = b*T + t and
+                              64-column group g, rowdot_out[(b * N/64 + g) * T + t] = sum_n C[m][n] * rowdot_with[m*ldc + n]
+                              over the bf16-rounded C -- attention's D = rowsum(dO * O) per head (dk = 64) from the
+                              out-projection data-gradient GEMM that produces dO.  NULL: off. */
+  float* rowdot_out;
+  int rowdot_T;
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 /* kernel-selection switch for A/B measurements: bit 0 = 256-row register-staged tiles allowed,
@@ -237,6 +243,12 @@ int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, const float* 
                  const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                  void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H,
                  int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream);
+/* The same with D = rowsum(dO * O) already in ws (cfm_gemm_desc.rowdot_* of the GEMM that produced dout):
+   the D kernel is skipped.  bf16 MFMA path only (no rel-pos, dk <= 64); others behave as cfm_attn_bwd. */
+int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* dout, const float* lse,
+                        const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
+                        void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H,
+                        int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream);
 
 /* ---------------------------------------------------------------- ConvSubSampling
  * lib/convsubsampling.py:16-45: Conv2d(1->C1, 7x7, s2) -> Conv2d(C1->C2, 3x3, s2), no padding.

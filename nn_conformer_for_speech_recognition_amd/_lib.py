@@ -41,6 +41,7 @@ class GemmDesc(ctypes.Structure):
         ("workspace", c_void_p),
         ("probe", c_void_p),
         ("a_colsum", c_void_p),
+        ("rowdot_with", c_void_p), ("rowdot_out", c_void_p), ("rowdot_T", c_int),
     ]
 
 
@@ -101,6 +102,9 @@ _SIGS = {
                              c_int, c_int, c_int, c_float, c_u64, c_void_p]),
     "cfm_attn_bwd_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "cfm_attn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
+                             c_u64, c_void_p, c_void_p]),
+    "cfm_attn_bwd_with_d": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
                              c_u64, c_void_p, c_void_p]),
     "cfm_conv1_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),

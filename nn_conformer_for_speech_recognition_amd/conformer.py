@@ -221,8 +221,16 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
     B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
     g4 = _g2(g, g2, "mha", cfg, seed)
     grads[10], grads[11] = _wgrad_bias(side, g4, o)
-    do = ops.linear_dgrad(g4, wout, wt=_wt(cfg, 10))
-    dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
+    wt = _wt(cfg, 10)
+    if wt is not None and not cfg.rel and d // H == 64 and cd == torch.bfloat16 and "rowdot" not in ops.DISABLED:
+        # D = rowsum(dO * O) per head from the epilogue of the GEMM producing dO (no separate pass)
+        Dh = torch.empty(B * H * T, device=g4.device, dtype=torch.float32)
+        do = ops.linear_dgrad(g4, wout, wt=wt, rowdot=(o, Dh, T))
+    else:
+        Dh = None
+        do = ops.linear_dgrad(g4, wout, wt=wt)
+    dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed,
+                                        D=Dh)
     if cfg.rel:
         rgrads[0] = ops.linear_wgrad(_w(dpos, cd), _w(cfg.pe, cd))
         rgrads[1] = dpu.view(H, d // H)
@@ -317,7 +325,12 @@ class _ConformerLayerFn(torch.autograd.Function):
         # each LayerNorm backward also emits the next module's dropout-scaled input gradient (g2)
         ffn2_in = _in_drop("ffn", cfg, s + 30)
         conv_in, mha_in, ffn1_in = _in_drop("conv", cfg, s + 10), _in_drop("mha", cfg, s + 20), _in_drop("ffn", cfg, s)
-        g, grads[28], grads[29], g2 = ops.layernorm_bwd(gout, x4, P[28], mu5, rs5, side=side, drop=ffn2_in)
+        if "lndrop" in ops.DISABLED:
+            ffn2_in = conv_in = mha_in = ffn1_in = None
+        if ffn2_in is None:
+            (g, grads[28], grads[29]), g2 = ops.layernorm_bwd(gout, x4, P[28], mu5, rs5, side=side), None
+        else:
+            g, grads[28], grads[29], g2 = ops.layernorm_bwd(gout, x4, P[28], mu5, rs5, side=side, drop=ffn2_in)
         if cfg.conv_first:
             g, g2 = _ffn_bwd(g, x3, sv4, P, 22, cfg, s + 30, grads, side, g2, mha_in)
             g, g2 = _mha_bwd(g, c1, sva, P, R, cfg, s + 20, lens, grads, rgrads, side, g2, conv_in)

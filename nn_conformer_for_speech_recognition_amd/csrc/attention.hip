@@ -920,14 +920,15 @@ CFM_EXPORT size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel, in
   return (size_t)B * H * T * sizeof(float);
 }
 
-CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, const float* lse,
-                            const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
-                            void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
-                            int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
+static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const float* lse,
+                         const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
+                         void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
+                         int dtype, float drop_p, uint64_t seed, float* ws, void* stream, bool d_ready) {
   CFM_REQUIRE(qkv && o && dout && lse && lengths && dqkv && ws, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0, CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(!pos || (pos_u && pos_v && dpos && dpos_u && dpos_v), CFM_ERR_ARG, "rel-pos grads need buffers");
   hipStream_t s = cfm::as_stream(stream);
+  CFM_REQUIRE(!d_ready || use_mfma(dtype, pos, dk), CFM_ERR_UNSUPPORTED, "precomputed D: bf16 MFMA path only");
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_bwd_launch(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B,
                                      T, H, dk, dtype, drop_p, seed, ws, s);
@@ -937,8 +938,9 @@ CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, co
   const long nrow = (long)B * H * T;
   (void)nrow;
   CFM_REQUIRE(H * dk <= 1024, CFM_ERR_UNSUPPORTED, "H*dk must be <= 1024");
-  hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s,
-                     (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
+  if (!d_ready)
+    hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s,
+                       (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
   if (use_head(T) && (g_attn_mode & 8) != 0)
     hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), dkdv_wave_lds_bytes(T), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);
@@ -955,6 +957,22 @@ CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, co
     hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse, ws,
                        (bf16*)dqkv);
   return cfm::check_launch("cfm_attn_bwd");
+}
+
+CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, const float* lse,
+                            const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
+                            void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
+                            int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
+  return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H, dk, dtype,
+                       drop_p, seed, ws, stream, false);
+}
+
+CFM_EXPORT int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* dout, const float* lse,
+                                   const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
+                                   void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
+                                   int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
+  return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H, dk, dtype,
+                       drop_p, seed, ws, stream, true);
 }
 
 CFM_EXPORT int cfm_attn_set_mode(int mode) {

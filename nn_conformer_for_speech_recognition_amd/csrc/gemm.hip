@@ -40,6 +40,9 @@ struct GemmP {
   int dbg;     // timing experiments only (cfm_gemm_set_mode bit 3): skip the epilogue's stores
   unsigned long long* probe;   // optional timing slot (cfm_gemm_desc.probe)
   float* acs_slab;             // A column-sum partials [split][M] (cfm_gemm_desc.a_colsum) or nullptr
+  const bf16* rd_with;         // per-64-column-group row dots with C (cfm_gemm_desc.rowdot_*) or nullptr
+  float* rd_out;
+  int rd_T;
 };
 
 __device__ __forceinline__ long out_row(const GemmP& p, int m) {
@@ -497,7 +500,24 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
       const float4 lo = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8);
       const float4 hi = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8 + 4);
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      epilogue_store8(p, z, zs, m0 + RC * hf + row, n0 + c8, v);
+      const int m = m0 + RC * hf + row;
+      epilogue_store8(p, z, zs, m, n0 + c8, v);
+      if (p.rd_out) {   // (vectorised bf16 epilogue: v now holds the stored values) 8-lane group = 64 columns
+        float t = 0.f;
+        if (m < p.M && n0 + c8 < p.N) {
+          const uint4 u = *reinterpret_cast<const uint4*>(p.rd_with + (long)m * p.ldc + n0 + c8);
+          const bf16x8 w = __builtin_bit_cast(bf16x8, u);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t += (float)(bf16)v[e] * (float)w[e];
+        }
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        if ((tid & 7) == 0 && m < p.M && n0 + c8 < p.N) {
+          const int b = m / p.rd_T, tt = m - b * p.rd_T, g = (n0 + c8) >> 6;
+          p.rd_out[((long)b * (p.N >> 6) + g) * p.rd_T + tt] = t;
+        }
+      }
     }
     if (hf + 1 < WM / CHB) __syncthreads();
   }
@@ -1075,6 +1095,15 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   if (split > 1 && d->workspace) {
     CFM_REQUIRE(d->N % 4 == 0 && d->ldc % 4 == 0, CFM_ERR_SHAPE, "slab split-K needs N % 4 == 0");
     p.slab = d->workspace;
+  }
+  if (d->rowdot_out) {
+    CFM_REQUIRE(bf && d->dtype_c == CFM_BF16 && d->rowdot_with && d->N % 64 == 0 && d->rowdot_T > 0 &&
+                d->M % d->rowdot_T == 0 && split == 1 && d->batch == 1 && (g_gemm_mode & 2) &&
+                pipe_ok(*d, p, va, vb) && ((uintptr_t)d->rowdot_with % 16) == 0,
+                CFM_ERR_UNSUPPORTED, "rowdot needs bf16 C on the LDS-DMA path, N % 64 == 0, no split-K, batch 1");
+    p.rd_with = (const bf16*)d->rowdot_with;
+    p.rd_out = d->rowdot_out;
+    p.rd_T = d->rowdot_T;
   }
   if (d->a_colsum) {
     CFM_REQUIRE(bf && !d->a_kmajor && p.slab && d->batch == 1 && (g_gemm_mode & 2) && pipe_ok(*d, p, va, vb),

@@ -21,7 +21,7 @@ def _gemm_desc(**kw):
 def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, alpha=1.0,
          bias=None, act=ACT_NONE, act_grad=False, pre=None, drop_p=0.0, seed=0, offset=0, out_scale=1.0,
          residual=None, ldr=None, split_k=1, batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None,
-         a_colsum=None):
+         a_colsum=None, rowdot=None):
     """C = epilogue(alpha * A·Bᵀ) — see cfm_gemm_desc in include/cfm.h."""
     if A.dtype != B.dtype:
         raise L.CfmError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
@@ -35,7 +35,9 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         drop_p=float(drop_p), drop_seed=int(seed) & (2**64 - 1), drop_offset=int(offset),
         out_scale=float(out_scale), residual=L.ptr(residual),
         ldr=ldr if ldr is not None else N, dtype_r=L.dt(residual) if residual is not None else F32,
-        split_k=int(split_k), workspace=L.ptr(workspace), a_colsum=L.ptr(a_colsum))
+        split_k=int(split_k), workspace=L.ptr(workspace), a_colsum=L.ptr(a_colsum),
+        rowdot_with=L.ptr(rowdot[0]) if rowdot else None, rowdot_out=L.ptr(rowdot[1]) if rowdot else None,
+        rowdot_T=int(rowdot[2]) if rowdot else 0)
     if PROBE is not None:
         PROBE("gemm", (M, N, K), d, lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
     else:
@@ -58,7 +60,7 @@ def linear(x, w, bias=None, out_dtype=None, act=ACT_NONE, pre=None, drop_p=0.0, 
 
 
 def linear_dgrad(dy, w, out_dtype=None, pre=None, act_grad=False, drop_p=0.0, seed=0, offset=0, out=None,
-                 wt=None):
+                 wt=None, rowdot=None):
     """dx = dy·w for dy (M, N), w (N, K); optional silu'/dropout-mask epilogue (backward of the
     producing GEMM's epilogue).  wt: optional (K, N) row-major copy of wᵀ (CastTBatch) -- then both
     operands are read K-major, the faster GEMM path."""
@@ -70,10 +72,13 @@ def linear_dgrad(dy, w, out_dtype=None, pre=None, act_grad=False, drop_p=0.0, se
         if tuple(wt.shape) != (K, N) or not wt.is_contiguous() or wt.dtype != dy.dtype:
             raise L.CfmError(f"linear_dgrad: wt must be a contiguous ({K}, {N}) {dy.dtype} copy of w^T")
         return gemm(dy, wt, out, M, K, N, a_kmajor=True, b_kmajor=True, lda=N, ldb=N, act_grad=act_grad, pre=pre,
-                    drop_p=drop_p, seed=seed, offset=offset)
+                    drop_p=drop_p, seed=seed, offset=offset, rowdot=rowdot)
     return gemm(dy, w, out, M, K, N, a_kmajor=True, b_kmajor=False, lda=N, ldb=K, act_grad=act_grad, pre=pre,
                 drop_p=drop_p, seed=seed, offset=offset)
 
+
+# fusions that can be switched off for same-box A/B timing: CFM_DISABLE="rowdot,lndrop,wgbias"
+DISABLED = frozenset(x for x in os.environ.get("CFM_DISABLE", "").split(",") if x)
 
 # target workgroup count (in 128x128-tile units) of the split-K weight-gradient GEMMs
 _WGRAD_WGS = int(os.environ.get("CFM_WGRAD_WGS", "512"))
@@ -350,14 +355,21 @@ def attn_fwd(qkv, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, dr
     return o, lse
 
 
-def attn_bwd(qkv, o, dout, lse, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, drop_p=0.0, seed=0):
+def attn_bwd(qkv, o, dout, lse, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, drop_p=0.0, seed=0,
+             D=None):
+    """D: optional (B*H*T,) fp32 rowsum(dO * O) per head, precomputed by the GEMM that produced dout
+    (linear_dgrad(rowdot=...)); bf16 MFMA path only."""
     rel = pos is not None
-    ws = workspace(L.size_call("cfm_attn_bwd_ws_bytes", B, T, H, dk, int(rel), L.dt(qkv)), qkv.device)
+    if D is not None:
+        ws = D
+    else:
+        ws = workspace(L.size_call("cfm_attn_bwd_ws_bytes", B, T, H, dk, int(rel), L.dt(qkv)), qkv.device)
     dqkv = torch.empty_like(qkv)
     dpos = torch.empty(pos.shape, device=qkv.device, dtype=torch.float32) if rel else None
     dpu = torch.empty(H * dk, device=qkv.device, dtype=torch.float32) if rel else None
     dpv = torch.empty(H * dk, device=qkv.device, dtype=torch.float32) if rel else None
-    L.call("cfm_attn_bwd", L.ptr(qkv), L.ptr(o), L.ptr(dout), L.ptr(lse), L.ptr(lengths_i32), L.ptr(pos),
+    L.call("cfm_attn_bwd_with_d" if D is not None else "cfm_attn_bwd", L.ptr(qkv), L.ptr(o), L.ptr(dout), L.ptr(lse),
+           L.ptr(lengths_i32), L.ptr(pos),
            L.ptr(pos_u), L.ptr(pos_v), L.ptr(dqkv), L.ptr(dpos), L.ptr(dpu), L.ptr(dpv), B, T, H, dk, L.dt(qkv),
            float(drop_p), int(seed) & (2**64 - 1), L.ptr(ws), L.stream())
     return dqkv, dpos, dpu, dpv

@@ -64,3 +64,23 @@ def test_attention_kernels_agree_under_dropout(attn_mode):
     for o, d in outs[1:]:
         assert _rel(o, outs[0][0]) < 1e-2
         assert _rel(d, outs[0][1]) < 2e-2
+
+
+def test_rowdot_epilogue_feeds_attention_bwd():
+    """D = rowsum(dO * O) per head from the out-projection dgrad GEMM's epilogue (cfm_gemm_desc.rowdot_*)
+    equals the separate D pass, and cfm_attn_bwd_with_d reproduces cfm_attn_bwd."""
+    B, T, H, dk = 3, 97, 8, 64
+    g = torch.Generator().manual_seed(21)
+    qkv = torch.randn(B * T, 3 * H * dk, generator=g).to(DEV, torch.bfloat16)
+    lens = torch.tensor([T, 80, 50], dtype=torch.int32, device=DEV)
+    o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=0.1, seed=4)
+    g4 = torch.randn(B * T, H * dk, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(H * dk, H * dk, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    D = torch.empty(B * H * T, device=DEV)
+    do = ops.linear_dgrad(g4, w, wt=w.t().contiguous(), rowdot=(o, D, T))
+    ref = (do.float() * o.float()).view(B, T, H, dk).sum(-1).permute(0, 2, 1).reshape(-1)
+    torch.cuda.synchronize()
+    assert _rel(D, ref) < 1e-5
+    d1, _, _, _ = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=0.1, seed=4)
+    d2, _, _, _ = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=0.1, seed=4, D=D)
+    assert _rel(d2.float(), d1.float()) < 1e-3
