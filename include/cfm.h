@@ -100,6 +100,21 @@ int cfm_cast_transpose_batch(const cfm_castT_task* tasks, int ntasks, long nbloc
 int cfm_specaug_apply(const float* x, float* y, int B, int F, int T, const int32_t* params,
                       int n_params, int intended, float mask_value, void* stream);
 
+/* ---------------------------------------------------------------- log-mel front-end
+ * Replaces the CPU feature step of lib/standard/speechcommands.py:113-119:
+ * librosa.feature.melspectrogram(y, sr, n_mels) (periodic Hann, center=True zero padding, |rfft|^2,
+ * Slaney mel bank) -> np.where(mel < 1e-10, 0, log(mel)) -> per-utterance min-max (normalize != 0),
+ * frames past 1 + lens[b] / hop zero (the collate's padding, speechcommands.py:188).
+ * wave (B, ld_wave) fp32, lens (B,) int32 samples; n_fft a power of two in [16, 4096];
+ * window (n_fft,) fp32; twiddle (n_fft/2) complex fp32 pairs exp(-2 pi i k / n_fft);
+ * filter m = mel_w[mel_off[m] ...+ mel_cnt[m]) applied to power bins mel_lo[m] ...;
+ * out (B, n_mels, nT) fp32; ws >= cfm_logmel_ws_bytes(B, nT). */
+size_t cfm_logmel_ws_bytes(int B, int nT);
+int cfm_logmel_fwd(const float* wave, long ld_wave, const int32_t* lens, int B, int n_fft, int hop,
+                   const float* window, const float* twiddle, const int32_t* mel_lo, const int32_t* mel_cnt,
+                   const int32_t* mel_off, const float* mel_w, int n_mels, int nT, int normalize, float* out,
+                   float* ws, void* stream);
+
 /* ---------------------------------------------------------------- GEMM (MFMA)
  * C[z][m][n] = epilogue( alpha * sum_k A(m,k) * B(n,k) )  for z in [0, batch).
  * Serves every dense contraction of the encoder (torch.nn.Linear / 1x1 Conv1d forward,
@@ -145,6 +160,17 @@ typedef struct cfm_gemm_desc {
   int rowdot_T;
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
+/* Grouped weight gradients: every dW_i (N_i x K_i, fp32) = dY_i^T X_i over the same M tokens (dY_i (M x N_i),
+   X_i (M x K_i) bf16 row-major) and optionally db_i = sum_rows dY_i, in ONE launch of 256x128 tiles that each
+   run the whole token reduction (no split-K).  The caller fills a HOST table (cfm_wgrad_group_fill, one
+   entry of cfm_wgrad_group_task_bytes() per GEMM, tile0 = running sum of cfm_wgrad_group_tiles), copies it
+   to the device and launches total_tiles workgroups.  Replaces the per-GEMM split-K weight gradients of
+   the encoder backward (torch autograd's per-Linear mm for grad_weight, FunctionsManual.cpp). */
+size_t cfm_wgrad_group_task_bytes(void);
+long cfm_wgrad_group_tiles(int N, int K);
+int cfm_wgrad_group_fill(void* host_table, int i, const void* dy, const void* x, float* dw, float* db, int M,
+                         int N, int K, long tile0);
+int cfm_wgrad_group(const void* dev_table, int ntasks, long total_tiles, void* stream);
 /* kernel-selection switch for A/B measurements: bit 0 = 256-row register-staged tiles allowed,
    bit 1 = LDS-DMA pipelined kernel allowed, bit 3 = timing experiment (pipelined kernel skips its
    stores), bits 4-5 = pipelined variant (0 auto, 1 256x128/BK64, 2 256x128/BK32 two per CU,

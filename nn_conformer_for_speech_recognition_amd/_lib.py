@@ -58,6 +58,11 @@ _SIGS = {
     "cfm_specaug_apply": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p]),
     "cfm_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "cfm_gemm_set_mode": (c_int, [c_int]),
+    "cfm_wgrad_group_task_bytes": (c_size_t, []),
+    "cfm_wgrad_group_tiles": (c_long, [c_int, c_int]),
+    "cfm_wgrad_group_fill": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                     c_long]),
+    "cfm_wgrad_group": (c_int, [c_void_p, c_int, c_long, c_void_p]),
     "cfm_attn_set_mode": (c_int, [c_int]),
     "cfm_colreduce": (c_int, [c_void_p, c_int, c_long, c_long, c_void_p, c_int, c_void_p]),
     "cfm_colsum": (c_int, [c_void_p, c_int, c_long, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p]),

@@ -96,7 +96,7 @@ _REL_PNAMES = ["self_attn.linear_pos.weight", "self_attn.pos_bias_u", "self_attn
 
 class _Cfg:
     __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
-                 "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t")
+                 "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t", "group_wgrad", "layer_index")
 
 
 # the 2-D (and pointwise-conv) weight matrices of _PNAMES: cast to the compute dtype once per step
@@ -121,6 +121,7 @@ class _Side:
             _SIDE_STREAMS[key] = torch.cuda.Stream(device)
         self.side = _SIDE_STREAMS[key]
         self.keep = []
+        self.group = None      # ops.WgradGroup when this layer's weight gradients are deferred
 
     def run(self, fn, *inputs):
         self.side.wait_stream(self.main)
@@ -134,8 +135,15 @@ class _Side:
         self.keep = []
 
 
+# weight gradients of the encoder deferred to ONE grouped launch at the end of its backward (per device)
+_WGRAD_GROUPS = {}
+
+
 def _wgrad_bias(side, dy, x):
-    """(dW, db) = (dyᵀ·x, Σ_rows dy) on the side stream (outputs allocated on the main stream)."""
+    """(dW, db) = (dyᵀ·x, Σ_rows dy): queued for the grouped launch (side.group) when the layer defers its
+    weight gradients, else on the side stream (outputs allocated on the main stream)."""
+    if side.group is not None and ops.wgrad_group_ok(dy, x):
+        return side.group.add(dy, x)
     dw = torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=torch.float32)
     db = torch.empty(dy.shape[1], device=dy.device, dtype=torch.float32)
     side.run(lambda: ops.linear_wgrad(dy, x, out=dw, bias_out=db), dy, x, dw, db)
@@ -322,6 +330,10 @@ class _ConformerLayerFn(torch.autograd.Function):
         s = cfg.seed
         gout = gout.contiguous()
         side = _Side(gout.device)
+        # defer this layer's weight-gradient GEMMs into the encoder-wide grouped launch (flushed by layer 0,
+        # the last to run backward) when no parameter accumulates into an existing .grad
+        if cfg.group_wgrad and all(p.grad is None for p in params):
+            side.group = _WGRAD_GROUPS.setdefault(str(gout.device), ops.WgradGroup())
         # each LayerNorm backward also emits the next module's dropout-scaled input gradient (g2)
         ffn2_in = _in_drop("ffn", cfg, s + 30)
         conv_in, mha_in, ffn1_in = _in_drop("conv", cfg, s + 10), _in_drop("mha", cfg, s + 20), _in_drop("ffn", cfg, s)
@@ -341,6 +353,10 @@ class _ConformerLayerFn(torch.autograd.Function):
             g, g2 = _mha_bwd(g, c0, sva, P, R, cfg, s + 20, lens, grads, rgrads, side, g2, ffn1_in)
         g, _ = _ffn_bwd(g, x0, sv1, P, 0, cfg, s, grads, side, g2, None)
         side.join()
+        if cfg.layer_index == 0:
+            grp = _WGRAD_GROUPS.get(str(gout.device))
+            if grp is not None:
+                grp.flush()
         ctx.sv = None
         return (g, None, None, *grads, *rgrads)
 
@@ -372,7 +388,8 @@ class ConformerLayer(nn.Module):
             ps += [sd[n] for n in _REL_PNAMES]
         return ps
 
-    def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None, shadow=None):
+    def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None, shadow=None, layer_index=0,
+                       group_wgrad=False):
         """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device; shadow: optional
         ({param index: compute-dtype copy}, {param index: its transposed K-major copy}) of this
         layer's weight matrices (see Conformer._shadows)."""
@@ -389,6 +406,8 @@ class ConformerLayer(nn.Module):
         cfg.bn_rm, cfg.bn_rv = bn.running_mean, bn.running_var
         cfg.bn_mom = bn.momentum if bn.momentum is not None else 0.1
         cfg.pe = pe
+        cfg.layer_index = layer_index
+        cfg.group_wgrad = bool(group_wgrad) and "wgroup" not in ops.DISABLED
         if self.training and bn.track_running_stats:
             bn.num_batches_tracked.add_(1)
         return _ConformerLayerFn.apply(x, lens_i32, cfg, *self.params())
@@ -451,8 +470,12 @@ class Conformer(nn.Module):
             self._step += 1
         pe = self._pe(T, x.device) if self.pos_enc == "rel" else None
         shadows = self._shadows(x.device)
+        # grouped weight gradients need layer 0 to run backward last (it flushes the group): true for the
+        # sequential encoder; deferral is per layer and falls back when a .grad accumulates
+        group = self.compute_dtype == torch.bfloat16
         for i, layer in enumerate(self.conformer_layers):
-            x = layer.forward_tokens(x, lens_i32, B, T, self.compute_dtype, seed + 100 * i, pe, shadows[i])
+            x = layer.forward_tokens(x, lens_i32, B, T, self.compute_dtype, seed + 100 * i, pe, shadows[i],
+                                     layer_index=i, group_wgrad=group)
         return x
 
     def forward(self, input, lengths):

@@ -556,6 +556,8 @@ struct GatherA {
   long sB;
   int sI, sJ, Cr, Ck, Ilim, Jlim;
   int di[9], dj[9], dR[9];
+  const void* group_tab;   // grouped launch (GROUP kernels): device WgTask table, one task per GEMM
+  int group_n;
 };
 
 // BMt x 128 tile, BKt-deep K steps, NST-stage ring, NWV waves; the f32 epilogue staging aliases the ring
@@ -570,9 +572,14 @@ struct PipeGeo {
   static_assert(AI * NW * 1024 == ABYTES && BI * NW * 1024 == BBYTES, "whole wave-instructions per stage");
 };
 
+// the descriptor is wave-uniform by construction; readfirstlane makes that visible to the compiler even
+// when the operand comes from memory (grouped launches), so no waterfall loop wraps the buffer loads
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pipe_rsrc(const PipeOp& o, int z) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(o.base + (long)z * o.bstride), (short)0, (int)o.bytes,
-                                           0x00020000);
+  const uint64_t a = (uint64_t)(uintptr_t)(o.base + (long)z * o.bstride);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane((int)o.bytes), 0x00020000);
 }
 
 // one wave-instruction of LDS-DMA: lane l's 16 B from rsrc + voff land at lds_base + 16 l
@@ -637,7 +644,11 @@ __device__ __forceinline__ void wait_stages(int younger) {
 // NWV waves as WM x WN, each owning FM x FN 32x32 accumulators: (BMt, NWV, WN) = (256, 8, 2) ->
 // 64x64 per wave; (192, 8, 4) -> 96x32 per wave (192-row tiles: 63 x N/128 tiles of the encoder's
 // M = 11,936 fill the 256 CUs in whole rounds); (128, 4, 2) -> 64x64.
-template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2, bool GA = false>
+struct WgTask;   // grouped weight-gradient task (below)
+__device__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn);
+
+template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2, bool GA = false,
+          bool GROUP = false>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(OCC * NWV / 4)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   typedef PipeGeo<BMt, BKt, NST, NWV> G;
@@ -650,12 +661,17 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   int tm, tn, zz;
-  xcd_tile3(tm, tn, zz);
+  if constexpr (GROUP) {
+    group_task(ga, p, oa, ob, tm, tn);   // this workgroup's GEMM and tile of a grouped launch
+    zz = 0;
+  } else {
+    xcd_tile3(tm, tn, zz);
+  }
   const int m0 = tm * BMt, n0 = tn * BN;
   const int z = zz / p.split_k, ks = zz % p.split_k;
   const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, z), rb = pipe_rsrc(ob, z);
-  const int kbeg = ks * p.k_per_split;
-  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int kbeg = __builtin_amdgcn_readfirstlane(ks * p.k_per_split);
+  const int kend = __builtin_amdgcn_readfirstlane(min(p.K, kbeg + p.k_per_split));
   const int nk = kend > kbeg ? (kend - kbeg + BKt - 1) / BKt : 0;
 
   // per-lane source offsets of stage 0; later stages add k0 * (row stride) (MN-major) or k0 * 2
@@ -790,6 +806,50 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   __syncthreads();   // every wave done with the ring (no DMA outstanding) -> reuse it for the epilogue
   tile_epilogue_g<FM, FN, WM, WN, G::NTt>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane, tid);
   probe_end(p.probe);
+}
+
+// ---------------------------------------------------------------- grouped weight gradients
+// All weight-gradient GEMMs dW_i = dY_iᵀ X_i (+ bias gradient sum_rows dY_i) of a backward pass in ONE
+// launch: every task reduces over the same token dimension, so each 256x128 output tile is one
+// workgroup running the whole K loop (no split-K slabs, no reduce pass), and the ~3000 tiles of the
+// encoder's 17 layers fill the chip in whole rounds.  Workgroup -> (task, tile): XCD-contiguous ids
+// (xcd_tile order), tasks back to back (tile0 ascending), tiles row-major inside a task.
+struct WgTask {
+  GemmP p;
+  PipeOp oa, ob;
+  long tile0;
+  int tiles_n;
+  int pad;
+};
+static_assert(sizeof(WgTask) % 4 == 0, "word-copied task");
+
+__device__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn) {
+  const WgTask* tab = reinterpret_cast<const WgTask*>(ga.group_tab);
+  const int nwg = gridDim.x, L = blockIdx.x;
+  int id = L;
+  if (nwg > 8 && ga.Jn == 0) {   // Jn != 0: plain dispatch order (A/B)
+    const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+  }
+  int lo = 0, hi = ga.group_n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (__builtin_amdgcn_readfirstlane((int)tab[mid].tile0) <= id) lo = mid; else hi = mid - 1;
+  }
+  lo = __builtin_amdgcn_readfirstlane(lo);
+  // copy the task word by word through readfirstlane: the compiler then knows every field (buffer
+  // descriptors, loop bounds) is wave-uniform -- SGPRs, no waterfall loops around the buffer loads
+  WgTask t;
+  const int* src = reinterpret_cast<const int*>(tab + lo);
+  int* dst = reinterpret_cast<int*>(&t);
+#pragma unroll
+  for (int w = 0; w < (int)(sizeof(WgTask) / 4); ++w) dst[w] = __builtin_amdgcn_readfirstlane(src[w]);
+  p = t.p;
+  oa = t.oa;
+  ob = t.ob;
+  const int local = (int)(id - t.tile0);
+  tm = local / t.tiles_n;
+  tn = local % t.tiles_n;
 }
 
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
@@ -1123,6 +1183,47 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
                        (float*)d->C, d->ldc, d->stride_c, d->bias, p.acs_slab, d->a_colsum);
   }
   return cfm::check_launch("cfm_gemm");
+}
+
+CFM_EXPORT size_t cfm_wgrad_group_task_bytes(void) { return sizeof(WgTask); }
+CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, BN); }
+
+// fill task i of a HOST table: dW (N x K, fp32) = dYᵀ X over M tokens, dY (M x N) / X (M x K) bf16
+// row-major; db (N, fp32, may be NULL) = sum_rows dY; tile0 = first workgroup id of the task
+CFM_EXPORT int cfm_wgrad_group_fill(void* host_tab, int i, const void* dy, const void* x, float* dw, float* db, int M,
+                                    int N, int K, long tile0) {
+  CFM_REQUIRE(host_tab && dy && x && dw && i >= 0, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % 8 == 0, CFM_ERR_SHAPE, "N, K multiples of 8");
+  CFM_REQUIRE((long)M * N * 2 < (1L << 31) && (long)M * K * 2 < (1L << 31), CFM_ERR_SHAPE, "operands < 2 GiB");
+  CFM_REQUIRE((uintptr_t)dy % 16 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)dw % 16 == 0, CFM_ERR_ALIGN,
+              "16-B aligned operands");
+  WgTask t{};
+  t.p = plain_params(N, K, M, dw, K, CFM_F32);
+  t.p.k_per_split = split_k_for(t.p, BK16);
+  t.p.vec_c = vec_epilogue_ok(t.p);
+  t.p.acs_slab = db;   // single K slice: the column sums go straight to db
+  t.oa = PipeOp{(const bf16*)dy, N, 0, N, (unsigned)((long)M * N * 2)};
+  t.ob = PipeOp{(const bf16*)x, K, 0, K, (unsigned)((long)M * K * 2)};
+  t.tile0 = tile0;
+  t.tiles_n = cdiv(K, BN);
+  reinterpret_cast<WgTask*>(host_tab)[i] = t;
+  return CFM_OK;
+}
+
+CFM_EXPORT int cfm_wgrad_group(const void* dev_tab, int ntasks, long total_tiles, void* stream) {
+  CFM_REQUIRE(dev_tab && ntasks > 0 && total_tiles > 0 && total_tiles < (1L << 31), CFM_ERR_ARG, "bad table");
+  GatherA ga{};
+  ga.group_tab = dev_tab;
+  ga.group_n = ntasks;
+  const int gv = (g_gemm_mode >> 8) & 3;   // A/B: 1 = BK32 two per CU, 2 = plain dispatch order
+  ga.Jn = gv == 2;
+  if (gv == 1)
+    hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, false, false, 8, 2, false, true>), dim3((unsigned)total_tiles),
+                       dim3(512), 0, cfm::as_stream(stream), GemmP{}, PipeOp{}, PipeOp{}, ga);
+  else
+    hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, false, false, 8, 2, false, true>), dim3((unsigned)total_tiles),
+                       dim3(512), 0, cfm::as_stream(stream), GemmP{}, PipeOp{}, PipeOp{}, ga);
+  return cfm::check_launch("cfm_wgrad_group");
 }
 
 // ---------------------------------------------------------------------------- conv2 (3x3, s2)

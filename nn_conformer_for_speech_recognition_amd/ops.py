@@ -112,6 +112,82 @@ def linear_wgrad(dy, x, out=None, split_k=None, bias_out=None):
     return out
 
 
+class WgradGroup:
+    """Deferred weight gradients: add(dy, x) returns (dW, db) tensors that flush() fills with ONE grouped
+    launch (cfm_wgrad_group) -- dW = dyᵀ·x, db = Σ_rows dy, bf16 operands sharing the token count M.
+    The returned tensors must not be read before flush() (they are views, so autograd's AccumulateGrad
+    adopts them without a copy).  Tables are cached by operand pointers (fixed under graph replay)."""
+
+    POOL_BYTES = 8 << 20     # pinned staging for the task tables (allocated at the first, eager, flush)
+
+    def __init__(self):
+        self.tasks = []
+        self._cache = {}
+        self._pool = None
+        self._off = 0
+
+    def _stage(self, host):
+        """Copy a host table to the device through a slice of the persistent pinned pool: legal inside a
+        HIP-graph capture (pageable copies and pinned allocations are not), and every captured copy
+        keeps reading its own slice on replay (the pool only wraps after POOL_BYTES of tables)."""
+        n = host.nbytes
+        if self._pool is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise L.CfmError("WgradGroup: first flush inside a graph capture; run one eager step first")
+            self._pool = torch.empty(max(self.POOL_BYTES, n), dtype=torch.uint8).pin_memory()
+        if self._off + n > self._pool.numel():
+            self._off = 0
+        dst = self._pool[self._off:self._off + n]
+        dst.numpy()[:] = host
+        self._off += (n + 255) // 256 * 256
+        return dst.to(self.tasks[0][0].device, non_blocking=True)
+
+    def __len__(self):
+        return len(self.tasks)
+
+    def add(self, dy, x):
+        M, N = dy.shape
+        K = x.shape[1]
+        dw = torch.empty(N, K, device=dy.device, dtype=torch.float32)
+        db = torch.empty(N, device=dy.device, dtype=torch.float32)
+        self.tasks.append((dy, x, dw, db))
+        return dw.view(N, K), db.view(N)
+
+    def flush(self):
+        if not self.tasks:
+            return
+        import numpy as np
+        dev = self.tasks[0][0].device
+        key = tuple((t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), t[0].shape[0],
+                     t[0].shape[1], t[1].shape[1]) for t in self.tasks)
+        hit = self._cache.get(key)
+        if hit is None:
+            lib = L.load()
+            tb = L.size_call("cfm_wgrad_group_task_bytes")
+            host = np.zeros(tb * len(self.tasks), dtype=np.uint8)
+            tile0 = 0
+            for i, (dy, x, dw, db) in enumerate(self.tasks):
+                M, N = dy.shape
+                K = x.shape[1]
+                L.call("cfm_wgrad_group_fill", host.ctypes.data, i, L.ptr(dy), L.ptr(x), L.ptr(dw), L.ptr(db), M, N,
+                       K, tile0)
+                tile0 += lib.cfm_wgrad_group_tiles(N, K)
+            table = self._stage(host)
+            hit = (None, table, tile0)
+            if len(self._cache) > 8:
+                self._cache.clear()
+            self._cache[key] = hit
+        L.call("cfm_wgrad_group", L.ptr(hit[1]), len(self.tasks), hit[2], L.stream())
+        self.tasks = []
+
+
+def wgrad_group_ok(dy, x):
+    """Operands the grouped weight-gradient launch takes (else linear_wgrad per GEMM)."""
+    return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.is_contiguous() and x.is_contiguous()
+            and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0
+            and dy.numel() * 2 < 2 ** 31 and x.numel() * 2 < 2 ** 31)
+
+
 _ws_cache = {}
 
 

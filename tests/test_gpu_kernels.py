@@ -352,3 +352,22 @@ def test_wgrad_fused_bias_grad(M, N, K, split):
     torch.cuda.synchronize()
     assert _rel(db, dy.double().sum(0)) < 1e-5
     assert _rel(dw, dy.double().t() @ x.double()) < 1e-5
+
+
+def test_wgrad_group_matches_per_gemm():
+    """cfm_wgrad_group (one launch, whole token reduction per tile) against fp64 dyᵀ x and sum_rows dy."""
+    g = torch.Generator().manual_seed(8)
+    M = 1500
+    shapes = [(2048, 512), (512, 2048), (1536, 512), (512, 512), (1024, 512), (136, 72)]
+    grp = ops.WgradGroup()
+    outs, refs = [], []
+    for N, K in shapes:
+        dy = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+        x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+        outs.append(grp.add(dy, x))
+        refs.append((dy.double().t() @ x.double(), dy.double().sum(0)))
+    grp.flush()
+    torch.cuda.synchronize()
+    for (dw, db), (rw, rb) in zip(outs, refs):
+        assert _rel(dw, rw) < 1e-5
+        assert _rel(db, rb) < 1e-5
