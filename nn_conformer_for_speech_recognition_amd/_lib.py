@@ -56,6 +56,9 @@ _SIGS = {
     "cfm_cast_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
     "cfm_cast_transpose_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
     "cfm_specaug_apply": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "cfm_logmel_ws_bytes": (c_size_t, [c_int, c_int]),
+    "cfm_logmel_fwd": (c_int, [c_void_p, c_long, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "cfm_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "cfm_gemm_set_mode": (c_int, [c_int]),
     "cfm_wgrad_group_task_bytes": (c_size_t, []),
