@@ -12,7 +12,7 @@ import subprocess
 import torch  # noqa: F401  (load torch's libamdhip64 first: libcfm resolves to the same runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcfm.so")
+LIB_PATH = os.environ.get("CFM_LIB") or os.path.join(_HERE, "libcfm.so")   # CFM_LIB: A/B builds only
 CSRC = os.path.join(_HERE, "csrc")
 
 F32, BF16 = 0, 1
