@@ -73,36 +73,52 @@ template <int V> __device__ __forceinline__ void stv(bf16* p, const float (&v)[V
 }
 
 // ---------------------------------------------------------------- vectorised kernels
+// LN_FWD_ROWS rows per wave: every row's load is issued before the first reduction, so a wave keeps
+// that many 2-KB row reads in flight (one row per wave left the kernel latency-bound at ~50 % of HBM)
+constexpr int LN_FWD_ROWS = 2;
 template <int V, typename TY>
 __global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, TY* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
                                                   float eps) {
-  constexpr int D = 64 * V;
+  constexpr int D = 64 * V, R = LN_FWD_ROWS;
   const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  float v[V], g[V], b[V];
-  ldv<V>(x + row * D + lane * V, v);
-  float s = 0.f;
+  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= M) return;
+  float v[R][V], g[V], b[V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) s += v[i];
-  const float mean = wave_sum(s) * (1.f / D);
-  float q = 0.f;
+  for (int r = 0; r < R; ++r) {
+    if (row0 + r < M) {
+      ldv<V>(x + (row0 + r) * D + lane * V, v[r]);
+    } else {
 #pragma unroll
-  for (int i = 0; i < V; ++i) {
-    v[i] -= mean;
-    q += v[i] * v[i];
+      for (int i = 0; i < V; ++i) v[r][i] = 0.f;
+    }
   }
-  const float rstd = rsqrtf(wave_sum(q) * (1.f / D) + eps);
   ldv<V>(gamma + lane * V, g);
   ldv<V>(beta + lane * V, b);
 #pragma unroll
-  for (int i = 0; i < V; ++i) v[i] = v[i] * rstd * g[i] + b[i];
-  stv<V>(y + row * D + lane * V, v);
-  if (lane == 0) {
-    mean_out[row] = mean;
-    rstd_out[row] = rstd;
+  for (int r = 0; r < R; ++r) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) s += v[r][i];
+    const float mean = wave_sum(s) * (1.f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      v[r][i] -= mean;
+      q += v[r][i] * v[r][i];
+    }
+    const float rstd = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+    if (row0 + r < M) {    // wave-uniform
+#pragma unroll
+      for (int i = 0; i < V; ++i) v[r][i] = v[r][i] * rstd * g[i] + b[i];
+      stv<V>(y + (row0 + r) * D + lane * V, v[r]);
+      if (lane == 0) {
+        mean_out[row0 + r] = mean;
+        rstd_out[row0 + r] = rstd;
+      }
+    }
   }
 }
 
@@ -287,7 +303,7 @@ bool ln_fwd_fast(const void* x, int dtx, const float* gamma, const float* beta, 
                  float* rstd, long M, int D, float eps, hipStream_t s) {
   if (D != 64 * V || dtx != CFM_F32 || !aligned16(x) || !aligned16(y) || !aligned16(gamma) || !aligned16(beta))
     return false;
-  dim3 g((unsigned)((M + 3) / 4));
+  dim3 g((unsigned)((M + 4 * LN_FWD_ROWS - 1) / (4 * LN_FWD_ROWS)));
   if (dty == CFM_BF16)
     hipLaunchKernelGGL((ln_fwd_vec<V, bf16>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (bf16*)y, mean, rstd, M,
                        eps);
