@@ -139,6 +139,14 @@ class _Side:
 _WGRAD_GROUPS = {}
 
 
+def _has_grad_hooks(p):
+    """True when p has tensor backward hooks or post-accumulate-grad hooks (DDP's reducer, a per-layer
+    all-reduce hook, user hooks): those read .grad as soon as AccumulateGrad runs, so the layer's weight
+    gradients must not be deferred to the grouped launch.  torch DDP must not wrap this model (it hooks
+    every parameter and would disable the grouping); use dist.GradAllReducer."""
+    return bool(getattr(p, "_backward_hooks", None)) or bool(getattr(p, "_post_accumulate_grad_hooks", None))
+
+
 def _wgrad_bias(side, dy, x):
     """(dW, db) = (dyᵀ·x, Σ_rows dy): queued for the grouped launch (side.group) when the layer defers its
     weight gradients, else on the side stream (outputs allocated on the main stream)."""
@@ -332,8 +340,10 @@ class _ConformerLayerFn(torch.autograd.Function):
         side = _Side(gout.device)
         # defer this layer's weight-gradient GEMMs into the encoder-wide grouped launch (flushed by layer 0,
         # the last to run backward) when no parameter accumulates into an existing .grad
-        if cfg.group_wgrad and all(p.grad is None for p in params):
+        # (never when a parameter carries a gradient hook: hooks fire as .grad lands, before the flush)
+        if cfg.group_wgrad and all(p.grad is None and not _has_grad_hooks(p) for p in params):
             side.group = _WGRAD_GROUPS.setdefault(str(gout.device), ops.WgradGroup())
+            side.group.arm_final_flush()
         # each LayerNorm backward also emits the next module's dropout-scaled input gradient (g2)
         ffn2_in = _in_drop("ffn", cfg, s + 30)
         conv_in, mha_in, ffn1_in = _in_drop("conv", cfg, s + 10), _in_drop("mha", cfg, s + 20), _in_drop("ffn", cfg, s)

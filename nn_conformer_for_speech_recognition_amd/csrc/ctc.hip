@@ -40,7 +40,7 @@ __device__ __forceinline__ float lse3(float a, float b, float c) {
 }
 
 // extended label of state s
-__device__ __forceinline__ int ext_label(const int32_t* tg, int s, int blank) { return (s & 1) ? tg[s >> 1] : blank; }
+// (defined after CtcP: ext_label clamps the label ids)
 
 struct CtcP {
   const float* logits; long sb, st;   // row (b, t) at logits + b*sb + t*st (batch- or time-major)
@@ -59,6 +59,14 @@ struct CtcP {
 __device__ __forceinline__ const int32_t* tgt_of(const CtcP& p, int b) {
   return p.tgt + (p.off ? (long)p.off[b] : (long)b * p.ldt);
 }
+// lengths are device data: clamp to the buffers' extents (in_len <= T, tgt_len <= Smax) so that a bad
+// length can only give a wrong loss, never an access outside lpe / alpha / beta / sh[] (torch raises
+// on such inputs; the host wrapper validates host-side lengths the same way)
+__device__ __forceinline__ int in_len_of(const CtcP& p, int b) { return min(max(p.in_len[b], 0), p.T); }
+__device__ __forceinline__ int tgt_len_of(const CtcP& p, int b) { return min(max(p.tgt_len[b], 0), p.Smax); }
+// label u of an utterance, clamped to the class range (an out-of-range id would index x / corr[] out of bounds)
+__device__ __forceinline__ int label_of(const CtcP& p, const int32_t* tg, int u) { return min(max(tg[u], 0), p.V - 1); }
+__device__ __forceinline__ int ext_label(const CtcP& p, const int32_t* tg, int s) { return (s & 1) ? label_of(p, tg, s >> 1) : p.blank; }
 
 // ---------------------------------------------------------------------------------- prep
 __global__ __launch_bounds__(256) void ctc_prep(CtcP p) {
@@ -66,7 +74,7 @@ __global__ __launch_bounds__(256) void ctc_prep(CtcP p) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)p.B * p.T) return;
   const int b = (int)(row / p.T), t = (int)(row % p.T);
-  if (t >= p.in_len[b]) return;
+  if (t >= in_len_of(p, b)) return;
   const float* x = p.logits + b * p.sb + t * p.st;
   float m = NEG_INF;
   const bool v4 = (p.V % 4 == 0) && (p.sb % 4 == 0) && (p.st % 4 == 0) && ((uintptr_t)p.logits % 16 == 0);
@@ -91,10 +99,10 @@ __global__ __launch_bounds__(256) void ctc_prep(CtcP p) {
   s = wave_sum(s);
   const float l = m + logf(s);
   if (lane == 0) p.lse[row] = l;
-  const int Sb = 2 * p.tgt_len[b] + 1;
+  const int Sb = 2 * tgt_len_of(p, b) + 1;
   const int32_t* tg = tgt_of(p, b);
   float* dst = p.lpe + row * p.S;
-  for (int st = lane; st < Sb; st += 64) dst[st] = x[ext_label(tg, st, p.blank)] - l;
+  for (int st = lane; st < Sb; st += 64) dst[st] = x[ext_label(p, tg, st)] - l;
 }
 
 // ---------------------------------------------------------------------------------- alpha / beta
@@ -104,7 +112,7 @@ template <int SPT>
 __global__ __launch_bounds__(AB_THREADS) void ctc_alphabeta(CtcP p) {
   extern __shared__ float sh[];        // [2][S]
   const int b = blockIdx.x, dir = blockIdx.y, tid = threadIdx.x;
-  const int Tb = p.in_len[b], L = p.tgt_len[b], Sb = 2 * L + 1;
+  const int Tb = in_len_of(p, b), L = tgt_len_of(p, b), Sb = 2 * L + 1;
   const int32_t* tg = tgt_of(p, b);
   float* out = (dir == 0 ? p.alpha : p.beta) + (long)b * p.T * p.S;
   const float* lp = p.lpe + (long)b * p.T * p.S;
@@ -119,8 +127,8 @@ __global__ __launch_bounds__(AB_THREADS) void ctc_alphabeta(CtcP p) {
   for (int j = 0; j < SPT; ++j) {
     const int s = tid + AB_THREADS * j;
     sidx[j] = s;
-    if (dir == 0) skip[j] = s < Sb && s >= 2 && (s & 1) && ext_label(tg, s, p.blank) != ext_label(tg, s - 2, p.blank);
-    else skip[j] = s + 2 < Sb && (s & 1) && ext_label(tg, s, p.blank) != ext_label(tg, s + 2, p.blank);
+    if (dir == 0) skip[j] = s < Sb && s >= 2 && (s & 1) && ext_label(p, tg, s) != ext_label(p, tg, s - 2);
+    else skip[j] = s + 2 < Sb && (s & 1) && ext_label(p, tg, s) != ext_label(p, tg, s + 2);
   }
   // frame order: step i handles t = i (alpha) or Tb-1-i (beta)
   auto frame = [&](int i) { return dir == 0 ? i : Tb - 1 - i; };
@@ -193,7 +201,7 @@ __global__ __launch_bounds__(256) void ctc_grad(CtcP p, const float* grad_out, i
   const long row = blockIdx.x;
   const int b = (int)(row / p.T), t = (int)(row % p.T);
   TG* dst = g + b * gsb + t * gst;
-  const int Tb = p.in_len[b], L = p.tgt_len[b];
+  const int Tb = in_len_of(p, b), L = tgt_len_of(p, b);
   const float nll = p.nll_raw[b];
   if (t >= Tb || (zero_inf && isinf(nll))) {   // as torch: padded frames and zeroed infinite losses
     for (int v = threadIdx.x; v < p.V; v += 256) dst[v] = from_f32<TG>(0.f);
@@ -217,13 +225,13 @@ __global__ __launch_bounds__(256) void ctc_grad(CtcP p, const float* grad_out, i
   }
   // labels: the first occurrence of each label sums all its occurrences in label order
   for (int u = threadIdx.x - 64; u >= 0 && u < L; u += 192) {
-    const int c = tg[u];
+    const int c = label_of(p, tg, u);
     bool first = true;
-    for (int w = 0; w < u; ++w) first = first && tg[w] != c;
+    for (int w = 0; w < u; ++w) first = first && label_of(p, tg, w) != c;
     if (!first) continue;
     float s = 0.f;
     for (int w = u; w < L; ++w)
-      if (tg[w] == c) {
+      if (label_of(p, tg, w) == c) {
         const int st = 2 * w + 1;
         s += expf(p.alpha[base + st] + p.beta[base + st] + nll - p.lpe[base + st]);
       }

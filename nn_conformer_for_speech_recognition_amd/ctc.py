@@ -24,14 +24,28 @@ from . import ops
 _RED = ("none", "mean", "sum")
 
 
-def _lengths(v, B, device):
+def _lengths(v, B, device, limit=None, what="lengths"):
+    """(B,) int32 device lengths.  Host-side lengths (lists, CPU tensors) are validated against
+    `limit` as torch.nn.functional.ctc_loss does (it raises); device lengths are not read back (no
+    sync) -- the kernels clamp them to the buffers' extents instead."""
     if isinstance(v, (list, tuple)):
         v = torch.tensor(v)
     if not torch.is_tensor(v):
         raise TypeError("lengths must be tensors or sequences of ints")
     if v.numel() != B:
         raise ValueError(f"expected {B} lengths, got {v.numel()}")
+    if not v.is_cuda and v.numel() > 0:
+        lo, hi = int(v.min()), int(v.max())
+        if lo < 0:
+            raise ValueError(f"{what} must be non-negative, got {lo}")
+        if limit is not None and hi > limit:
+            raise ValueError(f"expected {what} to have value at most {limit}, but got value {hi}")
     return v.to(device=device, dtype=torch.int32).contiguous()
+
+
+def _check_blank(blank, V):
+    if not 0 <= blank < V:
+        raise ValueError(f"blank must be in label range [0, {V}), got {blank}")
 
 
 def _prep_targets(targets, tgt_len, B, device):
@@ -62,8 +76,10 @@ class _CTCFn(torch.autograd.Function):
             raise RuntimeError("ctc_loss runs on libcfm: fp32 CUDA log-probs/logits required")
         x = x if x.stride(-1) == 1 else x.contiguous()
         B = x.shape[0] if batch_first else x.shape[1]
-        il = _lengths(in_len, B, x.device)
-        tl = _lengths(tgt_len, B, x.device)
+        T = x.shape[1] if batch_first else x.shape[0]
+        _check_blank(blank, x.shape[-1])
+        il = _lengths(in_len, B, x.device, T, "input_lengths")
+        tl = _lengths(tgt_len, B, x.device, targets.shape[1] if targets.dim() == 2 else None, "target_lengths")
         tg, ldt, off, smax = _prep_targets(targets, tl, B, x.device)
         nll, ws = ops.ctc_loss_fwd(x, tg, ldt, off, il, tl, smax, blank, zero_infinity, batch_first)
         ctx.save_for_backward(x, tg, off if off is not None else tg, il, tl, ws)
@@ -110,8 +126,9 @@ class _CTCHeadFn(torch.autograd.Function):
         yc = y if y.dtype == cd else ops.cast(y, cd)
         wc = w if w.dtype == cd else ops.cast(w, cd)
         logits = ops.linear(yc, wc, b, out_dtype=torch.float32).view(B, T, -1)
-        il = _lengths(in_len, B, y.device)
-        tl = _lengths(tgt_len, B, y.device)
+        _check_blank(blank, w.shape[0])
+        il = _lengths(in_len, B, y.device, T, "input_lengths")
+        tl = _lengths(tgt_len, B, y.device, targets.shape[1] if targets.dim() == 2 else None, "target_lengths")
         tg, ldt, off, smax = _prep_targets(targets, tl, B, y.device)
         nll, ws = ops.ctc_loss_fwd(logits, tg, ldt, off, il, tl, smax, blank, zero_infinity, True)
         ctx.save_for_backward(logits, yc, wc, tg, off if off is not None else tg, il, tl, ws)

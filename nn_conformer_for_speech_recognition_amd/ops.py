@@ -119,31 +119,60 @@ class WgradGroup:
     adopts them without a copy).  Tables are cached by operand pointers (fixed under graph replay)."""
 
     POOL_BYTES = 8 << 20     # pinned staging for the task tables (allocated at the first, eager, flush)
+    CAPTURE_POOL_BYTES = 2 << 20
 
     def __init__(self):
         self.tasks = []
         self._cache = {}
-        self._pool = None
+        self._pool = None        # eager tables: ring (a slice is only re-read by its own, finished, copy)
+        self._cpool = None       # tables staged inside a graph capture: bump-allocated, never reused
         self._off = 0
+        self._coff = 0
+        self._armed = False
+        self._stream = None
 
     def _stage(self, host):
-        """Copy a host table to the device through a slice of the persistent pinned pool: legal inside a
-        HIP-graph capture (pageable copies and pinned allocations are not), and every captured copy
-        keeps reading its own slice on replay (the pool only wraps after POOL_BYTES of tables)."""
+        """Copy a host table to the device through a slice of a persistent pinned pool: legal inside a
+        HIP-graph capture (pageable copies and pinned allocations are not).  A captured copy node re-reads
+        its host slice on every replay, so slices staged under capture come from a separate bump-only pool
+        that is never recycled (eager flushes wrapping the ring cannot overwrite them)."""
         n = host.nbytes
+        capturing = torch.cuda.is_current_stream_capturing()
         if self._pool is None:
-            if torch.cuda.is_current_stream_capturing():
+            if capturing:
                 raise L.CfmError("WgradGroup: first flush inside a graph capture; run one eager step first")
             self._pool = torch.empty(max(self.POOL_BYTES, n), dtype=torch.uint8).pin_memory()
-        if self._off + n > self._pool.numel():
-            self._off = 0
-        dst = self._pool[self._off:self._off + n]
+            self._cpool = torch.empty(self.CAPTURE_POOL_BYTES, dtype=torch.uint8).pin_memory()
+        if capturing:
+            if self._coff + n > self._cpool.numel():
+                raise L.CfmError("WgradGroup: capture staging pool exhausted (too many distinct captured flushes)")
+            dst = self._cpool[self._coff:self._coff + n]
+            self._coff += (n + 255) // 256 * 256
+        else:
+            if self._off + n > self._pool.numel():
+                self._off = 0
+            dst = self._pool[self._off:self._off + n]
+            self._off += (n + 255) // 256 * 256
         dst.numpy()[:] = host
-        self._off += (n + 255) // 256 * 256
         return dst.to(self.tasks[0][0].device, non_blocking=True)
 
     def __len__(self):
         return len(self.tasks)
+
+    def arm_final_flush(self):
+        """Safety net for a backward in which the flushing layer (layer 0) never runs (pruned node): an
+        end-of-backward engine callback flushes whatever is still queued, on the stream the tasks were
+        queued from, so no deferred gradient outlives its backward pass unfilled."""
+        if self._armed:
+            return
+        self._armed = True
+
+        def _final():
+            self._armed = False
+            if self.tasks:
+                with torch.cuda.stream(self._stream):
+                    self.flush()
+        torch.autograd.Variable._execution_engine.queue_callback(_final)
 
     def add(self, dy, x):
         M, N = dy.shape
@@ -151,6 +180,7 @@ class WgradGroup:
         dw = torch.empty(N, K, device=dy.device, dtype=torch.float32)
         db = torch.empty(N, device=dy.device, dtype=torch.float32)
         self.tasks.append((dy, x, dw, db))
+        self._stream = torch.cuda.current_stream(dy.device)
         return dw.view(N, K), db.view(N)
 
     def flush(self):
@@ -172,10 +202,12 @@ class WgradGroup:
                 L.call("cfm_wgrad_group_fill", host.ctypes.data, i, L.ptr(dy), L.ptr(x), L.ptr(dw), L.ptr(db), M, N,
                        K, tile0)
                 tile0 += lib.cfm_wgrad_group_tiles(N, K)
+            captured = torch.cuda.is_current_stream_capturing()
             table = self._stage(host)
-            hit = (None, table, tile0)
+            hit = (captured, table, tile0)
             if len(self._cache) > 8:
-                self._cache.clear()
+                # a captured graph's kernel node holds the device table's address: keep those entries
+                self._cache = {k: v for k, v in self._cache.items() if v[0]}
             self._cache[key] = hit
         L.call("cfm_wgrad_group", L.ptr(hit[1]), len(self.tasks), hit[2], L.stream())
         self.tasks = []

@@ -60,6 +60,27 @@ class Adafactor(torch.optim.Optimizer):
             st["RMS"] = 0
         return st
 
+    def _ptrkey(self, ps):
+        """Every buffer the cached task table points at: parameter, gradient AND optimizer state
+        (exp_avg, exp_avg_sq_row/col or exp_avg_sq).  A state swap (load_state_dict, a reset of
+        self.state) changes the key, so the kernel never writes through a stale table."""
+        key = []
+        for p in ps:
+            st = self.state.get(p, {})
+            key.append((p.data_ptr(), p.grad.data_ptr(),
+                        *(st[k].data_ptr() if torch.is_tensor(st.get(k)) else 0
+                          for k in ("exp_avg", "exp_avg_sq_row", "exp_avg_sq_col", "exp_avg_sq"))))
+        return tuple(key)
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        for st in self.state.values():     # the device step reads fp32 contiguous state on the param's device
+            for k in ("exp_avg", "exp_avg_sq_row", "exp_avg_sq_col", "exp_avg_sq"):
+                if torch.is_tensor(st.get(k)):
+                    st[k] = st[k].float().contiguous()
+        self._fast.clear()
+        self._tables.clear()
+
     def _lr(self, group, step):
         lr = group["lr"]
         if group["relative_step"]:
@@ -123,7 +144,7 @@ class Adafactor(torch.optim.Optimizer):
             # fast path: same parameter / gradient buffers as the cached table (every step of a
             # training loop whose gradients live in a captured graph's pool, or are re-used in
             # place): no per-parameter ctypes table build on the host, only the step counters
-            ptrkey = tuple((p.data_ptr(), p.grad.data_ptr()) for p in ps)
+            ptrkey = self._ptrkey(ps)
             fast = self._fast.get((id(group), dev))
             if fast is not None and fast[0] == ptrkey:
                 table, offs = fast[1], fast[2]
@@ -139,7 +160,7 @@ class Adafactor(torch.optim.Optimizer):
             else:
                 table, step, offs = self._build_table(group, ps, dev)
                 row_off, col_off, blk_off, rm_off, rm_toff, cp_off, part_off = offs
-                self._fast[(id(group), dev)] = (ptrkey, table, offs)
+                self._fast[(id(group), dev)] = (self._ptrkey(ps), table, offs)   # state now exists
             key = (id(group), dev)
             buf = self._dev.get(key)
             if (buf is None or buf[0].numel() < max(rm_off, 1) or buf[1].numel() < max(part_off, 1)

@@ -25,6 +25,8 @@ def rel_err(a, b):
 
 
 TOL = {torch.float32: (1e-4, 1e-3), torch.bfloat16: (3e-2, 5e-2)}
+# per valid row: max |err| / max |ref| (row_max_err)
+ROWTOL = {torch.float32: 1e-3, torch.bfloat16: 8e-2}
 
 
 @pytest.mark.parametrize("name", ["s_none", "s_rel", "m_rel", "l_none"])
@@ -88,6 +90,7 @@ def test_encoder_vs_oracle(case, cd):
     y.backward(gy.to(DEV))
     tol_y, tol_g = TOL[cd]
     assert rel_err(y.detach(), yr.detach()) < tol_y
+    assert row_max_err(y.detach(), yr.detach(), lens) < ROWTOL[cd]
     assert rel_err(xd.grad, xr.grad) < tol_g
     rp = dict(ref.named_parameters())
     for n, prm in m.named_parameters():
@@ -138,3 +141,43 @@ def test_dropout_train_is_stochastic_and_scaled():
 def test_even_kernel_raises():
     with pytest.raises(ValueError):
         Conformer(64, 2, 128, 1, 8)
+
+
+def test_grad_hooks_see_final_weight_gradients():
+    """Weight gradients deferred to the grouped launch are only filled when layer 0 flushes: a parameter
+    with a post-accumulate-grad hook (DDP-style reducer, per-layer all-reduce) must turn the deferral off
+    for its layer, so the hook reads the final value -- and the gradients equal the grouped run's."""
+    torch.manual_seed(11)
+    d, H, ffn, K, L, B, T = 128, 2, 256, 15, 3, 2, 64
+    m = Conformer(d, H, ffn, L, K, 0.0, compute_dtype=torch.bfloat16).to(DEV).train()
+    x = torch.randn(B, T, d, device=DEV)
+    ln = torch.tensor([T, 40], device=DEV)
+    gy = torch.randn(B, T, d, device=DEV)
+    y, _ = m(x, ln)
+    y.backward(gy)
+    grouped = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    seen = {}
+    watch = {n: p for n, p in m.named_parameters() if n.startswith("conformer_layers.1.") and p.dim() == 2}
+    for n, p in watch.items():
+        p.register_post_accumulate_grad_hook(lambda t, n=n: seen.__setitem__(n, t.grad.clone()))
+    y, _ = m(x, ln)
+    y.backward(gy)
+    torch.cuda.synchronize()
+    assert set(seen) == set(watch)
+    for n, p in watch.items():
+        assert torch.equal(seen[n], p.grad), n
+    for n, p in m.named_parameters():
+        assert rel_err(p.grad, grouped[n]) < 1e-5, n
+
+
+def row_max_err(y, yr, lens):
+    """max over valid frames (b, t < lens[b]) of max_c |y - yr| / max_c |yr| -- a per-row check next to
+    the whole-tensor relative L2 (a single bad padded-boundary row or head cannot hide under it)."""
+    y = torch.as_tensor(y).double().cpu()
+    yr = torch.as_tensor(yr).double().cpu()
+    worst = 0.0
+    for b, n in enumerate(lens):
+        d = (y[b, :n] - yr[b, :n]).abs().amax(-1) / yr[b, :n].abs().amax(-1).clamp_min(1e-30)
+        worst = max(worst, d.max().item())
+    return worst

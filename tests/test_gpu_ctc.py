@@ -129,3 +129,43 @@ def test_greedy_decode_vs_oracle(collapse):
     for b in range(B):
         assert out[b, :n[b]].cpu().tolist() == out_ref[b]
         assert (out[b, n[b]:] == -1).all()
+
+
+def test_ctc_bad_host_lengths_raise():
+    """torch.nn.functional.ctc_loss raises on input_lengths > T / target_lengths > S: so does the
+    drop-in when the lengths are host data (lengths are never trusted)."""
+    x, tgt, il, tl = _case(3)
+    xd = x.to(DEV)
+    T, S = x.shape[1], tgt.shape[1]
+    with pytest.raises(ValueError):
+        ctc.ctc_loss(xd, tgt.to(DEV), torch.tensor([T + 1, 3, 3, 2]), tl, batch_first=True)
+    with pytest.raises(ValueError):
+        ctc.ctc_loss(xd, tgt.to(DEV), il, torch.tensor([S + 2, 1, 1, 1]), batch_first=True)
+    with pytest.raises(ValueError):
+        ctc.ctc_loss(xd, tgt.to(DEV), il, tl, blank=x.shape[-1], batch_first=True)
+
+
+def test_ctc_bad_device_lengths_are_clamped():
+    """Device lengths are not read back (no sync): the kernels clamp in_len to T, tgt_len to S and
+    label ids to [0, V) -- the result equals the clamped inputs' loss and no memory outside the
+    buffers is touched (guard tensors around the workspace stay intact)."""
+    x, tgt, il, tl = _case(4)
+    B, T, V = x.shape
+    S = tgt.shape[1]
+    bad_il = torch.tensor([T + 50, T - 3, 10 ** 6, 2], dtype=torch.int32)
+    bad_tl = torch.tensor([S + 7, 2, 0, 10 ** 5], dtype=torch.int32)
+    bad_tg = tgt.clone()
+    bad_tg[1, 0] = V + 3
+    guard = torch.full((1 << 16,), 7.0, device=DEV)
+    xd = x.to(DEV).requires_grad_()
+    loss = ctc.ctc_loss(xd, bad_tg.to(DEV), bad_il.to(DEV), bad_tl.to(DEV), reduction="none", zero_infinity=True,
+                        batch_first=True)
+    loss.sum().backward()
+    torch.cuda.synchronize()
+    assert torch.all(guard == 7.0)
+    cl_il = bad_il.clamp(max=T)
+    cl_tl = bad_tl.clamp(max=S)
+    cl_tg = bad_tg.clamp(0, V - 1)
+    want, _ = oc.ctc_loss(x.double().numpy(), cl_tg.numpy(), cl_il.numpy(), cl_tl.numpy(), 0, "none", True)
+    np.testing.assert_allclose(loss.detach().cpu().double().numpy(), want, rtol=1e-5, atol=1e-6)
+    assert torch.isfinite(xd.grad).all()
