@@ -22,128 +22,20 @@ namespace cfm {
 int attn_simt_fwd_launch(const void*, void*, float*, const int32_t*, const void*, const float*, const float*, int,
                          int, int, int, int, float, uint64_t, hipStream_t);
 size_t attn_simt_ws_bytes(int B, int T, int H);
+size_t attn_rel_ws_bytes(int B, int T, int H, int dk);
+int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len, const void* pos, const float* pu,
+                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s);
+int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, const int32_t* len, const void* pos,
+                        const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
+                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s);
 int attn_simt_bwd_launch(const void*, const void*, const void*, const float*, const int32_t*, const void*,
                          const float*, const float*, void*, float*, float*, float*, int, int, int, int, int, float,
                          uint64_t, float*, hipStream_t);
 }  // namespace cfm
 
+#include "attn_common.h"
+
 namespace {
-
-constexpr int DKP = 64;      // padded head dim
-constexpr int KS = DKP + 8;  // LDS row stride (elements): 144-B rows, conflict-free ds_read_b128
-constexpr int TILE = 64;     // keys (fwd/dQ) or queries (dK/dV) per LDS tile
-constexpr float LOG2E = 1.4426950408889634f;
-constexpr float LN2 = 0.6931471805599453f;
-
-struct AttnM {
-  const bf16* qkv;
-  int B, T, H, dk, D3, HD;
-  const int32_t* len;
-  float scale;
-  float drop_p; uint64_t seed;
-  bool vec;    // 16-B vector loads legal
-  int dbg;     // timing experiments (cfm_attn_set_mode bits 1-2)
-  const uint64_t* salt;   // bound dropout step counter or nullptr
-};
-
-// attention-dropout element index: rows of an EVEN stride (T rounded up to even), so the keys 2m and
-// 2m+1 of one (query, key-pair) share one 32-bit hash (low / high 16 bits): kernels holding both keys of
-// a pair in one lane (accumulator registers r, r+1 for even r) hash once per pair (dropout_pair)
-__device__ __forceinline__ uint64_t didx(const AttnM& p, int b, int h, int i, int j) {
-  return (((uint64_t)b * p.H + h) * p.T + i) * (uint64_t)(p.T + (p.T & 1)) + j;
-}
-// keep-scales of elements idx (even) and idx + 1: one mix for both (== dropout_keyed of each)
-__device__ __forceinline__ void dropout_pair(uint32_t thr, float keep, uint32_t key, uint64_t idx, float& m0,
-                                             float& m1) {
-  const uint32_t h = cfm_mix32((uint32_t)(idx >> 1) ^ key);
-  m0 = (h & 0xFFFFu) >= thr ? keep : 0.f;
-  m1 = (h >> 16) >= thr ? keep : 0.f;
-}
-
-// 8 consecutive head-dim elements c..c+7 of row `row` of matrix base (row stride ld), zero-padded
-__device__ __forceinline__ uint4 ld8(const bf16* base, long ld, int row, int nrows, int c, int dk, bool vec) {
-  uint4 r = make_uint4(0, 0, 0, 0);
-  if (row >= nrows || c >= dk) return r;
-  const bf16* p = base + (long)row * ld + c;
-  if (vec && c + 8 <= dk) return *reinterpret_cast<const uint4*>(p);
-  unsigned short t[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) t[e] = (c + e < dk) ? reinterpret_cast<const unsigned short*>(p)[e] : 0;
-  r.x = t[0] | (t[1] << 16); r.y = t[2] | (t[3] << 16); r.z = t[4] | (t[5] << 16); r.w = t[6] | (t[7] << 16);
-  return r;
-}
-
-// A-operand fragment, natural k order, from a [row][KS] tile: lane (r, hh) gets row r0+r, cols k0+8hh..+7
-__device__ __forceinline__ bf16x8 rowfrag(const bf16* tile, int r0, int k0, int lane) {
-  return *reinterpret_cast<const bf16x8*>(tile + (r0 + (lane & 31)) * KS + k0 + 8 * (lane >> 5));
-}
-
-// A-operand fragment of the TRANSPOSED tile, k order permuted to match an accumulator used as the
-// B operand (element j of lane half hh <-> tile row r0 + 8(j>>2) + 4hh + (j&3)); column c0 + (lane&31).
-__device__ __forceinline__ bf16x8 trfrag_perm(const bf16* tile, int r0, int c0, int lane) {
-  const int hh = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
-  const bf16* base = tile + (r0 + 4 * hh + q) * KS + c0 + 16 * g1 + 4 * p4;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 8 * KS));
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// accumulator registers 8s..8s+7 -> bf16 B-operand fragment of k-step s
-__device__ __forceinline__ bf16x8 acc2frag(const f32x16& a, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
-  return r;
-}
-
-// accumulator row of register r for lane half hh
-__device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
-
-// stage a [64 rows][64 cols] bf16 tile (row r0.., column offset col of qkv) into LDS; 2 x 16 B per thread
-__device__ __forceinline__ void tile_load(const AttnM& p, int b, int r0, int col, uint4 (&reg)[2], int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int v = tid + 256 * i;
-    reg[i] = ld8(p.qkv + (long)b * p.T * p.D3 + col, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
-  }
-}
-__device__ __forceinline__ void tile_store(bf16* t, const uint4 (&reg)[2], int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int v = tid + 256 * i;
-    *reinterpret_cast<uint4*>(t + (v >> 3) * KS + (v & 7) * 8) = reg[i];
-  }
-}
-
-// B-operand fragments (natural k order) of a 32-row block: lane (r, hh) = row[r][16s + 8hh .. +7]
-__device__ __forceinline__ void load_bfrags(const AttnM& p, const bf16* base, long ld, int row, int nrows,
-                                            bf16x8 (&f)[4], int lane) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    uint4 u = ld8(base, ld, row, nrows, 16 * s + 8 * (lane >> 5), p.dk, p.vec);
-    f[s] = __builtin_bit_cast(bf16x8, u);
-  }
-}
-
-// write a wave's 64(d) x 32(cols) f32 accumulator pair (dt = 0, 1) transposed into a bf16 matrix:
-// out[(row0 + c) * ld + d] = acc[d][c] * mul_c  (c < ncols, d < dk), staged through LDS.
-__device__ void store_transposed(float* stage, const f32x16& a0, const f32x16& a1, float mulc, bf16* out, long ld,
-                                 int row0, int nvalid, int dk, int lane) {
-  const int hh = lane >> 5, c = lane & 31;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    stage[c * 65 + acc_row(r, hh)] = a0[r] * mulc;
-    stage[c * 65 + 32 + acc_row(r, hh)] = a1[r] * mulc;
-  }
-  __builtin_amdgcn_wave_barrier();
-  for (int idx = lane; idx < 32 * 64; idx += 64) {
-    const int cc = idx >> 6, d = idx & 63;
-    if (cc < nvalid && d < dk) out[(long)(row0 + cc) * ld + d] = (bf16)stage[cc * 65 + d];
-  }
-  __builtin_amdgcn_wave_barrier();
-}
 
 // ------------------------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnM p, bf16* __restrict__ o, float* __restrict__ lse) {
@@ -875,11 +767,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnM p, const bf16*
   store_transposed(stage, dv0, dv1, 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
 }
 
-bool use_mfma(int dtype, const void* pos, int dk) { return dtype == CFM_BF16 && pos == nullptr && dk <= DKP; }
+// bf16 runs on MFMA (pos != nullptr: attention_rel.hip); fp32 (the parity mode) on the SIMT kernels.
+// cfm_attn_set_mode bit 4 sends bf16 rel-pos back to SIMT (A/B, parity cross-check).
+int g_attn_mode = 0;
+bool use_mfma(int dtype, const void* pos, int dk) {
+  return dtype == CFM_BF16 && dk <= DKP && (pos == nullptr || (g_attn_mode & 16) == 0);
+}
 
 // whole-head kernels: T <= HEAD_TMAX; cfm_attn_set_mode bit 0 forces the tiled kernels, bit 3 selects
 // the wave-per-key-block dK/dV kernel (A/B)
-int g_attn_mode = 0;
 bool use_head(int T) { return T <= HEAD_TMAX && (g_attn_mode & 1) == 0; }
 size_t head_lds_bytes(int T) {
   const size_t rows = (size_t)cdiv(T, TILE) * TILE;
@@ -902,6 +798,7 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   hipStream_t s = cfm::as_stream(stream);
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, s);
+  if (pos) return cfm::attn_rel_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, drop_p, seed, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 6,
           cfm::g_rng_salt};
@@ -917,6 +814,7 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
 
 CFM_EXPORT size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel, int dtype) {
   if (!use_mfma(dtype, rel ? (const void*)1 : nullptr, dk)) return cfm::attn_simt_ws_bytes(B, T, H);
+  if (rel) return cfm::attn_rel_ws_bytes(B, T, H, dk);
   return (size_t)B * H * T * sizeof(float);
 }
 
@@ -928,7 +826,8 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
   CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0, CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(!pos || (pos_u && pos_v && dpos && dpos_u && dpos_v), CFM_ERR_ARG, "rel-pos grads need buffers");
   hipStream_t s = cfm::as_stream(stream);
-  CFM_REQUIRE(!d_ready || use_mfma(dtype, pos, dk), CFM_ERR_UNSUPPORTED, "precomputed D: bf16 MFMA path only");
+  CFM_REQUIRE(!d_ready || (use_mfma(dtype, pos, dk) && !pos), CFM_ERR_UNSUPPORTED,
+              "precomputed D: bf16 MFMA path without rel-pos only");
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_bwd_launch(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B,
                                      T, H, dk, dtype, drop_p, seed, ws, s);
@@ -941,6 +840,9 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
   if (!d_ready)
     hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s,
                        (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
+  if (pos)
+    return cfm::attn_rel_bwd_launch(qkv, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H,
+                                    dk, drop_p, seed, ws, s);
   if (use_head(T) && (g_attn_mode & 8) != 0)
     hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), dkdv_wave_lds_bytes(T), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);

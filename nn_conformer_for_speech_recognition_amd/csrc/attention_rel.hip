@@ -1,0 +1,704 @@
+// attention_rel.hip — relative-position multi-head self-attention on MFMA (bf16), fwd + bwd.
+//
+// Semantics (transformers Wav2Vec2ConformerSelfAttention, position_embeddings_type="relative",
+// modeling_wav2vec2_conformer.py:528-565), one (batch b, head h), scale = 1/sqrt(dk):
+//   s_ij = scale * ((q_i + u) . k_j + (q_i + v) . p_{T-1-i+j})      p = linear_pos(pe): (2T-1, H*dk)
+// keys j >= len[b] masked (key_padding_mask), attention dropout on the probabilities, o = P v.
+//
+// The rel-shift is never materialised.  For a block of 32 queries (one wave) and 64 keys the
+// relative rows r = T-1-i+j span a BAND of 32+64-1 rows of p.  The band is staged in LDS (a ring
+// of 64-row chunks: consecutive key tiles share 128 of their 192 rows, so each tile loads only 64
+// new rows), and one MFMA product  X[r'][i] = p_{rb+r'} . (q_i+v)  (12 x v_mfma_f32_32x32x16_bf16)
+// gives every bd term the block needs.  The skew bd[j][i] = X[j-i+31][i] is a per-lane column shift
+// in the accumulator, done through a per-wave LDS stage (column stride 100 floats: b128 writes and
+// the skewed b32 reads are both bank-conflict free).  ac and bd add in fp32 before the softmax.
+//
+// Backward (deterministic, no atomics):
+//   dQ kernel  (queries on the lanes, streams key tiles): recomputes S (same band), dP, dS;
+//              dq = scale * (sum_j dS k_j  +  sum_j dS p_{T-1-i+j}) -- the second sum is a plain
+//              MFMA over the band once dS^T is scattered into the stage in band coordinates;
+//              per-wave column sums of both terms -> du, dv partials (one reduction launch).
+//   dK/dV kernel (keys on the lanes, streams query tiles): recomputes S with the band in the
+//              transposed role, dV += dO^T P~, dK += (q+u)^T dS, and writes scale*dS (bf16,
+//              query-major) for the dpos pass.
+//   dpos kernel: dpos_r = sum_{b,i} scale*dS[i, i+r-(T-1)] (q_i+v) -- in (i, r) coordinates a plain
+//              GEMM over i whose dS operand rows are contiguous runs of the stored dS rows.
+#include "attn_common.h"
+
+namespace {
+
+constexpr int SS = 100;     // fwd / dQ stage column stride (floats): 100 = 4 mod 32, 99 odd
+constexpr int SS2 = 68;     // dK/dV stage column stride (floats): 68 = 4 mod 32
+constexpr int RING = 4;     // p-band ring: chunks of TILE rows
+
+struct RelP {
+  const bf16* pos;          // (2T-1, H*dk) projected relative table
+  const float* pu;          // (H*dk) pos_bias_u
+  const float* pv;          // (H*dk) pos_bias_v
+  bool pvec;                // 16-B vector loads of pos legal
+};
+
+// 8 head-dim elements c..c+7 of relative row `row` (valid rows [0, 2T-1)), zero outside
+__device__ __forceinline__ uint4 ld8p(const AttnM& p, const RelP& rp, int h, int row, int c) {
+  if (row < 0 || row >= 2 * p.T - 1) return make_uint4(0, 0, 0, 0);
+  return ld8(rp.pos + h * p.dk, p.HD, row, 2 * p.T - 1, c, p.dk, rp.pvec);
+}
+
+// (q + u) and (q + v) B-operand fragments of query row `row` (zero past T / past dk)
+__device__ __forceinline__ void load_q_uv(const AttnM& p, const RelP& rp, int b, int h, int row, bf16x8 (&qu)[4],
+                                          bf16x8 (&qv)[4], int lane) {
+  const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int c = 16 * s + 8 * (lane >> 5);
+    const bf16x8 q = __builtin_bit_cast(bf16x8, ld8(qbase, p.D3, row, p.T, c, p.dk, p.vec));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int d = c + e;
+      const float u = d < p.dk ? rp.pu[h * p.dk + d] : 0.f;
+      const float v = d < p.dk ? rp.pv[h * p.dk + d] : 0.f;
+      qu[s][e] = (bf16)((float)q[e] + u);
+      qv[s][e] = (bf16)((float)q[e] + v);
+    }
+  }
+}
+
+// 16-B chunk `v` (0..511) of a 64-row chunk of the band: row v>>3, columns (v&7)*8
+__device__ __forceinline__ uint4 ring_chunk_load(const AttnM& p, const RelP& rp, int h, int row0, int v) {
+  return ld8p(p, rp, h, row0 + (v >> 3), (v & 7) * 8);
+}
+__device__ __forceinline__ void ring_chunk_store(bf16* slot, const uint4 (&reg)[2], int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + 256 * i;
+    *reinterpret_cast<uint4*>(slot + (v >> 3) * KS + (v & 7) * 8) = reg[i];
+  }
+}
+
+// accumulator pair (a0 rows 0..31, a1 rows 32..63; lanes = 32 columns) -> per row d = lane: sum over
+// the 32 columns, through the wave's LDS stage [c * 65 + d]
+__device__ __forceinline__ float wave_rowsum(float* stage, const f32x16& a0, const f32x16& a1, int lane) {
+  const int hh = lane >> 5, c = lane & 31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    stage[c * 65 + acc_row(r, hh)] = a0[r];
+    stage[c * 65 + 32 + acc_row(r, hh)] = a1[r];
+  }
+  __builtin_amdgcn_wave_barrier();
+  float s = 0.f;
+  for (int cc = 0; cc < 32; ++cc) s += stage[cc * 65 + lane];
+  __builtin_amdgcn_wave_barrier();
+  return s;
+}
+
+// ------------------------------------------------------------------------------------ S^T for a key tile
+// queries on the lanes (wave = 32 queries), 64 keys on the accumulator rows (s0: keys 0..31, s1: 32..63):
+// S^T = K (q+u)^T + skew(P_band (q+v)^T), unscaled.  band: the ring slot base of each 32-row block.
+struct BandRows {
+  const bf16* blk[3];       // LDS row 0 of the wave's three 32-row band blocks
+};
+
+__device__ __forceinline__ void scores_qlanes(const bf16* sK, const BandRows& br, const bf16x8 (&qu)[4],
+                                              const bf16x8 (&qv)[4], float* st, f32x16& s0, f32x16& s1, int lane) {
+  const int hh = lane >> 5, ii = lane & 31;
+  s0 = (f32x16){0};
+  s1 = (f32x16){0};
+  f32x16 x0 = (f32x16){0}, x1 = (f32x16){0}, x2 = (f32x16){0};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qu[s], s0, 0, 0, 0);
+    s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
+    x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(br.blk[0], 0, 16 * s, lane), qv[s], x0, 0, 0, 0);
+    x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(br.blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
+    x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(br.blk[2], 0, 16 * s, lane), qv[s], x2, 0, 0, 0);
+  }
+  // X[r'][i] -> stage[i][r'] (16-B stores of 4 consecutive accumulator rows)
+  float* col = st + ii * SS;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int r0 = 8 * g + 4 * hh;
+    *reinterpret_cast<float4*>(col + r0) = make_float4(x0[4 * g], x0[4 * g + 1], x0[4 * g + 2], x0[4 * g + 3]);
+    *reinterpret_cast<float4*>(col + 32 + r0) = make_float4(x1[4 * g], x1[4 * g + 1], x1[4 * g + 2], x1[4 * g + 3]);
+    *reinterpret_cast<float4*>(col + 64 + r0) = make_float4(x2[4 * g], x2[4 * g + 1], x2[4 * g + 2], x2[4 * g + 3]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  // bd[j][i] = X[j - i + 31][i]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int jj = acc_row(r, hh);
+    s0[r] += col[jj - ii + 31];
+    s1[r] += col[jj + 32 - ii + 31];
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// the wave's three band blocks for key tile kt: band rows 32(3-w) + 32m of the tile's 192-row window,
+// which starts at ring chunk kt
+__device__ __forceinline__ BandRows band_rows_q(const bf16* ring, int kt, int wv) {
+  BandRows br;
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int off = 32 * (3 - wv) + 32 * m;
+    br.blk[m] = ring + ((kt + (off >> 6)) & (RING - 1)) * TILE * KS + (off & 63) * KS;
+  }
+  return br;
+}
+
+// ------------------------------------------------------------------------------------ forward
+// grid (ceil(T/128), H, B), 4 waves x 32 queries; K/V tiles of 64 keys double-buffered, band ring.
+__global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf16* __restrict__ o,
+                                                           float* __restrict__ lse) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  __shared__ __attribute__((aligned(16))) bf16 skv[2 * 2 * TILE * KS];    // [buf][K,V][64][72]   36 KiB
+  __shared__ __attribute__((aligned(16))) bf16 sring[RING * TILE * KS];   // band ring            36 KiB
+  __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SS];          // per-wave skew stage  50 KiB
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int Q0 = blockIdx.x * 128, q0 = Q0 + wv * 32;
+  const int qi = q0 + (lane & 31);
+  const int len = p.len[b];
+  const int rbase = p.T - 1 - Q0 - 127;          // relative row of band row 0 at key tile 0
+  bf16x8 qu[4], qv[4];
+  load_q_uv(p, rp, b, h, qi, qu, qv, lane);
+  float* st = sst + wv * 32 * SS;
+  f32x16 o0 = (f32x16){0}, o1 = (f32x16){0};
+  float m = -INFINITY, l = 0.f;
+  const float c = p.scale * LOG2E;
+  const int nkt = (len + TILE - 1) / TILE;
+  uint4 rk[2], rv[2], rq[2];
+  const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
+  if (nkt > 0) {
+    tile_load(p, b, 0, kcol, rk, tid);
+    tile_load(p, b, 0, vcol, rv, tid);
+    tile_store(skv, rk, tid);
+    tile_store(skv + TILE * KS, rv, tid);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load(p, rp, h, rbase + ch * TILE, tid + 256 * i);
+      ring_chunk_store(sring + ch * TILE * KS, rq, tid);
+    }
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* sK = skv + (kt & 1) * 2 * TILE * KS;
+    const bf16* sV = sK + TILE * KS;
+    if (kt + 1 < nkt) {
+      tile_load(p, b, (kt + 1) * TILE, kcol, rk, tid);
+      tile_load(p, b, (kt + 1) * TILE, vcol, rv, tid);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
+    }
+    f32x16 s0, s1;
+    scores_qlanes(sK, band_rows_q(sring, kt, wv), qu, qv, st, s0, s1, lane);
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k0 = kt * TILE + acc_row(r, hh);
+      s0[r] = (k0 < len) ? s0[r] * c : -INFINITY;
+      s1[r] = (k0 + 32 < len) ? s1[r] * c : -INFINITY;
+      mloc = fmaxf(mloc, fmaxf(s0[r], s1[r]));
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float mn = fmaxf(m, mloc);
+    const float alpha = exp2f(m - mn);
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = exp2f(s0[r] - mn);
+      s1[r] = exp2f(s1[r] - mn);
+      ls += s0[r] + s1[r];
+    }
+    ls += __shfl_xor(ls, 32, 64);
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      o0[r] *= alpha;
+      o1[r] *= alpha;
+    }
+    if (p.drop_p > 0.f) {
+      const uint64_t rowi = didx(p, b, h, qi, kt * TILE);
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int k0 = acc_row(r, hh);
+        float m0, m1, m2, m3;
+        dropout_pair(dthr, dkeep, dkey, rowi + k0, m0, m1);
+        dropout_pair(dthr, dkeep, dkey, rowi + k0 + 32, m2, m3);
+        s0[r] *= m0; s0[r + 1] *= m1;
+        s1[r] *= m2; s1[r + 1] *= m3;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 0, lane), pf, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 32, lane), pf, o1, 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nkt) {
+      bf16* nK = skv + ((kt + 1) & 1) * 2 * TILE * KS;
+      tile_store(nK, rk, tid);
+      tile_store(nK + TILE * KS, rv, tid);
+      ring_chunk_store(sring + ((kt + 3) & (RING - 1)) * TILE * KS, rq, tid);
+    }
+    __syncthreads();
+  }
+  const float inv = 1.f / l;
+  if (q0 < p.T)
+    store_transposed(st, o0, o1, inv, o + (long)b * p.T * p.HD + h * p.dk, p.HD, q0, min(32, p.T - q0), p.dk, lane);
+  if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
+}
+
+// ------------------------------------------------------------------------------------ dQ (+ du, dv partials)
+// grid (ceil(T/128), H, B).  part: (B * 4*gridDim.x, 2*H*dk) fp32 -- row (b, 32-query block): per-column
+// sums over the block's queries of scale * sum_j dS k_j (u half) and scale * sum_j dS p_r (v half).
+__global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, const bf16* __restrict__ dout,
+                                                              const float* __restrict__ lse,
+                                                              const float* __restrict__ Dg, bf16* __restrict__ dqkv,
+                                                              float* __restrict__ part) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  __shared__ __attribute__((aligned(16))) bf16 skv[2 * 2 * TILE * KS];
+  __shared__ __attribute__((aligned(16))) bf16 sring[RING * TILE * KS];
+  __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, ii = lane & 31;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int Q0 = blockIdx.x * 128, q0 = Q0 + wv * 32;
+  const int qi = q0 + ii;
+  const int len = p.len[b];
+  const int rbase = p.T - 1 - Q0 - 127;
+  bf16x8 qu[4], qv[4], gf[4];
+  load_q_uv(p, rp, b, h, qi, qu, qv, lane);
+  load_bfrags(p, dout + (long)b * p.T * p.HD + h * p.dk, p.HD, qi, p.T, gf, lane);
+  const bool qvalid = qi < p.T;
+  const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : 0.f;
+  const float Dq = qvalid ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
+  const float c = p.scale * LOG2E;
+  float* st = sst + wv * 32 * SS;
+  float* col = st + ii * SS;
+  f32x16 a0 = (f32x16){0}, a1 = (f32x16){0}, e0 = (f32x16){0}, e1 = (f32x16){0};   // K-term, band term
+  const int nkt = (len + TILE - 1) / TILE;
+  uint4 rk[2], rv[2], rq[2];
+  const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
+  if (nkt > 0) {
+    tile_load(p, b, 0, kcol, rk, tid);
+    tile_load(p, b, 0, vcol, rv, tid);
+    tile_store(skv, rk, tid);
+    tile_store(skv + TILE * KS, rv, tid);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load(p, rp, h, rbase + ch * TILE, tid + 256 * i);
+      ring_chunk_store(sring + ch * TILE * KS, rq, tid);
+    }
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* sK = skv + (kt & 1) * 2 * TILE * KS;
+    const bf16* sV = sK + TILE * KS;
+    if (kt + 1 < nkt) {
+      tile_load(p, b, (kt + 1) * TILE, kcol, rk, tid);
+      tile_load(p, b, (kt + 1) * TILE, vcol, rv, tid);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
+    }
+    const BandRows br = band_rows_q(sring, kt, wv);
+    f32x16 s0, s1;
+    scores_qlanes(sK, br, qu, qv, st, s0, s1, lane);
+    f32x16 d0 = (f32x16){0}, d1 = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 0, 16 * s, lane), gf[s], d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32, 16 * s, lane), gf[s], d1, 0, 0, 0);
+    }
+    if (p.drop_p > 0.f) {
+      const uint64_t rowi = didx(p, b, h, qi, kt * TILE);
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int k0 = acc_row(r, hh);
+        float m0, m1, m2, m3;
+        dropout_pair(dthr, dkeep, dkey, rowi + k0, m0, m1);
+        dropout_pair(dthr, dkeep, dkey, rowi + k0 + 32, m2, m3);
+        d0[r] *= m0; d0[r + 1] *= m1;
+        d1[r] *= m2; d1[r + 1] *= m3;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k0 = kt * TILE + acc_row(r, hh);
+      const float p0 = (k0 < len && qvalid) ? exp2f(s0[r] * c - L2) : 0.f;
+      const float p1 = (k0 + 32 < len && qvalid) ? exp2f(s1[r] * c - L2) : 0.f;
+      s0[r] = p0 * (d0[r] - Dq);
+      s1[r] = p1 * (d1[r] - Dq);
+    }
+    // K-term: dQ^T[d][q] += sum_key K[key][d] dS^T[key][q]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 0, lane), pf, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 32, lane), pf, a1, 0, 0, 0);
+      }
+    }
+    // band term: dS^T scattered to band coordinates stage[i][j - i + 31] (zero elsewhere), then
+    // dQ^T[d][q] += sum_r' P_band[r'][d] dS_band^T[r'][q]
+#pragma unroll
+    for (int g = 0; g < 12; ++g) *reinterpret_cast<float4*>(col + 48 * hh + 4 * g) = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jj = acc_row(r, hh);
+      col[jj - ii + 31] = s0[r];
+      col[jj + 32 - ii + 31] = s1[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const float4 lo = *reinterpret_cast<const float4*>(col + 16 * s + 4 * hh);
+      const float4 hi = *reinterpret_cast<const float4*>(col + 16 * s + 8 + 4 * hh);
+      bf16x8 bfr;
+      bfr[0] = (bf16)lo.x; bfr[1] = (bf16)lo.y; bfr[2] = (bf16)lo.z; bfr[3] = (bf16)lo.w;
+      bfr[4] = (bf16)hi.x; bfr[5] = (bf16)hi.y; bfr[6] = (bf16)hi.z; bfr[7] = (bf16)hi.w;
+      const bf16* blk = br.blk[s >> 1];
+      e0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(blk, 16 * (s & 1), 0, lane), bfr, e0, 0, 0, 0);
+      e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(blk, 16 * (s & 1), 32, lane), bfr, e1, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (kt + 1 < nkt) {
+      bf16* nK = skv + ((kt + 1) & 1) * 2 * TILE * KS;
+      tile_store(nK, rk, tid);
+      tile_store(nK + TILE * KS, rv, tid);
+      ring_chunk_store(sring + ((kt + 3) & (RING - 1)) * TILE * KS, rq, tid);
+    }
+    __syncthreads();
+  }
+  // per-wave column sums (queries) of both terms -> du / dv partial rows (zeros for blocks past T)
+  const float su = wave_rowsum(st, a0, a1, lane) * p.scale;
+  const float sv = wave_rowsum(st, e0, e1, lane) * p.scale;
+  const long prow = (long)b * (4 * gridDim.x) + blockIdx.x * 4 + wv;
+  if (lane < p.dk) {
+    part[prow * 2 * p.HD + h * p.dk + lane] = su;
+    part[prow * 2 * p.HD + p.HD + h * p.dk + lane] = sv;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    a0[r] += e0[r];
+    a1[r] += e1[r];
+  }
+  if (q0 < p.T)
+    store_transposed(st, a0, a1, p.scale, dqkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, q0, min(32, p.T - q0),
+                     p.dk, lane);
+}
+
+// ------------------------------------------------------------------------------------ dK, dV (+ dS store)
+// grid (ceil(T/128), H, B); wave = 32 keys on the lanes; query tiles of 64 (two 32-query sub-blocks)
+// staged in LDS as q+u, q+v, dO (+ lse, D).  The band for (query tile qt, 128 keys) is 192 rows
+// starting at relative row T-64-64qt+J0; it moves DOWN one chunk per query tile (ring chunk kc holds
+// rows T-64+J0-64(kc-2) ..+63, tile qt uses chunks qt, qt+1, qt+2).
+// dsbuf: (B, H, T, ldS) bf16, scale * dS, query-major.
+__global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp, const bf16* __restrict__ dout,
+                                                                const float* __restrict__ lse,
+                                                                const float* __restrict__ Dg,
+                                                                bf16* __restrict__ dqkv, bf16* __restrict__ dsbuf,
+                                                                int ldS) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  __shared__ __attribute__((aligned(16))) bf16 sq[2 * 3 * TILE * KS];      // [buf][Qu, Qv, dO][64][72] 54 KiB
+  __shared__ __attribute__((aligned(16))) bf16 sring[RING * TILE * KS];    // 36 KiB
+  __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SS2];          // 34 KiB
+  __shared__ float sLD[2][2][TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, jj = lane & 31;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int J0 = blockIdx.x * 128;
+  const int k0w = J0 + wv * 32;
+  const int kj = k0w + jj;
+  const int len = p.len[b];
+  const bool kvalid = kj < len;
+  bf16x8 kf[4], vf[4];
+  load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + p.HD + h * p.dk, p.D3, kj, p.T, kf, lane);
+  load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + 2 * p.HD + h * p.dk, p.D3, kj, p.T, vf, lane);
+  const float c = p.scale * LOG2E;
+  f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
+  const bool block_live = J0 < len;
+  const int nqt = block_live ? (p.T + TILE - 1) / TILE : 0;
+  const int cb = p.T - 64 + J0;                  // relative row of band row 0 at query tile 0
+  float* st = sst + wv * 32 * SS2;
+  uint4 rq[2], rg[2], rr[2];
+  float rl = 0.f, rd = 0.f;
+  const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
+  const bf16* gbase = dout + (long)b * p.T * p.HD + h * p.dk;
+  auto gload = [&](int qt) {
+    const int r0 = qt * TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int v = tid + 256 * i;
+      rq[i] = ld8(qbase, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+      rg[i] = ld8(gbase, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+    }
+    if (tid < TILE) {
+      const int qi = r0 + tid;
+      rl = qi < p.T ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : INFINITY;
+      rd = qi < p.T ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
+    }
+  };
+  auto sstore = [&](int buf) {
+    bf16* t = sq + buf * 3 * TILE * KS;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int v = tid + 256 * i;
+      const int row = v >> 3, c8 = (v & 7) * 8;
+      const bf16x8 q = __builtin_bit_cast(bf16x8, rq[i]);
+      bf16x8 qu, qv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int d = c8 + e;
+        const float u = d < p.dk ? rp.pu[h * p.dk + d] : 0.f;
+        const float w = d < p.dk ? rp.pv[h * p.dk + d] : 0.f;
+        qu[e] = (bf16)((float)q[e] + u);
+        qv[e] = (bf16)((float)q[e] + w);
+      }
+      *reinterpret_cast<bf16x8*>(t + row * KS + c8) = qu;
+      *reinterpret_cast<bf16x8*>(t + TILE * KS + row * KS + c8) = qv;
+      *reinterpret_cast<uint4*>(t + 2 * TILE * KS + row * KS + c8) = rg[i];
+    }
+    if (tid < TILE) {
+      sLD[buf][0][tid] = rl;
+      sLD[buf][1][tid] = rd;
+    }
+  };
+  if (nqt > 0) {
+    gload(0);
+    sstore(0);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load(p, rp, h, cb - 64 * (ch - 2), tid + 256 * i);
+      ring_chunk_store(sring + ch * TILE * KS, rr, tid);
+    }
+    __syncthreads();
+  }
+  bf16* dsb = dsbuf + ((long)b * p.H + h) * p.T * (long)ldS;
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int cur = qt & 1;
+    const bf16* sQu = sq + cur * 3 * TILE * KS;
+    const bf16* sQv = sQu + TILE * KS;
+    const bf16* sG = sQv + TILE * KS;
+    if (qt + 1 < nqt) {
+      gload(qt + 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load(p, rp, h, cb - 64 * (qt + 1), tid + 256 * i);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      // S[q][key], dP[q][key] of queries 32t..32t+31 of the tile (accumulator rows) x the wave's 32 keys
+      f32x16 sa = (f32x16){0}, ga = (f32x16){0}, x0 = (f32x16){0}, x1 = (f32x16){0};
+      const int o = 32 * (1 + wv - t);           // band offset of the wave's 64 rows in the tile window
+      const bf16* blk0 = sring + ((qt + 2 - (o >> 6)) & (RING - 1)) * TILE * KS + (o & 63) * KS;
+      const bf16* blk1 = sring + ((qt + 2 - ((o + 32) >> 6)) & (RING - 1)) * TILE * KS + ((o + 32) & 63) * KS;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQu, 32 * t, 16 * s, lane), kf[s], sa, 0, 0, 0);
+        ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sG, 32 * t, 16 * s, lane), vf[s], ga, 0, 0, 0);
+        const bf16x8 qvf = rowfrag(sQv, 32 * t, 16 * s, lane);     // queries as the B operand
+        x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk0, 0, 16 * s, lane), qvf, x0, 0, 0, 0);
+        x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk1, 0, 16 * s, lane), qvf, x1, 0, 0, 0);
+      }
+      // X[r'][i] (lanes = queries) -> stage[i][r']; bd[i][j] = X[j - i + 31][i]
+      {
+        float* colw = st + jj * SS2;       // lane's column = query jj of the sub-block
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int r0 = 8 * g + 4 * hh;
+          *reinterpret_cast<float4*>(colw + r0) = make_float4(x0[4 * g], x0[4 * g + 1], x0[4 * g + 2], x0[4 * g + 3]);
+          *reinterpret_cast<float4*>(colw + 32 + r0) =
+              make_float4(x1[4 * g], x1[4 * g + 1], x1[4 * g + 2], x1[4 * g + 3]);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qa = acc_row(r, hh);
+          sa[r] += st[qa * SS2 + jj - qa + 31];
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      const float* tL = sLD[cur][0] + 32 * t;
+      const float* tD = sLD[cur][1] + 32 * t;
+      f32x16 pd;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qa = acc_row(r, hh);
+        const int qia = qt * TILE + 32 * t + qa;
+        const float pa = kvalid ? exp2f(sa[r] * c - tL[qa]) : 0.f;     // lse = +inf for q >= T
+        float ma = 1.f;
+        if (p.drop_p > 0.f) ma = dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qia, kj));
+        pd[r] = pa * ma;
+        sa[r] = pa * (ga[r] * ma - tD[qa]);
+      }
+      // scale * dS -> dsbuf[i][j] (query-major: lanes = consecutive keys)
+      if (kj < p.T) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qia = qt * TILE + 32 * t + acc_row(r, hh);
+          if (qia < p.T) dsb[(long)qia * ldS + kj] = (bf16)(sa[r] * p.scale);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = acc2frag(pd, s2);
+        const bf16x8 sf = acc2frag(sa, s2);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 0, lane), pf, dv0, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 32, lane), pf, dv1, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 0, lane), sf, dk0, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 32, lane), sf, dk1, 0, 0, 0);
+      }
+    }
+    if (qt + 1 < nqt) {
+      sstore(cur ^ 1);
+      ring_chunk_store(sring + ((qt + 3) & (RING - 1)) * TILE * KS, rr, tid);
+    }
+    __syncthreads();
+  }
+  float* stage = sst + wv * 32 * SS2;    // 32 x 68 >= 32 x 65 floats
+  const int nvalid = min(32, p.T - k0w);
+  if (nvalid > 0) {
+    bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
+    store_transposed(stage, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
+    store_transposed(stage, dv0, dv1, 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
+  }
+}
+
+// ------------------------------------------------------------------------------------ dpos
+// grid (ceil((2T-1)/64), H): 64 relative rows R0.. of head h; 4 waves = (d half, r half).
+// dpos[r][h*dk+d] = sum_b sum_i dsbuf[b,h,i, i+r-(T-1)] * (q_i + v)[d]   (keys j < len[b] only)
+__global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp, const bf16* __restrict__ dsbuf,
+                                                                int ldS, float* __restrict__ dpos) {
+  __shared__ __attribute__((aligned(16))) bf16 sA[TILE * KS];    // (q+v)[ii][d]
+  __shared__ __attribute__((aligned(16))) bf16 sB[TILE * KS];    // dS_diag[ii][rr]
+  __shared__ float sO[TILE * 65];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int R0 = blockIdx.x * TILE, h = blockIdx.y;
+  const int dh = wv & 1, rh = wv >> 1;
+  const int T = p.T, nrel = 2 * T - 1;
+  f32x16 acc = (f32x16){0};
+  for (int b = 0; b < p.B; ++b) {
+    const int len = min(p.len[b], T);
+    // i range with a key j = i + r - (T-1) in [0, len) for some r in the tile
+    const int ilo = max(0, T - 1 - (R0 + TILE - 1));
+    const int ihi = min(T - 1, len - 1 + T - 1 - R0);
+    if (len <= 0 || ihi < ilo) continue;
+    const bf16* dsb = dsbuf + ((long)b * p.H + h) * T * (long)ldS;
+    const bf16* qbase = p.qkv + (long)b * T * p.D3 + h * p.dk;
+    for (int I0 = ilo & ~(TILE - 1); I0 <= ihi; I0 += TILE) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int v = tid + 256 * k;
+        const int row = v >> 3, c8 = (v & 7) * 8;
+        const int i = I0 + row;
+        // (q_i + v) chunk
+        const bf16x8 q = __builtin_bit_cast(bf16x8, ld8(qbase, p.D3, i, T, c8, p.dk, p.vec));
+        bf16x8 qv, dv8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int d = c8 + e;
+          qv[e] = (bf16)(i < T && d < p.dk ? (float)q[e] + rp.pv[h * p.dk + d] : 0.f);
+        }
+        // dS_diag[i][R0 + c8 + e] = ds[i][i + R0 + c8 + e - (T-1)]
+        const int j0 = i + R0 + c8 - (T - 1);
+        const unsigned short* srow = reinterpret_cast<const unsigned short*>(dsb + (long)min(i, T - 1) * ldS);
+        unsigned short t8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int j = j0 + e;
+          t8[e] = (i < T && j >= 0 && j < len && R0 + c8 + e < nrel) ? srow[j] : (unsigned short)0;
+        }
+        dv8 = __builtin_bit_cast(bf16x8, make_uint4(t8[0] | (t8[1] << 16), t8[2] | (t8[3] << 16),
+                                                    t8[4] | (t8[5] << 16), t8[6] | (t8[7] << 16)));
+        *reinterpret_cast<bf16x8*>(sA + row * KS + c8) = qv;
+        *reinterpret_cast<bf16x8*>(sB + row * KS + c8) = dv8;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sA, 16 * s, 32 * dh, lane),
+                                                      trfrag_perm(sB, 16 * s, 32 * rh, lane), acc, 0, 0, 0);
+      __syncthreads();
+    }
+  }
+  // acc: rows d (32 dh + acc_row), lanes rr (32 rh + lane&31) -> sO[rr][d] -> dpos rows
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sO[(32 * rh + (lane & 31)) * 65 + 32 * dh + acc_row(r, hh)] = acc[r];
+  __syncthreads();
+  for (int idx = tid; idx < TILE * 64; idx += 256) {
+    const int rr = idx >> 6, d = idx & 63;
+    if (R0 + rr < nrel && d < p.dk) dpos[(long)(R0 + rr) * p.HD + h * p.dk + d] = sO[rr * 65 + d];
+  }
+}
+
+}  // namespace
+
+namespace cfm {
+
+// workspace of the rel-pos MFMA backward: [D (B*H*T f32)] [du/dv partials] [scale*dS (B*H*T*ldS bf16)]
+static inline int rel_ldS(int T) { return (T + 7) & ~7; }
+static inline size_t rel_part_floats(int B, int T, int H, int dk) { return (size_t)B * 4 * cdiv(T, 128) * 2 * H * dk; }
+
+size_t attn_rel_ws_bytes(int B, int T, int H, int dk) {
+  const size_t d = (size_t)B * H * T * sizeof(float);
+  const size_t part = rel_part_floats(B, T, H, dk) * sizeof(float);
+  const size_t ds = (size_t)B * H * T * rel_ldS(T) * sizeof(bf16);
+  return ((d + 255) & ~(size_t)255) + ((part + 255) & ~(size_t)255) + ds;
+}
+
+static RelP make_relp(const void* pos, const float* pu, const float* pv, int dk) {
+  return RelP{(const bf16*)pos, pu, pv, ((uintptr_t)pos % 16 == 0) && (dk % 8 == 0)};
+}
+
+static AttnM make_attnm(const void* qkv, const void* dout, const int32_t* len, int B, int T, int H, int dk,
+                        float drop_p, uint64_t seed) {
+  AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, len, 1.f / sqrtf((float)dk), drop_p, seed,
+          ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), 0,
+          g_rng_salt};
+  return p;
+}
+
+int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len, const void* pos, const float* pu,
+                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s) {
+  const AttnM p = make_attnm(qkv, qkv, len, B, T, H, dk, drop_p, seed);
+  hipLaunchKernelGGL(attn_rel_fwd_kernel, dim3(cdiv(p.T, 128), p.H, p.B), dim3(256), 0, s, p,
+                     make_relp(pos, pu, pv, p.dk), (bf16*)o, lse);
+  return check_launch("cfm_attn_fwd(rel)");
+}
+
+// D (rowsum dO*O per head) must already be in ws[0 .. B*H*T)
+int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, const int32_t* len, const void* pos,
+                        const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
+                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s) {
+  const AttnM p = make_attnm(qkv, dout, len, B, T, H, dk, drop_p, seed);
+  const RelP rp = make_relp(pos, pu, pv, p.dk);
+  const size_t d_bytes = ((size_t)p.B * p.H * p.T * sizeof(float) + 255) & ~(size_t)255;
+  float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + d_bytes);
+  const size_t part_bytes = (rel_part_floats(p.B, p.T, p.H, p.dk) * sizeof(float) + 255) & ~(size_t)255;
+  bf16* dsbuf = reinterpret_cast<bf16*>(reinterpret_cast<char*>(part) + part_bytes);
+  const int ldS = rel_ldS(p.T);
+  const dim3 grid(cdiv(p.T, 128), p.H, p.B);
+  hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws, (bf16*)dqkv,
+                     dsbuf, ldS);
+  hipLaunchKernelGGL(attn_rel_bwd_dq_kernel, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws, (bf16*)dqkv,
+                     part);
+  hipLaunchKernelGGL(attn_rel_bwd_dpos_kernel, dim3(cdiv(2 * p.T - 1, TILE), p.H), dim3(256), 0, s, p, rp,
+                     (const bf16*)dsbuf, ldS, dpos);
+  const int nrows = p.B * 4 * cdiv(p.T, 128);
+  colreduce(part, nrows, (long)p.HD, dpu, 0, s, 2L * p.HD);
+  colreduce(part + p.HD, nrows, (long)p.HD, dpv, 0, s, 2L * p.HD);
+  return check_launch("cfm_attn_bwd(rel)");
+}
+
+}  // namespace cfm

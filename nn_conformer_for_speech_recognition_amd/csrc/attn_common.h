@@ -1,0 +1,125 @@
+// attn_common.h — shared pieces of the MFMA attention kernels (attention.hip, attention_rel.hip):
+// tile geometry, the per-(b,h) parameter block, attention-dropout indexing, and the fragment
+// helpers that move 32x32x16 bf16 MFMA operands between LDS tiles, registers and accumulators.
+#pragma once
+#include "cfm_common.h"
+
+namespace {
+
+constexpr int DKP = 64;      // padded head dim
+constexpr int KS = DKP + 8;  // LDS row stride (elements): 144-B rows, conflict-free ds_read_b128
+constexpr int TILE = 64;     // keys (fwd/dQ) or queries (dK/dV) per LDS tile
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+struct AttnM {
+  const bf16* qkv;
+  int B, T, H, dk, D3, HD;
+  const int32_t* len;
+  float scale;
+  float drop_p; uint64_t seed;
+  bool vec;    // 16-B vector loads legal
+  int dbg;     // timing experiments (cfm_attn_set_mode bits 1-2)
+  const uint64_t* salt;   // bound dropout step counter or nullptr
+};
+
+// attention-dropout element index: rows of an EVEN stride (T rounded up to even), so the keys 2m and
+// 2m+1 of one (query, key-pair) share one 32-bit hash (low / high 16 bits): kernels holding both keys of
+// a pair in one lane (accumulator registers r, r+1 for even r) hash once per pair (dropout_pair)
+__device__ __forceinline__ uint64_t didx(const AttnM& p, int b, int h, int i, int j) {
+  return (((uint64_t)b * p.H + h) * p.T + i) * (uint64_t)(p.T + (p.T & 1)) + j;
+}
+// keep-scales of elements idx (even) and idx + 1: one mix for both (== dropout_keyed of each)
+__device__ __forceinline__ void dropout_pair(uint32_t thr, float keep, uint32_t key, uint64_t idx, float& m0,
+                                             float& m1) {
+  const uint32_t h = cfm_mix32((uint32_t)(idx >> 1) ^ key);
+  m0 = (h & 0xFFFFu) >= thr ? keep : 0.f;
+  m1 = (h >> 16) >= thr ? keep : 0.f;
+}
+
+// 8 consecutive head-dim elements c..c+7 of row `row` of matrix base (row stride ld), zero-padded
+__device__ __forceinline__ uint4 ld8(const bf16* base, long ld, int row, int nrows, int c, int dk, bool vec) {
+  uint4 r = make_uint4(0, 0, 0, 0);
+  if (row >= nrows || c >= dk) return r;
+  const bf16* p = base + (long)row * ld + c;
+  if (vec && c + 8 <= dk) return *reinterpret_cast<const uint4*>(p);
+  unsigned short t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = (c + e < dk) ? reinterpret_cast<const unsigned short*>(p)[e] : 0;
+  r.x = t[0] | (t[1] << 16); r.y = t[2] | (t[3] << 16); r.z = t[4] | (t[5] << 16); r.w = t[6] | (t[7] << 16);
+  return r;
+}
+
+// A-operand fragment, natural k order, from a [row][KS] tile: lane (r, hh) gets row r0+r, cols k0+8hh..+7
+__device__ __forceinline__ bf16x8 rowfrag(const bf16* tile, int r0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(tile + (r0 + (lane & 31)) * KS + k0 + 8 * (lane >> 5));
+}
+
+// A-operand fragment of the TRANSPOSED tile, k order permuted to match an accumulator used as the
+// B operand (element j of lane half hh <-> tile row r0 + 8(j>>2) + 4hh + (j&3)); column c0 + (lane&31).
+__device__ __forceinline__ bf16x8 trfrag_perm(const bf16* tile, int r0, int c0, int lane) {
+  const int hh = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+  const bf16* base = tile + (r0 + 4 * hh + q) * KS + c0 + 16 * g1 + 4 * p4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 8 * KS));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// accumulator registers 8s..8s+7 -> bf16 B-operand fragment of k-step s
+__device__ __forceinline__ bf16x8 acc2frag(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
+  return r;
+}
+
+// accumulator row of register r for lane half hh
+__device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+// stage a [64 rows][64 cols] bf16 tile (row r0.., column offset col of qkv) into LDS; 2 x 16 B per thread
+__device__ __forceinline__ void tile_load(const AttnM& p, int b, int r0, int col, uint4 (&reg)[2], int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + 256 * i;
+    reg[i] = ld8(p.qkv + (long)b * p.T * p.D3 + col, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+  }
+}
+__device__ __forceinline__ void tile_store(bf16* t, const uint4 (&reg)[2], int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + 256 * i;
+    *reinterpret_cast<uint4*>(t + (v >> 3) * KS + (v & 7) * 8) = reg[i];
+  }
+}
+
+// B-operand fragments (natural k order) of a 32-row block: lane (r, hh) = row[r][16s + 8hh .. +7]
+__device__ __forceinline__ void load_bfrags(const AttnM& p, const bf16* base, long ld, int row, int nrows,
+                                            bf16x8 (&f)[4], int lane) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint4 u = ld8(base, ld, row, nrows, 16 * s + 8 * (lane >> 5), p.dk, p.vec);
+    f[s] = __builtin_bit_cast(bf16x8, u);
+  }
+}
+
+// write a wave's 64(d) x 32(cols) f32 accumulator pair (dt = 0, 1) transposed into a bf16 matrix:
+// out[(row0 + c) * ld + d] = acc[d][c] * mul_c  (c < ncols, d < dk), staged through LDS.
+__device__ void store_transposed(float* stage, const f32x16& a0, const f32x16& a1, float mulc, bf16* out, long ld,
+                                 int row0, int nvalid, int dk, int lane) {
+  const int hh = lane >> 5, c = lane & 31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    stage[c * 65 + acc_row(r, hh)] = a0[r] * mulc;
+    stage[c * 65 + 32 + acc_row(r, hh)] = a1[r] * mulc;
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int idx = lane; idx < 32 * 64; idx += 64) {
+    const int cc = idx >> 6, d = idx & 63;
+    if (cc < nvalid && d < dk) out[(long)(row0 + cc) * ld + d] = (bf16)stage[cc * 65 + d];
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+}  // namespace

@@ -84,3 +84,80 @@ def test_rowdot_epilogue_feeds_attention_bwd():
     d1, _, _, _ = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=0.1, seed=4)
     d2, _, _, _ = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=0.1, seed=4, D=D)
     assert _rel(d2.float(), d1.float()) < 1e-3
+
+
+# ------------------------------------------------------------------------------------ relative positions
+def _ref_rel(qkv, pos, pu, pv, lens, B, T, H, dk, do):
+    """fp32 torch restatement of transformers' rel-pos attention core (modeling_wav2vec2_conformer.py:528-565):
+    scores = ((q+u) k^T + rel_shift((q+v) p^T)) / sqrt(dk), bd[i, j] uses p row (T-1) - i + j."""
+    x = qkv.float().view(B, T, 3, H, dk).requires_grad_()
+    P = pos.float().view(2 * T - 1, H, dk).requires_grad_()
+    u = pu.float().view(H, dk).requires_grad_()
+    v = pv.float().view(H, dk).requires_grad_()
+    q, k, vv = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+    ac = (q + u[None, :, None, :]) @ k.transpose(-1, -2)
+    full = (q + v[None, :, None, :]) @ P.permute(1, 2, 0)[None]          # (B, H, T, 2T-1)
+    ar = torch.arange(T, device=qkv.device)
+    idx = (T - 1 - ar[:, None] + ar[None, :]).expand(B, H, T, T)
+    s = (ac + full.gather(-1, idx)) / dk ** 0.5
+    mask = ar[None, :] >= lens[:, None].long()
+    s = s.masked_fill(mask[:, None, None, :], float("-inf"))
+    o = (s.softmax(-1) @ vv).transpose(1, 2).reshape(B * T, H * dk)
+    o.backward(do.float())
+    return o.detach(), x.grad.view(B * T, 3 * H * dk), P.grad.view(2 * T - 1, H * dk), u.grad.reshape(-1), \
+        v.grad.reshape(-1)
+
+
+def _rel_case(B, T, H, dk, lens, seed):
+    g = torch.Generator().manual_seed(seed)
+    qkv = torch.randn(B * T, 3 * H * dk, generator=g).to(DEV, torch.bfloat16)
+    pos = (0.5 * torch.randn(2 * T - 1, H * dk, generator=g)).to(DEV, torch.bfloat16)
+    pu = (0.3 * torch.randn(H * dk, generator=g)).to(DEV)
+    pv = (0.3 * torch.randn(H * dk, generator=g)).to(DEV)
+    do = torch.randn(B * T, H * dk, generator=g).to(DEV, torch.bfloat16)
+    ln = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    return qkv, pos, pu, pv, do, ln
+
+
+@pytest.mark.parametrize("B,T,H,dk,lens", [
+    (3, 373, 2, 64, [373, 300, 41]),       # the metric's T_enc, ragged
+    (1, 1498, 2, 64, [1498]),              # config 5: 60 s long-form (T_enc = 1498)
+    (2, 1498, 1, 64, [1498, 1001]),
+    (2, 97, 4, 36, [97, 60]),              # Conformer-S head dim (zero-padded to 64)
+    (2, 64, 1, 64, [64, 1]),
+])
+def test_rel_attention_vs_torch(B, T, H, dk, lens):
+    """MFMA rel-pos kernels (attention_rel.hip) vs the fp32 torch restatement: outputs and every
+    gradient (q/k/v, projected table p, pos_bias_u, pos_bias_v).  Tolerance: relative L2 1e-2 (o),
+    2e-2 (dqkv, dpos), 3e-2 (du, dv: sums over all queries of bf16-rounded dS products)."""
+    qkv, pos, pu, pv, do, ln = _rel_case(B, T, H, dk, lens, T + H)
+    o, lse = ops.attn_fwd(qkv, ln, B, T, H, dk, pos, pu, pv)
+    dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, ln, B, T, H, dk, pos, pu, pv)
+    ro, rg, rp, ru, rv = _ref_rel(qkv, pos, pu, pv, ln, B, T, H, dk, do)
+    torch.cuda.synchronize()
+    assert _rel(o.float(), ro) < 1e-2
+    assert _rel(dqkv.float(), rg) < 2e-2
+    assert _rel(dpos, rp) < 2e-2
+    assert _rel(dpu, ru) < 3e-2
+    assert _rel(dpv, rv) < 3e-2
+    # per valid query row, worst max-abs error relative to the row's max (a bad row cannot hide in the L2)
+    ob = o.float().view(B, T, -1).cpu()
+    rb = ro.view(B, T, -1).cpu()
+    for b, n in enumerate(lens):
+        d = (ob[b, :n] - rb[b, :n]).abs().amax(-1) / rb[b, :n].abs().amax(-1).clamp_min(1e-30)
+        assert d.max().item() < 5e-2, (b, d.argmax().item())
+
+
+def test_rel_attention_mfma_matches_simt_under_dropout(attn_mode):
+    """Same counter-based attention-dropout masks on both rel-pos paths: MFMA (default) and the SIMT
+    kernels (cfm_attn_set_mode bit 4), fwd + every gradient."""
+    B, T, H, dk = 2, 150, 2, 64
+    qkv, pos, pu, pv, do, ln = _rel_case(B, T, H, dk, [150, 111], 3)
+    outs = []
+    for mode in (0, 16):
+        attn_mode(mode)
+        o, lse = ops.attn_fwd(qkv, ln, B, T, H, dk, pos, pu, pv, drop_p=0.15, seed=77)
+        g = ops.attn_bwd(qkv, o, do, lse, ln, B, T, H, dk, pos, pu, pv, drop_p=0.15, seed=77)
+        outs.append((o.float(), g[0].float(), g[1], g[2], g[3]))
+    for a, b in zip(outs[0], outs[1]):
+        assert _rel(a, b) < 3e-2

@@ -63,6 +63,9 @@ CASES = [
     (144, 4, 576, 31, 2, 3, 130, [130, 129, 64], True, "none"),
     (512, 8, 2048, 31, 1, 2, 373, [373, 300], False, "none"),
     (128, 2, 256, 15, 1, 2, 96, [96, 50], False, "rel"),
+    (512, 8, 2048, 31, 1, 2, 373, [373, 290], False, "rel"),     # Conformer-L dims at the metric's T_enc
+    (512, 8, 2048, 31, 1, 1, 1498, [1498], False, "rel"),        # config 5 length (60 s), B = 1
+    (512, 8, 2048, 31, 1, 2, 1498, [1498, 1100], False, "none"),
 ]
 
 
