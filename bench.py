@@ -31,6 +31,7 @@ sys.path.insert(0, REPO)
 from nn_conformer_for_speech_recognition_amd import _lib  # noqa: E402
 from nn_conformer_for_speech_recognition_amd import dist as cdist  # noqa: E402
 from nn_conformer_for_speech_recognition_amd import ops  # noqa: E402
+from nn_conformer_for_speech_recognition_amd import specaugment  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.ctc import ctc_head_loss  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.conformer import Conformer  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.frontend import linear  # noqa: E402
@@ -39,22 +40,29 @@ from nn_conformer_for_speech_recognition_amd.lib.hparams import HParams  # noqa:
 from nn_conformer_for_speech_recognition_amd.optim import Adafactor  # noqa: E402
 
 METRIC = "mel-frames/sec/GPU Conformer-L encoder fwd+bwd; 1/2/4/8-GPU scaling"
-# (name, layers, d, heads, ffn, K, batch per GPU, seconds)
+# (name, layers, d, heads, ffn, K, batch per GPU, seconds, positional encoding) -- BASELINE.json configs:
+# S15 = configs[1], M15 = configs[2] (run with --specaug), L15 = the metric's model at configs[1]'s shape
+# (the headline line), L60 = configs[4] (60 s long-form, relative-position attention)
 CONFIGS = {
-    "L15": ("Conformer-L", 17, 512, 8, 2048, 31, 32, 15),
-    "M15": ("Conformer-M", 16, 256, 4, 1024, 31, 32, 15),
-    "S15": ("Conformer-S", 16, 144, 4, 576, 31, 32, 15),
+    "L15": ("Conformer-L", 17, 512, 8, 2048, 31, 32, 15, "none"),
+    "M15": ("Conformer-M", 16, 256, 4, 1024, 31, 32, 15, "none"),
+    "S15": ("Conformer-S", 16, 144, 4, 576, 31, 32, 15, "none"),
+    "L60": ("Conformer-L", 17, 512, 8, 2048, 31, 8, 60, "rel"),
 }
 PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
-def algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, F2, C1=512, C2=128):
-    """per-layer per-encoder-frame MACs 4*d*ffn + 4d^2 + 3d^2 + K*d + 2*T*d, the
+def algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, F2, C1=512, C2=128, rel=False, B=1):
+    """per-layer per-encoder-frame MACs 4*d*ffn + 4d^2 + 3d^2 + K*d + 2*T*d
+    (+ T*d + (2T-1)*d^2/(B*T) with relative positions: the bd scores and linear_pos), the
     front-end (conv1 + conv2 + frame projection), x2 FLOPs, fwd+bwd = 3x fwd minus conv1's dgrad."""
     F1, T1 = (80 - 7) // 2 + 1, (T_in - 7) // 2 + 1
-    enc = L * T2 * (4 * d * ffn + 7 * d * d + K * d + 2 * T2 * d)
+    per = 4 * d * ffn + 7 * d * d + K * d + 2 * T2 * d
+    if rel:
+        per += T2 * d + (2 * T2 - 1) * d * d / (B * T2)
+    enc = L * T2 * per
     conv1 = C1 * 49 * F1 * T1
     conv2 = C2 * C1 * 9 * F2 * T2
     proj = T2 * F2 * C2 * d
@@ -66,7 +74,7 @@ def algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, F2, C1=512, C2=128):
 class EncoderCTC(torch.nn.Module):
     """Front-end + Conformer encoder + CTC head (the hot path of SURVEY.md §8a, 'frame' mode)."""
 
-    def __init__(self, L, d, H, ffn, K, V, F_bins, T_in, dropout, cd):
+    def __init__(self, L, d, H, ffn, K, V, F_bins, T_in, dropout, cd, pos_enc="none"):
         super().__init__()
         hp = HParams(None)
         hp.set_input_dim(F_bins, T_in)
@@ -76,15 +84,19 @@ class EncoderCTC(torch.nn.Module):
         self.F1, self.T1 = (F_bins - 7) // 2 + 1, (T_in - 7) // 2 + 1
         self.F2, self.T2 = (self.F1 - 3) // 2 + 1, (self.T1 - 3) // 2 + 1
         self.standard_linear = torch.nn.Linear(self.F2 * hp.conv_sub_2_nodes, d)
-        self.conformers = Conformer(d, H, ffn, L, K, dropout, compute_dtype=cd)
+        self.conformers = Conformer(d, H, ffn, L, K, dropout, pos_enc=pos_enc, compute_dtype=cd)
         self.ctc_fc = torch.nn.Linear(d, V)
         self.dropout = dropout
 
-    def forward(self, x, lens_i32, targets_i32, tgt_lens_i32, seed):
+    def forward(self, x, lens_i32, targets_i32, tgt_lens_i32, seed, specaug_params=None):
         """-> (CTC loss (mean, zero_infinity), logits (B, T2, V)).  The head is the fused
         Linear + log_softmax + CTC node (ctc.hip); dropout seeds are offset on the device by the
-        bound step counter, so one captured graph replays with fresh masks."""
+        bound step counter, so one captured graph replays with fresh masks.  specaug_params: the
+        device parameter block of this step's SpecAugment draws (specaugment.pack) -- the warp +
+        masks then run as the first kernel of the step (asrnn.py:196-197)."""
         B = x.shape[0]
+        if specaug_params is not None:
+            x = specaugment.apply(x, specaug_params, intended=True)
         h2 = self.conv_sub_sampling.forward_frames(x, self.cd)
         p = self.dropout if self.training else 0.0
         h = linear(h2.view(B * self.T2, -1), self.standard_linear.weight, self.standard_linear.bias, cd=self.cd,
@@ -135,10 +147,11 @@ class KernelProbe:
 
 def cpu_baseline(cfg, threads, steps=2):
     """The CPU oracle (torch fp32 restatement of the same composition) on a bounded sample:
-    1 utterance x 15 s through front-end + encoder + CTC, fwd+bwd, 1 warm-up then `steps` timed."""
+    1 utterance of the config's length through front-end + encoder + CTC, fwd+bwd, 1 warm-up then
+    `steps` timed."""
     from oracle import conformer as oc
     from oracle import frontend as of
-    name, L, d, H, ffn, K, _, secs = cfg
+    name, L, d, H, ffn, K, _, secs, pos = cfg
     torch.set_num_threads(threads)
     T_in = 100 * secs + 1
     g = torch.Generator().manual_seed(0)
@@ -150,7 +163,7 @@ def cpu_baseline(cfg, threads, steps=2):
     T2 = ((T_in - 7) // 2 + 1 - 3) // 2 + 1
     wf = (torch.randn(d, 18 * 128, generator=g) * 0.02).requires_grad_()
     bf = torch.zeros(d, requires_grad=True)
-    conf = oc.ConformerRef(d, H, ffn, L, K, 0.0).train()
+    conf = oc.ConformerRef(d, H, ffn, L, K, 0.0, pos_enc=pos).train()
     wc = (torch.randn(1024, d, generator=g) * 0.02).requires_grad_()
     tgt = torch.randint(1, 1024, (1, T2 // 4), generator=g)
     lens = torch.tensor([T2])
@@ -169,7 +182,39 @@ def cpu_baseline(cfg, threads, steps=2):
     dt = (time.perf_counter() - t0) / steps
     return {"value": round(T_in / dt, 1), "unit": "mel-frames/s", "cores": threads, "kind": "port",
             "sample": f"{name} fp32 oracle (torch CPU), 1 x {secs} s utterance ({T_in} frames), front-end + "
-                      f"{L} layers + CTC, fwd+bwd, mean of {steps} steps after 1 warm-up"}
+                      f"{L} layers ({pos} pos) + CTC, fwd+bwd, mean of {steps} steps after 1 warm-up"}
+
+
+def cpu_baseline_s10(threads, steps=2):
+    """BASELINE.json configs[0]: Conformer-S (16 L, d 144, 4 heads, ffn 576, K 31) forward on 4 x 10 s
+    80-bin mel clips, the CPU plumbing path -- the fp32 oracle (front-end + frame projection + encoder),
+    eval mode, no autograd."""
+    from oracle import conformer as oc
+    from oracle import frontend as of
+    torch.set_num_threads(threads)
+    B, T_in, d = 4, 1001, 144
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(B, 1, 80, T_in, generator=g)
+    w1 = torch.randn(512, 1, 7, 7, generator=g) * 0.1
+    b1 = torch.zeros(512)
+    w2 = torch.randn(128, 512, 3, 3, generator=g) * 0.01
+    b2 = torch.zeros(128)
+    T2 = ((T_in - 7) // 2 + 1 - 3) // 2 + 1
+    wf = torch.randn(d, 18 * 128, generator=g) * 0.02
+    bf = torch.zeros(d)
+    conf = oc.ConformerRef(d, 4, 576, 16, 31, 0.1).eval()
+    lens = torch.full((B,), T2)
+    with torch.no_grad():
+        def fwd():
+            return conf(of.frame_projection(of.convsub_forward(x, w1, b1, w2, b2), wf, bf), lens)
+        fwd()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fwd()
+        dt = (time.perf_counter() - t0) / steps
+    return {"value": round(B * T_in / dt, 1), "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "sample": f"configs[0]: Conformer-S fp32 oracle forward (eval), 4 x 10 s clips ({T_in} frames), "
+                      f"front-end + frame projection + 16 layers, mean of {steps} after 1 warm-up"}
 
 
 def main():
@@ -184,6 +229,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--gemm-mode", type=int, default=None, help="cfm_gemm_set_mode value (A/B tuning)")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no HIP graph)")
+    ap.add_argument("--specaug", action="store_true",
+                    help="SpecAugment inside the step (host draws in the reference order, one warp+mask kernel)")
+    ap.add_argument("--pos-enc", choices=("none", "rel"), default=None, help="override the config's pos encoding")
     ap.add_argument("--probe-inline", action="store_true",
                     help="put the roofline probe kernels inside the timed graph (default: a separate probed graph)")
     args = ap.parse_args()
@@ -194,12 +242,14 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = CONFIGS[args.config]
-    name, L, d, H, ffn, K, B, secs = cfg
+    if args.pos_enc is not None:
+        cfg = cfg[:8] + (args.pos_enc,)
+    name, L, d, H, ffn, K, B, secs, pos_enc = cfg
     T_in, Fb, V = 100 * secs + 1, 80, 1024
     cd = torch.bfloat16
 
     torch.manual_seed(1234)                      # identical init on every rank (then broadcast)
-    model = EncoderCTC(L, d, H, ffn, K, V, Fb, T_in, args.dropout, cd).to(dev).train()
+    model = EncoderCTC(L, d, H, ffn, K, V, Fb, T_in, args.dropout, cd, pos_enc).to(dev).train()
     cdist.broadcast_parameters(model)
     params = [p for p in model.parameters() if p.requires_grad]
     reducer = cdist.GradAllReducer(params)
@@ -221,9 +271,28 @@ def main():
     tlen_i32 = torch.full((B,), U, dtype=torch.int32, device=dev)
     seed0 = 17 * rank + 1
 
+    # SpecAugment (configs[2]): the global batch's draws on the host in the reference's order
+    # (specaugment.draw, python random seeded as speechcommands.py:18), this rank's slice packed into
+    # a STATIC device block that the captured step reads; refreshed before every step
+    sa_params = None
+    if args.specaug:
+        import random as _random
+        sa_rng = _random.Random(42)
+        sa_hp = HParams(None)
+        tau_glob = [T_in] * (B * world)
+
+        def specaug_refresh():
+            dr = specaugment.draw(B * world, Fb, tau_glob, sa_hp, sa_rng)
+            blk = specaugment.pack(dr, tau_glob, rank * B, (rank + 1) * B)
+            if sa_params is None:
+                return blk.to(dev)
+            sa_params.copy_(blk.pin_memory(), non_blocking=True)
+            return sa_params
+        sa_params = specaug_refresh()
+
     def fwd_bwd():
         rng.add_(1)
-        loss, _ = model(x, lens_i32, tgt_i32, tlen_i32, seed=seed0)
+        loss, _ = model(x, lens_i32, tgt_i32, tlen_i32, seed=seed0, specaug_params=sa_params)
         loss.backward()
         return loss
 
@@ -238,11 +307,15 @@ def main():
     # bias + SiLU epilogue on K-major operands, not the shape alone)
     probe = KernelProbe(lambda kind, shape, dsc: kind == "gemm" and shape == (M_ffn, ffn, d) and dsc.act == 1
                         and not dsc.act_grad and dsc.a_kmajor and dsc.b_kmajor, dev)
-    ops.PROBE = probe
+    # second probed family: the grouped weight-gradient launch (one per step)
+    wprobe = KernelProbe(lambda kind, shape, dsc: kind == "wgroup", dev)
+    ops.PROBE = lambda kind, shape, dsc, launch: probe(kind, shape, dsc, lambda: wprobe(kind, shape, dsc, launch))
     graph = probe_graph = None
     if args.eager:
         def step(i):
             opt.zero_grad(set_to_none=True)
+            if sa_params is not None:
+                specaug_refresh()
             loss = fwd_bwd()
             post()
             return loss
@@ -272,24 +345,26 @@ def main():
         if not args.probe_inline:
             opt.zero_grad(set_to_none=True)
             probe_graph = torch.cuda.CUDAGraph()
-            probe.active = True
+            probe.active = wprobe.active = True
             with torch.cuda.graph(probe_graph):
                 fwd_bwd()
-            probe.active = False
+            probe.active = wprobe.active = False
             for p, g in zip(params, grads_timed):
                 p.grad = g           # the timed replays' optimizer steps read the timed graph's grads
         else:
             graph = torch.cuda.CUDAGraph()    # legacy: probes inside the timed graph
             opt.zero_grad(set_to_none=True)
-            probe.active = True
+            probe.active = wprobe.active = True
             with torch.cuda.graph(graph):
                 static_loss = fwd_bwd()
-            probe.active = False
+            probe.active = wprobe.active = False
 
         host_t = []
 
         def step(i):
             t_a = time.perf_counter()
+            if sa_params is not None:
+                specaug_refresh()
             graph.replay()
             t_b = time.perf_counter()
             post()
@@ -298,12 +373,13 @@ def main():
         step(0)                      # one replay outside the timed region
         torch.cuda.synchronize()
         probe.reset()
+        wprobe.reset()
 
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     if graph is None:
-        probe.active = True
+        probe.active = wprobe.active = True
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(args.warmup + i)
@@ -311,7 +387,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
-    probe.active = False
+    probe.active = wprobe.active = False
     ops.PROBE = None
     elapsed = t1 - t0
     if world > 1:
@@ -339,9 +415,40 @@ def main():
         timing = ("in-kernel s_memrealtime first-start / last-end of every matching launch in the timed "
                   "region" + (" (graph replays)" if graph is not None else ""))
     gemm_flops = 2.0 * M_ffn * ffn * d
-    achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
-    _, fpf = algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, model.F2)
+    # algorithmic bytes of one FFN up-projection launch: A (M x d) + W (ffn x d) bf16 reads, bias fp32,
+    # y and the saved pre-activation (M x ffn each, bf16) written
+    gemm_bytes = 2.0 * (M_ffn * d + ffn * d) + 4.0 * ffn + 2.0 * 2.0 * M_ffn * ffn
+    wg_ms, wg_n = wprobe.mean_ms()
+    wg_shapes = [(d, ffn), (ffn, d)] * 2 + [(3 * d, d), (d, d), (2 * d, d), (d, d)]   # (N, K) per layer
+    wg_flops = 2.0 * M_ffn * L * sum(n * k for n, k in wg_shapes)
+    wg_bytes = L * sum(2.0 * M_ffn * (n + k) + 4.0 * n * k + 4.0 * n for n, k in wg_shapes)
+    _, fpf = algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, model.F2, rel=pos_enc == "rel", B=B)
     step_tflops = fpf * B * T_in / (ms_step * 1e-3) / 1e12
+
+    def roofline_entry(kernel, flops, nbytes, ms, n_launch, pmc_file):
+        """bound from the kernel's arithmetic intensity against the machine balance (peak FLOP/s over peak
+        HBM B/s); `achieved`/`peak`/`frac` in the bound's unit, both fractions reported."""
+        intensity = flops / nbytes
+        balance = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+        tflops = flops / (ms * 1e-3) / 1e12
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        hbm = intensity < balance
+        e = {"kernel": kernel, "bound": "hbm" if hbm else "mfma",
+             "achieved": round(gbs if hbm else tflops, 1), "peak": PEAK_HBM_GBS if hbm else PEAK_BF16_TFLOPS,
+             "unit": "GB/s" if hbm else "TFLOP/s",
+             "frac": round(gbs / PEAK_HBM_GBS if hbm else tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
+             "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+             "intensity_flop_per_byte": round(intensity, 1), "machine_balance_flop_per_byte": round(balance, 1),
+             "avg_launch_ms": round(ms, 4), "launches_timed": n_launch, "timing": timing,
+             "flops_per_launch": flops, "algorithmic_bytes": nbytes}
+        path = os.path.join(REPO, "profiles", "r02", pmc_file)
+        if os.path.exists(path):
+            with open(path) as f:
+                rec = json.load(f)
+            if rec.get("shape_key") == [M_ffn, d, ffn, L] and rec.get("hbm_bytes_per_launch"):
+                e["traffic"] = rec["hbm_bytes_per_launch"]
+                e["traffic_source"] = f"profiles/r02/{pmc_file} ({rec.get('kernel', '?')[:80]})"
+        return e
 
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps,
@@ -349,6 +456,7 @@ def main():
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic (uniform min-max-normalised 80-bin mels, random init)",
         "config": {"workload": f"{name} encoder fwd+bwd + CTC head, {B} x {secs} s utterances per GPU",
                    "model": name, "layers": L, "d_model": d, "heads": H, "ffn": ffn, "conv_kernel": K,
+                   "pos_enc": pos_enc, "specaug": bool(args.specaug),
                    "global_batch": B * world, "seq_len": T_in, "enc_frames": T2, "frontend": "frame",
                    "dropout": args.dropout, "optimizer": None if args.no_optimizer else "adafactor",
                    "parallelism": f"dp{world}", "launch": "eager" if args.eager else "hip-graph (fwd+bwd)"},
@@ -356,24 +464,16 @@ def main():
         "step_algorithmic_tflops": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
         "loss": float(loss.item()),
-        "roofline": {"kernel": f"gemm_bf16 FFN up-projection M={M_ffn} N={ffn} K={d} (+bias+SiLU epilogue)",
-                     "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                     "avg_launch_ms": round(gemm_ms, 4), "launches_timed": n_launch,
-                     "timing": timing,
-                     "flops_per_launch": gemm_flops},
+        "roofline": roofline_entry(f"gemm_pipe FFN up-projection M={M_ffn} N={ffn} K={d} (+bias+SiLU+dropout, "
+                                   f"y and pre-activation stored)", gemm_flops, gemm_bytes, gemm_ms, n_launch,
+                                   "gemm_ffn_up_pmc.json"),
+        "roofline_wgrad": roofline_entry(f"grouped weight gradients (cfm_wgrad_group): {L} layers x 8 GEMMs, "
+                                         f"M={M_ffn} tokens", wg_flops, wg_bytes, wg_ms, wg_n,
+                                         "wgrad_group_pmc.json"),
     }
-    pmc = os.path.join(REPO, "profiles", "r01", "gemm_ffn_up_pmc.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            rec = json.load(f)
-        shp = rec.get("kernel_shape", {})
-        if (shp.get("M"), shp.get("N"), shp.get("K")) == (M_ffn, ffn, d):
-            result["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
-            result["roofline"]["traffic_source"] = "profiles/r01/gemm_ffn_up_pmc.json (rocprofv3 --pmc, fetch x2)"
-            result["roofline"]["algorithmic_bytes"] = rec["algorithmic_bytes_per_launch"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
+        result["cpu_baseline_configs0"] = cpu_baseline_s10(args.cpu_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -171,6 +171,9 @@ long cfm_wgrad_group_tiles(int N, int K);
 int cfm_wgrad_group_fill(void* host_table, int i, const void* dy, const void* x, float* dw, float* db, int M,
                          int N, int K, long tile0);
 int cfm_wgrad_group(const void* dev_table, int ntasks, long total_tiles, void* stream);
+/* the same launch with a timing slot (as cfm_gemm_desc.probe: first-workgroup start / last-workgroup end) */
+int cfm_wgrad_group_probed(const void* dev_table, int ntasks, long total_tiles, unsigned long long* probe,
+                           void* stream);
 /* kernel-selection switch for A/B measurements: bit 0 = 256-row register-staged tiles allowed,
    bit 1 = LDS-DMA pipelined kernel allowed, bit 3 = timing experiment (pipelined kernel skips its
    stores), bits 4-5 = pipelined variant (0 auto, 1 256x128/BK64, 2 256x128/BK32 two per CU,

@@ -66,6 +66,7 @@ _SIGS = {
     "cfm_wgrad_group_fill": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                      c_long]),
     "cfm_wgrad_group": (c_int, [c_void_p, c_int, c_long, c_void_p]),
+    "cfm_wgrad_group_probed": (c_int, [c_void_p, c_int, c_long, c_void_p, c_void_p]),
     "cfm_attn_set_mode": (c_int, [c_int]),
     "cfm_colreduce": (c_int, [c_void_p, c_int, c_long, c_long, c_void_p, c_int, c_void_p]),
     "cfm_colsum": (c_int, [c_void_p, c_int, c_long, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p]),

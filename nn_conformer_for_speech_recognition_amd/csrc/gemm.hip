@@ -662,7 +662,9 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   const int wm = wid / WN, wn = wid % WN;
   int tm, tn, zz;
   if constexpr (GROUP) {
+    unsigned long long* const probe = p.probe;   // the launch's timing slot survives the task's parameters
     group_task(ga, p, oa, ob, tm, tn);   // this workgroup's GEMM and tile of a grouped launch
+    p.probe = probe;
     zz = 0;
   } else {
     xcd_tile3(tm, tn, zz);
@@ -1210,8 +1212,11 @@ CFM_EXPORT int cfm_wgrad_group_fill(void* host_tab, int i, const void* dy, const
   return CFM_OK;
 }
 
-CFM_EXPORT int cfm_wgrad_group(const void* dev_tab, int ntasks, long total_tiles, void* stream) {
+CFM_EXPORT int cfm_wgrad_group_probed(const void* dev_tab, int ntasks, long total_tiles, unsigned long long* probe,
+                                      void* stream) {
   CFM_REQUIRE(dev_tab && ntasks > 0 && total_tiles > 0 && total_tiles < (1L << 31), CFM_ERR_ARG, "bad table");
+  GemmP gp{};
+  gp.probe = probe;
   GatherA ga{};
   ga.group_tab = dev_tab;
   ga.group_n = ntasks;
@@ -1219,11 +1224,15 @@ CFM_EXPORT int cfm_wgrad_group(const void* dev_tab, int ntasks, long total_tiles
   ga.Jn = gv == 2;
   if (gv == 1)
     hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, false, false, 8, 2, false, true>), dim3((unsigned)total_tiles),
-                       dim3(512), 0, cfm::as_stream(stream), GemmP{}, PipeOp{}, PipeOp{}, ga);
+                       dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
   else
     hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, false, false, 8, 2, false, true>), dim3((unsigned)total_tiles),
-                       dim3(512), 0, cfm::as_stream(stream), GemmP{}, PipeOp{}, PipeOp{}, ga);
+                       dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
   return cfm::check_launch("cfm_wgrad_group");
+}
+
+CFM_EXPORT int cfm_wgrad_group(const void* dev_tab, int ntasks, long total_tiles, void* stream) {
+  return cfm_wgrad_group_probed(dev_tab, ntasks, total_tiles, nullptr, stream);
 }
 
 // ---------------------------------------------------------------------------- conv2 (3x3, s2)

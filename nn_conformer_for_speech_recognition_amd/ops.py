@@ -112,6 +112,11 @@ def linear_wgrad(dy, x, out=None, split_k=None, bias_out=None):
     return out
 
 
+class _ProbeDesc:
+    """Launch descriptor stand-in for PROBE hooks of non-GEMM launches (only .probe is read)."""
+    probe = None
+
+
 class WgradGroup:
     """Deferred weight gradients: add(dy, x) returns (dW, db) tensors that flush() fills with ONE grouped
     launch (cfm_wgrad_group) -- dW = dyᵀ·x, db = Σ_rows dy, bf16 operands sharing the token count M.
@@ -209,7 +214,15 @@ class WgradGroup:
                 # a captured graph's kernel node holds the device table's address: keep those entries
                 self._cache = {k: v for k, v in self._cache.items() if v[0]}
             self._cache[key] = hit
-        L.call("cfm_wgrad_group", L.ptr(hit[1]), len(self.tasks), hit[2], L.stream())
+        desc = _ProbeDesc()
+        n = len(self.tasks)
+
+        def launch():
+            L.call("cfm_wgrad_group_probed", L.ptr(hit[1]), n, hit[2], desc.probe, L.stream())
+        if PROBE is not None:
+            PROBE("wgroup", (n, hit[2]), desc, launch)
+        else:
+            launch()
         self.tasks = []
 
 
