@@ -106,6 +106,70 @@ class EncoderCTC(torch.nn.Module):
                              self.T2, blank=0, reduction="mean", zero_infinity=True, compute_dtype=self.cd)
 
 
+def run_nst(args, model, x, lens_i32, dev, cfg, rank, world):
+    """BASELINE.json configs[3]: the NST pseudo-label pass (runner.py:253-281) -- eval-mode front-end +
+    Conformer-L encoder (BatchNorm running stats, no dropout) + CTC head logits + device greedy decode
+    with <pad>/<blank> stripped on the device (cfm_ctc_greedy_decode), one HIP graph per batch.  Weak
+    scaling: each rank labels its own shard of B utterances; the label lists would be all-gathered once
+    per pass (Runner.generate_labels), outside the per-batch loop timed here."""
+    from nn_conformer_for_speech_recognition_amd.ctc import greedy_decode
+    name, L, d, H, ffn, K, B, secs, pos_enc = cfg
+    T_in = x.shape[-1]
+    model.eval()
+
+    def label_pass():
+        with torch.no_grad():
+            h2 = model.conv_sub_sampling.forward_frames(x, model.cd)
+            h = linear(h2.view(B * model.T2, -1), model.standard_linear.weight, model.standard_linear.bias,
+                       cd=model.cd)
+            y = model.conformers.forward_tokens(h, lens_i32, B, model.T2, seed=1)
+            logits = linear(y, model.ctc_fc.weight, model.ctc_fc.bias, cd=model.cd).view(B, model.T2, -1)
+            return greedy_decode(logits, lens_i32, blank=0, pad=-1, collapse=False)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(max(args.warmup, 1)):
+            label_pass()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = label_pass()
+    graph.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = tt.item()
+    fwd_pf, _ = algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, model.T2, model.F2, rel=pos_enc == "rel", B=B)
+    ms = 1000.0 * elapsed / args.steps
+    value = B * T_in * world * args.steps / elapsed
+    res = {"metric": "mel-frames/sec/GPU Conformer-L NST pseudo-label pass (eval fwd + greedy CTC decode)",
+           "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "bf16", "data": "synthetic (uniform min-max-normalised 80-bin mels, random init)",
+           "config": {"workload": f"BASELINE configs[3]: {name} NST label pass, {B} x {secs} s utterances per GPU",
+                      "model": name, "layers": L, "d_model": d, "pos_enc": pos_enc, "global_batch": B * world,
+                      "seq_len": T_in, "enc_frames": model.T2, "parallelism": f"dp{world} (sharded utterances)",
+                      "launch": "hip-graph (fwd + decode)"},
+           "per_gpu_value": round(value / world, 1),
+           "step_algorithmic_tflops": round(fwd_pf * B * T_in / (ms * 1e-3) / 1e12, 1),
+           "labels_nonempty": int((out[2] > 0).sum().item())}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 class KernelProbe:
     """Timing of one kernel family, installed as ops.PROBE.  Each matching launch gets a probe slot
     (cfm_gemm_desc.probe): the kernel itself records its first workgroup's start and its last
@@ -232,6 +296,7 @@ def main():
     ap.add_argument("--specaug", action="store_true",
                     help="SpecAugment inside the step (host draws in the reference order, one warp+mask kernel)")
     ap.add_argument("--pos-enc", choices=("none", "rel"), default=None, help="override the config's pos encoding")
+    ap.add_argument("--nst", action="store_true", help="configs[3]: the NST pseudo-label pass (eval fwd + decode)")
     ap.add_argument("--probe-inline", action="store_true",
                     help="put the roofline probe kernels inside the timed graph (default: a separate probed graph)")
     args = ap.parse_args()
@@ -251,6 +316,12 @@ def main():
     torch.manual_seed(1234)                      # identical init on every rank (then broadcast)
     model = EncoderCTC(L, d, H, ffn, K, V, Fb, T_in, args.dropout, cd, pos_enc).to(dev).train()
     cdist.broadcast_parameters(model)
+    if args.nst:
+        gx = torch.Generator(device="cpu").manual_seed(1234 + rank)
+        xs = torch.rand(B, Fb, T_in, generator=gx)
+        xs = (xs - xs.amin((1, 2), keepdim=True)) / (xs.amax((1, 2), keepdim=True) - xs.amin((1, 2), keepdim=True))
+        return run_nst(args, model, xs.to(dev), torch.full((B,), model.T2, dtype=torch.int32, device=dev), dev, cfg,
+                       rank, world)
     params = [p for p in model.parameters() if p.requires_grad]
     reducer = cdist.GradAllReducer(params)
     opt = Adafactor(params, lr=2e-5, beta1=0.9, scale_parameter=False, relative_step=False)

@@ -159,12 +159,13 @@ def ctc_head_loss(y, weight, bias, targets, input_lengths, target_lengths, B, T,
                             reduction, bool(zero_infinity), compute_dtype)
 
 
-def greedy_decode(logits, lengths=None, blank=0, pad=-1, collapse=False, batch_first=True):
+def greedy_decode(logits, lengths=None, blank=0, pad=-1, collapse=False, batch_first=True, compact=True):
     """ASRNN.predict + Vocab.decode's id filter on the device.
-    Returns (ids (B, T) int64 = torch.argmax(logits, -1), tokens (B, T) int32 padded with -1, n (B,))."""
+    Returns (ids (B, T) int64 = torch.argmax(logits, -1), tokens (B, T) int32 padded with -1, n (B,));
+    compact=False: ids only (tokens, n are None)."""
     if not logits.is_cuda or logits.dtype != torch.float32:
         raise RuntimeError("greedy_decode runs on libcfm: fp32 CUDA logits required")
     x = logits if logits.stride(-1) == 1 else logits.contiguous()
     B = x.shape[0] if batch_first else x.shape[1]
     ln = None if lengths is None else _lengths(lengths, B, x.device)
-    return ops.ctc_greedy_decode(x, ln, blank, pad, collapse, batch_first)
+    return ops.ctc_greedy_decode(x, ln, blank, pad, collapse, batch_first, compact)

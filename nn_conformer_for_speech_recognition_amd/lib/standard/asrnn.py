@@ -22,6 +22,7 @@ import torch.nn as nn
 
 from ... import specaugment as _sa
 from ...conformer import Conformer
+from ...ctc import greedy_decode as _greedy_decode
 from ...frontend import linear as _linear, projection_block as _projection_block
 from ..convsubsampling import ConvSubSampling
 
@@ -72,14 +73,16 @@ class ASRNN(nn.Module):
 
     # ------------------------------------------------------------------ reference surface
     def predict(self, x):
-        """Greedy labels (asrnn.py:48-58)."""
-        return torch.argmax(x, -1)
+        """Greedy labels (asrnn.py:48-58): argmax over the classes, on the device
+        (cfm_ctc_greedy_decode: first maximum wins, exactly torch.argmax's rule)."""
+        ids, _, _ = _greedy_decode(x.float() if x.dtype != torch.float32 else x, compact=False)
+        return ids
 
-    def conformer_blocks(self, x):
-        """asrnn.py:60-71 (kept for API parity): apply the layers in turn."""
-        for layer in self.conformers.conformer_layers:
-            x = layer(x)
-        return x
+    def conformer_blocks(self, x, lengths=None):
+        """asrnn.py:60-71 (kept for API parity): x (B, T, d) through the Conformer layers in turn."""
+        if lengths is None:
+            lengths = torch.full((x.shape[0],), x.shape[1], dtype=torch.int32, device=x.device)
+        return self.conformers(x, lengths)[0]
 
     def projection_block(self, x, finetuning=False):
         fc = self.projection_fc_1 if finetuning else self.projection_fc

@@ -1,0 +1,138 @@
+"""Config 4 on the device: the NST pseudo-label pass (Runner.generate_labels, runner.py:253-281) and
+ASRNN.predict (asrnn.py:48-58) on cfm_ctc_greedy_decode, plus the Runner / FineTune drivers.
+
+Parity: Conformer-L dims (d 512, 8 heads, ffn 2048, K 31), eval mode (BatchNorm running stats, no
+dropout), fp32 parity mode, against the CPU oracle composition with the same weights.  Decoded ids
+are compared BIT-EXACT at every frame whose oracle top-2 log-prob margin exceeds 1e-3 (frames closer
+than that are legitimately tie-sensitive to 1e-4-level fp32 differences, and are counted); the label
+strings follow the reference's no-collapse <pad>/<blank> strip (myvocab.py:211-231)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from nn_conformer_for_speech_recognition_amd.lib.hparams import HParams
+from nn_conformer_for_speech_recognition_amd.lib.standard.asrnn import ASRNN
+from nn_conformer_for_speech_recognition_amd.lib.standard.myvocab import build_vocab
+from nn_conformer_for_speech_recognition_amd.lib.standard.runner import Runner
+from nn_conformer_for_speech_recognition_amd.lib.standard.speechcommands import MelDataset
+from oracle import conformer as oc
+from oracle import frontend as of
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+WORDS = "yes no up down left right on off stop go zero one two three four five six seven eight nine".split()
+
+
+def test_predict_is_torch_argmax_with_ties():
+    from types import SimpleNamespace
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(5, 37, 29, generator=g)
+    x[:, :, 7] = x.amax(-1)                       # exact ties: torch.argmax picks the first maximum
+    x[1, 3] = 0.0
+    x = x.to(DEV)
+    ids = ASRNN.predict(SimpleNamespace(), x)
+    assert torch.equal(ids, torch.argmax(x, -1))
+
+
+def _vocab():
+    return build_vocab([" ".join(WORDS)])
+
+
+def _hp(vocab, L, d, H, ffn, K, cd, B):
+    hp = HParams(None)
+    hp.batch_size = B
+    hp.standard_linear_nodes, hp.mhsa_num_heads, hp.conformer_ff1_linear1_nodes = d, H, ffn
+    hp.conformer_depthwise_conv_kernel, hp.n_conformers, hp.dropout = K, L, 0.1
+    hp.frontend_proj, hp.compute_dtype = "frame", cd
+    hp.projection_out_size, hp.standard_decoder_nodes = 256, 128
+    hp.set_blank_index(vocab.blank_idx)
+    hp.device = torch.device(DEV)
+    return hp
+
+
+def _dataset(hp, vocab, n_lab, n_unlab, T, seed, labelled_words=2):
+    rng = np.random.default_rng(seed)
+    mk = lambda n, lab: [(rng.random((80, int(T - rng.integers(0, T // 3))), dtype=np.float32),
+                          " ".join(rng.choice(WORDS, labelled_words)) if lab else None) for _ in range(n)]
+    return MelDataset(hp, vocab, {"train": mk(n_lab, True), "validation": mk(2, True), "pretrain": mk(n_unlab, False)})
+
+
+def test_generate_labels_conformer_L_eval_vs_oracle():
+    vocab = _vocab()
+    hp = _hp(vocab, 2, 512, 8, 2048, 31, "fp32", 4)
+    ds = _dataset(hp, vocab, 2, 6, 301, 5)
+    torch.manual_seed(3)
+    m = ASRNN(hp)
+    with torch.no_grad():                                  # non-trivial running statistics
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.normal_(0, 0.2)
+                mod.running_var.uniform_(0.5, 2.0)
+        m.final_fc.weight.mul_(8.0)                        # sharper posteriors: fewer near-tied frames
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    runner = Runner(m, hp)
+    labels = runner.generate_labels(ds)
+    assert len(labels) == 6
+    # oracle: same composition on the CPU (fp32), eval mode
+    conf = oc.ConformerRef(512, 8, 2048, 2, 31, 0.1).eval()
+    conf.load_state_dict({k[len("conformers."):]: v for k, v in sd.items() if k.startswith("conformers.")})
+    lstm = torch.nn.LSTM(256, 128, bidirectional=True)
+    lstm.load_state_dict({k[len("lstm."):]: v for k, v in sd.items() if k.startswith("lstm.")})
+    lstm.eval()
+    n_amb = n_cmp = 0
+    want_labels = []
+    with torch.no_grad():
+        for bi in range(2):
+            batch = ds.get_batch(bi, "pretrain")["input"]
+            x, tau = batch["mels"].cpu(), batch["tau"].cpu()
+            h = of.convsub_forward(x.unsqueeze(1), sd["conv_sub_sampling.conv_sub_1.weight"],
+                                   sd["conv_sub_sampling.conv_sub_1.bias"], sd["conv_sub_sampling.conv_sub_2.weight"],
+                                   sd["conv_sub_sampling.conv_sub_2.bias"])
+            h = of.frame_projection(h, sd["standard_linear.weight"], sd["standard_linear.bias"])
+            lens = of.frame_lengths(tau).clamp(min=1)
+            h, _ = conf(h, lens)
+            B, T2 = h.shape[:2]
+            h = F.silu(F.linear(h.flatten(0, 1), sd["projection_fc.weight"], sd["projection_fc.bias"]))
+            h = F.batch_norm(h, sd["projection_batch_norm.running_mean"], sd["projection_batch_norm.running_var"],
+                             sd["projection_batch_norm.weight"], sd["projection_batch_norm.bias"], training=False)
+            y = F.linear(lstm(h)[0], sd["final_fc.weight"], sd["final_fc.bias"]).view(B, T2, -1)
+            lp = F.log_softmax(y, -1)
+            want = lp.argmax(-1)
+            top2 = lp.topk(2, -1).values
+            sure = (top2[..., 0] - top2[..., 1]) > 1e-3
+            got_lp, _ = runner.model(batch["mels"], batch["tau"])
+            got = runner.model.predict(got_lp).cpu()
+            assert torch.equal(got[sure], want[sure])
+            n_amb += int((~sure).sum())
+            n_cmp += sure.numel()
+            # the device strip == the reference's decode rule on the device ids, bit-exact
+            drop = {vocab.pad_idx, vocab.blank_idx}
+            ref_rule = [" ".join(vocab.itos[i] for i in row if i not in drop) for row in got.tolist()]
+            rows = min(4, 6 - 4 * bi)
+            assert labels[4 * bi:4 * bi + rows] == ref_rule[:rows]
+            want_labels += [" ".join(vocab.itos[i] for i in row if i not in drop) for row in want.tolist()][:rows]
+    assert n_amb <= 0.01 * n_cmp, (n_amb, n_cmp)
+    if n_amb == 0:
+        assert labels == want_labels
+
+
+def test_runner_train_test_and_finetune_nst():
+    """Runner.train / test (CTC on libcfm, Adafactor on libcfm, SpecAugment kernel) and the NST loop of
+    FineTune: pseudo-labels are generated, mixed into S, and training continues on the mix."""
+    from nn_conformer_for_speech_recognition_amd.lib.finetuning.finetune import FineTune
+    vocab = _vocab()
+    hp = _hp(vocab, 1, 144, 4, 576, 15, "bf16", 4)
+    hp.ft_epochs, hp.ft_train_epochs, hp.nst = 1, 1, True
+    ds = _dataset(hp, vocab, 6, 5, 201, 9)
+    U = _dataset(hp, vocab, 1, 5, 201, 10)
+    torch.manual_seed(0)
+    m = ASRNN(hp)
+    r = Runner(m, hp)
+    r.train(ds, 1)
+    assert len(r.history["loss"]) == 1 and np.isfinite(r.history["loss"][0])
+    loss, metric = r.test(ds, "validation")
+    assert np.isfinite(loss) and 0.0 <= metric
+    runner = FineTune(hp).fine_tuning(m, ds, U)
+    assert "mix" in ds.data and len(ds.data["mix"]) >= len(ds.data["train"])
+    assert len(runner.history["loss"]) >= 2
