@@ -73,7 +73,7 @@ def test_generate_labels_conformer_L_eval_vs_oracle():
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     runner = Runner(m, hp)
     labels = runner.generate_labels(ds)
-    assert len(labels) == 6
+    assert len(labels) == 8          # whole padded batches, as runner.py:276-277 (mix_datasets trims to len(U))
     # oracle: same composition on the CPU (fp32), eval mode
     conf = oc.ConformerRef(512, 8, 2048, 2, 31, 0.1).eval()
     conf.load_state_dict({k[len("conformers."):]: v for k, v in sd.items() if k.startswith("conformers.")})
