@@ -297,9 +297,13 @@ def main():
                     help="SpecAugment inside the step (host draws in the reference order, one warp+mask kernel)")
     ap.add_argument("--pos-enc", choices=("none", "rel"), default=None, help="override the config's pos encoding")
     ap.add_argument("--nst", action="store_true", help="configs[3]: the NST pseudo-label pass (eval fwd + decode)")
+    ap.add_argument("--dp-overlap", action="store_true",
+                    help="N>1: eager backward with bucket all-reduces overlapped (default: graph + reduce after)")
     ap.add_argument("--probe-inline", action="store_true",
                     help="put the roofline probe kernels inside the timed graph (default: a separate probed graph)")
     args = ap.parse_args()
+    if args.dp_overlap:
+        args.eager = True
     if args.gemm_mode is not None:
         _lib.call("cfm_gemm_set_mode", args.gemm_mode)
 
@@ -323,7 +327,9 @@ def main():
         return run_nst(args, model, xs.to(dev), torch.full((B,), model.T2, dtype=torch.int32, device=dev), dev, cfg,
                        rank, world)
     params = [p for p in model.parameters() if p.requires_grad]
-    reducer = cdist.GradAllReducer(params)
+    # DP: the Conformer's grouped weight gradients are written straight into flat all-reduce buckets; with
+    # --dp-overlap (eager) each chunk's bucket is reduced while the lower layers' backward still runs
+    reducer = cdist.GradAllReducer(params, model=model, overlap=bool(args.dp_overlap))
     opt = Adafactor(params, lr=2e-5, beta1=0.9, scale_parameter=False, relative_step=False)
 
     # synthetic data: per-utterance min-max-normalised uniform mels, full lengths

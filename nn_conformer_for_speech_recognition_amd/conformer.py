@@ -96,7 +96,8 @@ _REL_PNAMES = ["self_attn.linear_pos.weight", "self_attn.pos_bias_u", "self_attn
 
 class _Cfg:
     __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
-                 "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t", "group_wgrad", "layer_index")
+                 "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t", "group_wgrad", "layer_index",
+                 "grad_dest", "flush_here", "on_flushed")
 
 
 # the 2-D (and pointwise-conv) weight matrices of _PNAMES: cast to the compute dtype once per step
@@ -122,6 +123,7 @@ class _Side:
         self.side = _SIDE_STREAMS[key]
         self.keep = []
         self.group = None      # ops.WgradGroup when this layer's weight gradients are deferred
+        self.dest = None       # {weight index: (dW view, db view)} in a data-parallel gradient bucket
 
     def run(self, fn, *inputs):
         self.side.wait_stream(self.main)
@@ -147,11 +149,14 @@ def _has_grad_hooks(p):
     return bool(getattr(p, "_backward_hooks", None)) or bool(getattr(p, "_post_accumulate_grad_hooks", None))
 
 
-def _wgrad_bias(side, dy, x):
+def _wgrad_bias(side, dy, x, widx=None):
     """(dW, db) = (dyᵀ·x, Σ_rows dy): queued for the grouped launch (side.group) when the layer defers its
-    weight gradients, else on the side stream (outputs allocated on the main stream)."""
+    weight gradients, else on the side stream (outputs allocated on the main stream).  widx: _PNAMES index
+    of the weight; with a data-parallel gradient bucket attached (side.dest, dist.GradAllReducer) the
+    grouped launch writes straight into the bucket (autograd adopts the returned views as .grad)."""
     if side.group is not None and ops.wgrad_group_ok(dy, x):
-        return side.group.add(dy, x)
+        dest = side.dest.get(widx) if (side.dest and widx is not None) else None
+        return side.group.add(dy, x, dest)
     dw = torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=torch.float32)
     db = torch.empty(dy.shape[1], device=dy.device, dtype=torch.float32)
     side.run(lambda: ops.linear_wgrad(dy, x, out=dw, bias_out=db), dy, x, dw, db)
@@ -206,9 +211,9 @@ def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads, side, g2=None, nxt=None):
     xn, mu, rs, pre, h, w1, w2 = sv
     cd = cfg.cd
     g2 = _g2(g, g2, "ffn", cfg, seed)
-    grads[o + 4], grads[o + 5] = _wgrad_bias(side, g2, h)
+    grads[o + 4], grads[o + 5] = _wgrad_bias(side, g2, h, o + 4)
     da = ops.linear_dgrad(g2, w2, pre=pre, act_grad=True, drop_p=cfg.p, seed=seed, wt=_wt(cfg, o + 4))
-    grads[o + 2], grads[o + 3] = _wgrad_bias(side, da, xn)
+    grads[o + 2], grads[o + 3] = _wgrad_bias(side, da, xn, o + 2)
     dxn = ops.linear_dgrad(da, w1, wt=_wt(cfg, o + 2))
     dx, grads[o], grads[o + 1], g2n = _ln_bwd(dxn, x, P, o, mu, rs, g, side, nxt)
     return dx, g2n
@@ -236,7 +241,7 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
     cd = cfg.cd
     B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
     g4 = _g2(g, g2, "mha", cfg, seed)
-    grads[10], grads[11] = _wgrad_bias(side, g4, o)
+    grads[10], grads[11] = _wgrad_bias(side, g4, o, 10)
     wt = _wt(cfg, 10)
     if wt is not None and not cfg.rel and d // H == 64 and cd == torch.bfloat16 and "rowdot" not in ops.DISABLED:
         # D = rowsum(dO * O) per head from the epilogue of the GEMM producing dO (no separate pass)
@@ -251,7 +256,7 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
         rgrads[0] = ops.linear_wgrad(_w(dpos, cd), _w(cfg.pe, cd))
         rgrads[1] = dpu.view(H, d // H)
         rgrads[2] = dpv.view(H, d // H)
-    grads[8], grads[9] = _wgrad_bias(side, dqkv, xn)
+    grads[8], grads[9] = _wgrad_bias(side, dqkv, xn, 8)
     dxn = ops.linear_dgrad(dqkv, win, wt=_wt(cfg, 8))
     dx, grads[6], grads[7], g2n = _ln_bwd(dxn, x, P, 6, mu, rs, g, side, nxt)
     return dx, g2n
@@ -277,14 +282,14 @@ def _conv_bwd(g, x, sv, P, cfg, seed, grads, side, g2=None, nxt=None):
     cd = cfg.cd
     B, T, d, K = cfg.B, cfg.T, cfg.d, cfg.K
     g3 = _g2(g, g2, "conv", cfg, seed)
-    dw, grads[21] = _wgrad_bias(side, g3, z)
+    dw, grads[21] = _wgrad_bias(side, g3, z, 20)
     grads[20] = dw.view(d, d, 1)
     dz = ops.linear_dgrad(g3, wp2, wt=_wt(cfg, 20))
     ws = ops.convmod_ws(B, T, d, K, x.device)
     dy, grads[18], grads[19] = ops.bn_silu_bwd(dz, yv, P[18], P[19], bmean, binv, cfg.training, ws)
     da, dwdw, grads[17] = ops.glu_dwconv_bwd(dy, a, wdw, B, T, d, K, ws, cd, side=side)
     grads[16] = dwdw.view(d, 1, K)
-    dw, grads[15] = _wgrad_bias(side, da, xn)
+    dw, grads[15] = _wgrad_bias(side, da, xn, 14)
     grads[14] = dw.view(2 * d, d, 1)
     dxn = ops.linear_dgrad(da, wp1, wt=_wt(cfg, 14))
     dx, grads[12], grads[13], g2n = _ln_bwd(dxn, x, P, 12, mu, rs, g, side, nxt)
@@ -344,6 +349,7 @@ class _ConformerLayerFn(torch.autograd.Function):
         if cfg.group_wgrad and all(p.grad is None and not _has_grad_hooks(p) for p in params):
             side.group = _WGRAD_GROUPS.setdefault(str(gout.device), ops.WgradGroup())
             side.group.arm_final_flush()
+            side.dest = cfg.grad_dest
         # each LayerNorm backward also emits the next module's dropout-scaled input gradient (g2)
         ffn2_in = _in_drop("ffn", cfg, s + 30)
         conv_in, mha_in, ffn1_in = _in_drop("conv", cfg, s + 10), _in_drop("mha", cfg, s + 20), _in_drop("ffn", cfg, s)
@@ -363,10 +369,14 @@ class _ConformerLayerFn(torch.autograd.Function):
             g, g2 = _mha_bwd(g, c0, sva, P, R, cfg, s + 20, lens, grads, rgrads, side, g2, ffn1_in)
         g, _ = _ffn_bwd(g, x0, sv1, P, 0, cfg, s, grads, side, g2, None)
         side.join()
-        if cfg.layer_index == 0:
+        if cfg.layer_index == 0 or cfg.flush_here:
+            # layer 0 runs backward last: everything deferred is flushed; data-parallel runs also flush at
+            # bucket boundaries so the bucket's all-reduce (on_flushed) overlaps the remaining backward
             grp = _WGRAD_GROUPS.get(str(gout.device))
             if grp is not None:
                 grp.flush()
+            if cfg.on_flushed is not None:
+                cfg.on_flushed(cfg.layer_index)
         ctx.sv = None
         return (g, None, None, *grads, *rgrads)
 
@@ -399,7 +409,7 @@ class ConformerLayer(nn.Module):
         return ps
 
     def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None, shadow=None, layer_index=0,
-                       group_wgrad=False):
+                       group_wgrad=False, grad_dest=None, flush_here=False, on_flushed=None):
         """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device; shadow: optional
         ({param index: compute-dtype copy}, {param index: its transposed K-major copy}) of this
         layer's weight matrices (see Conformer._shadows)."""
@@ -418,6 +428,7 @@ class ConformerLayer(nn.Module):
         cfg.pe = pe
         cfg.layer_index = layer_index
         cfg.group_wgrad = bool(group_wgrad) and "wgroup" not in ops.DISABLED
+        cfg.grad_dest, cfg.flush_here, cfg.on_flushed = grad_dest, flush_here, on_flushed
         if self.training and bn.track_running_stats:
             bn.num_batches_tracked.add_(1)
         return _ConformerLayerFn.apply(x, lens_i32, cfg, *self.params())
@@ -448,6 +459,11 @@ class Conformer(nn.Module):
         self._pe_cache = {}
         self._step = 0
         self._shadow = None
+        # data-parallel hooks (dist.GradAllReducer.attach): per-layer {weight index: (dW, db) bucket views},
+        # the layers whose backward flushes the grouped launch, and the callback run after each flush
+        self.grad_dest = None
+        self.flush_layers = frozenset()
+        self.on_flushed = None
 
     def _pe(self, T, device):
         key = (T, str(device))
@@ -485,7 +501,9 @@ class Conformer(nn.Module):
         group = self.compute_dtype == torch.bfloat16
         for i, layer in enumerate(self.conformer_layers):
             x = layer.forward_tokens(x, lens_i32, B, T, self.compute_dtype, seed + 100 * i, pe, shadows[i],
-                                     layer_index=i, group_wgrad=group)
+                                     layer_index=i, group_wgrad=group,
+                                     grad_dest=self.grad_dest[i] if self.grad_dest else None,
+                                     flush_here=i in self.flush_layers, on_flushed=self.on_flushed)
         return x
 
     def forward(self, input, lengths):

@@ -179,11 +179,18 @@ class WgradGroup:
                     self.flush()
         torch.autograd.Variable._execution_engine.queue_callback(_final)
 
-    def add(self, dy, x):
+    def add(self, dy, x, dest=None):
+        """dest: optional (dW (N, K), db (N,)) fp32 destinations (e.g. views of a data-parallel gradient
+        bucket); fresh views of them are returned, so autograd adopts them as .grad without a copy."""
         M, N = dy.shape
         K = x.shape[1]
-        dw = torch.empty(N, K, device=dy.device, dtype=torch.float32)
-        db = torch.empty(N, device=dy.device, dtype=torch.float32)
+        if dest is not None:
+            dw, db = dest
+            if tuple(dw.shape) != (N, K) or tuple(db.shape) != (N,) or not dw.is_contiguous():
+                raise L.CfmError("WgradGroup.add: destination shapes do not match the GEMM")
+        else:
+            dw = torch.empty(N, K, device=dy.device, dtype=torch.float32)
+            db = torch.empty(N, device=dy.device, dtype=torch.float32)
         self.tasks.append((dy, x, dw, db))
         self._stream = torch.cuda.current_stream(dy.device)
         return dw.view(N, K), db.view(N)
