@@ -237,6 +237,19 @@ int cfm_bn_silu_fwd(const float* y, const float* gamma, const float* beta, float
 int cfm_bn_silu_bwd(const void* dz, int dtype_dz, const float* y, const float* gamma,
                     const float* beta, const float* mean, const float* invstd, int training,
                     float* dy, float* dgamma, float* dbeta, long M, int C, float* ws, void* stream);
+/* SyncBatchNorm split of cfm_bn_silu_fwd / cfm_bn_silu_bwd (the host all-reduces `sums` / the dbeta|dgamma
+   sums between the halves; M_total = rows over all replicas).  Replaces torch.nn.SyncBatchNorm over the
+   ConvModule's BatchNorm1d (torchaudio conformer, asrnn.py:29) under data parallelism. */
+int cfm_bn_silu_fwd_sums(const float* ws, int B, int T, int C, float* sums, void* stream);
+int cfm_bn_silu_fwd_apply(const float* y, const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, float momentum, float eps, const float* sums, long M_total, float* mean,
+                          float* invstd, void* z, int dtz, long M, int C, void* stream);
+int cfm_bn_silu_bwd_sums(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
+                         const float* mean, const float* invstd, long M, int C, float* ws, float* dbeta, float* dgamma,
+                         void* stream);
+int cfm_bn_silu_bwd_apply(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
+                          const float* mean, const float* invstd, const float* dbeta_total, const float* dgamma_total,
+                          long M_total, float* dy, long M, int C, void* stream);
 /* Generic BatchNorm1d over (M, C) rows with optional SiLU after the normalisation (act = 1) —
  * the projection block's BatchNorm1d(256) (lib/standard/asrnn.py:32,88).  ws: cfm_bn_ws_bytes(C). */
 size_t cfm_bn_ws_bytes(int C);

@@ -87,6 +87,13 @@ _SIGS = {
                                 c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "cfm_bn_silu_bwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                 c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p]),
+    "cfm_bn_silu_fwd_sums": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "cfm_bn_silu_fwd_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p,
+                                      c_long, c_void_p, c_void_p, c_void_p, c_int, c_long, c_int, c_void_p]),
+    "cfm_bn_silu_bwd_sums": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
+                                     c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cfm_bn_silu_bwd_apply": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_long, c_void_p, c_long, c_int, c_void_p]),
     "cfm_adafactor_table_bytes": (c_size_t, [c_int]),
     "cfm_adafactor_fill_table": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
                                          c_int, c_int, c_int, c_long, c_long, c_long, c_long, c_long, c_long,

@@ -97,7 +97,7 @@ _REL_PNAMES = ["self_attn.linear_pos.weight", "self_attn.pos_bias_u", "self_attn
 class _Cfg:
     __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
                  "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t", "group_wgrad", "layer_index",
-                 "grad_dest", "flush_here", "on_flushed")
+                 "grad_dest", "flush_here", "on_flushed", "sync_bn")
 
 
 # the 2-D (and pointwise-conv) weight matrices of _PNAMES: cast to the compute dtype once per step
@@ -271,8 +271,12 @@ def _conv_fwd(x, P, cfg, seed):
     a = ops.linear(xn, wp1, P[15])
     ws = ops.convmod_ws(B, T, d, K, x.device)
     yv = ops.glu_dwconv_fwd(a, wdw, P[17], B, T, d, K, ws)
-    z, bmean, binv = ops.bn_silu_fwd(yv, P[18], P[19], cfg.bn_rm, cfg.bn_rv, cfg.bn_mom, _EPS, cfg.training, B, T,
-                                     d, ws, cd)
+    if cfg.sync_bn is not None and cfg.training:
+        z, bmean, binv = ops.bn_silu_fwd_sync(yv, P[18], P[19], cfg.bn_rm, cfg.bn_rv, cfg.bn_mom, _EPS, B, T, d, ws,
+                                              cd, cfg.sync_bn[0], cfg.sync_bn[1])
+    else:
+        z, bmean, binv = ops.bn_silu_fwd(yv, P[18], P[19], cfg.bn_rm, cfg.bn_rv, cfg.bn_mom, _EPS, cfg.training, B,
+                                         T, d, ws, cd)
     y = ops.linear(z, wp2, P[21], out_dtype=torch.float32, drop_p=cfg.p, seed=seed, residual=x)
     return y, (xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw)
 
@@ -286,7 +290,11 @@ def _conv_bwd(g, x, sv, P, cfg, seed, grads, side, g2=None, nxt=None):
     grads[20] = dw.view(d, d, 1)
     dz = ops.linear_dgrad(g3, wp2, wt=_wt(cfg, 20))
     ws = ops.convmod_ws(B, T, d, K, x.device)
-    dy, grads[18], grads[19] = ops.bn_silu_bwd(dz, yv, P[18], P[19], bmean, binv, cfg.training, ws)
+    if cfg.sync_bn is not None and cfg.training:
+        dy, grads[18], grads[19] = ops.bn_silu_bwd_sync(dz, yv, P[18], P[19], bmean, binv, ws, cfg.sync_bn[0],
+                                                        cfg.sync_bn[1])
+    else:
+        dy, grads[18], grads[19] = ops.bn_silu_bwd(dz, yv, P[18], P[19], bmean, binv, cfg.training, ws)
     da, dwdw, grads[17] = ops.glu_dwconv_bwd(dy, a, wdw, B, T, d, K, ws, cd, side=side)
     grads[16] = dwdw.view(d, 1, K)
     dw, grads[15] = _wgrad_bias(side, da, xn, 14)
@@ -409,7 +417,7 @@ class ConformerLayer(nn.Module):
         return ps
 
     def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None, shadow=None, layer_index=0,
-                       group_wgrad=False, grad_dest=None, flush_here=False, on_flushed=None):
+                       group_wgrad=False, grad_dest=None, flush_here=False, on_flushed=None, sync_bn=None):
         """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device; shadow: optional
         ({param index: compute-dtype copy}, {param index: its transposed K-major copy}) of this
         layer's weight matrices (see Conformer._shadows)."""
@@ -429,6 +437,7 @@ class ConformerLayer(nn.Module):
         cfg.layer_index = layer_index
         cfg.group_wgrad = bool(group_wgrad) and "wgroup" not in ops.DISABLED
         cfg.grad_dest, cfg.flush_here, cfg.on_flushed = grad_dest, flush_here, on_flushed
+        cfg.sync_bn = sync_bn
         if self.training and bn.track_running_stats:
             bn.num_batches_tracked.add_(1)
         return _ConformerLayerFn.apply(x, lens_i32, cfg, *self.params())
@@ -464,6 +473,7 @@ class Conformer(nn.Module):
         self.grad_dest = None
         self.flush_layers = frozenset()
         self.on_flushed = None
+        self.sync_bn = None     # (reduce_sums(t) in-place all-reduce, world) -> cross-replica BatchNorm
 
     def _pe(self, T, device):
         key = (T, str(device))
@@ -490,6 +500,19 @@ class Conformer(nn.Module):
         self._shadow[1].refresh()
         return self._shadow[2]
 
+    def set_sync_batchnorm(self, group=None):
+        """torch.nn.SyncBatchNorm semantics for every ConvModule BatchNorm (train mode): batch statistics and
+        the input-gradient sums over all replicas of `group` (default: the default process group), one
+        all-reduce of 2*d floats per BN per pass; each rank's weight/bias gradients stay local (the data-
+        parallel gradient all-reduce averages them).  group=False turns it off."""
+        import torch.distributed as dist
+        if group is False or not (dist.is_available() and dist.is_initialized()):
+            self.sync_bn = None
+            return self
+        world = dist.get_world_size(group)
+        self.sync_bn = (lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group), world)
+        return self
+
     def forward_tokens(self, x, lens_i32, B, T, seed=None):
         if seed is None:
             seed = (self._step * 1000003 + 12345) & 0x7FFFFFFF
@@ -503,7 +526,8 @@ class Conformer(nn.Module):
             x = layer.forward_tokens(x, lens_i32, B, T, self.compute_dtype, seed + 100 * i, pe, shadows[i],
                                      layer_index=i, group_wgrad=group,
                                      grad_dest=self.grad_dest[i] if self.grad_dest else None,
-                                     flush_here=i in self.flush_layers, on_flushed=self.on_flushed)
+                                     flush_here=i in self.flush_layers, on_flushed=self.on_flushed,
+                                     sync_bn=self.sync_bn)
         return x
 
     def forward(self, input, lengths):

@@ -233,6 +233,22 @@ __global__ void bn_bwd_apply_kernel(const void* __restrict__ dz, int dtdz, const
   }
 }
 
+// SyncBatchNorm input gradient: the sums are over M_total rows of all replicas (invM = 1 / M_total)
+__global__ void bn_bwd_apply_total_kernel(const void* __restrict__ dz, int dtdz, const float* __restrict__ y,
+                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                          const float* __restrict__ mean, const float* __restrict__ invstd,
+                                          const float* __restrict__ dgamma, const float* __restrict__ dbeta,
+                                          float* __restrict__ dy, long M, int C, float invM) {
+  const long n = M * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float is = invstd[c], g = gamma[c];
+    const float yh = (y[i] - mean[c]) * is;
+    const float du = ld_dyn(dz, dtdz, i) * silu_grad_f(yh * g + beta[c]);
+    dy[i] = g * is * (du - dbeta[c] * invM - yh * dgamma[c] * invM);
+  }
+}
+
 // backward of y = dwconv(GLU(a)).  grid (ceil(C/CT), ceil(T/TT), B)
 // part: [nparts][K+1][C] per-block partial dw (K taps) and db (tap K).
 template <int KT, typename TA>
@@ -555,4 +571,54 @@ CFM_EXPORT int cfm_glu_dwconv_bwd_wgrad(float* ws, int B, int T, int C, int K, f
   cfm::colreduce(ws, (int)np, (long)C * (K + 1), sums, 0, s);
   hipLaunchKernelGGL(dwconv_scatter_kernel, dim3(cdiv((long)C * (K + 1), 256)), dim3(256), 0, s, sums, C, K, dw, db);
   return cfm::check_launch("cfm_glu_dwconv_bwd_wgrad");
+}
+
+// ----------------------------------------------------------------------------- SyncBatchNorm split
+// Cross-replica BatchNorm (the ConvModule BN under data parallelism, SURVEY.md §8e caveat): the host
+// all-reduces the per-channel sums between the two halves of each pass.
+//   fwd: cfm_bn_silu_fwd_sums (sum, sumsq of this rank's rows, from cfm_glu_dwconv_fwd's partials)
+//        -> all-reduce -> cfm_bn_silu_fwd_apply (batch stats over M_total rows, running stats, z)
+//   bwd: cfm_bn_silu_bwd_sums (sum du, sum du*yhat: this rank's dbeta, dgamma)
+//        -> all-reduce a copy -> cfm_bn_silu_bwd_apply (dy with the global sums over M_total rows)
+CFM_EXPORT int cfm_bn_silu_fwd_sums(const float* ws, int B, int T, int C, float* sums, void* stream) {
+  CFM_REQUIRE(ws && sums && B > 0 && T > 0 && C > 0, CFM_ERR_ARG, "bad args");
+  const long np = conv_nparts(B, T);
+  cfm::colreduce_pair(ws, ws + np * C, (int)np, C, sums, sums + C, cfm::as_stream(stream));
+  return cfm::check_launch("cfm_bn_silu_fwd_sums");
+}
+
+CFM_EXPORT int cfm_bn_silu_fwd_apply(const float* y, const float* gamma, const float* beta, float* running_mean,
+                                     float* running_var, float momentum, float eps, const float* sums, long M_total,
+                                     float* mean, float* invstd, void* z, int dtz, long M, int C, void* stream) {
+  CFM_REQUIRE(y && gamma && beta && sums && mean && invstd && z && M_total > 0 && M > 0 && C > 0, CFM_ERR_ARG,
+              "bad args");
+  hipStream_t s = cfm::as_stream(stream);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, sums + C, M_total, C, mean,
+                     invstd, running_mean, running_var, momentum, eps);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z, dtz,
+                     M, C, 1);
+  return cfm::check_launch("cfm_bn_silu_fwd_apply");
+}
+
+CFM_EXPORT int cfm_bn_silu_bwd_sums(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
+                                    const float* mean, const float* invstd, long M, int C, float* ws, float* dbeta,
+                                    float* dgamma, void* stream) {
+  CFM_REQUIRE(dz && y && gamma && beta && mean && invstd && ws && dbeta && dgamma && M > 0 && C > 0, CFM_ERR_ARG,
+              "bad args");
+  hipStream_t s = cfm::as_stream(stream);
+  const long rows_per = (M + BN_PARTS - 1) / BN_PARTS;
+  hipLaunchKernelGGL(bn_bwd_rows_kernel, dim3(cdiv(C, 64), BN_PARTS), dim3(256), 0, s, dz, dtdz, y, gamma, beta, mean,
+                     invstd, M, C, rows_per > 0 ? rows_per : 1, ws, 1);
+  cfm::colreduce_pair(ws, ws + (long)BN_PARTS * C, BN_PARTS, C, dbeta, dgamma, s);
+  return cfm::check_launch("cfm_bn_silu_bwd_sums");
+}
+
+CFM_EXPORT int cfm_bn_silu_bwd_apply(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
+                                     const float* mean, const float* invstd, const float* dbeta_total,
+                                     const float* dgamma_total, long M_total, float* dy, long M, int C, void* stream) {
+  CFM_REQUIRE(dz && y && gamma && beta && mean && invstd && dbeta_total && dgamma_total && dy && M_total > 0,
+              CFM_ERR_ARG, "bad args");
+  hipLaunchKernelGGL(bn_bwd_apply_total_kernel, dim3(ew_grid(M * C)), dim3(256), 0, cfm::as_stream(stream), dz, dtdz,
+                     y, gamma, beta, mean, invstd, dgamma_total, dbeta_total, dy, M, C, 1.f / (float)M_total);
+  return cfm::check_launch("cfm_bn_silu_bwd_apply");
 }

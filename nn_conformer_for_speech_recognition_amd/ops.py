@@ -450,6 +450,37 @@ def bn_silu_fwd(y, gamma, beta, running_mean, running_var, momentum, eps, traini
     return z, mean, invstd
 
 
+def bn_silu_fwd_sync(y, gamma, beta, running_mean, running_var, momentum, eps, B, T, C, ws, out_dtype, reduce_sums,
+                     world):
+    """SyncBatchNorm forward (train mode): this rank's (sum, sumsq) from the dwconv partials in ws, summed
+    over the replicas by reduce_sums(tensor) (an in-place all-reduce), then stats over world*B*T rows."""
+    sums = torch.empty(2 * C, device=y.device, dtype=torch.float32)
+    L.call("cfm_bn_silu_fwd_sums", L.ptr(ws), B, T, C, L.ptr(sums), L.stream())
+    reduce_sums(sums)
+    mean = torch.empty(C, device=y.device, dtype=torch.float32)
+    invstd = torch.empty(C, device=y.device, dtype=torch.float32)
+    z = torch.empty(B * T, C, device=y.device, dtype=out_dtype)
+    L.call("cfm_bn_silu_fwd_apply", L.ptr(y), L.ptr(gamma), L.ptr(beta), L.ptr(running_mean), L.ptr(running_var),
+           float(momentum), float(eps), L.ptr(sums), int(world) * B * T, L.ptr(mean), L.ptr(invstd), L.ptr(z), L.dt(z),
+           B * T, C, L.stream())
+    return z, mean, invstd
+
+
+def bn_silu_bwd_sync(dz, y, gamma, beta, mean, invstd, ws, reduce_sums, world):
+    """SyncBatchNorm backward: (dgamma, dbeta) stay this rank's (the parameter gradients, averaged later
+    with the others); a summed copy over the replicas feeds the input gradient."""
+    M, C = y.shape
+    dbg = torch.empty(2, C, device=y.device, dtype=torch.float32)
+    L.call("cfm_bn_silu_bwd_sums", L.ptr(dz), L.dt(dz), L.ptr(y), L.ptr(gamma), L.ptr(beta), L.ptr(mean),
+           L.ptr(invstd), M, C, L.ptr(ws), L.ptr(dbg[0]), L.ptr(dbg[1]), L.stream())
+    tot = dbg.clone()
+    reduce_sums(tot)
+    dy = torch.empty(M, C, device=y.device, dtype=torch.float32)
+    L.call("cfm_bn_silu_bwd_apply", L.ptr(dz), L.dt(dz), L.ptr(y), L.ptr(gamma), L.ptr(beta), L.ptr(mean),
+           L.ptr(invstd), L.ptr(tot[0]), L.ptr(tot[1]), int(world) * M, L.ptr(dy), M, C, L.stream())
+    return dy, dbg[1], dbg[0]
+
+
 def bn_silu_bwd(dz, y, gamma, beta, mean, invstd, training, ws):
     M, C = y.shape
     dy = torch.empty(M, C, device=y.device, dtype=torch.float32)
