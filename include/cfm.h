@@ -25,6 +25,7 @@ extern "C" {
 
 #define CFM_F32 0
 #define CFM_BF16 1
+#define CFM_FP8 2   /* OCP e4m3fn (gfx950), GEMM operands only (cfm_gemm, cfm_quant_fp8) */
 
 #define CFM_OK 0
 #define CFM_ERR_ARG (-1)
@@ -158,8 +159,18 @@ typedef struct cfm_gemm_desc {
                               out-projection data-gradient GEMM that produces dO.  NULL: off. */
   float* rowdot_out;
   int rowdot_T;
+  /* dtype_ab == CFM_FP8: device scalars multiplied into alpha (the per-tensor dequantisation scales
+     written by cfm_quant_fp8); NULL: 1 */
+  const float* alpha_a_dev;
+  const float* alpha_b_dev;
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
+/* Per-tensor fp8 (e4m3fn) quantisation for the fp8 GEMM path (configs[4]; no reference counterpart -- the
+   reference computes in fp32): y = e4m3(x * 448/amax(|x|)), *inv_scale = amax/448 (device scalar for
+   cfm_gemm_desc.alpha_*_dev); amax_ws: one device word of scratch.  x fp32 or bf16, 16-B aligned. */
+int cfm_quant_fp8(const void* x, int dtype_x, long n, void* y, float* inv_scale, unsigned* amax_ws, void* stream);
+/* y = float(x) * inv_scale (inv_scale NULL: 1) -- the dequantised view, for tests. */
+int cfm_dequant_fp8(const void* x, long n, const float* inv_scale, float* y, void* stream);
 /* Grouped weight gradients: every dW_i (N_i x K_i, fp32) = dY_i^T X_i over the same M tokens (dY_i (M x N_i),
    X_i (M x K_i) bf16 row-major) and optionally db_i = sum_rows dY_i, in ONE launch of 256x128 tiles that each
    run the whole token reduction (no split-K).  The caller fills a HOST table (cfm_wgrad_group_fill, one

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CFM_LIB") or os.path.join(_HERE, "libcfm.so")   # CFM_LIB: A/B builds only
 CSRC = os.path.join(_HERE, "csrc")
 
-F32, BF16 = 0, 1
+F32, BF16, FP8 = 0, 1, 2
 ACT_NONE, ACT_SILU = 0, 1
 
 c_void_p, c_int, c_long, c_float, c_size_t = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_size_t
@@ -42,6 +42,7 @@ class GemmDesc(ctypes.Structure):
         ("probe", c_void_p),
         ("a_colsum", c_void_p),
         ("rowdot_with", c_void_p), ("rowdot_out", c_void_p), ("rowdot_T", c_int),
+        ("alpha_a_dev", c_void_p), ("alpha_b_dev", c_void_p),
     ]
 
 
@@ -61,6 +62,8 @@ _SIGS = {
                                c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "cfm_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "cfm_gemm_set_mode": (c_int, [c_int]),
+    "cfm_quant_fp8": (c_int, [c_void_p, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cfm_dequant_fp8": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     "cfm_wgrad_group_task_bytes": (c_size_t, []),
     "cfm_wgrad_group_tiles": (c_long, [c_int, c_int]),
     "cfm_wgrad_group_fill": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -214,6 +217,8 @@ def dt(t):
         return F32
     if t.dtype == torch.bfloat16:
         return BF16
+    if t.dtype in (torch.uint8, torch.float8_e4m3fn):
+        return FP8
     raise CfmError(f"unsupported dtype {t.dtype}")
 
 

@@ -1,0 +1,95 @@
+// fp8.hip — per-tensor e4m3 quantisation for the fp8 GEMM path (BASELINE.json configs[4]: the 60 s long-form
+// Conformer-L with fp8 MFMA).  Current scaling: amax over the tensor -> scale = 448 / amax (e4m3fn's largest
+// finite value) -> y = e4m3(x * scale), and the dequantisation factor 1/scale is written to a device scalar
+// that the GEMM epilogue multiplies in (cfm_gemm_desc.alpha_a_dev / alpha_b_dev).  Everything stays on the
+// device (no host sync), so quantisation sits inside a captured HIP graph.  The scale is the power of two
+// just below 448/amax (at most one bit of range unused; exact scaling and dequantisation).
+#include "cfm_common.h"
+
+namespace {
+
+// |x| max, one vector atomic per wave (non-negative floats order as their bit patterns)
+__global__ __launch_bounds__(256) void amax_kernel(const void* __restrict__ x, int dt, long n,
+                                                   unsigned* __restrict__ amax) {
+  float m = 0.f;
+  const long n8 = n / 8;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float v[8];
+    ld8_dyn(x, dt, i * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+  }
+  for (long i = n8 * 8 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    m = fmaxf(m, fabsf(ld_dyn(x, dt, i)));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));
+}
+
+// power-of-two scale 2^k, k the largest integer with amax * 2^k <= 448 (= 1.75 * 2^8): exact in both
+// directions (x * 2^k and the dequantisation 2^-k lose nothing), bit-reproducible against any host restatement
+__device__ __forceinline__ float fp8_scale(const unsigned* amax) {
+  const unsigned u = amax[0];
+  const float a = __uint_as_float(u);
+  if (!(a > 0.f) || !(a < INFINITY)) return 1.f;
+  int e;
+  const float m = 2.f * frexpf(a, &e);          // a = m * 2^(e-1), m in [1, 2)
+  const int k = (m <= 1.75f ? 8 : 7) - (e - 1);
+  return ldexpf(1.f, k < 126 ? (k > -126 ? k : -126) : 126);
+}
+
+__global__ __launch_bounds__(256) void quant_fp8_kernel(const void* __restrict__ x, int dt, long n,
+                                                        const unsigned* __restrict__ amax, uint8_t* __restrict__ y,
+                                                        float* __restrict__ inv_scale) {
+  const float sc = fp8_scale(amax);
+  if (blockIdx.x == 0 && threadIdx.x == 0) inv_scale[0] = 1.f / sc;
+  const long n8 = n / 8;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float v[8];
+    ld8_dyn(x, dt, i * 8, v);
+    int lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * sc, v[1] * sc, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * sc, v[3] * sc, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * sc, v[5] * sc, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * sc, v[7] * sc, hi, true);
+    *reinterpret_cast<uint2*>(y + i * 8) = make_uint2((unsigned)lo, (unsigned)hi);
+  }
+  for (long i = n8 * 8 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int w = __builtin_amdgcn_cvt_pk_fp8_f32(ld_dyn(x, dt, i) * sc, 0.f, 0, false);
+    y[i] = (uint8_t)(w & 0xFF);
+  }
+}
+
+// e4m3 -> f32 (for tests / dequantised views): byte i of x times inv_scale
+__global__ __launch_bounds__(256) void dequant_fp8_kernel(const uint8_t* __restrict__ x, long n,
+                                                          const float* __restrict__ inv_scale, float* __restrict__ y) {
+  const float s = inv_scale ? inv_scale[0] : 1.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    y[i] = __builtin_amdgcn_cvt_f32_fp8((int)x[i], 0) * s;
+}
+
+int grid_for(long n) {
+  long b = (n / 8 + 255) / 256;
+  return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+}
+
+}  // namespace
+
+CFM_EXPORT int cfm_quant_fp8(const void* x, int dtx, long n, void* y, float* inv_scale, unsigned* amax_ws,
+                             void* stream) {
+  CFM_REQUIRE(x && y && inv_scale && amax_ws && n > 0, CFM_ERR_ARG, "null pointer / empty tensor");
+  CFM_REQUIRE(dtx == CFM_F32 || dtx == CFM_BF16, CFM_ERR_DTYPE, "x must be fp32 or bf16");
+  CFM_REQUIRE((uintptr_t)x % 16 == 0 && (uintptr_t)y % 8 == 0, CFM_ERR_ALIGN, "16-B aligned x, 8-B aligned y");
+  hipStream_t s = cfm::as_stream(stream);
+  (void)hipMemsetAsync(amax_ws, 0, sizeof(unsigned), s);
+  hipLaunchKernelGGL(amax_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, dtx, n, amax_ws);
+  hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, dtx, n, amax_ws, (uint8_t*)y,
+                     inv_scale);
+  return cfm::check_launch("cfm_quant_fp8");
+}
+
+CFM_EXPORT int cfm_dequant_fp8(const void* x, long n, const float* inv_scale, float* y, void* stream) {
+  CFM_REQUIRE(x && y && n > 0, CFM_ERR_ARG, "null pointer / empty tensor");
+  hipLaunchKernelGGL(dequant_fp8_kernel, dim3(grid_for(8 * n)), dim3(256), 0, cfm::as_stream(stream),
+                     (const uint8_t*)x, n, inv_scale, y);
+  return cfm::check_launch("cfm_dequant_fp8");
+}

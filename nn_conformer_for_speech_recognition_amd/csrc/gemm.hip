@@ -43,6 +43,8 @@ struct GemmP {
   const bf16* rd_with;         // per-64-column-group row dots with C (cfm_gemm_desc.rowdot_*) or nullptr
   float* rd_out;
   int rd_T;
+  const float* alpha_a;        // fp8 operands: per-tensor dequantisation scales (device) or nullptr
+  const float* alpha_b;
 };
 
 __device__ __forceinline__ long out_row(const GemmP& p, int m) {
@@ -647,10 +649,16 @@ __device__ __forceinline__ void wait_stages(int younger) {
 struct WgTask;   // grouped weight-gradient task (below)
 __device__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn);
 
+// F8: A and B are fp8 e4m3 (OCP), K-major, viewed as bf16 PAIRS by everything up to the LDS image (K, ld and
+// the tile geometry in 2-byte units, so DMA, swizzle and ring are byte-identical to the bf16 kernel); each
+// 64-fp8 k-step (4 16-B chunks of a row) feeds one v_mfma_scale_f32_32x32x64_f8f6f4: lane (r, h) holds the
+// 32 bytes k = 32h .. 32h+31 (chunks 2h, 2h+1).  Unit block scales; the per-tensor dequantisation
+// (alpha_a * alpha_b) is applied in the epilogue.
 template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2, bool GA = false,
-          bool GROUP = false>
+          bool GROUP = false, bool F8 = false>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(OCC * NWV / 4)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
+  static_assert(!F8 || (AK && BKM && !GA && !GROUP && BKt % 32 == 0), "fp8: K-major plain operands");
   typedef PipeGeo<BMt, BKt, NST, NWV> G;
   constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BN / WN / 32;
   static_assert(WM * FM * 32 == BMt && WN * FN * 32 == BN, "wave tiling");
@@ -750,6 +758,38 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     if (kt + NST - 1 < nk) issue(kt + NST - 1);   // refills the stage every wave finished reading at kt-1
     const char* sa = lds + (kt % NST) * G::STAGE;
     const char* sb = sa + G::ABYTES;
+    if constexpr (F8) {
+      typedef KmSw<BKt> S;
+      typedef int i32x8 __attribute__((ext_vector_type(8)));
+      constexpr int KS8 = BKt / 32;    // 64-fp8 k-steps per stage
+      i32x8 a8[KS8][FM], b8[KS8][FN];
+      auto frag8 = [&](const char* img, int row0, int q) {
+        const int r = row0 + (lane & 31), c = 4 * q + 2 * (lane >> 5);
+        const uint4 lo = *reinterpret_cast<const uint4*>(img + r * S::RB + 16 * S::slot(r, c));
+        const uint4 hi = *reinterpret_cast<const uint4*>(img + r * S::RB + 16 * S::slot(r, c + 1));
+        i32x8 v;
+        v[0] = (int)lo.x; v[1] = (int)lo.y; v[2] = (int)lo.z; v[3] = (int)lo.w;
+        v[4] = (int)hi.x; v[5] = (int)hi.y; v[6] = (int)hi.z; v[7] = (int)hi.w;
+        return v;
+      };
+#pragma unroll
+      for (int q = 0; q < KS8; ++q) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b8[q][j] = frag8(sb, wn * FN * 32 + j * 32, q);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a8[q][i] = frag8(sa, wm * FM * 32 + i * 32, q);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < KS8; ++q)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8[q][i], b8[q][j], acc[i][j], 0, 0, 0,
+                                                                        127, 0, 127);
+      continue;
+    }
     // every fragment of the stage is read up front (the stage is complete after the barrier), so the
     // LDS latency of later k-steps hides under the MFMAs of earlier ones
     constexpr int KST = BKt / 16;
@@ -806,6 +846,10 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     return;
   }
   __syncthreads();   // every wave done with the ring (no DMA outstanding) -> reuse it for the epilogue
+  if constexpr (F8) {   // per-tensor dequantisation of the fp8 operands (device scalars)
+    if (p.alpha_a) p.alpha *= p.alpha_a[0];
+    if (p.alpha_b) p.alpha *= p.alpha_b[0];
+  }
   tile_epilogue_g<FM, FN, WM, WN, G::NTt>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane, tid);
   probe_end(p.probe);
 }
@@ -1106,6 +1150,29 @@ int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   return CFM_OK;
 }
 
+// fp8 e4m3 x e4m3 (K-major both) on the LDS-DMA pipeline with the block-scaled MFMA (2x the bf16 rate):
+// operands viewed as bf16 pairs (K/2 "elements" per row), so DMA / swizzle / epilogue are the bf16 kernel's
+int launch_fp8(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
+  p.K = d.K / 2;
+  p.split_k = 1;
+  p.k_per_split = p.K;
+  p.vec_c = vec_epilogue_ok(p);
+  p.alpha_a = d.alpha_a_dev;
+  p.alpha_b = d.alpha_b_dev;
+  const PipeOp oa{(const bf16*)d.A, d.lda / 2, 0, d.M, (unsigned)((long)d.M * d.lda)};
+  const PipeOp ob{(const bf16*)d.B, d.ldb / 2, 0, d.N, (unsigned)((long)d.N * d.ldb)};
+  if (p.N <= 512) {
+    const dim3 g(cdiv(p.N, BN), cdiv(p.M, 192), 1);
+    hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, true, true, 8, 4, false, false, true>), g, dim3(512), 0, s, p,
+                       oa, ob, GatherA{});
+  } else {
+    const dim3 g(cdiv(p.N, BN), cdiv(p.M, 256), 1);
+    hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, true, true, 8, 2, false, false, true>), g, dim3(512), 0, s, p,
+                       oa, ob, GatherA{});
+  }
+  return cfm::check_launch("cfm_gemm(fp8)");
+}
+
 }  // namespace
 
 CFM_EXPORT int cfm_gemm_set_mode(int mode) {
@@ -1116,7 +1183,7 @@ CFM_EXPORT int cfm_gemm_set_mode(int mode) {
 CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   CFM_REQUIRE(d != nullptr, CFM_ERR_ARG, "null descriptor");
   CFM_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0 && d->batch >= 1, CFM_ERR_SHAPE, "bad M/N/K/batch");
-  CFM_REQUIRE(d->dtype_ab == CFM_F32 || d->dtype_ab == CFM_BF16, CFM_ERR_DTYPE, "dtype_ab");
+  CFM_REQUIRE(d->dtype_ab == CFM_F32 || d->dtype_ab == CFM_BF16 || d->dtype_ab == CFM_FP8, CFM_ERR_DTYPE, "dtype_ab");
   CFM_REQUIRE(d->A && d->B && d->C, CFM_ERR_ARG, "null operand");
   CFM_REQUIRE(d->act == CFM_ACT_NONE || d->act == CFM_ACT_SILU, CFM_ERR_ARG, "act");
   CFM_REQUIRE(!d->act_grad || d->pre, CFM_ERR_ARG, "act_grad needs pre");
@@ -1137,6 +1204,14 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   p.out_scale = d->out_scale; p.res = d->residual; p.ldr = d->ldr; p.dtr = d->dtype_r;
   p.split_k = split;
   p.probe = d->probe;
+  if (d->dtype_ab == CFM_FP8) {
+    CFM_REQUIRE(d->a_kmajor && d->b_kmajor && d->K % 128 == 0 && d->lda % 16 == 0 && d->ldb % 16 == 0 &&
+                    (uintptr_t)d->A % 16 == 0 && (uintptr_t)d->B % 16 == 0 && split == 1 && d->batch == 1 &&
+                    !d->rowdot_out && !d->a_colsum && (long)d->M * d->lda < (1L << 31) &&
+                    (long)d->N * d->ldb < (1L << 31),
+                CFM_ERR_UNSUPPORTED, "fp8: K-major A and B, K % 128 == 0, 16-B aligned rows, no split-K / batch");
+    return launch_fp8(*d, p, cfm::as_stream(stream));
+  }
   const bool bf = d->dtype_ab == CFM_BF16;
   p.k_per_split = split_k_for(p, bf ? BK16 : BK32);
   const int vlen = bf ? 8 : 4;

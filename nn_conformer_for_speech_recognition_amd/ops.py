@@ -21,8 +21,9 @@ def _gemm_desc(**kw):
 def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, alpha=1.0,
          bias=None, act=ACT_NONE, act_grad=False, pre=None, drop_p=0.0, seed=0, offset=0, out_scale=1.0,
          residual=None, ldr=None, split_k=1, batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None,
-         a_colsum=None, rowdot=None):
-    """C = epilogue(alpha * A·Bᵀ) — see cfm_gemm_desc in include/cfm.h."""
+         a_colsum=None, rowdot=None, alpha_a=None, alpha_b=None):
+    """C = epilogue(alpha * A·Bᵀ) — see cfm_gemm_desc in include/cfm.h.  fp8 (e4m3fn) A and B: alpha_a /
+    alpha_b are their device dequantisation scalars (quant_fp8)."""
     if A.dtype != B.dtype:
         raise L.CfmError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
     d = _gemm_desc(
@@ -37,7 +38,7 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         ldr=ldr if ldr is not None else N, dtype_r=L.dt(residual) if residual is not None else F32,
         split_k=int(split_k), workspace=L.ptr(workspace), a_colsum=L.ptr(a_colsum),
         rowdot_with=L.ptr(rowdot[0]) if rowdot else None, rowdot_out=L.ptr(rowdot[1]) if rowdot else None,
-        rowdot_T=int(rowdot[2]) if rowdot else 0)
+        rowdot_T=int(rowdot[2]) if rowdot else 0, alpha_a_dev=L.ptr(alpha_a), alpha_b_dev=L.ptr(alpha_b))
     if PROBE is not None:
         PROBE("gemm", (M, N, K), d, lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
     else:
@@ -49,14 +50,28 @@ PROBE = None   # optional timing hook (bench.py KernelProbe): PROBE(kind, shape,
 
 
 def linear(x, w, bias=None, out_dtype=None, act=ACT_NONE, pre=None, drop_p=0.0, seed=0, offset=0,
-           out_scale=1.0, residual=None, out=None):
-    """y = x·wᵀ (+bias, epilogue) for x (M, K), w (N, K)."""
+           out_scale=1.0, residual=None, out=None, x_scale=None, w_scale=None):
+    """y = x·wᵀ (+bias, epilogue) for x (M, K), w (N, K).  fp8 operands (quant_fp8 outputs) pass their
+    dequantisation scalars as x_scale / w_scale; the output then defaults to bf16."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
-        out = torch.empty(M, N, device=x.device, dtype=out_dtype or x.dtype)
+        od = out_dtype or (torch.bfloat16 if x.dtype == torch.float8_e4m3fn else x.dtype)
+        out = torch.empty(M, N, device=x.device, dtype=od)
     return gemm(x, w, out, M, N, K, bias=bias, act=act, pre=pre, drop_p=drop_p, seed=seed, offset=offset,
-                out_scale=out_scale, residual=residual)
+                out_scale=out_scale, residual=residual, alpha_a=x_scale, alpha_b=w_scale)
+
+
+def quant_fp8(x, out=None, inv_scale=None):
+    """Per-tensor e4m3fn quantisation on the device: (y float8_e4m3fn of x's shape, inv_scale (1,) fp32)
+    with y = e4m3(x * 448 / amax|x|) and inv_scale = amax / 448 (cfm_quant_fp8)."""
+    if not x.is_contiguous():
+        raise L.CfmError("quant_fp8: contiguous input required")
+    y = out if out is not None else torch.empty(x.shape, device=x.device, dtype=torch.float8_e4m3fn)
+    sc = inv_scale if inv_scale is not None else torch.empty(1, device=x.device, dtype=torch.float32)
+    ws = torch.empty(1, device=x.device, dtype=torch.int32)
+    L.call("cfm_quant_fp8", L.ptr(x), L.dt(x), x.numel(), L.ptr(y), L.ptr(sc), L.ptr(ws), L.stream())
+    return y, sc
 
 
 def linear_dgrad(dy, w, out_dtype=None, pre=None, act_grad=False, drop_p=0.0, seed=0, offset=0, out=None,

@@ -1,0 +1,75 @@
+"""fp8 (e4m3fn, OCP) path of BASELINE.json configs[4] -- no reference counterpart (the reference is fp32):
+per-tensor quantisation (cfm_quant_fp8, power-of-two scales) and the block-scaled-MFMA GEMM (v_mfma_scale_f32_32x32x64_f8f6f4,
+unit block scales, per-tensor dequantisation in the epilogue).
+
+Tolerances: the GEMM against an fp64 product of the SAME quantised operands -- relative L2 5e-5 with fp32
+output (exact fp8 products, fp32 accumulation) and 8e-3 with bf16 output; the quantisation itself
+bit-exact against torch's float8_e4m3fn conversion of x * 2^k (the largest k with amax * 2^k <= 448); the whole fp8 path against the fp32
+product of the unquantised operands: relative L2 <= 6e-2 (e4m3's 3 mantissa bits)."""
+import pytest
+import torch
+
+from nn_conformer_for_speech_recognition_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_quant_fp8_bit_exact(dt):
+    g = torch.Generator().manual_seed(1)
+    x = (torch.randn(1000, 264, generator=g) * 3).to(dt)
+    x[3, 7] = -17.25
+    y, sc = ops.quant_fp8(x.to(DEV))
+    amax = x.float().abs().max().item()
+    k = 0                                           # largest k with amax * 2^k <= 448
+    while amax * 2.0 ** (k + 1) <= 448.0:
+        k += 1
+    while amax * 2.0 ** k > 448.0:
+        k -= 1
+    assert sc.item() == 2.0 ** -k
+    ref = (x.float() * 2.0 ** k).to(torch.float8_e4m3fn)
+    assert torch.equal(y.cpu().view(torch.uint8), ref.view(torch.uint8))
+
+
+@pytest.mark.parametrize("M,N,K", [(11936, 2048, 512), (11936, 512, 2048), (1000, 1536, 512), (77, 512, 128)])
+def test_fp8_gemm_vs_fp64_of_quantised(M, N, K):
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g)).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    xq, sx = ops.quant_fp8(x)
+    wq, sw = ops.quant_fp8(w)
+    ref = (xq.cpu().double() * sx.item()) @ (wq.cpu().double() * sw.item()).t() + b.cpu().double()
+    y32 = ops.linear(xq, wq, b, out_dtype=torch.float32, x_scale=sx, w_scale=sw)
+    assert _rel(y32, ref) < 5e-5
+    y16 = ops.linear(xq, wq, b, x_scale=sx, w_scale=sw)
+    assert y16.dtype == torch.bfloat16 and _rel(y16.float(), ref) < 8e-3
+    full = x.double().cpu() @ w.double().cpu().t() + b.cpu().double()
+    assert _rel(y32, full) < 6e-2
+
+
+def test_fp8_gemm_silu_dropout_epilogue():
+    """The FFN up-projection's epilogue (bias + SiLU + dropout + saved pre-activation) on fp8 operands equals
+    the bf16 kernel's epilogue applied to the same (dequantised) product."""
+    M, N, K = 2000, 1024, 256
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g)).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    xq, sx = ops.quant_fp8(x)
+    wq, sw = ops.quant_fp8(w)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y = ops.linear(xq, wq, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=5, x_scale=sx, w_scale=sw)
+    z = (xq.float() * sx) @ (wq.float() * sw).t() + b
+    assert _rel(pre.float(), z) < 8e-3
+    keep = (y.float() != 0)
+    frac = keep.float().mean().item()
+    assert 0.88 < frac < 0.92
+    want = torch.nn.functional.silu(pre.float()) / 0.9
+    assert _rel(y.float()[keep], want[keep]) < 1e-2
