@@ -74,7 +74,7 @@ def algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, F2, C1=512, C2=128, r
 class EncoderCTC(torch.nn.Module):
     """Front-end + Conformer encoder + CTC head (the hot path of SURVEY.md §8a, 'frame' mode)."""
 
-    def __init__(self, L, d, H, ffn, K, V, F_bins, T_in, dropout, cd, pos_enc="none"):
+    def __init__(self, L, d, H, ffn, K, V, F_bins, T_in, dropout, cd, pos_enc="none", fp8=False):
         super().__init__()
         hp = HParams(None)
         hp.set_input_dim(F_bins, T_in)
@@ -84,7 +84,7 @@ class EncoderCTC(torch.nn.Module):
         self.F1, self.T1 = (F_bins - 7) // 2 + 1, (T_in - 7) // 2 + 1
         self.F2, self.T2 = (self.F1 - 3) // 2 + 1, (self.T1 - 3) // 2 + 1
         self.standard_linear = torch.nn.Linear(self.F2 * hp.conv_sub_2_nodes, d)
-        self.conformers = Conformer(d, H, ffn, L, K, dropout, pos_enc=pos_enc, compute_dtype=cd)
+        self.conformers = Conformer(d, H, ffn, L, K, dropout, pos_enc=pos_enc, compute_dtype=cd, fp8=fp8)
         self.ctc_fc = torch.nn.Linear(d, V)
         self.dropout = dropout
 
@@ -297,6 +297,8 @@ def main():
                     help="SpecAugment inside the step (host draws in the reference order, one warp+mask kernel)")
     ap.add_argument("--pos-enc", choices=("none", "rel"), default=None, help="override the config's pos encoding")
     ap.add_argument("--nst", action="store_true", help="configs[3]: the NST pseudo-label pass (eval fwd + decode)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="configs[4]: forward FFN / QKV / out-projection GEMMs on fp8 e4m3 MFMA (backward bf16)")
     ap.add_argument("--dp-overlap", action="store_true",
                     help="N>1: eager backward with bucket all-reduces overlapped (default: graph + reduce after)")
     ap.add_argument("--probe-inline", action="store_true",
@@ -318,7 +320,7 @@ def main():
     cd = torch.bfloat16
 
     torch.manual_seed(1234)                      # identical init on every rank (then broadcast)
-    model = EncoderCTC(L, d, H, ffn, K, V, Fb, T_in, args.dropout, cd, pos_enc).to(dev).train()
+    model = EncoderCTC(L, d, H, ffn, K, V, Fb, T_in, args.dropout, cd, pos_enc, args.fp8).to(dev).train()
     cdist.broadcast_parameters(model)
     if args.nst:
         gx = torch.Generator(device="cpu").manual_seed(1234 + rank)
@@ -530,7 +532,8 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (uniform min-max-normalised 80-bin mels, random init)",
+        "vs_baseline": None, "dtype": "fp8-e4m3 fwd GEMMs + bf16" if args.fp8 else "bf16",
+        "data": "synthetic (uniform min-max-normalised 80-bin mels, random init)",
         "config": {"workload": f"{name} encoder fwd+bwd + CTC head, {B} x {secs} s utterances per GPU",
                    "model": name, "layers": L, "d_model": d, "heads": H, "ffn": ffn, "conv_kernel": K,
                    "pos_enc": pos_enc, "specaug": bool(args.specaug),

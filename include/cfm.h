@@ -166,8 +166,9 @@ typedef struct cfm_gemm_desc {
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 /* Per-tensor fp8 (e4m3fn) quantisation for the fp8 GEMM path (configs[4]; no reference counterpart -- the
-   reference computes in fp32): y = e4m3(x * 448/amax(|x|)), *inv_scale = amax/448 (device scalar for
-   cfm_gemm_desc.alpha_*_dev); amax_ws: one device word of scratch.  x fp32 or bf16, 16-B aligned. */
+   reference computes in fp32): y = e4m3(x * 2^k), k the largest with amax(|x|) * 2^k <= 448, *inv_scale = 2^-k (device scalar for
+   cfm_gemm_desc.alpha_*_dev); amax_ws: cfm_quant_fp8_ws_bytes() of scratch.  x fp32 or bf16, 16-B aligned. */
+size_t cfm_quant_fp8_ws_bytes(void);
 int cfm_quant_fp8(const void* x, int dtype_x, long n, void* y, float* inv_scale, unsigned* amax_ws, void* stream);
 /* y = float(x) * inv_scale (inv_scale NULL: 1) -- the dequantised view, for tests. */
 int cfm_dequant_fp8(const void* x, long n, const float* inv_scale, float* y, void* stream);

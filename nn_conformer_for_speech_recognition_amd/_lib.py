@@ -63,6 +63,7 @@ _SIGS = {
     "cfm_gemm": (c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "cfm_gemm_set_mode": (c_int, [c_int]),
     "cfm_quant_fp8": (c_int, [c_void_p, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cfm_quant_fp8_ws_bytes": (c_size_t, []),
     "cfm_dequant_fp8": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     "cfm_wgrad_group_task_bytes": (c_size_t, []),
     "cfm_wgrad_group_tiles": (c_long, [c_int, c_int]),

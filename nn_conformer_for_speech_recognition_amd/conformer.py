@@ -97,11 +97,13 @@ _REL_PNAMES = ["self_attn.linear_pos.weight", "self_attn.pos_bias_u", "self_attn
 class _Cfg:
     __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
                  "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t", "group_wgrad", "layer_index",
-                 "grad_dest", "flush_here", "on_flushed", "sync_bn")
+                 "grad_dest", "flush_here", "on_flushed", "sync_bn", "shadow8")
 
 
 # the 2-D (and pointwise-conv) weight matrices of _PNAMES: cast to the compute dtype once per step
 _WIDX = (2, 4, 8, 10, 14, 20, 24, 26)
+# weights of the forward GEMMs that run on fp8 in fp8 mode: FFN up/down (both FFNs), QKV, out-projection
+_FP8_W = (2, 4, 8, 10, 24, 26)
 
 
 _SIDE_STREAMS = {}
@@ -173,13 +175,30 @@ def _wt(cfg, i):
     return cfg.shadow_t.get(i) if cfg.shadow_t else None
 
 
+def _fp8_linear(x, cfg, i, **kw):
+    """Forward GEMM with fp8 (e4m3fn) operands when the layer runs the fp8 path (BASELINE.json configs[4]):
+    x quantised per tensor on the device, weight i from the per-step fp8 shadow; else None.  The backward
+    keeps the bf16 operands (x, the bf16 weight shadow)."""
+    if not cfg.shadow8 or i not in cfg.shadow8 or x.shape[1] % 128:
+        return None
+    wq, sw = cfg.shadow8[i]
+    xq, sx = ops.quant_fp8(x)
+    return ops.linear(xq, wq, x_scale=sx, w_scale=sw, **kw)
+
+
 def _ffn_fwd(x, P, o, cfg, seed):
     cd = cfg.cd
     xn, mu, rs = ops.layernorm_fwd(x, P[o], P[o + 1], _EPS, out_dtype=cd)
     w1, w2 = _w(P[o + 2], cd), _w(P[o + 4], cd)
     pre = torch.empty(x.shape[0], cfg.ffn, device=x.device, dtype=cd)
-    h = ops.linear(xn, w1, P[o + 3], act=ACT_SILU, pre=pre, drop_p=cfg.p, seed=seed)
-    y = ops.linear(h, w2, P[o + 5], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, out_scale=0.5, residual=x)
+    h = _fp8_linear(xn, cfg, o + 2, bias=P[o + 3], act=ACT_SILU, pre=pre, drop_p=cfg.p, seed=seed)
+    if h is None:
+        h = ops.linear(xn, w1, P[o + 3], act=ACT_SILU, pre=pre, drop_p=cfg.p, seed=seed)
+    y = _fp8_linear(h, cfg, o + 4, bias=P[o + 5], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1,
+                    out_scale=0.5, residual=x)
+    if y is None:
+        y = ops.linear(h, w2, P[o + 5], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, out_scale=0.5,
+                       residual=x)
     return y, (xn, mu, rs, pre, h, w1, w2)
 
 
@@ -224,7 +243,9 @@ def _mha_fwd(x, P, R, cfg, seed, lens):
     B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
     xn, mu, rs = ops.layernorm_fwd(x, P[6], P[7], _EPS, out_dtype=cd)
     win, wout = _w(P[8], cd), _w(P[10], cd)
-    qkv = ops.linear(xn, win, P[9])
+    qkv = _fp8_linear(xn, cfg, 8, bias=P[9])
+    if qkv is None:
+        qkv = ops.linear(xn, win, P[9])
     pos = pu = pv = None
     if cfg.rel:
         wpos = _w(R[0], cd)
@@ -232,7 +253,9 @@ def _mha_fwd(x, P, R, cfg, seed, lens):
         pu = R[1].reshape(-1).float().contiguous()
         pv = R[2].reshape(-1).float().contiguous()
     o, lse = ops.attn_fwd(qkv, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
-    y = ops.linear(o, wout, P[11], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, residual=x)
+    y = _fp8_linear(o, cfg, 10, bias=P[11], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, residual=x)
+    if y is None:
+        y = ops.linear(o, wout, P[11], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, residual=x)
     return y, (xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv)
 
 
@@ -315,8 +338,9 @@ class _ConformerLayerFn(torch.autograd.Function):
             for i, t in cfg.shadow[0].items():
                 P[i] = t
             cfg.shadow_t = cfg.shadow[1]
+            cfg.shadow8 = cfg.shadow[2] if len(cfg.shadow) > 2 else None
         else:
-            cfg.shadow_t = None
+            cfg.shadow_t = cfg.shadow8 = None
         s = cfg.seed
         x0 = x
         x1, sv1 = _ffn_fwd(x0, P, 0, cfg, s)
@@ -451,7 +475,8 @@ class Conformer(nn.Module):
     forward(input (B, T, D), lengths (B,)) -> (output (B, T, D), lengths)."""
 
     def __init__(self, input_dim, num_heads, ffn_dim, num_layers, depthwise_conv_kernel_size, dropout=0.0,
-                 use_group_norm=False, convolution_first=False, pos_enc="none", compute_dtype=torch.bfloat16):
+                 use_group_norm=False, convolution_first=False, pos_enc="none", compute_dtype=torch.bfloat16,
+                 fp8=False):
         super().__init__()
         if depthwise_conv_kernel_size % 2 != 1:
             raise ValueError("depthwise_conv_kernel_size must be odd to achieve 'SAME' padding.")
@@ -465,6 +490,10 @@ class Conformer(nn.Module):
         self.input_dim = input_dim
         self.pos_enc = pos_enc
         self.compute_dtype = compute_dtype
+        if fp8 and compute_dtype != torch.bfloat16:
+            raise ValueError("fp8=True needs compute_dtype=torch.bfloat16 (the backward runs in bf16)")
+        # fp8 (e4m3fn) forward GEMMs (FFN up/down, QKV, out-projection; K % 128 == 0): BASELINE configs[4]
+        self.fp8 = bool(fp8)
         self._pe_cache = {}
         self._step = 0
         self._shadow = None
@@ -498,7 +527,15 @@ class Conformer(nn.Module):
                    for j in range(len(self.conformer_layers))]
             self._shadow = (key, ops.CastTBatch(srcs2, dsts_t, dsts), per)   # one launch, one read
         self._shadow[1].refresh()
-        return self._shadow[2]
+        if not self.fp8:
+            return self._shadow[2]
+        # per-step fp8 copies (+ dequantisation scalars) of the forward GEMM weights, from the fp32 masters
+        out = []
+        for layer, (plain, trans) in zip(self.conformer_layers, self._shadow[2]):
+            ps = layer.params()
+            q8 = {i: ops.quant_fp8(ps[i].detach().view(ps[i].shape[0], -1)) for i in _FP8_W}
+            out.append((plain, trans, q8))
+        return out
 
     def set_sync_batchnorm(self, group=None):
         """torch.nn.SyncBatchNorm semantics for every ConvModule BatchNorm (train mode): batch statistics and

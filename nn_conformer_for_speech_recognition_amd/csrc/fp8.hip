@@ -1,6 +1,6 @@
 // fp8.hip — per-tensor e4m3 quantisation for the fp8 GEMM path (BASELINE.json configs[4]: the 60 s long-form
-// Conformer-L with fp8 MFMA).  Current scaling: amax over the tensor -> scale = 448 / amax (e4m3fn's largest
-// finite value) -> y = e4m3(x * scale), and the dequantisation factor 1/scale is written to a device scalar
+// Conformer-L with fp8 MFMA).  Current scaling: amax over the tensor (256 partial maxima, no atomics) ->
+// scale = the power of two just below 448 / amax (448: e4m3fn's largest finite value) -> y = e4m3(x * scale), and the dequantisation factor 1/scale is written to a device scalar
 // that the GEMM epilogue multiplies in (cfm_gemm_desc.alpha_a_dev / alpha_b_dev).  Everything stays on the
 // device (no host sync), so quantisation sits inside a captured HIP graph.  The scale is the power of two
 // just below 448/amax (at most one bit of range unused; exact scaling and dequantisation).
@@ -8,9 +8,12 @@
 
 namespace {
 
-// |x| max, one vector atomic per wave (non-negative floats order as their bit patterns)
+constexpr int AMAX_BLOCKS = 256;   // partial maxima: no atomics (one word would serialise every wave)
+
+// |x| max: block b writes its partial maximum to part[b] (grid AMAX_BLOCKS, grid-stride)
 __global__ __launch_bounds__(256) void amax_kernel(const void* __restrict__ x, int dt, long n,
-                                                   unsigned* __restrict__ amax) {
+                                                   float* __restrict__ part) {
+  __shared__ float red[4];
   float m = 0.f;
   const long n8 = n / 8;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
@@ -22,14 +25,25 @@ __global__ __launch_bounds__(256) void amax_kernel(const void* __restrict__ x, i
   for (long i = n8 * 8 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
     m = fmaxf(m, fabsf(ld_dyn(x, dt, i)));
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// every block of the cast reduces the AMAX_BLOCKS partials itself (1 KiB, L2-resident): no extra launch
+__device__ __forceinline__ float block_amax(const float* part) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < AMAX_BLOCKS; i += 256) m = fmaxf(m, part[i]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
 // power-of-two scale 2^k, k the largest integer with amax * 2^k <= 448 (= 1.75 * 2^8): exact in both
 // directions (x * 2^k and the dequantisation 2^-k lose nothing), bit-reproducible against any host restatement
-__device__ __forceinline__ float fp8_scale(const unsigned* amax) {
-  const unsigned u = amax[0];
-  const float a = __uint_as_float(u);
+__device__ __forceinline__ float fp8_scale(float a) {
   if (!(a > 0.f) || !(a < INFINITY)) return 1.f;
   int e;
   const float m = 2.f * frexpf(a, &e);          // a = m * 2^(e-1), m in [1, 2)
@@ -38,9 +52,9 @@ __device__ __forceinline__ float fp8_scale(const unsigned* amax) {
 }
 
 __global__ __launch_bounds__(256) void quant_fp8_kernel(const void* __restrict__ x, int dt, long n,
-                                                        const unsigned* __restrict__ amax, uint8_t* __restrict__ y,
+                                                        const float* __restrict__ part, uint8_t* __restrict__ y,
                                                         float* __restrict__ inv_scale) {
-  const float sc = fp8_scale(amax);
+  const float sc = fp8_scale(block_amax(part));
   if (blockIdx.x == 0 && threadIdx.x == 0) inv_scale[0] = 1.f / sc;
   const long n8 = n / 8;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
@@ -74,16 +88,17 @@ int grid_for(long n) {
 
 }  // namespace
 
+CFM_EXPORT size_t cfm_quant_fp8_ws_bytes(void) { return AMAX_BLOCKS * sizeof(float); }
+
 CFM_EXPORT int cfm_quant_fp8(const void* x, int dtx, long n, void* y, float* inv_scale, unsigned* amax_ws,
                              void* stream) {
   CFM_REQUIRE(x && y && inv_scale && amax_ws && n > 0, CFM_ERR_ARG, "null pointer / empty tensor");
   CFM_REQUIRE(dtx == CFM_F32 || dtx == CFM_BF16, CFM_ERR_DTYPE, "x must be fp32 or bf16");
   CFM_REQUIRE((uintptr_t)x % 16 == 0 && (uintptr_t)y % 8 == 0, CFM_ERR_ALIGN, "16-B aligned x, 8-B aligned y");
   hipStream_t s = cfm::as_stream(stream);
-  (void)hipMemsetAsync(amax_ws, 0, sizeof(unsigned), s);
-  hipLaunchKernelGGL(amax_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, dtx, n, amax_ws);
-  hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, dtx, n, amax_ws, (uint8_t*)y,
-                     inv_scale);
+  hipLaunchKernelGGL(amax_kernel, dim3(AMAX_BLOCKS), dim3(256), 0, s, x, dtx, n, (float*)amax_ws);
+  hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, dtx, n, (const float*)amax_ws,
+                     (uint8_t*)y, inv_scale);
   return cfm::check_launch("cfm_quant_fp8");
 }
 

@@ -64,12 +64,12 @@ def linear(x, w, bias=None, out_dtype=None, act=ACT_NONE, pre=None, drop_p=0.0, 
 
 def quant_fp8(x, out=None, inv_scale=None):
     """Per-tensor e4m3fn quantisation on the device: (y float8_e4m3fn of x's shape, inv_scale (1,) fp32)
-    with y = e4m3(x * 448 / amax|x|) and inv_scale = amax / 448 (cfm_quant_fp8)."""
+    with y = e4m3(x * 2^k), k the largest with amax|x| * 2^k <= 448, and inv_scale = 2^-k (cfm_quant_fp8)."""
     if not x.is_contiguous():
         raise L.CfmError("quant_fp8: contiguous input required")
     y = out if out is not None else torch.empty(x.shape, device=x.device, dtype=torch.float8_e4m3fn)
     sc = inv_scale if inv_scale is not None else torch.empty(1, device=x.device, dtype=torch.float32)
-    ws = torch.empty(1, device=x.device, dtype=torch.int32)
+    ws = workspace(L.size_call("cfm_quant_fp8_ws_bytes"), x.device)
     L.call("cfm_quant_fp8", L.ptr(x), L.dt(x), x.numel(), L.ptr(y), L.ptr(sc), L.ptr(ws), L.stream())
     return y, sc
 
