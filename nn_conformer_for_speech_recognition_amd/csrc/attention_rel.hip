@@ -575,70 +575,86 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
 }
 
 // ------------------------------------------------------------------------------------ dpos
-// grid (ceil((2T-1)/64), H): 64 relative rows R0.. of head h; 4 waves = (d half, r half).
-// dpos[r][h*dk+d] = sum_b sum_i dsbuf[b,h,i, i+r-(T-1)] * (q_i + v)[d]   (keys j < len[b] only)
+// grid (ceil((2T-1)/64), H, B): 64 relative rows R0.. of head h for utterance b -> part[b] (the per-utterance
+// partials are summed by one deterministic column reduction); 4 waves = (d half, r half).
+// part[b][r][h*dk+d] = sum_i dsbuf[b,h,i, i+r-(T-1)] * (q_i + v)[d]   (keys j < len[b] only)
+// The next 64-query tile is loaded into registers while the current one runs through the MFMAs.
 __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp, const bf16* __restrict__ dsbuf,
-                                                                int ldS, float* __restrict__ dpos) {
-  __shared__ __attribute__((aligned(16))) bf16 sA[TILE * KS];    // (q+v)[ii][d]
-  __shared__ __attribute__((aligned(16))) bf16 sB[TILE * KS];    // dS_diag[ii][rr]
+                                                                int ldS, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) bf16 sA[2][TILE * KS];    // (q+v)[ii][d]
+  __shared__ __attribute__((aligned(16))) bf16 sB[2][TILE * KS];    // dS_diag[ii][rr]
   __shared__ float sO[TILE * 65];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int R0 = blockIdx.x * TILE, h = blockIdx.y;
+  const int R0 = blockIdx.x * TILE, h = blockIdx.y, b = blockIdx.z;
   const int dh = wv & 1, rh = wv >> 1;
   const int T = p.T, nrel = 2 * T - 1;
-  f32x16 acc = (f32x16){0};
-  for (int b = 0; b < p.B; ++b) {
-    const int len = min(p.len[b], T);
-    // i range with a key j = i + r - (T-1) in [0, len) for some r in the tile
-    const int ilo = max(0, T - 1 - (R0 + TILE - 1));
-    const int ihi = min(T - 1, len - 1 + T - 1 - R0);
-    if (len <= 0 || ihi < ilo) continue;
-    const bf16* dsb = dsbuf + ((long)b * p.H + h) * T * (long)ldS;
-    const bf16* qbase = p.qkv + (long)b * T * p.D3 + h * p.dk;
-    for (int I0 = ilo & ~(TILE - 1); I0 <= ihi; I0 += TILE) {
+  const int len = min(p.len[b], T);
+  // i range with a key j = i + r - (T-1) in [0, len) for some r of the tile
+  const int ilo = max(0, T - 1 - (R0 + TILE - 1));
+  const int ihi = min(T - 1, len - 1 + T - 1 - R0);
+  const bf16* dsb = dsbuf + ((long)b * p.H + h) * T * (long)ldS;
+  const bf16* qbase = p.qkv + (long)b * T * p.D3 + h * p.dk;
+  // this thread's two 8-column chunks: rows (tid + 256k) >> 3, columns c8 (the same for both)
+  const int c8 = (tid & 7) * 8;
+  float pv8[8];
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int v = tid + 256 * k;
-        const int row = v >> 3, c8 = (v & 7) * 8;
-        const int i = I0 + row;
-        // (q_i + v) chunk
-        const bf16x8 q = __builtin_bit_cast(bf16x8, ld8(qbase, p.D3, i, T, c8, p.dk, p.vec));
-        bf16x8 qv, dv8;
+  for (int e = 0; e < 8; ++e) pv8[e] = c8 + e < p.dk ? rp.pv[h * p.dk + c8 + e] : 0.f;
+  uint4 ra[2], rb[2];
+  auto load = [&](int I0) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int d = c8 + e;
-          qv[e] = (bf16)(i < T && d < p.dk ? (float)q[e] + rp.pv[h * p.dk + d] : 0.f);
-        }
-        // dS_diag[i][R0 + c8 + e] = ds[i][i + R0 + c8 + e - (T-1)]
-        const int j0 = i + R0 + c8 - (T - 1);
-        const unsigned short* srow = reinterpret_cast<const unsigned short*>(dsb + (long)min(i, T - 1) * ldS);
-        unsigned short t8[8];
+    for (int k = 0; k < 2; ++k) {
+      const int row = (tid + 256 * k) >> 3, i = I0 + row;
+      const bf16x8 q = __builtin_bit_cast(bf16x8, ld8(qbase, p.D3, i, T, c8, p.dk, p.vec));
+      bf16x8 qv;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int j = j0 + e;
-          t8[e] = (i < T && j >= 0 && j < len && R0 + c8 + e < nrel) ? srow[j] : (unsigned short)0;
-        }
-        dv8 = __builtin_bit_cast(bf16x8, make_uint4(t8[0] | (t8[1] << 16), t8[2] | (t8[3] << 16),
-                                                    t8[4] | (t8[5] << 16), t8[6] | (t8[7] << 16)));
-        *reinterpret_cast<bf16x8*>(sA + row * KS + c8) = qv;
-        *reinterpret_cast<bf16x8*>(sB + row * KS + c8) = dv8;
+      for (int e = 0; e < 8; ++e) qv[e] = (bf16)(i < T && c8 + e < p.dk ? (float)q[e] + pv8[e] : 0.f);
+      ra[k] = __builtin_bit_cast(uint4, qv);
+      const int j0 = i + R0 + c8 - (T - 1);
+      const unsigned short* srow = reinterpret_cast<const unsigned short*>(dsb + (long)min(i, T - 1) * ldS);
+      unsigned short t8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int j = j0 + e;
+        t8[e] = (i < T && j >= 0 && j < len && R0 + c8 + e < nrel) ? srow[j] : (unsigned short)0;
       }
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sA, 16 * s, 32 * dh, lane),
-                                                      trfrag_perm(sB, 16 * s, 32 * rh, lane), acc, 0, 0, 0);
-      __syncthreads();
+      rb[k] = make_uint4(t8[0] | (t8[1] << 16), t8[2] | (t8[3] << 16), t8[4] | (t8[5] << 16), t8[6] | (t8[7] << 16));
     }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = (tid + 256 * k) >> 3;
+      *reinterpret_cast<uint4*>(sA[buf] + row * KS + c8) = ra[k];
+      *reinterpret_cast<uint4*>(sB[buf] + row * KS + c8) = rb[k];
+    }
+  };
+  f32x16 acc = (f32x16){0};
+  const int it0 = ilo & ~(TILE - 1);
+  const int nit = (len > 0 && ihi >= ilo) ? (ihi - it0) / TILE + 1 : 0;
+  if (nit > 0) {
+    load(it0);
+    store(0);
+    __syncthreads();
   }
-  // acc: rows d (32 dh + acc_row), lanes rr (32 rh + lane&31) -> sO[rr][d] -> dpos rows
+  for (int it = 0; it < nit; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nit) load(it0 + (it + 1) * TILE);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sA[cur], 16 * s, 32 * dh, lane),
+                                                    trfrag_perm(sB[cur], 16 * s, 32 * rh, lane), acc, 0, 0, 0);
+    if (it + 1 < nit) store(cur ^ 1);
+    __syncthreads();
+  }
+  // acc: rows d (32 dh + acc_row), lanes rr (32 rh + lane&31) -> sO[rr][d] -> this utterance's partial rows
   const int hh = lane >> 5;
 #pragma unroll
   for (int r = 0; r < 16; ++r) sO[(32 * rh + (lane & 31)) * 65 + 32 * dh + acc_row(r, hh)] = acc[r];
   __syncthreads();
+  float* dst = part + (long)b * nrel * p.HD;
   for (int idx = tid; idx < TILE * 64; idx += 256) {
     const int rr = idx >> 6, d = idx & 63;
-    if (R0 + rr < nrel && d < p.dk) dpos[(long)(R0 + rr) * p.HD + h * p.dk + d] = sO[rr * 65 + d];
+    if (R0 + rr < nrel && d < p.dk) dst[(long)(R0 + rr) * p.HD + h * p.dk + d] = sO[rr * 65 + d];
   }
 }
 
@@ -647,6 +663,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp
 namespace cfm {
 
 // workspace of the rel-pos MFMA backward: [D (B*H*T f32)] [du/dv partials] [scale*dS (B*H*T*ldS bf16)]
+// [per-utterance dpos partials (B*(2T-1)*H*dk f32)]
 static inline int rel_ldS(int T) { return (T + 7) & ~7; }
 static inline size_t rel_part_floats(int B, int T, int H, int dk) { return (size_t)B * 4 * cdiv(T, 128) * 2 * H * dk; }
 
@@ -654,7 +671,8 @@ size_t attn_rel_ws_bytes(int B, int T, int H, int dk) {
   const size_t d = (size_t)B * H * T * sizeof(float);
   const size_t part = rel_part_floats(B, T, H, dk) * sizeof(float);
   const size_t ds = (size_t)B * H * T * rel_ldS(T) * sizeof(bf16);
-  return ((d + 255) & ~(size_t)255) + ((part + 255) & ~(size_t)255) + ds;
+  const size_t dpos_part = (size_t)B * (2 * T - 1) * H * dk * sizeof(float);
+  return ((d + 255) & ~(size_t)255) + ((part + 255) & ~(size_t)255) + ((ds + 255) & ~(size_t)255) + dpos_part;
 }
 
 static RelP make_relp(const void* pos, const float* pu, const float* pv, int dk) {
@@ -693,8 +711,11 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
                      dsbuf, ldS);
   hipLaunchKernelGGL(attn_rel_bwd_dq_kernel, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws, (bf16*)dqkv,
                      part);
-  hipLaunchKernelGGL(attn_rel_bwd_dpos_kernel, dim3(cdiv(2 * p.T - 1, TILE), p.H), dim3(256), 0, s, p, rp,
-                     (const bf16*)dsbuf, ldS, dpos);
+  const size_t ds_bytes = ((size_t)p.B * p.H * p.T * ldS * sizeof(bf16) + 255) & ~(size_t)255;
+  float* dpos_part = reinterpret_cast<float*>(reinterpret_cast<char*>(dsbuf) + ds_bytes);
+  hipLaunchKernelGGL(attn_rel_bwd_dpos_kernel, dim3(cdiv(2 * p.T - 1, TILE), p.H, p.B), dim3(256), 0, s, p, rp,
+                     (const bf16*)dsbuf, ldS, dpos_part);
+  colreduce(dpos_part, p.B, (long)(2 * p.T - 1) * p.HD, dpos, 0, s);
   const int nrows = p.B * 4 * cdiv(p.T, 128);
   colreduce(part, nrows, (long)p.HD, dpu, 0, s, 2L * p.HD);
   colreduce(part + p.HD, nrows, (long)p.HD, dpv, 0, s, 2L * p.HD);
