@@ -179,3 +179,33 @@ class ConformerRef(nn.Module):
         for layer in self.conformer_layers:
             x = layer(x, mask)
         return x, lengths
+
+
+def seeded_hf_compatible(d, H, ffn, L, K, pos_enc, seed):
+    """Deterministic Conformer weights for the golden fixtures (test infrastructure): torch.manual_seed(seed)
+    init, then non-trivial biases / LayerNorm / BatchNorm affine params, conv-module conv biases zeroed
+    (transformers' Wav2Vec2Conformer conv module has none).  The CPU generator makes this reproducible on
+    any machine, so big fixtures store the seed instead of the weights."""
+    torch.manual_seed(seed)
+    ref = ConformerRef(d, H, ffn, L, K, 0.0, pos_enc=pos_enc)
+    with torch.no_grad():
+        for layer in ref.conformer_layers:
+            for m in (layer.conv_module.sequential[0], layer.conv_module.sequential[2],
+                      layer.conv_module.sequential[5]):
+                m.bias.zero_()
+            for nm, p in layer.named_parameters():
+                if nm.endswith("bias") and "conv_module.sequential" not in nm:
+                    p.normal_(0, 0.1)
+                if "layer_norm" in nm and nm.endswith("weight"):
+                    p.uniform_(0.5, 1.5)
+            layer.conv_module.sequential[3].weight.uniform_(0.5, 1.5)
+            layer.conv_module.sequential[3].bias.normal_(0, 0.1)
+    return ref
+
+
+def grad_probes(name, g, k=16):
+    """k fixed random projections of a (large) gradient tensor -- the compact fixture form of a weight
+    gradient: probes[i] = <R_i, g> with R_i ~ N(0, 1) from a generator seeded by the parameter name."""
+    gen = torch.Generator().manual_seed(sum(ord(c) * (i + 1) for i, c in enumerate(name)) % (2 ** 31))
+    R = torch.randn(k, g.numel(), generator=gen, dtype=torch.float64)
+    return R @ g.reshape(-1).double()

@@ -189,7 +189,7 @@ def gen_conformer_layers():
         ("s_none", dict(d=144, H=4, ffn=576, K=31, B=3, T=57, lens=[57, 40, 9], pos=None)),
         ("s_rel", dict(d=144, H=4, ffn=576, K=31, B=3, T=57, lens=[57, 40, 9], pos="relative")),
         ("m_rel", dict(d=64, H=2, ffn=256, K=7, B=2, T=33, lens=[33, 20], pos="relative")),
-        ("l_none", dict(d=128, H=2, ffn=512, K=15, B=2, T=70, lens=[70, 64], pos=None)),
+        ("d128_none", dict(d=128, H=2, ffn=512, K=15, B=2, T=70, lens=[70, 64], pos=None)),
     ]
     arrays = {}
     for ci, (name, c) in enumerate(cases):
@@ -254,6 +254,80 @@ def gen_conformer_layers():
     print("conformer_layers.npz")
 
 
+# ------------------------------------------------- Conformer-L dims, two layers (seeded weights)
+HF_GRAD_NAMES = {   # transformers parameter -> torchaudio name (per layer)
+    "ffn1.intermediate_dense.weight": "ffn1.sequential.1.weight",
+    "ffn1.output_dense.weight": "ffn1.sequential.4.weight",
+    "ffn2.intermediate_dense.weight": "ffn2.sequential.1.weight",
+    "ffn2.output_dense.weight": "ffn2.sequential.4.weight",
+    "self_attn.linear_out.weight": "self_attn.out_proj.weight",
+    "conv_module.pointwise_conv1.weight": "conv_module.sequential.0.weight",
+    "conv_module.depthwise_conv.weight": "conv_module.sequential.2.weight",
+    "conv_module.pointwise_conv2.weight": "conv_module.sequential.5.weight",
+    "conv_module.batch_norm.weight": "conv_module.sequential.3.weight",
+    "final_layer_norm.weight": "final_layer_norm.weight",
+    "self_attn.linear_pos.weight": "self_attn.linear_pos.weight",
+    "self_attn.pos_bias_u": "self_attn.pos_bias_u",
+    "self_attn.pos_bias_v": "self_attn.pos_bias_v",
+}
+
+
+def gen_conformer_L():
+    """Two Conformer-L layers (d 512, 8 heads, ffn 2048, K 31), ragged lengths, pos none and rel, through
+    transformers' encoder layers.  Weights are regenerated from the seed (oracle.conformer.seeded_hf_compatible)
+    so the fixture stays small: inputs, outputs, input gradient, BN running stats, and 16 random
+    projections of each weight gradient (oracle.conformer.grad_probes)."""
+    from oracle.conformer import grad_probes, seeded_hf_compatible
+    from transformers import Wav2Vec2ConformerConfig
+    from transformers.models.wav2vec2_conformer.modeling_wav2vec2_conformer import (
+        Wav2Vec2ConformerRelPositionalEmbedding)
+    d, H, ffn, K, L, B, T, lens = 512, 8, 2048, 31, 2, 2, 96, [96, 61]
+    arrays = {}
+    for ci, (name, pos) in enumerate((("L512_none", None), ("L512_rel", "relative"))):
+        seed = 3000 + ci
+        ref = seeded_hf_compatible(d, H, ffn, L, K, "rel" if pos else "none", seed)
+        hfs = [_hf_layer_from_ref(layer, d, H, ffn, K, pos) for layer in ref.conformer_layers]
+        for hf in hfs:
+            hf.train()
+        g = torch.Generator().manual_seed(seed)
+        x = torch.randn(B, T, d, generator=g).requires_grad_()
+        ln = torch.tensor(lens)
+        valid = torch.arange(T)[None, :] < ln[:, None]
+        amask = (1.0 - valid[:, None, None, :].float()) * torch.finfo(torch.float32).min
+        rel = None
+        if pos:
+            rel = Wav2Vec2ConformerRelPositionalEmbedding(Wav2Vec2ConformerConfig(hidden_size=d,
+                                                                                  max_source_positions=512))(x)
+        y = x
+        for hf in hfs:
+            y, _ = hf(y, attention_mask=amask, relative_position_embeddings=rel)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy)
+        p = name + "_"
+        arrays[p + "cfg"] = np.array([d, H, ffn, K, B, T, L, seed], dtype=np.int64)
+        arrays[p + "lens"] = ln.numpy()
+        arrays[p + "x"] = x.detach().numpy()
+        arrays[p + "y"] = y.detach().numpy()
+        arrays[p + "gy"] = gy.numpy()
+        arrays[p + "gx"] = x.grad.numpy()
+        for li, hf in enumerate(hfs):
+            named = dict(hf.named_parameters())
+            for hn, tn in HF_GRAD_NAMES.items():
+                if hn in named:
+                    gr = named[hn].grad
+                    key = f"{p}g.conformer_layers.{li}.{tn}"
+                    arrays[key] = grad_probes(f"conformer_layers.{li}.{tn}", gr).numpy()
+            gin = torch.cat([hf.self_attn.linear_q.weight.grad, hf.self_attn.linear_k.weight.grad,
+                             hf.self_attn.linear_v.weight.grad])
+            arrays[f"{p}g.conformer_layers.{li}.self_attn.in_proj_weight"] = grad_probes(
+                f"conformer_layers.{li}.self_attn.in_proj_weight", gin).numpy()
+            arrays[f"{p}bn_running_mean.{li}"] = hf.conv_module.batch_norm.running_mean.numpy()
+            arrays[f"{p}bn_running_var.{li}"] = hf.conv_module.batch_norm.running_var.numpy()
+        print(name, "y", tuple(y.shape))
+    np.savez_compressed(os.path.join(HERE, "conformer_L.npz"), **arrays)
+    print("conformer_L.npz")
+
+
 # ------------------------------------------------------------ ASRNN (reference glue, shrunken)
 def gen_asrnn(tmp):
     from lib.standard.asrnn import ASRNN
@@ -297,6 +371,7 @@ def main():
         gen_specaug(tmp)
         gen_convsub(tmp)
         gen_conformer_layers()
+        gen_conformer_L()
         gen_asrnn(tmp)
 
 

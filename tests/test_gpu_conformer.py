@@ -29,7 +29,7 @@ TOL = {torch.float32: (1e-4, 1e-3), torch.bfloat16: (3e-2, 5e-2)}
 ROWTOL = {torch.float32: 1e-3, torch.bfloat16: 8e-2}
 
 
-@pytest.mark.parametrize("name", ["s_none", "s_rel", "m_rel", "l_none"])
+@pytest.mark.parametrize("name", ["s_none", "s_rel", "m_rel", "d128_none"])
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
 def test_layer_vs_transformers_fixture(golden_dir, name, cd):
     z = np.load(os.path.join(golden_dir, "conformer_layers.npz"))
@@ -184,3 +184,37 @@ def row_max_err(y, yr, lens):
         d = (y[b, :n] - yr[b, :n]).abs().amax(-1) / yr[b, :n].abs().amax(-1).clamp_min(1e-30)
         worst = max(worst, d.max().item())
     return worst
+
+
+@pytest.mark.parametrize("name", ["L512_none", "L512_rel"])
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_conformer_L_two_layers_vs_transformers_fixture(golden_dir, name, cd):
+    """Conformer-L dims, two layers, ragged lengths (96, 61), pos none and rel, vs transformers' encoder
+    layers (conformer_L.npz; weights regenerated from the fixture's seed): output (relative L2 and per-row
+    max-abs), input gradient, 16-probe projections of the weight gradients, BN running stats."""
+    z = np.load(os.path.join(golden_dir, "conformer_L.npz"))
+    p = name + "_"
+    d, H, ffn, K, B, T, L, seed = [int(v) for v in z[p + "cfg"]]
+    pos = "rel" if name.endswith("rel") else "none"
+    ref = oc.seeded_hf_compatible(d, H, ffn, L, K, pos, seed)
+    m = Conformer(d, H, ffn, L, K, 0.0, pos_enc=pos, compute_dtype=cd)
+    m.load_state_dict(ref.state_dict())
+    m = m.to(DEV).train()
+    x = torch.tensor(z[p + "x"], device=DEV, requires_grad=True)
+    lens = z[p + "lens"]
+    y, _ = m(x, torch.tensor(lens, device=DEV))
+    tol_y, tol_g = TOL[cd]
+    assert rel_err(y.detach(), z[p + "y"]) < tol_y
+    assert row_max_err(y.detach(), z[p + "y"], [int(v) for v in lens]) < ROWTOL[cd]
+    y.backward(torch.tensor(z[p + "gy"], device=DEV))
+    assert rel_err(x.grad, z[p + "gx"]) < tol_g
+    named = dict(m.named_parameters())
+    for k in z.files:
+        if k.startswith(p + "g."):
+            nm = k[len(p) + 2:]
+            got = oc.grad_probes(nm, named[nm].grad.detach().cpu())
+            assert rel_err(got, z[k]) < tol_g * (3 if "pos_bias" in nm else 1), nm
+    for li in range(L):
+        bn = m.conformer_layers[li].conv_module.sequential[3]
+        assert rel_err(bn.running_mean, z[f"{p}bn_running_mean.{li}"]) < tol_y
+        assert rel_err(bn.running_var, z[f"{p}bn_running_var.{li}"]) < tol_y

@@ -94,7 +94,7 @@ def test_convsub_matches_reference(golden_dir):
         assert of.stage_len(of.stage_len(T, 7, 2), 3, 2) == Tp
 
 
-LAYER_CASES = ["s_none", "s_rel", "m_rel", "l_none"]
+LAYER_CASES = ["s_none", "s_rel", "m_rel", "d128_none"]
 
 
 def load_layer_case(z, name):
@@ -164,3 +164,30 @@ def test_asrnn_encoder_glue_matches_reference(golden_dir):
                                        w["projection_batch_norm.bias"], training=True)
     np.testing.assert_allclose(h.detach().numpy(), z["enc"], rtol=1e-4, atol=1e-5)
     np.testing.assert_array_equal(out_lens.numpy(), z["out_lens"])
+
+
+@pytest.mark.parametrize("name", ["L512_none", "L512_rel"])
+def test_conformer_L_two_layers_match_transformers(golden_dir, name):
+    """Conformer-L dims (d 512, 8 heads, ffn 2048, K 31), two layers, ragged lengths: the oracle with the
+    seeded weights (oracle.conformer.seeded_hf_compatible) vs transformers' encoder layers (fixture):
+    outputs, input gradient, 16 random projections of every compared weight gradient, BN running stats."""
+    z = np.load(os.path.join(golden_dir, "conformer_L.npz"))
+    p = name + "_"
+    d, H, ffn, K, B, T, L, seed = [int(v) for v in z[p + "cfg"]]
+    pos = "rel" if name.endswith("rel") else "none"
+    ref = oc.seeded_hf_compatible(d, H, ffn, L, K, pos, seed).train()
+    x = torch.tensor(z[p + "x"], requires_grad=True)
+    y, _ = ref(x, torch.tensor(z[p + "lens"]))
+    np.testing.assert_allclose(y.detach().numpy(), z[p + "y"], rtol=1e-4, atol=5e-5)
+    y.backward(torch.tensor(z[p + "gy"]))
+    np.testing.assert_allclose(x.grad.numpy(), z[p + "gx"], rtol=1e-3, atol=2e-4)
+    named = dict(ref.named_parameters())
+    for k in z.files:
+        if k.startswith(p + "g."):
+            nm = k[len(p) + 2:]
+            got = oc.grad_probes(nm, named[nm].grad).numpy()
+            np.testing.assert_allclose(got, z[k], rtol=2e-3, atol=2e-3 * np.abs(z[k]).max(), err_msg=nm)
+    for li in range(L):
+        bn = ref.conformer_layers[li].conv_module.sequential[3]
+        np.testing.assert_allclose(bn.running_mean.numpy(), z[f"{p}bn_running_mean.{li}"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(bn.running_var.numpy(), z[f"{p}bn_running_var.{li}"], rtol=1e-5, atol=1e-6)
