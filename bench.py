@@ -292,6 +292,8 @@ def main():
     ap.add_argument("--no-optimizer", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--gemm-mode", type=int, default=None, help="cfm_gemm_set_mode value (A/B tuning)")
+    ap.add_argument("--attn-mode", type=int, default=int(os.environ.get("CFM_ATTN_MODE", "0")),
+                    help="cfm_attn_set_mode value (A/B tuning; env CFM_ATTN_MODE)")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no HIP graph)")
     ap.add_argument("--specaug", action="store_true",
                     help="SpecAugment inside the step (host draws in the reference order, one warp+mask kernel)")
@@ -308,6 +310,8 @@ def main():
         args.eager = True
     if args.gemm_mode is not None:
         _lib.call("cfm_gemm_set_mode", args.gemm_mode)
+    if args.attn_mode:
+        _lib.call("cfm_attn_set_mode", args.attn_mode)
 
     rank, world, local = cdist.init_from_env()
     torch.cuda.set_device(local)

@@ -183,6 +183,16 @@ long cfm_wgrad_group_tiles(int N, int K);
 int cfm_wgrad_group_fill(void* host_table, int i, const void* dy, const void* x, float* dw, float* db, int M,
                          int N, int K, long tile0);
 int cfm_wgrad_group(const void* dev_table, int ntasks, long total_tiles, void* stream);
+/* Grouped deterministic column reductions: the small deferred reductions of a backward pass (LayerNorm
+   dgamma|dbeta partial rows -- torch's LayerNorm backward weight/bias sums --, depthwise-conv weight/bias
+   partials) in ONE launch.  Host table of cfm_colreduce_group_task_bytes() per task (block0 = running sum of
+   cfm_colreduce_group_blocks(N)); mode 0: out[n] = sum_p part[p*ldp + n]; mode 1: the depthwise-conv
+   [K+1][C] sums scattered to dw (C x K) and db (C). */
+size_t cfm_colreduce_group_task_bytes(void);
+long cfm_colreduce_group_blocks(long N);
+int cfm_colreduce_group_fill(void* host_table, int i, const float* part, int nparts, long N, long ldp, float* out,
+                             float* out2, int mode, int C, int K, long block0);
+int cfm_colreduce_group(const void* dev_table, int ntasks, long total_blocks, void* stream);
 /* the same launch with a timing slot (as cfm_gemm_desc.probe: first-workgroup start / last-workgroup end) */
 int cfm_wgrad_group_probed(const void* dev_table, int ntasks, long total_tiles, unsigned long long* probe,
                            void* stream);
@@ -236,6 +246,8 @@ int cfm_silu_bwd(const void* dy, int dtype_dy, const void* pre, int dtype_pre, v
  * a: (B*T, 2C) token-major; w_dw: (C, K) fp32; y: (B*T, C) fp32.
  * cfm_glu_dwconv_fwd also produces per-channel partial (sum, sumsq) into ws for BN. */
 size_t cfm_convmod_ws_bytes(int B, int T, int C, int K);
+/* rows of cfm_glu_dwconv_bwd's [nparts][K+1][C] weight-gradient partials in ws (mode 1 of cfm_colreduce_group) */
+long cfm_convmod_nparts(int B, int T);
 int cfm_glu_dwconv_fwd(const void* a, int dtype_a, const float* w_dw, const float* b_dw, float* y,
                        int B, int T, int C, int K, float* ws, void* stream);
 /* z = silu(bn(y)).  training: batch stats finalised from the partial sums cfm_glu_dwconv_fwd left

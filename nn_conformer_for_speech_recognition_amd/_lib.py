@@ -71,6 +71,11 @@ _SIGS = {
                                      c_long]),
     "cfm_wgrad_group": (c_int, [c_void_p, c_int, c_long, c_void_p]),
     "cfm_wgrad_group_probed": (c_int, [c_void_p, c_int, c_long, c_void_p, c_void_p]),
+    "cfm_colreduce_group_task_bytes": (c_size_t, []),
+    "cfm_colreduce_group_blocks": (c_long, [c_long]),
+    "cfm_colreduce_group_fill": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_long, c_void_p, c_void_p, c_int,
+                                         c_int, c_int, c_long]),
+    "cfm_colreduce_group": (c_int, [c_void_p, c_int, c_long, c_void_p]),
     "cfm_attn_set_mode": (c_int, [c_int]),
     "cfm_colreduce": (c_int, [c_void_p, c_int, c_long, c_long, c_void_p, c_int, c_void_p]),
     "cfm_colsum": (c_int, [c_void_p, c_int, c_long, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p]),
@@ -85,6 +90,7 @@ _SIGS = {
     "cfm_scale_dropout": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_float, c_float, c_u64, c_u64,
                                   c_void_p]),
     "cfm_convmod_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "cfm_convmod_nparts": (c_long, [c_int, c_int]),
     "cfm_glu_dwconv_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                    c_void_p, c_void_p]),
     "cfm_bn_silu_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_int,

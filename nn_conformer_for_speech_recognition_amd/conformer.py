@@ -126,6 +126,7 @@ class _Side:
         self.keep = []
         self.group = None      # ops.WgradGroup when this layer's weight gradients are deferred
         self.dest = None       # {weight index: (dW view, db view)} in a data-parallel gradient bucket
+        self.rgroup = None     # ops.ReduceGroup: this layer's small column reductions, deferred likewise
 
     def run(self, fn, *inputs):
         self.side.wait_stream(self.main)
@@ -139,8 +140,10 @@ class _Side:
         self.keep = []
 
 
-# weight gradients of the encoder deferred to ONE grouped launch at the end of its backward (per device)
+# weight gradients of the encoder deferred to ONE grouped launch at the end of its backward (per device),
+# and the small column reductions (LayerNorm dgamma|dbeta, depthwise conv dw|db) to one more
 _WGRAD_GROUPS = {}
+_RED_GROUPS = {}
 
 
 def _has_grad_hooks(p):
@@ -382,6 +385,9 @@ class _ConformerLayerFn(torch.autograd.Function):
             side.group = _WGRAD_GROUPS.setdefault(str(gout.device), ops.WgradGroup())
             side.group.arm_final_flush()
             side.dest = cfg.grad_dest
+            if "rgroup" not in ops.DISABLED:     # (CFM_DISABLE=rgroup: per-layer side-stream reductions, A/B)
+                side.rgroup = _RED_GROUPS.setdefault(str(gout.device), ops.ReduceGroup())
+                side.rgroup.arm_final_flush()
         # each LayerNorm backward also emits the next module's dropout-scaled input gradient (g2)
         ffn2_in = _in_drop("ffn", cfg, s + 30)
         conv_in, mha_in, ffn1_in = _in_drop("conv", cfg, s + 10), _in_drop("mha", cfg, s + 20), _in_drop("ffn", cfg, s)
@@ -407,6 +413,9 @@ class _ConformerLayerFn(torch.autograd.Function):
             grp = _WGRAD_GROUPS.get(str(gout.device))
             if grp is not None:
                 grp.flush()
+            rgrp = _RED_GROUPS.get(str(gout.device))
+            if rgrp is not None:
+                rgrp.flush()
             if cfg.on_flushed is not None:
                 cfg.on_flushed(cfg.layer_index)
         ctx.sv = None

@@ -461,14 +461,20 @@ __global__ __launch_bounds__(64 * DKDV_WAVES) void attn_bwd_dkdv_head_kernel(Att
 }
 
 // dK, dV, one wave per 32-key block: grid (B*H), block 64 * ceil(T/32) (three waves per SIMD at
-// T = 373); the head's whole Q and dO (and lse, D) are staged once and every wave sweeps 32-query
-// steps over them with no further barriers.  Per step 16 MFMAs (S, dP, dV^T += dO^T P, dK^T +=
-// Q^T dS) on ~150 live registers: P / dS are formed in place in the S / dP accumulators.
+// T = 373, <= 168 registers); the head's whole Q and dO (and lse, D) are staged once and every wave
+// sweeps 32-query steps over them with no further barriers.  Per step 16 MFMAs (S, dP, dV^T += dO^T P,
+// dK^T += Q^T dS), P / dS formed in place in the S / dP accumulators, branch-free (masked keys enter the
+// exponential as -inf).  Attention dropout: the hash index of element (q, kj) is
+// (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2 (T2 = even T / 2; exact: didx < 2^33), so lanes kj and kj^1
+// share one 32-bit hash per query: the even lane hashes the query of accumulator register r, the odd lane
+// that of r + 1, and one DPP swap hands each lane its partner's -- one hash per two elements, 32-bit
+// index arithmetic with per-register offsets that are wave-uniform.
 __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel(AttnM p, const bf16* __restrict__ dout,
                                                                                  const float* __restrict__ lse,
                                                                                  const float* __restrict__ Dg,
                                                                                  bf16* __restrict__ dqkv) {
-  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const bool drop = p.drop_p > 0.f;
+  if (drop) p.seed = salted_seed(p.seed, p.salt);
   const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
   const float dkeep = drop_keep_scale(dthr);
   extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
@@ -496,7 +502,9 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
   const float c = p.scale * LOG2E;
   f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
   const int nqs = k0w < len ? nq : 0;      // key blocks past len: zero gradients
-  const uint64_t dbase = didx(p, b, h, 0, kj);
+  const int odd = lane & 1, sh = 16 * odd;
+  const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
+  const uint32_t hbase = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)(4 * hh + odd)) * T2 + (uint32_t)(kj >> 1);
   for (int qt = 0; qt < nqs; ++qt) {
     const int q0 = qt * 32;
     f32x16 sa = (f32x16){0}, ga = (f32x16){0};
@@ -504,28 +512,46 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
     for (int s4 = 0; s4 < 4; ++s4) {
       sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, q0, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
       ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sGall, q0, 16 * s4, lane), vf[s4], ga, 0, 0, 0);
+      if (s4 == 1) __builtin_amdgcn_sched_barrier(0);   // at most 4 operand fragments in flight (VGPR cap)
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the next phase's LDS reads from being hoisted (VGPR cap)
+    bf16x8 pf[2], sf[2];                   // P and dS as bf16 B-operand fragments (k-steps 0, 1)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int q = q0 + acc_row(r, hh);
-      const float pa = kvalid ? fast_exp2(sa[r] * c - sL[q]) : 0.f;   // lse = +inf for q >= T
-      float ma = 1.f;
-      if (p.drop_p > 0.f) ma = dropout_keyed(dthr, dkeep, dkey, dbase + (uint64_t)q * (p.T + (p.T & 1)));
-      sa[r] = pa * ma;                       // P (dropped)
-      ga[r] = pa * (ga[r] * ma - sD[q]);     // dS
+    for (int g = 0; g < 4; ++g) {          // registers 4g .. 4g+3 = queries q0 + 8g + 4hh + 0..3
+      const float4 Lg = *reinterpret_cast<const float4*>(sL + q0 + 8 * g + 4 * hh);
+      const float4 Dq = *reinterpret_cast<const float4*>(sD + q0 + 8 * g + 4 * hh);
+      const float Lr[4] = {Lg.x, Lg.y, Lg.z, Lg.w}, Dr[4] = {Dq.x, Dq.y, Dq.z, Dq.w};
+      float mk[4] = {1.f, 1.f, 1.f, 1.f};
+      if (drop) {
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          // (the wave-uniform offset through readfirstlane: otherwise the 8 per-register bases are hoisted
+          // out of the loop as VGPRs and spilled)
+          const uint32_t hm = cfm_mix32((hbase + __builtin_amdgcn_readfirstlane((q0 + 8 * g + e) * (int)T2)) ^ dkey);
+          const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+          const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
+          mk[e] = ((h0 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
+          mk[e + 1] = ((h1 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * g + e;
+        const float pa = fast_exp2(kvalid ? sa[r] * c - Lr[e] : -INFINITY);   // lse = +inf for q >= T
+        pf[r >> 3][r & 7] = (bf16)(pa * mk[e]);                       // P (dropped)
+        sf[r >> 3][r & 7] = (bf16)(pa * (ga[r] * mk[e] - Dr[e]));     // dS
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one group's lse / D in registers at a time (VGPR cap)
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pf = acc2frag(sa, s2);
-      const bf16x8 sf = acc2frag(ga, s2);
-      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 0, lane), pf, dv0, 0, 0, 0);
-      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 32, lane), pf, dv1, 0, 0, 0);
-      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 0, lane), sf, dk0, 0, 0, 0);
-      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 32, lane), sf, dk1, 0, 0, 0);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 0, lane), pf[s2], dv0, 0, 0, 0);
+      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 32, lane), pf[s2], dv1, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 0, lane), sf[s2], dk0, 0, 0, 0);
+      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 32, lane), sf[s2], dk1, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();     // every wave is done with Q / dO: the images become the epilogue staging
   float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
@@ -775,7 +801,7 @@ bool use_mfma(int dtype, const void* pos, int dk) {
 }
 
 // whole-head kernels: T <= HEAD_TMAX; cfm_attn_set_mode bit 0 forces the tiled kernels, bit 3 selects
-// the wave-per-key-block dK/dV kernel (A/B)
+// the four-wave dK/dV kernel instead of the wave-per-key-block one (A/B)
 bool use_head(int T) { return T <= HEAD_TMAX && (g_attn_mode & 1) == 0; }
 size_t head_lds_bytes(int T) {
   const size_t rows = (size_t)cdiv(T, TILE) * TILE;
@@ -843,7 +869,7 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
   if (pos)
     return cfm::attn_rel_bwd_launch(qkv, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H,
                                     dk, drop_p, seed, ws, s);
-  if (use_head(T) && (g_attn_mode & 8) != 0)
+  if (use_head(T) && (g_attn_mode & 8) == 0)
     hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), dkdv_wave_lds_bytes(T), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);
   else if (use_head(T))

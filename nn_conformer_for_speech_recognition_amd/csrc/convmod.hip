@@ -452,6 +452,9 @@ CFM_EXPORT size_t cfm_convmod_ws_bytes(int B, int T, int C, int K) {
   return (size_t)m * sizeof(float);
 }
 
+// partial-sum rows of the depthwise conv's weight-gradient partials (for a deferred cfm_colreduce_group task)
+CFM_EXPORT long cfm_convmod_nparts(int B, int T) { return conv_nparts(B, T); }
+
 CFM_EXPORT size_t cfm_bn_ws_bytes(int C) { return (size_t)(2L * BN_PARTS * C + 2L * C) * sizeof(float); }
 
 CFM_EXPORT int cfm_glu_dwconv_fwd(const void* a, int dta, const float* w, const float* bias, float* y, int B,

@@ -248,6 +248,52 @@ class WgradGroup:
         self.tasks = []
 
 
+class ReduceGroup(WgradGroup):
+    """Deferred small column reductions of a backward pass (LayerNorm dgamma|dbeta partial rows, depthwise-conv
+    weight/bias partials) flushed as ONE cfm_colreduce_group launch -- instead of ~85 tiny side-stream
+    launches per Conformer-L step.  Outputs must not be read before flush() (same contract as WgradGroup;
+    the staging pools and the capture rules are WgradGroup's)."""
+
+    def add_sum(self, part, nparts, N, ldp, out):
+        """out[n] = sum_p part[p*ldp + n]; the caller hands autograd fresh views of out (see add_dwconv)."""
+        self.tasks.append((part, out, None, int(nparts), int(N), int(ldp), 0, 0, 0))
+        self._stream = torch.cuda.current_stream(part.device)
+
+    def add_dwconv(self, part, nparts, C, K, dw, db):
+        """the depthwise conv's [nparts][K+1][C] partials -> dw (C, K), db (C).  Returns fresh views of
+        dw / db: the task keeps the tensors themselves, and autograd adopts a gradient without a copy only
+        when nothing else references it (a copy taken before flush() would hold garbage)."""
+        N = C * (K + 1)
+        self.tasks.append((part, dw, db, int(nparts), N, N, 1, int(C), int(K)))
+        self._stream = torch.cuda.current_stream(part.device)
+        return dw.view(C, K), db.view(C)
+
+    def flush(self):
+        if not self.tasks:
+            return
+        import numpy as np
+        key = tuple((t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr() if t[2] is not None else 0) + t[3:]
+                    for t in self.tasks)
+        hit = self._cache.get(key)
+        if hit is None:
+            lib = L.load()
+            tb = L.size_call("cfm_colreduce_group_task_bytes")
+            host = np.zeros(tb * len(self.tasks), dtype=np.uint8)
+            blk0 = 0
+            for i, (part, out, out2, nparts, N, ldp, mode, C, K) in enumerate(self.tasks):
+                L.call("cfm_colreduce_group_fill", host.ctypes.data, i, L.ptr(part), nparts, N, ldp, L.ptr(out),
+                       L.ptr(out2), mode, C, K, blk0)
+                blk0 += lib.cfm_colreduce_group_blocks(N)
+            captured = torch.cuda.is_current_stream_capturing()
+            table = self._stage(host)
+            hit = (captured, table, blk0)
+            if len(self._cache) > 8:
+                self._cache = {k: v for k, v in self._cache.items() if v[0]}
+            self._cache[key] = hit
+        L.call("cfm_colreduce_group", L.ptr(hit[1]), len(self.tasks), hit[2], L.stream())
+        self.tasks = []
+
+
 def wgrad_group_ok(dy, x):
     """Operands the grouped weight-gradient launch takes (else linear_wgrad per GEMM)."""
     return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.is_contiguous() and x.is_contiguous()
@@ -392,7 +438,10 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dres=None, dx_dtype=torch.float32, s
             g2 = scale_dropout(dx, drop[0], drop[1], drop[2], 0, out_dtype=drop[3])
     if defer:
         nb = (L.size_call("cfm_layernorm_ws_bytes", M, D) // 4 - 2 * D) // (2 * D)
-        side.run(lambda: L.call("cfm_colreduce", L.ptr(ws), nb, 2 * D, 2 * D, L.ptr(gb), 0, L.stream()), ws, gb)
+        if getattr(side, "rgroup", None) is not None:      # one grouped reduction at the end of backward
+            side.rgroup.add_sum(ws, nb, 2 * D, 2 * D, gb)
+        else:
+            side.run(lambda: L.call("cfm_colreduce", L.ptr(ws), nb, 2 * D, 2 * D, L.ptr(gb), 0, L.stream()), ws, gb)
     if drop is not None:
         return dx, dgamma, dbeta, g2
     return dx, dgamma, dbeta
@@ -515,8 +564,12 @@ def glu_dwconv_bwd(dy, a, w_dw, B, T, C, K, ws, da_dtype, side=None):
     L.call("cfm_glu_dwconv_bwd", L.ptr(dy), L.ptr(a), L.dt(a), L.ptr(w_dw), L.ptr(da), L.dt(da),
            None if defer else L.ptr(dw), None if defer else L.ptr(db), B, T, C, K, L.ptr(ws), L.stream())
     if defer:
-        side.run(lambda: L.call("cfm_glu_dwconv_bwd_wgrad", L.ptr(ws), B, T, C, K, L.ptr(dw), L.ptr(db), L.stream()),
-                 ws, dw, db)
+        if getattr(side, "rgroup", None) is not None:
+            np_ = L.load().cfm_convmod_nparts(B, T)
+            dw, db = side.rgroup.add_dwconv(ws, np_, C, K, dw, db)
+        else:
+            side.run(lambda: L.call("cfm_glu_dwconv_bwd_wgrad", L.ptr(ws), B, T, C, K, L.ptr(dw), L.ptr(db),
+                                    L.stream()), ws, dw, db)
     return da, dw, db
 
 

@@ -1,7 +1,8 @@
 """MFMA attention kernels (cfm_attn_fwd / cfm_attn_bwd, bf16) against a torch fp32 reference of
 nn.MultiheadAttention's core: softmax(q k^T / sqrt(dk) + key_padding_mask) v, ragged lengths.
-Every kernel family is checked: whole-head (default), tiled (mode 1), wave-per-key-block dK/dV
-(mode 8); and the three must agree with each other under dropout (same counter-based masks)."""
+Every kernel family is checked: whole-head with the wave-per-key-block dK/dV (default), tiled (mode 1),
+four-wave whole-head dK/dV (mode 8); and the three must agree with each other under dropout (same
+counter-based masks; the dQ, dK and dV slices compared separately)."""
 import pytest
 import torch
 
@@ -61,9 +62,11 @@ def test_attention_kernels_agree_under_dropout(attn_mode):
         o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=0.1, seed=9)
         dqkv, _, _, _ = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=0.1, seed=9)
         outs.append((o.float(), dqkv.float()))
+    HD = H * dk
     for o, d in outs[1:]:
         assert _rel(o, outs[0][0]) < 1e-2
-        assert _rel(d, outs[0][1]) < 2e-2
+        for sl in range(3):      # dQ, dK, dV: a mask that differs on ~10 % of the entries fails these
+            assert _rel(d[:, sl * HD:(sl + 1) * HD], outs[0][1][:, sl * HD:(sl + 1) * HD]) < 1e-2
 
 
 def test_rowdot_epilogue_feeds_attention_bwd():
