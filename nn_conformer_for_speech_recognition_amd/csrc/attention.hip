@@ -324,46 +324,44 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
   const float c = p.scale * LOG2E;
   __syncthreads();
   f32x16 a0 = (f32x16){0}, a1 = (f32x16){0};
-  for (int kt = 0; kt < nkt; ++kt) {
-    const bf16* sK = sKall + kt * TILE * KS;
-    const bf16* sV = sVall + kt * TILE * KS;
-    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0}, d0 = (f32x16){0}, d1 = (f32x16){0};
+  // 32-key steps (S^T, dP^T: 32 accumulator registers live -> no spill under the 12-wave cap); dropout
+  // pairs (keys k, k+1 in registers r, r+1) hash (didx >> 1) mod 2^32 = (bh T + qi) T2 + k/2 in 32 bits
+  const int nks = (len + 31) / 32;
+  const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
+  const uint32_t hq = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)qi) * T2 + (uint32_t)(2 * hh);
+  for (int ks = 0; ks < nks; ++ks) {
+    const int k0 = ks * 32;
+    f32x16 s0 = (f32x16){0}, d0 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
-      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
-      d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 0, 16 * s, lane), gf[s], d0, 0, 0, 0);
-      d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32, 16 * s, lane), gf[s], d1, 0, 0, 0);
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sKall, k0, 16 * s, lane), qf[s], s0, 0, 0, 0);
+      d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sVall, k0, 16 * s, lane), gf[s], d0, 0, 0, 0);
+      if (s == 1) __builtin_amdgcn_sched_barrier(0);
     }
+    __builtin_amdgcn_sched_barrier(0);
     if (p.drop_p > 0.f) {
-      const uint64_t rowi = didx(p, b, h, qi, kt * TILE);
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
-        const int k0 = acc_row(r, hh);
-        float m0, m1, m2, m3;
-        dropout_pair(dthr, dkeep, dkey, rowi + k0, m0, m1);
-        dropout_pair(dthr, dkeep, dkey, rowi + k0 + 32, m2, m3);
-        d0[r] *= m0; d0[r + 1] *= m1;
-        d1[r] *= m2; d1[r + 1] *= m3;
+        const uint32_t hsh = cfm_mix32(
+            (hq + __builtin_amdgcn_readfirstlane((k0 + (r & 3) + 8 * (r >> 2)) >> 1)) ^ dkey);
+        d0[r] *= (hsh & 0xFFFFu) >= dthr ? dkeep : 0.f;
+        d0[r + 1] *= (hsh >> 16) >= dthr ? dkeep : 0.f;
       }
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int k0 = kt * TILE + acc_row(r, hh);
-      const float p0 = (k0 < len && qvalid) ? fast_exp2(s0[r] * c - L2) : 0.f;
-      const float p1 = (k0 + 32 < len && qvalid) ? fast_exp2(s1[r] * c - L2) : 0.f;
+      const int kk = k0 + acc_row(r, hh);
+      const float p0 = fast_exp2(kk < len && qvalid ? s0[r] * c - L2 : -INFINITY);
       s0[r] = p0 * (d0[r] - Dq);
-      s1[r] = p1 * (d1[r] - Dq);
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 0, lane), pf, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 32, lane), pf, a1, 0, 0, 0);
-      }
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pf = acc2frag(s0, s);
+      a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sKall, k0 + 16 * s, 0, lane), pf, a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sKall, k0 + 16 * s, 32, lane), pf, a1, 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();
   float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
@@ -460,15 +458,43 @@ __global__ __launch_bounds__(64 * DKDV_WAVES) void attn_bwd_dkdv_head_kernel(Att
   }
 }
 
+// write a wave's 64(d) x 32(key) f32 accumulator pair transposed into bf16 rows, straight from the
+// registers: lane (key c, half hh) owns d = 32t + 8g + 4hh .. +3 of register group g -> one 8-byte store
+// each (rows row0 + c < row0 + nvalid, d < dk)
+__device__ __forceinline__ void store_acc_rows(const f32x16& a0, const f32x16& a1, float mul, bf16* out, long ld,
+                                               int row0, int nvalid, int dk, bool v8, int lane) {
+  const int hh = lane >> 5, c = lane & 31;
+  if (c >= nvalid) return;
+  bf16* o = out + (long)(row0 + c) * ld;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const f32x16& a = t ? a1 : a0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * t + 8 * g + 4 * hh;
+      if (v8 && d + 4 <= dk) {
+        bf16x4 v = {(bf16)(a[4 * g] * mul), (bf16)(a[4 * g + 1] * mul), (bf16)(a[4 * g + 2] * mul),
+                    (bf16)(a[4 * g + 3] * mul)};
+        *reinterpret_cast<bf16x4*>(o + d) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (d + e < dk) o[d + e] = (bf16)(a[4 * g + e] * mul);
+      }
+    }
+  }
+}
+
 // dK, dV, one wave per 32-key block: grid (B*H), block 64 * ceil(T/32) (three waves per SIMD at
-// T = 373, <= 168 registers); the head's whole Q and dO (and lse, D) are staged once and every wave
-// sweeps 32-query steps over them with no further barriers.  Per step 16 MFMAs (S, dP, dV^T += dO^T P,
-// dK^T += Q^T dS), P / dS formed in place in the S / dP accumulators, branch-free (masked keys enter the
-// exponential as -inf).  Attention dropout: the hash index of element (q, kj) is
-// (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2 (T2 = even T / 2; exact: didx < 2^33), so lanes kj and kj^1
-// share one 32-bit hash per query: the even lane hashes the query of accumulator register r, the odd lane
-// that of r + 1, and one DPP swap hands each lane its partner's -- one hash per two elements, 32-bit
-// index arithmetic with per-register offsets that are wave-uniform.
+// T = 373); the head's whole Q and dO (and lse, D) are staged once and every wave sweeps 32-query
+// steps over them with no further barriers.  Two passes keep every wave under the three-wave register
+// cap with nothing spilled: pass 1 forms P and accumulates dV^T += dO^T P (8 MFMAs per step), stores dV
+// straight from the registers, and leaves the step's dropout keep bits in LDS; pass 2 recomputes S,
+// forms dP and dS and accumulates dK^T += Q^T dS (12 MFMAs per step).  Masked keys enter the exponential
+// as -inf (branch-free).  Attention dropout: the hash index of element (q, kj) is (didx >> 1) mod 2^32
+// = (bh T + q) T2 + kj/2 (T2 = even T / 2; exact: didx < 2^33), so lanes kj and kj^1 share one 32-bit
+// hash per query: the even lane hashes the query of accumulator register r, the odd lane that of r + 1,
+// and one DPP swap hands each lane its partner's -- one hash per two elements, 32-bit index arithmetic.
 __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel(AttnM p, const bf16* __restrict__ dout,
                                                                                  const float* __restrict__ lse,
                                                                                  const float* __restrict__ Dg,
@@ -486,6 +512,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
   bf16* sGall = hsm + (long)Tq * KS;
   float* sL = reinterpret_cast<float*>(sGall + (long)Tq * KS);      // [Tq] lse * log2(e) (+inf past T)
   float* sD = sL + Tq;                                              // [Tq] D
+  unsigned short* sM = reinterpret_cast<unsigned short*>(sD + Tq);  // [wave][step][lane] pass-1 keep bits
   const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
   head_stage(p, qbase, dout + (long)b * p.T * p.HD + h * p.dk, p.D3, p.HD, Tq, sQall, sGall, tid, blockDim.x);
   for (int i = tid; i < Tq; i += blockDim.x) {
@@ -500,74 +527,111 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
   load_bfrags(p, qbase + 2 * p.HD, p.D3, kj, p.T, vf, lane);
   __syncthreads();
   const float c = p.scale * LOG2E;
-  f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
   const int nqs = k0w < len ? nq : 0;      // key blocks past len: zero gradients
   const int odd = lane & 1, sh = 16 * odd;
   const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
   const uint32_t hbase = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)(4 * hh + odd)) * T2 + (uint32_t)(kj >> 1);
-  for (int qt = 0; qt < nqs; ++qt) {
-    const int q0 = qt * 32;
-    f32x16 sa = (f32x16){0}, ga = (f32x16){0};
+  unsigned short* myM = sM + (long)wv * nq * 64 + lane;
+  bf16* obase = dqkv + (long)b * p.T * p.D3 + h * p.dk;
+  const int nvalid = min(32, p.T - k0w);
+  const bool v8 = p.vec && ((uintptr_t)dqkv & 7) == 0;
+
+  // ---- pass 1: P, dV^T += dO^T P
+  {
+    f32x16 dv0 = (f32x16){0}, dv1 = (f32x16){0};
+    for (int qt = 0; qt < nqs; ++qt) {
+      const int q0 = qt * 32;
+      f32x16 sa = (f32x16){0};
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, q0, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
-      ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sGall, q0, 16 * s4, lane), vf[s4], ga, 0, 0, 0);
-      if (s4 == 1) __builtin_amdgcn_sched_barrier(0);   // at most 4 operand fragments in flight (VGPR cap)
-    }
-    __builtin_amdgcn_sched_barrier(0);   // keep the next phase's LDS reads from being hoisted (VGPR cap)
-    bf16x8 pf[2], sf[2];                   // P and dS as bf16 B-operand fragments (k-steps 0, 1)
+      for (int s4 = 0; s4 < 4; ++s4)
+        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, q0, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 pf[2];
+      unsigned bits = 0;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {          // registers 4g .. 4g+3 = queries q0 + 8g + 4hh + 0..3
-      const float4 Lg = *reinterpret_cast<const float4*>(sL + q0 + 8 * g + 4 * hh);
-      const float4 Dq = *reinterpret_cast<const float4*>(sD + q0 + 8 * g + 4 * hh);
-      const float Lr[4] = {Lg.x, Lg.y, Lg.z, Lg.w}, Dr[4] = {Dq.x, Dq.y, Dq.z, Dq.w};
-      float mk[4] = {1.f, 1.f, 1.f, 1.f};
-      if (drop) {
+      for (int g = 0; g < 4; ++g) {          // registers 4g .. 4g+3 = queries q0 + 8g + 4hh + 0..3
+        const float4 Lg = *reinterpret_cast<const float4*>(sL + q0 + 8 * g + 4 * hh);
+        const float Lr[4] = {Lg.x, Lg.y, Lg.z, Lg.w};
+        float mk[4] = {1.f, 1.f, 1.f, 1.f};
+        if (drop) {
 #pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          // (the wave-uniform offset through readfirstlane: otherwise the 8 per-register bases are hoisted
-          // out of the loop as VGPRs and spilled)
-          const uint32_t hm = cfm_mix32((hbase + __builtin_amdgcn_readfirstlane((q0 + 8 * g + e) * (int)T2)) ^ dkey);
-          const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);  // lane ^ 1
-          const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
-          mk[e] = ((h0 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
-          mk[e + 1] = ((h1 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
+          for (int e = 0; e < 4; e += 2) {
+            // (the wave-uniform offset through readfirstlane: otherwise the per-register bases are
+            // hoisted out of the loop as VGPRs)
+            const uint32_t hm = cfm_mix32((hbase + __builtin_amdgcn_readfirstlane((q0 + 8 * g + e) * (int)T2)) ^ dkey);
+            const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+            const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
+            const bool k0 = ((h0 >> sh) & 0xFFFFu) >= dthr, k1 = ((h1 >> sh) & 0xFFFFu) >= dthr;
+            mk[e] = k0 ? dkeep : 0.f;
+            mk[e + 1] = k1 ? dkeep : 0.f;
+            bits |= (k0 ? 1u : 0u) << (4 * g + e);
+            bits |= (k1 ? 2u : 0u) << (4 * g + e);
+          }
         }
-      }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 4 * g + e;
-        const float pa = fast_exp2(kvalid ? sa[r] * c - Lr[e] : -INFINITY);   // lse = +inf for q >= T
-        pf[r >> 3][r & 7] = (bf16)(pa * mk[e]);                       // P (dropped)
-        sf[r >> 3][r & 7] = (bf16)(pa * (ga[r] * mk[e] - Dr[e]));     // dS
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          const float pa = fast_exp2(sa[r] * c - Lr[e]);   // lse = +inf for q >= T
+          pf[r >> 3][r & 7] = (bf16)(pa * mk[e]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);   // one group's lse / D in registers at a time (VGPR cap)
-    }
-    __builtin_amdgcn_sched_barrier(0);
+      if (drop) myM[qt * 64] = (unsigned short)bits;
+      if (!kvalid) pf[0] = pf[1] = (bf16x8){0};     // keys past len: P = 0 (one select per packed register)
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 0, lane), pf[s2], dv0, 0, 0, 0);
-      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 32, lane), pf[s2], dv1, 0, 0, 0);
-      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 0, lane), sf[s2], dk0, 0, 0, 0);
-      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 32, lane), sf[s2], dk1, 0, 0, 0);
+      for (int s2 = 0; s2 < 2; ++s2) {
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 0, lane), pf[s2], dv0, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 32, lane), pf[s2], dv1, 0, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
+    store_acc_rows(dv0, dv1, 1.f, obase + 2 * p.HD, p.D3, k0w, nvalid, p.dk, v8, lane);
   }
-  __syncthreads();     // every wave is done with Q / dO: the images become the epilogue staging
-  float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
-  if (k0w < p.T) {
-    bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
-    const int nvalid = min(32, p.T - k0w);
-    store_transposed(stage, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
-    store_transposed(stage, dv0, dv1, 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
+  // ---- pass 2: dP, dS, dK^T += Q^T dS
+  {
+    const float keep = drop ? dkeep : 1.f;
+    f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0};
+    for (int qt = 0; qt < nqs; ++qt) {
+      const int q0 = qt * 32;
+      f32x16 sa = (f32x16){0}, ga = (f32x16){0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, q0, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
+        ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sGall, q0, 16 * s4, lane), vf[s4], ga, 0, 0, 0);
+        if (s4 == 1) __builtin_amdgcn_sched_barrier(0);   // at most 4 operand fragments in flight
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned bits = drop ? (unsigned)myM[qt * 64] : 0xFFFFu;
+      bf16x8 sf[2];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 Lg = *reinterpret_cast<const float4*>(sL + q0 + 8 * g + 4 * hh);
+        const float4 Dq = *reinterpret_cast<const float4*>(sD + q0 + 8 * g + 4 * hh);
+        const float Lr[4] = {Lg.x, Lg.y, Lg.z, Lg.w}, Dr[4] = {Dq.x, Dq.y, Dq.z, Dq.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          const float pa = fast_exp2(sa[r] * c - Lr[e]);
+          const float m = (bits >> r) & 1u ? keep : 0.f;
+          sf[r >> 3][r & 7] = (bf16)(pa * (ga[r] * m - Dr[e]));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (!kvalid) sf[0] = sf[1] = (bf16x8){0};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 0, lane), sf[s2], dk0, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 32, lane), sf[s2], dk1, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    store_acc_rows(dk0, dk1, p.scale, obase + p.HD, p.D3, k0w, nvalid, p.dk, v8, lane);
   }
 }
 
 size_t dkdv_wave_lds_bytes(int T) {
-  const size_t rows = (size_t)cdiv(T, 32) * 32;
-  const size_t img = 2 * rows * KS * sizeof(bf16) + 2 * rows * sizeof(float);
-  const size_t stage = rows * 65 * sizeof(float);
-  return img > stage ? img : stage;
+  const size_t nq = (size_t)cdiv(T, 32), rows = nq * 32;
+  return 2 * rows * KS * sizeof(bf16) + 2 * rows * sizeof(float) + nq * nq * 64 * sizeof(unsigned short);
 }
 
 size_t dkdv_head_lds_bytes(int T) {
