@@ -23,3 +23,14 @@ for e in prof.events():
         cnt[(e.name, " <- ".join(st))] += 1
 for (n, st), c in cnt.most_common(15):
     print(c, n, st)
+
+# stackless fills (autograd worker thread): the ops issued just before them on the same thread
+evs = sorted([e for e in prof.events()], key=lambda e: (e.thread, e.time_range.start))
+ctx = collections.Counter()
+for i, e in enumerate(evs):
+    if e.name in ("aten::fill_", "aten::zero_") and not e.stack and e.cpu_parent is None:
+        prev = [evs[j].name for j in range(max(0, i - 4), i) if evs[j].thread == e.thread]
+        ctx[(e.name, " | ".join(prev))] += 1
+print("--- stackless fills by preceding ops")
+for (n, p), c in ctx.most_common(12):
+    print(c, n, "after:", p)

@@ -12,5 +12,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
 cat $O/bench.json
 bash benchmarks/prof_bench.sh $O/kernel_stats.csv --steps 5 --warmup 2 --no-cpu-baseline || { echo "prof failed"; tail -20 $O/kernel_stats.log; exit 1; }
-python profiles/summarize.py $O/kernel_stats.csv 7 40 > $O/kernel_summary.txt
+python profiles/summarize.py $O/kernel_stats.csv auto 40 > $O/kernel_summary.txt
 head -45 $O/kernel_summary.txt

@@ -450,7 +450,8 @@ class ConformerLayer(nn.Module):
         return ps
 
     def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None, shadow=None, layer_index=0,
-                       group_wgrad=False, grad_dest=None, flush_here=False, on_flushed=None, sync_bn=None):
+                       group_wgrad=False, grad_dest=None, flush_here=False, on_flushed=None, sync_bn=None,
+                       count_batches=True):
         """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device; shadow: optional
         ({param index: compute-dtype copy}, {param index: its transposed K-major copy}) of this
         layer's weight matrices (see Conformer._shadows)."""
@@ -471,7 +472,7 @@ class ConformerLayer(nn.Module):
         cfg.group_wgrad = bool(group_wgrad) and "wgroup" not in ops.DISABLED
         cfg.grad_dest, cfg.flush_here, cfg.on_flushed = grad_dest, flush_here, on_flushed
         cfg.sync_bn = sync_bn
-        if self.training and bn.track_running_stats:
+        if count_batches and self.training and bn.track_running_stats:
             bn.num_batches_tracked.add_(1)
         return _ConformerLayerFn.apply(x, lens_i32, cfg, *self.params())
 
@@ -573,7 +574,12 @@ class Conformer(nn.Module):
                                      layer_index=i, group_wgrad=group,
                                      grad_dest=self.grad_dest[i] if self.grad_dest else None,
                                      flush_here=i in self.flush_layers, on_flushed=self.on_flushed,
-                                     sync_bn=self.sync_bn)
+                                     sync_bn=self.sync_bn, count_batches=False)
+        # every layer's BatchNorm num_batches_tracked += 1 in one multi-tensor launch (not one per layer)
+        counters = [ly.conv_module.sequential[3].num_batches_tracked for ly in self.conformer_layers
+                    if self.training and ly.conv_module.sequential[3].track_running_stats]
+        if counters:
+            torch._foreach_add_(counters, 1)
         return x
 
     def forward(self, input, lengths):

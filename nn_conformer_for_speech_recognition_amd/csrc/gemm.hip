@@ -886,6 +886,201 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   probe_end(p.probe);
 }
 
+// ---------------------------------------------------------------- persistent, interleaved epilogue
+// For K-major bf16 GEMMs whose epilogue loads nothing but the bias (forward projections incl. the FFN
+// up-projection's bias + SiLU + dropout + pre-activation store, and the plain data-gradient GEMMs): one
+// workgroup per CU loops over 192 x 128 tiles (XCD-contiguous tile ranges), and the epilogue of tile i
+// -- staged in its own LDS buffer as f32 -- is stored one 8-column unit per thread per K step INSIDE
+// tile i+1's main loop, so its VALU work and HBM writes overlap the MFMAs instead of following them.
+// The stores are range-checked buffer stores (rows past M are dropped by the hardware, not skipped),
+// so every unit issues exactly E vector-memory ops and the ring's counted vmcnt waits stay exact.
+// Status: bit-identical to the pipeline kernels (test_gemm_interleaved_epilogue_matches_pipeline) but
+// SLOWER on the encoder's shapes (profiles/r02/gemm_ie_ab.txt: its BK-32 single-workgroup main loop loses
+// more than the overlap gains; only the N = 1024 / 1536 SiLU cases won) -- off by default (mode bit 9).
+constexpr int IE_BM = 192, IE_BK = 32, IE_NST = 3, IE_NWV = 8, IE_WN = 4;
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+template <int N>
+__device__ __forceinline__ void vm_wait_le() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// wait until at most (stages * PER + stores * E) vector-memory ops are outstanding
+template <int PER, int E>
+__device__ __forceinline__ void ie_wait(int stages, int stores) {
+  const int sel = stages * 3 + stores;   // stages in {0, 1}, stores in {0, 1, 2}
+  switch (sel) {
+    case 0: vm_wait_le<0>(); break;
+    case 1: vm_wait_le<E>(); break;
+    case 2: vm_wait_le<2 * E>(); break;
+    case 3: vm_wait_le<PER>(); break;
+    case 4: vm_wait_le<PER + E>(); break;
+    default: vm_wait_le<PER + 2 * E>(); break;
+  }
+}
+
+template <bool PRE>
+__global__ __launch_bounds__(IE_NWV * 64) void gemm_pipe_ie_kernel(GemmP p, PipeOp oa, PipeOp ob, int ntm, int ntn) {
+  constexpr int BMt = IE_BM, BKt = IE_BK, NST = IE_NST, NWV = IE_NWV, WN = IE_WN;
+  constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BN / WN / 32;
+  constexpr int NTt = NWV * 64, UPT = BMt * 16 / NTt;   // 8-column units per thread per tile (6)
+  constexpr int ABYTES = BMt * BKt * 2, BBYTES = BN * BKt * 2, STAGE = ABYTES + BBYTES;
+  constexpr int AW = ABYTES / 1024, BW = BBYTES / 1024;  // wave-instructions of DMA per stage (12, 8)
+  static_assert(BW == NWV && AW > NWV && AW <= 2 * NWV, "A: every wave one piece, waves < AW-NWV a second");
+  constexpr int E = PRE ? 2 : 1;
+  constexpr int RING = NST * STAGE, STG = BMt * EP_STRIDE * 4;
+  static_assert(UPT * NTt == BMt * 16 && RING + STG + 512 <= 163840, "ie geometry");
+  __shared__ __attribute__((aligned(1024))) char lds[RING + STG + 512];
+  float* st = reinterpret_cast<float*>(lds + RING);
+  float* sbias = reinterpret_cast<float*>(lds + RING + STG);
+  probe_begin(p.probe);
+  gemm_drop_prep(p);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntiles = ntm * ntn, GW = gridDim.x, Lb = blockIdx.x;
+  const int pos = (GW % 8 == 0) ? (Lb & 7) * (GW / 8) + (Lb >> 3) : Lb;   // XCD-contiguous tile ranges
+  const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, 0), rb = pipe_rsrc(ob, 0);
+  // bf16 C (and pre): rows past M fall outside num_records and their stores are dropped
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      p.C, (short)0, __builtin_amdgcn_readfirstlane((int)((long)p.M * p.ldc * 2)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+      PRE ? p.pre : p.C, (short)0, __builtin_amdgcn_readfirstlane((int)((long)p.M * p.ldc * 2)), 0x00020000);
+  const int nk = (p.K + BKt - 1) / BKt;
+  int pm0 = -1, pn0 = 0;   // pending staged tile (its epilogue runs inside the next main loop)
+
+  // unit j of this thread of the pending tile: 8 consecutive columns of one row -> E buffer stores
+  const bool two = wid < AW - NWV;         // this wave issues a second A piece per stage (wave-uniform)
+  auto unit = [&](int j) {
+    const int u = j * NTt + tid, row = u >> 4, c8 = (u & 15) * 8;
+    const float4 lo = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8);
+    const float4 hi = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8 + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const int m = pm0 + row, n = pn0 + c8;
+    if (p.alpha != 1.f) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+    }
+    if (p.bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += sbias[c8 + e];
+    }
+    const unsigned off = (unsigned)(((long)m * p.ldc + n) * 2);
+    if constexpr (PRE) {
+      bf16x8 pv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pv[e] = (bf16)v[e];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, pv), rp,
+                                             (unsigned)(((long)m * p.ldc + n) * 2), 0, 0);
+    }
+    if (p.act == CFM_ACT_SILU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
+    }
+    if (p.drop_p > 0.f) {
+      const uint64_t base = p.doff + (uint64_t)((long)m * p.N + n);
+      const uint32_t j0 = (uint32_t)(base >> 1);
+      uint32_t h[5];
+#pragma unroll
+      for (int q = 0; q < 5; ++q) h[q] = cfm_mix32((j0 + q) ^ p.dkey0);
+      const int odd = (int)(base & 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int q = (odd + e) >> 1;
+        const uint32_t b = ((odd + e) & 1) ? (h[q] >> 16) : (h[q] & 0xFFFFu);
+        v[e] *= b >= p.dthr ? p.dkeep : 0.f;
+      }
+    }
+    if (p.out_scale != 1.f) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
+    }
+    bf16x8 cv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cv[e] = (bf16)v[e];
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, cv), rc, off, 0, 0);
+  };
+
+  for (int tile = pos; tile < ntiles; tile += GW) {
+    const int tm = tile / ntn, tn = tile % ntn;
+    const int m0 = tm * BMt, n0 = tn * BN;
+    const unsigned offa0 = pipe_src<true, BMt, BKt>(oa, wid * 64 + lane, m0, 0);
+    const unsigned offa1 = pipe_src<true, BMt, BKt>(oa, ((NWV + wid) * 64 + lane) % (AW * 64), m0, 0);
+    const unsigned offb0 = pipe_src<true, BN, BKt>(ob, wid * 64 + lane, n0, 0);
+    auto issue = [&](int kt) {
+      char* sa = lds + (kt % NST) * STAGE;
+      char* sb = sa + ABYTES;
+      dma16(ra, sa + wid * 1024, offa0 + kt * (BKt * 2));
+      if (two) dma16(ra, sa + (NWV + wid) * 1024, offa1 + kt * (BKt * 2));
+      dma16(rb, sb + wid * 1024, offb0 + kt * (BKt * 2));
+    };
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x16){0};
+    vm_wait_le<0>();   // nothing of the previous tile outstanding: the counted waits below are exact
+#pragma unroll
+    for (int s2 = 0; s2 < NST - 1; ++s2)
+      if (s2 < nk) issue(s2);
+    const bool pend = pm0 >= 0;
+    // unit j of the pending tile runs at K step j (front-loaded: spreading the units over the whole loop
+    // measured slower); short K: the rest after the loop
+    auto unit_at = [&](int k) -> int { return (pend && k >= 0 && k < nk && k < UPT) ? k : -1; };
+    for (int kt = 0; kt < nk; ++kt) {
+      // outstanding after stage kt's DMA: stage kt+1 (issued at kt-1) and the units of kt-1, kt-2
+      const int ys = min(NST - 2, nk - 1 - kt);
+      const int yu = (unit_at(kt - 1) >= 0 ? 1 : 0) + (unit_at(kt - 2) >= 0 ? 1 : 0);
+      if (two) ie_wait<3, E>(ys, yu);
+      else ie_wait<2, E>(ys, yu);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + NST - 1 < nk) issue(kt + NST - 1);
+      const char* sa = lds + (kt % NST) * STAGE;
+      const char* sb = sa + ABYTES;
+      constexpr int KST = BKt / 16;
+      bf16x8 af[KST][FM], bfr[KST][FN];
+#pragma unroll
+      for (int q = 0; q < KST; ++q) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[q][j] = pipe_frag<true, BN, BKt>(sb, wn * FN * 32 + j * 32, 16 * q, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[q][i] = pipe_frag<true, BMt, BKt>(sa, wm * FM * 32 + i * 32, 16 * q, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < KST; ++q)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[q][i], bfr[q][j], acc[i][j], 0, 0, 0);
+      const int uj = unit_at(kt);
+      if (uj >= 0) unit(uj);             // the previous tile's epilogue, spread over the K steps
+    }
+    if (pend)
+      for (int j = nk; j < UPT; ++j) unit(j);   // short K: the rest after the loop
+    __syncthreads();   // ring and staging free (every wave past its last reads)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * FM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int col = wn * FN * 32 + j * 32 + (lane & 31);
+          st[row * EP_STRIDE + col] = acc[i][j][r];
+        }
+    if (p.bias && tid < BN) sbias[tid] = p.bias[n0 + tid];
+    pm0 = m0;
+    pn0 = n0;
+    __syncthreads();   // staging + bias visible before the next tile's units read them
+  }
+  if (pm0 >= 0) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) unit(j);
+  }
+  probe_end(p.probe);
+}
+
 // ---------------------------------------------------------------- grouped weight gradients
 // All weight-gradient GEMMs dW_i = dY_iᵀ X_i (+ bias gradient sum_rows dY_i) of a backward pass in ONE
 // launch: every task reduces over the same token dimension, so each 256x128 output tile is one
@@ -1166,6 +1361,25 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
   else hipLaunchKernelGGL((gemm_pipe_kernel<128, 64, 3, 1, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob, GatherA{});
 }
 
+// the persistent interleaved-epilogue kernel takes K-major bf16 GEMMs whose epilogue needs no global
+// loads besides the bias (cfm_gemm_set_mode bit 9 enables it)
+bool ie_ok(const cfm_gemm_desc& d, const GemmP& p) {
+  return (g_gemm_mode & 512) && d.a_kmajor && d.b_kmajor && d.batch == 1 && p.split_k == 1 && !p.res &&
+         !p.act_grad && !p.cmap && !p.rd_out && !p.acs_slab && !p.slab && p.vec_c && p.N % BN == 0 &&
+         p.dtc == CFM_BF16 && (p.act == 0 || p.act == CFM_ACT_SILU) && (!p.pre || p.dtpre == CFM_BF16) &&
+         (long)p.M * p.ldc * 2 < (1L << 31) && !p.dbg && p.alpha_a == nullptr && p.alpha_b == nullptr;
+}
+
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   p.vec_c = vec_epilogue_ok(p);
   p.dbg = ((g_gemm_mode & 8) ? 1 : 0) | ((g_gemm_mode & 256) ? 2 : 0);   // bit 8: generic dropout path (A/B)
@@ -1175,6 +1389,15 @@ int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   const PipeOp oa{(const bf16*)d.A, d.lda, d.stride_a, d.M, (unsigned)(ea * 2)};
   const PipeOp ob{(const bf16*)d.B, d.ldb, d.stride_b, d.N, (unsigned)(eb * 2)};
   const bool ak = d.a_kmajor != 0, bkm = d.b_kmajor != 0;
+  if (ie_ok(d, p)) {
+    const int ntm = cdiv(p.M, IE_BM), ntn = p.N / BN;
+    const int grid = min(ntm * ntn, num_cus());
+    if (p.pre)
+      hipLaunchKernelGGL((gemm_pipe_ie_kernel<true>), dim3(grid), dim3(IE_NWV * 64), 0, s, p, oa, ob, ntm, ntn);
+    else
+      hipLaunchKernelGGL((gemm_pipe_ie_kernel<false>), dim3(grid), dim3(IE_NWV * 64), 0, s, p, oa, ob, ntm, ntn);
+    return CFM_OK;
+  }
   if (ak && bkm) launch_pipe_t<true, true>(p, oa, ob, d.batch, s);
   else if (ak) launch_pipe_t<true, false>(p, oa, ob, d.batch, s);
   else if (bkm) launch_pipe_t<false, true>(p, oa, ob, d.batch, s);

@@ -3,7 +3,13 @@ import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
+arg = sys.argv[2] if len(sys.argv) > 2 else "1"
+if arg == "auto":
+    # executed training steps = launches of the grouped weight-gradient kernel (one per step, eager warm-up,
+    # timed replays and probe-graph replays alike)
+    steps = sum(float(r["Calls"]) for r in rows if "gemm_pipe_kernel" in r["Name"] and "false, true, false>" in r["Name"])
+else:
+    steps = float(arg)
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print(f"total kernel time {tot/1e6:.2f} ms over {steps:g} steps = {tot/1e6/steps:.2f} ms/step")
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[: int(sys.argv[3]) if len(sys.argv) > 3 else 30]:

@@ -371,3 +371,31 @@ def test_wgrad_group_matches_per_gemm():
     for (dw, db), (rw, rb) in zip(outs, refs):
         assert _rel(dw, rw) < 1e-5
         assert _rel(db, rb) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 512, 512), (11936 // 8, 2048, 512), (200, 256, 64), (385, 384, 2048)])
+@pytest.mark.parametrize("epi", ["bias", "silu_pre_drop", "plain_scaled"])
+def test_gemm_interleaved_epilogue_matches_pipeline(gemm_mode, M, N, K, epi):
+    """The persistent interleaved-epilogue kernel (cfm_gemm_set_mode bit 9) against the default LDS-DMA
+    pipeline on the same inputs: identical K loops and epilogue arithmetic -> bit-identical outputs
+    (ragged M, short K with the epilogue finished after the loop, several tiles per workgroup)."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    outs = []
+    for mode in (3, 3 | 512):
+        gemm_mode(mode)
+        y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        if epi == "bias":
+            ops.linear(x, w, b, out=y)
+        elif epi == "silu_pre_drop":
+            ops.linear(x, w, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=5, out=y)
+        else:
+            ops.gemm(x, w, y, M, N, K, a_kmajor=True, b_kmajor=True, alpha=0.5)
+        torch.cuda.synchronize()
+        outs.append((y.clone(), pre.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if epi == "silu_pre_drop":
+        assert torch.equal(outs[0][1], outs[1][1])
