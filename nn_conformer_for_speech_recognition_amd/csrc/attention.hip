@@ -144,8 +144,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnM p, bf16* __restrict
 // ceil(T/128)*B*H workgroups that each re-stream K/V tile by tile behind a barrier per tile.
 constexpr int HEAD_TMAX = 384;      // 12 waves of 32 queries; K+V images 2 * 384 * 144 B = 108 KiB
 
-// 2^x for softmax arguments <= 0: the bare v_exp_f32 (results below 2^-126 flush to 0)
-__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // stage rows [0, nrows) of two head slices (dk <= 64 columns at base0 / base1, row stride ld) into
 // LDS images [nrows][KS]; rows >= T read as zero
@@ -258,13 +256,13 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
       o1[r] *= alpha;
     }
     if (p.drop_p > 0.f) {
-      const uint64_t rowi = didx(p, b, h, qi, kt * TILE);
+      const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
         const int k0 = acc_row(r, hh);
         float m0, m1, m2, m3;
-        dropout_pair(dthr, dkeep, dkey, rowi + k0, m0, m1);
-        dropout_pair(dthr, dkeep, dkey, rowi + k0 + 32, m2, m3);
+        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
+        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
         s0[r] *= m0; s0[r + 1] *= m1;
         s1[r] *= m2; s1[r + 1] *= m3;
       }

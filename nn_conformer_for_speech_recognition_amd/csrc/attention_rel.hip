@@ -203,12 +203,12 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
     }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     const float mn = fmaxf(m, mloc);
-    const float alpha = exp2f(m - mn);
+    const float alpha = fast_exp2(m - mn);
     float ls = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      s0[r] = exp2f(s0[r] - mn);
-      s1[r] = exp2f(s1[r] - mn);
+      s0[r] = fast_exp2(s0[r] - mn);
+      s1[r] = fast_exp2(s1[r] - mn);
       ls += s0[r] + s1[r];
     }
     ls += __shfl_xor(ls, 32, 64);
@@ -220,13 +220,13 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
       o1[r] *= alpha;
     }
     if (p.drop_p > 0.f) {
-      const uint64_t rowi = didx(p, b, h, qi, kt * TILE);
+      const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const int k0 = acc_row(r, hh);
         float m0, m1, m2, m3;
-        dropout_pair(dthr, dkeep, dkey, rowi + k0, m0, m1);
-        dropout_pair(dthr, dkeep, dkey, rowi + k0 + 32, m2, m3);
+        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
+        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
         s0[r] *= m0; s0[r + 1] *= m1;
         s1[r] *= m2; s1[r + 1] *= m3;
       }
@@ -318,13 +318,13 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
       d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32, 16 * s, lane), gf[s], d1, 0, 0, 0);
     }
     if (p.drop_p > 0.f) {
-      const uint64_t rowi = didx(p, b, h, qi, kt * TILE);
+      const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const int k0 = acc_row(r, hh);
         float m0, m1, m2, m3;
-        dropout_pair(dthr, dkeep, dkey, rowi + k0, m0, m1);
-        dropout_pair(dthr, dkeep, dkey, rowi + k0 + 32, m2, m3);
+        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
+        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
         d0[r] *= m0; d0[r + 1] *= m1;
         d1[r] *= m2; d1[r + 1] *= m3;
       }
@@ -332,8 +332,8 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int k0 = kt * TILE + acc_row(r, hh);
-      const float p0 = (k0 < len && qvalid) ? exp2f(s0[r] * c - L2) : 0.f;
-      const float p1 = (k0 + 32 < len && qvalid) ? exp2f(s1[r] * c - L2) : 0.f;
+      const float p0 = fast_exp2(k0 < len && qvalid ? s0[r] * c - L2 : -INFINITY);
+      const float p1 = fast_exp2(k0 + 32 < len && qvalid ? s1[r] * c - L2 : -INFINITY);
       s0[r] = p0 * (d0[r] - Dq);
       s1[r] = p1 * (d1[r] - Dq);
     }
@@ -407,7 +407,8 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
                                                                 const float* __restrict__ Dg,
                                                                 bf16* __restrict__ dqkv, bf16* __restrict__ dsbuf,
                                                                 int ldS) {
-  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const bool drop = p.drop_p > 0.f;
+  if (drop) p.seed = salted_seed(p.seed, p.salt);
   const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
   const float dkeep = drop_keep_scale(dthr);
   __shared__ __attribute__((aligned(16))) bf16 sq[2 * 3 * TILE * KS];      // [buf][Qu, Qv, dO][64][72] 54 KiB
@@ -421,6 +422,9 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
   const int kj = k0w + jj;
   const int len = p.len[b];
   const bool kvalid = kj < len;
+  const int odd = lane & 1, sh = 16 * odd;
+  const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
+  const uint32_t hbase = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)(4 * hh + odd)) * T2 + (uint32_t)(kj >> 1);
   bf16x8 kf[4], vf[4];
   load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + p.HD + h * p.dk, p.D3, kj, p.T, kf, lane);
   load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + 2 * p.HD + h * p.dk, p.D3, kj, p.T, vf, lane);
@@ -532,14 +536,27 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
       const float* tD = sLD[cur][1] + 32 * t;
       f32x16 pd;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qa = acc_row(r, hh);
-        const int qia = qt * TILE + 32 * t + qa;
-        const float pa = kvalid ? exp2f(sa[r] * c - tL[qa]) : 0.f;     // lse = +inf for q >= T
-        float ma = 1.f;
-        if (p.drop_p > 0.f) ma = dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qia, kj));
-        pd[r] = pa * ma;
-        sa[r] = pa * (ga[r] * ma - tD[qa]);
+      for (int r = 0; r < 16; r += 2) {
+        // dropout of (query of register r / r+1, key kj): lanes kj, kj^1 share one 32-bit hash per query
+        // (index (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2); the even lane hashes register r's query,
+        // the odd lane register r+1's, and a DPP swap hands each lane its partner's
+        float m0 = 1.f, m1 = 1.f;
+        if (drop) {
+          const uint32_t hm = cfm_mix32(
+              (hbase + __builtin_amdgcn_readfirstlane((qt * TILE + 32 * t + (r & 3) + 8 * (r >> 2)) * (int)T2)) ^ dkey);
+          const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
+          const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
+          m0 = ((h0 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
+          m1 = ((h1 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int qa = acc_row(r + e, hh);
+          const float ma = e ? m1 : m0;
+          const float pa = fast_exp2(kvalid ? sa[r + e] * c - tL[qa] : -INFINITY);   // lse = +inf for q >= T
+          pd[r + e] = pa * ma;
+          sa[r + e] = pa * (ga[r + e] * ma - tD[qa]);
+        }
       }
       // scale * dS -> dsbuf[i][j] (query-major: lanes = consecutive keys)
       if (kj < p.T) {

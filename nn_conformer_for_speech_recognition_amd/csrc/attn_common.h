@@ -37,6 +37,17 @@ __device__ __forceinline__ void dropout_pair(uint32_t thr, float keep, uint32_t 
   m1 = (h >> 16) >= thr ? keep : 0.f;
 }
 
+// 2^x for softmax arguments <= 0: the bare v_exp_f32 (results below 2^-126 flush to 0)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// the same with the pair's hash index j = (idx >> 1) mod 2^32 supplied in 32 bits (idx < 2^33)
+__device__ __forceinline__ void dropout_pair32(uint32_t thr, float keep, uint32_t key, uint32_t j, float& m0,
+                                               float& m1) {
+  const uint32_t h = cfm_mix32(j ^ key);
+  m0 = (h & 0xFFFFu) >= thr ? keep : 0.f;
+  m1 = (h >> 16) >= thr ? keep : 0.f;
+}
+
 // 8 consecutive head-dim elements c..c+7 of row `row` of matrix base (row stride ld), zero-padded
 __device__ __forceinline__ uint4 ld8(const bf16* base, long ld, int row, int nrows, int c, int dk, bool vec) {
   uint4 r = make_uint4(0, 0, 0, 0);

@@ -896,7 +896,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
 // so every unit issues exactly E vector-memory ops and the ring's counted vmcnt waits stay exact.
 // Status: bit-identical to the pipeline kernels (test_gemm_interleaved_epilogue_matches_pipeline) but
 // SLOWER on the encoder's shapes (profiles/r02/gemm_ie_ab.txt: its BK-32 single-workgroup main loop loses
-// more than the overlap gains; only the N = 1024 / 1536 SiLU cases won) -- off by default (mode bit 9).
+// more than the overlap gains; only the N = 1024 / 1536 SiLU cases won) -- off by default (mode bit 11).
 constexpr int IE_BM = 192, IE_BK = 32, IE_NST = 3, IE_NWV = 8, IE_WN = 4;
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
@@ -1362,9 +1362,9 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
 }
 
 // the persistent interleaved-epilogue kernel takes K-major bf16 GEMMs whose epilogue needs no global
-// loads besides the bias (cfm_gemm_set_mode bit 9 enables it)
+// loads besides the bias (cfm_gemm_set_mode bit 11 enables it; bits 8-9 select grouped-wgrad A/B variants)
 bool ie_ok(const cfm_gemm_desc& d, const GemmP& p) {
-  return (g_gemm_mode & 512) && d.a_kmajor && d.b_kmajor && d.batch == 1 && p.split_k == 1 && !p.res &&
+  return (g_gemm_mode & 2048) && d.a_kmajor && d.b_kmajor && d.batch == 1 && p.split_k == 1 && !p.res &&
          !p.act_grad && !p.cmap && !p.rd_out && !p.acs_slab && !p.slab && p.vec_c && p.N % BN == 0 &&
          p.dtc == CFM_BF16 && (p.act == 0 || p.act == CFM_ACT_SILU) && (!p.pre || p.dtpre == CFM_BF16) &&
          (long)p.M * p.ldc * 2 < (1L << 31) && !p.dbg && p.alpha_a == nullptr && p.alpha_b == nullptr;
@@ -1382,7 +1382,7 @@ int num_cus() {
 
 int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   p.vec_c = vec_epilogue_ok(p);
-  p.dbg = ((g_gemm_mode & 8) ? 1 : 0) | ((g_gemm_mode & 256) ? 2 : 0);   // bit 8: generic dropout path (A/B)
+  p.dbg = ((g_gemm_mode & 8) ? 1 : 0) | ((g_gemm_mode & 1024) ? 2 : 0);   // bit 10: generic dropout path (A/B)
   if (cdiv(p.M, 128) > 65535 || (long)d.batch * p.split_k > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
   const long ea = d.a_kmajor ? (long)d.M * d.lda : (long)d.K * d.lda;
   const long eb = d.b_kmajor ? (long)d.N * d.ldb : (long)d.K * d.ldb;

@@ -376,7 +376,7 @@ def test_wgrad_group_matches_per_gemm():
 @pytest.mark.parametrize("M,N,K", [(1000, 512, 512), (11936 // 8, 2048, 512), (200, 256, 64), (385, 384, 2048)])
 @pytest.mark.parametrize("epi", ["bias", "silu_pre_drop", "plain_scaled"])
 def test_gemm_interleaved_epilogue_matches_pipeline(gemm_mode, M, N, K, epi):
-    """The persistent interleaved-epilogue kernel (cfm_gemm_set_mode bit 9) against the default LDS-DMA
+    """The persistent interleaved-epilogue kernel (cfm_gemm_set_mode bit 11) against the default LDS-DMA
     pipeline on the same inputs: identical K loops and epilogue arithmetic -> bit-identical outputs
     (ragged M, short K with the epilogue finished after the loop, several tiles per workgroup)."""
     g = torch.Generator().manual_seed(M + N + K)
@@ -384,7 +384,7 @@ def test_gemm_interleaved_epilogue_matches_pipeline(gemm_mode, M, N, K, epi):
     w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
     b = torch.randn(N, generator=g).to(DEV)
     outs = []
-    for mode in (3, 3 | 512):
+    for mode in (3, 3 | 2048):
         gemm_mode(mode)
         y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
