@@ -291,7 +291,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-optimizer", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--gemm-mode", type=int, default=None, help="cfm_gemm_set_mode value (A/B tuning)")
+    ap.add_argument("--gemm-mode", type=int, default=int(os.environ["CFM_GEMM_MODE"]) if "CFM_GEMM_MODE" in os.environ
+                    else None, help="cfm_gemm_set_mode value (A/B tuning; env CFM_GEMM_MODE)")
     ap.add_argument("--attn-mode", type=int, default=int(os.environ.get("CFM_ATTN_MODE", "0")),
                     help="cfm_attn_set_mode value (A/B tuning; env CFM_ATTN_MODE)")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no HIP graph)")

@@ -25,5 +25,5 @@ run wg_fetch FETCH_SIZE $BE
 run wg_write WRITE_SIZE $BE
 run wg_mfma "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" $BE
 python3 $R/benchmarks/pmc_to_json.py "$OUT" ffn "gemm_pipe_kernel" "gemm_ffn_up_pmc.json" "$GP"
-python3 $R/benchmarks/pmc_to_json.py "$OUT" wg "false, true, false>" "wgrad_group_pmc.json" "$BE"
+python3 $R/benchmarks/pmc_to_json.py "$OUT" wg "false, true, false, " "wgrad_group_pmc.json" "$BE"
 rm -f "$OUT"/*.csv

@@ -493,12 +493,14 @@ __device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2
 // rows).  Rows are staged through LDS in chunks of CHB bands (<= 128 rows), then every thread
 // finishes 8 consecutive columns of a row (16-B / 32-B vector stores).  The caller guarantees every
 // wave is done reading the staging LDS (`st`, >= 128 x EP_STRIDE floats).
-template <int FM, int FN, int WM, int WN, int NTt>
+template <int FM, int FN, int WM, int WN, int NTt, int BNt = BN>
 __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM][FN], float* st, int z, int zs,
                                                 int m0, int n0, int wm, int wn, int lane, int tid) {
   constexpr int BAND = FM * 32, CHB = (128 / BAND) >= 1 && WM % (128 / BAND) == 0 ? 128 / BAND : 1;
   constexpr int RC = CHB * BAND;
-  static_assert(WN * FN * 32 == BN, "tile width");
+  constexpr int EPS = BNt + 4;         // staging row stride (floats): = 4 mod 32 for both widths
+  constexpr int CPW = BNt / 8;         // 8-column chunks per row
+  static_assert(WN * FN * 32 == BNt, "tile width");
   if (p.split_k > 1 && !p.slab) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -523,15 +525,15 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
           for (int r = 0; r < 16; ++r) {
             const int row = (wm % CHB) * BAND + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
             const int col = wn * FN * 32 + j * 32 + (lane & 31);
-            st[row * EP_STRIDE + col] = acc[i][j][r];
+            st[row * EPS + col] = acc[i][j][r];
           }
     }
     __syncthreads();
 #pragma unroll 2
-    for (int it = 0; it < RC * 16 / NTt; ++it) {
-      const int row = it * (NTt / 16) + (tid >> 4), c8 = (tid & 15) * 8;
-      const float4 lo = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8);
-      const float4 hi = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8 + 4);
+    for (int it = 0; it < RC * CPW / NTt; ++it) {
+      const int row = it * (NTt / CPW) + tid / CPW, c8 = (tid % CPW) * 8;
+      const float4 lo = *reinterpret_cast<const float4*>(st + row * EPS + c8);
+      const float4 hi = *reinterpret_cast<const float4*>(st + row * EPS + c8 + 4);
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       const int m = m0 + RC * hf + row;
       epilogue_store8(p, z, zs, m, n0 + c8, v);
@@ -594,12 +596,12 @@ struct GatherA {
 };
 
 // BMt x 128 tile, BKt-deep K steps, NST-stage ring, NWV waves; the f32 epilogue staging aliases the ring
-template <int BMt, int BKt, int NST, int NWV>
+template <int BMt, int BKt, int NST, int NWV, int BNt = BN>
 struct PipeGeo {
   static constexpr int NTt = NWV * 64, NW = NWV;
-  static constexpr int ABYTES = BMt * BKt * 2, BBYTES = BN * BKt * 2;
+  static constexpr int ABYTES = BMt * BKt * 2, BBYTES = BNt * BKt * 2;
   static constexpr int STAGE = ABYTES + BBYTES;
-  static constexpr int RING = NST * STAGE, EPI = 128 * EP_STRIDE * 4;
+  static constexpr int RING = NST * STAGE, EPI = 128 * (BNt + 4) * 4;
   static constexpr int LDS = RING > EPI ? RING : EPI;
   static constexpr int AI = ABYTES / 1024 / NW, BI = BBYTES / 1024 / NW;   // DMA per wave per stage
   static_assert(AI * NW * 1024 == ABYTES && BI * NW * 1024 == BBYTES, "whole wave-instructions per stage");
@@ -669,7 +671,9 @@ __device__ __forceinline__ bf16x8 pipe_frag(const char* img, int row0, int kk, i
 // wait until at most `younger` stages (of PER DMA instructions each) are still in flight
 template <int PER>
 __device__ __forceinline__ void wait_stages(int younger) {
-  if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+  if (younger >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PER) : "memory");
+  else if (younger == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory");
+  else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
   else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -686,16 +690,16 @@ __device__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, 
 // 32 bytes k = 32h .. 32h+31 (chunks 2h, 2h+1).  Unit block scales; the per-tensor dequantisation
 // (alpha_a * alpha_b) is applied in the epilogue.
 template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2, bool GA = false,
-          bool GROUP = false, bool F8 = false>
+          bool GROUP = false, bool F8 = false, int BNt = BN>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(OCC * NWV / 4)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   static_assert(!F8 || (AK && BKM && !GA && !GROUP && BKt % 32 == 0), "fp8: K-major plain operands");
-  typedef PipeGeo<BMt, BKt, NST, NWV> G;
-  constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BN / WN / 32;
-  static_assert(WM * FM * 32 == BMt && WN * FN * 32 == BN, "wave tiling");
+  typedef PipeGeo<BMt, BKt, NST, NWV, BNt> G;
+  constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BNt / WN / 32;
+  static_assert(WM * FM * 32 == BMt && WN * FN * 32 == BNt, "wave tiling");
   probe_begin(p.probe);
   gemm_drop_prep(p);
-  static_assert(NST >= 3 && NST <= 4, "ring depth");
+  static_assert(NST >= 3 && NST <= 6, "ring depth");
   __shared__ __attribute__((aligned(1024))) char lds[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -709,7 +713,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   } else {
     xcd_tile3(tm, tn, zz);
   }
-  const int m0 = tm * BMt, n0 = tn * BN;
+  const int m0 = tm * BMt, n0 = tn * BNt;
   const int z = zz / p.split_k, ks = zz % p.split_k;
   const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, z), rb = pipe_rsrc(ob, z);
   const int kbeg = __builtin_amdgcn_readfirstlane(ks * p.k_per_split);
@@ -739,7 +743,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     for (int i = 0; i < G::AI; ++i) offa[i] = pipe_src<AK, BMt, BKt>(oa, (i * G::NW + wid) * 64 + lane, m0, kbeg);
   }
 #pragma unroll
-  for (int i = 0; i < G::BI; ++i) offb[i] = pipe_src<BKM, BN, BKt>(ob, (i * G::NW + wid) * 64 + lane, n0, kbeg);
+  for (int i = 0; i < G::BI; ++i) offb[i] = pipe_src<BKM, BNt, BKt>(ob, (i * G::NW + wid) * 64 + lane, n0, kbeg);
   const unsigned stepa = AK ? BKt * 2 : (unsigned)(BKt * oa.ld * 2);
   const unsigned stepb = BKM ? BKt * 2 : (unsigned)(BKt * ob.ld * 2);
 
@@ -829,7 +833,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
 #pragma unroll
     for (int q = 0; q < KST; ++q) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[q][j] = pipe_frag<BKM, BN, BKt>(sb, wn * FN * 32 + j * 32, 16 * q, lane);
+      for (int j = 0; j < FN; ++j) bfr[q][j] = pipe_frag<BKM, BNt, BKt>(sb, wn * FN * 32 + j * 32, 16 * q, lane);
 #pragma unroll
       for (int i = 0; i < FM; ++i) af[q][i] = pipe_frag<AK, BMt, BKt>(sa, wm * FM * 32 + i * 32, 16 * q, lane);
     }
@@ -882,7 +886,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     if (p.alpha_a) p.alpha *= p.alpha_a[0];
     if (p.alpha_b) p.alpha *= p.alpha_b[0];
   }
-  tile_epilogue_g<FM, FN, WM, WN, G::NTt>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane, tid);
+  tile_epilogue_g<FM, FN, WM, WN, G::NTt, BNt>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane, tid);
   probe_end(p.probe);
 }
 
@@ -1518,7 +1522,12 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
 }
 
 CFM_EXPORT size_t cfm_wgrad_group_task_bytes(void) { return sizeof(WgTask); }
-CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, BN); }
+// grouped weight-gradient launch (cfm_gemm_set_mode bits 8-9): 0 = 256 x 256 tiles, BK 32, 4-deep ring (half
+// the dY panel re-reads of 256 x 128; 17 layers 5.46 -> 4.89 ms, L15 step -0.8 ms same-box), 1 = 256 x 128 BK 32
+// two per CU, 2 = variant 0 in plain dispatch order, 3 = 256 x 128 BK 64 (round-2 default until then)
+int wg_variant() { return (g_gemm_mode >> 8) & 3; }
+int wg_bn() { return (wg_variant() == 1 || wg_variant() == 3) ? BN : 256; }
+CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, wg_bn()); }
 
 // fill task i of a HOST table: dW (N x K, fp32) = dYᵀ X over M tokens, dY (M x N) / X (M x K) bf16
 // row-major; db (N, fp32, may be NULL) = sum_rows dY; tile0 = first workgroup id of the task
@@ -1537,7 +1546,7 @@ CFM_EXPORT int cfm_wgrad_group_fill(void* host_tab, int i, const void* dy, const
   t.oa = PipeOp{(const bf16*)dy, N, 0, N, (unsigned)((long)M * N * 2)};
   t.ob = PipeOp{(const bf16*)x, K, 0, K, (unsigned)((long)M * K * 2)};
   t.tile0 = tile0;
-  t.tiles_n = cdiv(K, BN);
+  t.tiles_n = cdiv(K, wg_bn());
   reinterpret_cast<WgTask*>(host_tab)[i] = t;
   return CFM_OK;
 }
@@ -1550,9 +1559,12 @@ CFM_EXPORT int cfm_wgrad_group_probed(const void* dev_tab, int ntasks, long tota
   GatherA ga{};
   ga.group_tab = dev_tab;
   ga.group_n = ntasks;
-  const int gv = (g_gemm_mode >> 8) & 3;   // A/B: 1 = BK32 two per CU, 2 = plain dispatch order
+  const int gv = wg_variant();   // (tables filled with the same variant's wg_bn())
   ga.Jn = gv == 2;
-  if (gv == 1)
+  if (gv == 0 || gv == 2)   // 256 x 256 tiles (8 waves of 64 x 128), BK 32, 4-deep ring
+    hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 4, 1, false, false, 8, 2, false, true, false, 256>),
+                       dim3((unsigned)total_tiles), dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
+  else if (gv == 1)
     hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, false, false, 8, 2, false, true>), dim3((unsigned)total_tiles),
                        dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
   else

@@ -215,8 +215,9 @@ class WgradGroup:
             return
         import numpy as np
         dev = self.tasks[0][0].device
+        # (the tile width of the launch variant is part of the table: cfm_wgrad_group_tiles(256, 256) is 1 or 2)
         key = tuple((t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), t[0].shape[0],
-                     t[0].shape[1], t[1].shape[1]) for t in self.tasks)
+                     t[0].shape[1], t[1].shape[1]) for t in self.tasks) + (L.load().cfm_wgrad_group_tiles(256, 256),)
         hit = self._cache.get(key)
         if hit is None:
             lib = L.load()

@@ -7,7 +7,7 @@ arg = sys.argv[2] if len(sys.argv) > 2 else "1"
 if arg == "auto":
     # executed training steps = launches of the grouped weight-gradient kernel (one per step, eager warm-up,
     # timed replays and probe-graph replays alike)
-    steps = sum(float(r["Calls"]) for r in rows if "gemm_pipe_kernel" in r["Name"] and "false, true, false>" in r["Name"])
+    steps = sum(float(r["Calls"]) for r in rows if "gemm_pipe_kernel" in r["Name"] and "false, true, false, " in r["Name"])
 else:
     steps = float(arg)
 tot = sum(float(r["TotalDurationNs"]) for r in rows)

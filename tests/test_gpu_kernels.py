@@ -399,3 +399,25 @@ def test_gemm_interleaved_epilogue_matches_pipeline(gemm_mode, M, N, K, epi):
     assert torch.equal(outs[0][0], outs[1][0])
     if epi == "silu_pre_drop":
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_wgrad_group_wide_tiles_match_per_gemm(gemm_mode):
+    """The 256 x 256-tile grouped weight-gradient launch (default) against the 256 x 128 one
+    (cfm_gemm_set_mode bits 8-9 = 3) on the encoder's shapes, incl. the fused bias gradient and ragged N / K."""
+    g = torch.Generator().manual_seed(11)
+    M = 1000
+    shapes = [(2048, 512), (512, 2048), (1536, 512), (512, 512), (136, 264)]
+    ops_ = [(torch.randn(M, N, generator=g).to(DEV, torch.bfloat16), torch.randn(M, K, generator=g).to(DEV, torch.bfloat16))
+            for N, K in shapes]
+    outs = []
+    for mode in (3, 3 | 768):
+        gemm_mode(mode)
+        grp = ops.WgradGroup()
+        res = [grp.add(d, x) for d, x in ops_]
+        grp.flush()
+        torch.cuda.synchronize()
+        outs.append([(dw.clone(), db.clone()) for dw, db in res])
+    for (a, ab), (b, bb), (d, x) in zip(outs[0], outs[1], ops_):
+        ref = d.float().T @ x.float()
+        assert _rel(b, ref) < 1e-5 and _rel(a, ref) < 1e-5
+        assert _rel(bb, d.float().sum(0)) < 1e-5
