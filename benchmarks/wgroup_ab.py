@@ -13,7 +13,7 @@ for nl in (1, 17):
             for _ in range(nl) for (N, K) in layer]
     fl = sum(2.0 * M * d.shape[1] * x.shape[1] for d, x in ops_)
     grp = ops.WgradGroup()
-    for mode in (3, 3 | 256, 3 | 768, 3, 3 | 768):   # 0: 256x256 (default), 256: 256x128 BK32 x2, 768: 256x128 BK64
+    for mode in (3, 3 | 256, 3 | 768, 3, 3 | 768):   # bits 8-9: 0 256x256 (default), 1 256x128 BK32 x2, 3 256x128 BK64
         _lib.call("cfm_gemm_set_mode", mode)
         ts = []
         for it in range(6):

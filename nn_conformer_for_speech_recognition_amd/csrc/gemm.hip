@@ -1524,7 +1524,8 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
 CFM_EXPORT size_t cfm_wgrad_group_task_bytes(void) { return sizeof(WgTask); }
 // grouped weight-gradient launch (cfm_gemm_set_mode bits 8-9): 0 = 256 x 256 tiles, BK 32, 4-deep ring (half
 // the dY panel re-reads of 256 x 128; 17 layers 5.46 -> 4.89 ms, L15 step -0.8 ms same-box), 1 = 256 x 128 BK 32
-// two per CU, 2 = variant 0 in plain dispatch order, 3 = 256 x 128 BK 64 (round-2 default until then)
+// two per CU, 2 = variant 0 in plain dispatch order, 3 = 256 x 128 BK 64 (round-2 default until then; a
+// 256 x 256 BK 64 double-buffered form spilled and ran 2.4x slower)
 int wg_variant() { return (g_gemm_mode >> 8) & 3; }
 int wg_bn() { return (wg_variant() == 1 || wg_variant() == 3) ? BN : 256; }
 CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, wg_bn()); }
