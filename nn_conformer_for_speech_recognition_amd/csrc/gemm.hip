@@ -603,9 +603,24 @@ struct PipeGeo {
   static constexpr int STAGE = ABYTES + BBYTES;
   static constexpr int RING = NST * STAGE, EPI = 128 * (BNt + 4) * 4;
   static constexpr int LDS = RING > EPI ? RING : EPI;
-  static constexpr int AI = ABYTES / 1024 / NW, BI = BBYTES / 1024 / NW;   // DMA per wave per stage
-  static_assert(AI * NW * 1024 == ABYTES && BI * NW * 1024 == BBYTES, "whole wave-instructions per stage");
+  // 1-KiB DMA pieces per stage, spread over the waves: wave w issues pieces w, w + NW, ... (AI / BI rounds;
+  // when a count is not a multiple of NW the first waves issue one more piece, and their counted waits say so)
+  static constexpr int AP = ABYTES / 1024, BP = BBYTES / 1024;
+  static constexpr int AI = (AP + NW - 1) / NW, BI = (BP + NW - 1) / NW;
+  static_assert(AP * 1024 == ABYTES && BP * 1024 == BBYTES, "whole wave-instructions per stage");
+  static constexpr bool EVEN = AI * NW == AP && BI * NW == BP;
 };
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (switch over the immediates a ring can need)
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  switch (n) {
+#define W(k) case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(k) : "memory"); break;
+    W(0) W(1) W(2) W(3) W(4) W(5) W(6) W(7) W(8) W(9) W(10) W(11) W(12) W(13) W(14) W(15) W(16)
+    W(17) W(18) W(19) W(20) W(21) W(22) W(23) W(24)
+#undef W
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
 
 // the descriptor is wave-uniform by construction; readfirstlane makes that visible to the compiler even
 // when the operand comes from memory (grouped launches), so no waterfall loop wraps the buffer loads
@@ -697,6 +712,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   typedef PipeGeo<BMt, BKt, NST, NWV, BNt> G;
   constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BNt / WN / 32;
   static_assert(WM * FM * 32 == BMt && WN * FN * 32 == BNt, "wave tiling");
+  static_assert(G::EVEN || (!GA && !GROUP), "uneven DMA split: plain operands only");
   probe_begin(p.probe);
   gemm_drop_prep(p);
   static_assert(NST >= 3 && NST <= 6, "ring depth");
@@ -740,10 +756,15 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < G::AI; ++i) offa[i] = pipe_src<AK, BMt, BKt>(oa, (i * G::NW + wid) * 64 + lane, m0, kbeg);
+    for (int i = 0; i < G::AI; ++i)
+      offa[i] = pipe_src<AK, BMt, BKt>(oa, ((i * G::NW + wid) % G::AP) * 64 + lane, m0, kbeg);
   }
 #pragma unroll
-  for (int i = 0; i < G::BI; ++i) offb[i] = pipe_src<BKM, BNt, BKt>(ob, (i * G::NW + wid) * 64 + lane, n0, kbeg);
+  for (int i = 0; i < G::BI; ++i)
+    offb[i] = pipe_src<BKM, BNt, BKt>(ob, ((i * G::NW + wid) % G::BP) * 64 + lane, n0, kbeg);
+  // this wave's DMA pieces per stage (all waves alike unless the piece counts do not divide evenly)
+  const int per_w = G::EVEN ? G::AI + G::BI
+                            : (G::AP / G::NW + (wid < G::AP % G::NW)) + (G::BP / G::NW + (wid < G::BP % G::NW));
   const unsigned stepa = AK ? BKt * 2 : (unsigned)(BKt * oa.ld * 2);
   const unsigned stepb = BKM ? BKt * 2 : (unsigned)(BKt * ob.ld * 2);
 
@@ -763,11 +784,11 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     } else {
 #pragma unroll
       for (int i = 0; i < G::AI; ++i)
-        dma16(ra, sa + (i * G::NW + wid) * 1024, offa[i] + kt * stepa);
+        if (G::EVEN || i * G::NW + wid < G::AP) dma16(ra, sa + (i * G::NW + wid) * 1024, offa[i] + kt * stepa);
     }
 #pragma unroll
     for (int i = 0; i < G::BI; ++i)
-      dma16(rb, sb + (i * G::NW + wid) * 1024, offb[i] + kt * stepb);
+      if (G::EVEN || i * G::NW + wid < G::BP) dma16(rb, sb + (i * G::NW + wid) * 1024, offb[i] + kt * stepb);
   };
 
   f32x16 acc[FM][FN];
@@ -788,7 +809,8 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed once only the younger issued stages are outstanding
     const int younger = min(NST - 2, nk - 1 - kt);
-    wait_stages<G::AI + G::BI>(younger);
+    if constexpr (G::EVEN) wait_stages<G::AI + G::BI>(younger);
+    else wait_vm_rt(per_w * younger);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + NST - 1 < nk) issue(kt + NST - 1);   // refills the stage every wave finished reading at kt-1
@@ -1331,7 +1353,7 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 //          workgroups of 4 waves per CU) -- narrow outputs (N = 512) fill the chip
 template <bool AK, bool BKM>
 void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
-  const int sel = (g_gemm_mode >> 4) & 7;   // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S, 5 V192, 6 V192S
+  const int sel = (g_gemm_mode >> 4) & 7;   // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S, 5 V192, 6 V192S, 7 V192S8
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k), g128(cdiv(p.N, BN), cdiv(p.M, 128), batch * p.split_k);
   int v = sel;
   if constexpr (AK) {
@@ -1342,9 +1364,16 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
       hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob, GatherA{});
       return;
     }
-    if (v == 7) {   // V192 with a 4-deep ring (160 KiB: three K tiles in flight)
+    // auto: 1024- / 1536-wide outputs of short reductions (QKV, pointwise-conv-1 forward) take 192-row tiles
+    // two per CU: 504 / 756 tiles fill the 512 slots in whole rounds where 256-row tiles leave a sliver
+    // (A/B, profiles/r02/gemm_v192s8_ab.txt: QKV 41.1 -> 36.1 us, pw1 27.7 -> 24.8 us)
+    // (cfm_gemm_set_mode bit 12 turns this rule off for A/B)
+    if (v == 0 && p.N > 512 && p.N <= 1536 && p.k_per_split <= 512 && p.split_k == 1 && p.M >= 4096 &&
+        !(g_gemm_mode & 4096))
+      v = 7;
+    if (v == 7) {   // 192 x 128 tiles, 8 waves of 96 x 32, BK 32 (uneven A DMA split): two per CU
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
-      hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 4, 1, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob, GatherA{});
+      hipLaunchKernelGGL((gemm_pipe_kernel<192, 32, 3, 2, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob, GatherA{});
       return;
     }
     if (v == 6) {   // 192 x 128 tiles, 4 waves of 96x64, BK 32: two workgroups per CU

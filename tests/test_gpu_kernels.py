@@ -46,7 +46,7 @@ def gemm_mode():
     _lib.call("cfm_gemm_set_mode", 3)
 
 
-@pytest.mark.parametrize("mode", [1, 18, 34, 50, 82, 98])   # register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128 / 192x128 BK64, BK32 (AK only)
+@pytest.mark.parametrize("mode", [1, 18, 34, 50, 82, 98, 114])   # register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128 / 192x128 BK64, BK32 4 waves, BK32 8 waves (AK only)
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(1000, 512, 512), (264, 136, 192), (520, 264, 1000), (8, 8, 64)])
 def test_gemm_kernel_variants(gemm_mode, mode, ak, bk, M, N, K):
