@@ -92,7 +92,8 @@ __global__ __launch_bounds__(EB) void ada_colpart(const AdaP* __restrict__ t, in
 // row tasks of NARROW factored tensors: 64 rows per wave (lane = row)
 __global__ void ada_rows(const AdaP* __restrict__ t, int n, long ntasks, float b2t, float eps1) {
   const int lane = threadIdx.x & 63;
-  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform task made provably uniform: the parameter search and the table fields become scalar loads
+  const long task = (long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (task >= ntasks) return;
   const AdaP& q = t[find_param(t, n, task, 0)];
   const long lt = task - q.row_toff;
@@ -108,6 +109,7 @@ __global__ void ada_rows(const AdaP* __restrict__ t, int n, long ntasks, float b
   if (lr < (long)q.nb * q.R) {
     const float* g = q.g + lr * q.C;
     float s = 0.f;
+#pragma unroll 8     // independent loads in flight (a serial chain of load latencies otherwise)
     for (int c = 0; c < q.C; ++c) s += g[c] * g[c] + eps1;
     row_update(q, lr, s, b2t);
   }
@@ -119,16 +121,21 @@ __global__ void ada_cols(const AdaP* __restrict__ t, int n, long ncols, float b2
                          const float* __restrict__ part) {
   const long cidx = (long)blockIdx.x * EB + threadIdx.x;
   if (cidx >= ncols) return;
-  const AdaP& q = t[find_param(t, n, cidx, 1)];
+  // the block's first column's parameter by a uniform (scalar) search, then a short per-lane forward scan
+  int pi = find_param(t, n, (long)blockIdx.x * EB, 1);
+  while (pi + 1 < n && t[pi + 1].col_off <= cidx) ++pi;
+  const AdaP& q = t[pi];
   const long lc = cidx - q.col_off;     // = b*C + j
   const int b = (int)(lc / q.C), j = (int)(lc % q.C);
   float s = 0.f;
   if (is_wide(q.C)) {
     const int nrb = (q.R + RB - 1) / RB;
     const float* pp = part + q.part_off + (long)b * nrb * q.C + j;
+#pragma unroll 8     // (fixed order kept: the unrolled adds still run k = 0, 1, 2, ...)
     for (int k = 0; k < nrb; ++k) s += pp[(long)k * q.C];
   } else {
     const float* g = q.g + (long)b * q.R * q.C + j;
+#pragma unroll 8
     for (int r = 0; r < q.R; ++r) {
       const float v = g[(long)r * q.C];
       s += v * v + eps1;
@@ -140,13 +147,14 @@ __global__ void ada_cols(const AdaP* __restrict__ t, int n, long ncols, float b2
 // mean over R of the row state per (param, b): wide R -> one wave per b; narrow -> 64 b per wave
 __global__ void ada_rowmean(const AdaP* __restrict__ t, int n, long ntasks, float* __restrict__ rowmean) {
   const int lane = threadIdx.x & 63;
-  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long task = (long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (task >= ntasks) return;
   const AdaP& q = t[find_param(t, n, task, 3)];
   if (!q.factored) return;
   const long lt = task - q.rm_toff;
   if (q.R >= 64) {
     float s = 0.f;
+#pragma unroll 8
     for (int r = lane; r < q.R; r += 64) s += q.row[lt * q.R + r];
     s = wave_sum(s);
     if (lane == 0) rowmean[q.rm_off + lt] = s / q.R;
@@ -154,6 +162,7 @@ __global__ void ada_rowmean(const AdaP* __restrict__ t, int n, long ntasks, floa
     const long b = lt * 64 + lane;
     if (b < q.nb) {
       float s = 0.f;
+#pragma unroll 8
       for (int r = 0; r < q.R; ++r) s += q.row[b * q.R + r];
       rowmean[q.rm_off + b] = s / q.R;
     }
