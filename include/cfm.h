@@ -399,6 +399,21 @@ int cfm_ctc_greedy_decode(const float* logits, long sb, long st, const int32_t* 
                           int V, int blank, int pad, int collapse, int64_t* ids, int32_t* out,
                           int32_t* out_len, void* stream);
 
+/* BiLSTM decoder recurrence: replaces the cuDNN/MIOpen recurrence of the
+ * reference's nn.LSTM (asrnn.py:38 construct, :252 call on the 2-D encoder output = ONE unbatched
+ * sequence of L = B*T_enc steps).  Gate order i, f, g, o (torch).  One cooperative launch per pass;
+ * the input part x W_ih^T + b_ih + b_hh (gx) and the weight / input gradients are cfm_gemm calls.
+ *   gx (L, ndir*4H) fp32, whh (ndir, 4H, H) fp32, y (L, ndir*H) = torch's output layout,
+ *   gates (L, ndir*4H) post-activation, c (L, ndir*H) cell states (both saved for the backward),
+ *   dg (L, ndir*4H) pre-activation gate gradients.  H % 8 == 0, H <= 1024, ndir 1 or 2.
+ * ws: cfm_lstm_ws_bytes(L, ndir) of device scratch (step counters + error flags: after a pass,
+ * ws[2*ndir*L] (fwd) / ws[2*ndir*L+1] (bwd) != 0 means a step wait hit its 2-s limit). */
+size_t cfm_lstm_ws_bytes(int L, int ndir);
+int cfm_lstm_fwd(const float* gx, const float* whh, float* y, float* gates, float* c, int L, int H,
+                 int ndir, int* ws, void* stream);
+int cfm_lstm_bwd(const float* dy, const float* whh, const float* gates, const float* c, float* dg,
+                 int L, int H, int ndir, int* ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

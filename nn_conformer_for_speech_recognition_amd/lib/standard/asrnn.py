@@ -2,8 +2,8 @@
 
 Hot path on HIP kernels: SpecAugment (one fused kernel, host draws in
 the reference's order), ConvSubSampling (direct conv1 + implicit-GEMM conv2), the front-end
-projection, the Conformer layers, the projection block.  Outside the hot path and kept as
-torch modules (SURVEY.md §8f "next" rows): the BiLSTM decoder, final_fc, log_softmax.
+projection, the Conformer layers, the projection block, and the BiLSTM
+decoder's recurrence (lstm.LSTM, csrc/lstm.hip).  Kept as torch modules: final_fc, log_softmax.
 
 Front-end projection (hp.frontend_proj):
   'utterance'  the reference's whole-utterance Linear(out_size, d*max_len) (asrnn.py:28,207-209),
@@ -24,6 +24,7 @@ from ... import specaugment as _sa
 from ...conformer import Conformer
 from ...ctc import greedy_decode as _greedy_decode
 from ...frontend import linear as _linear, projection_block as _projection_block
+from ...lstm import LSTM
 from ..convsubsampling import ConvSubSampling
 
 _DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, torch.bfloat16: torch.bfloat16,
@@ -61,7 +62,7 @@ class ASRNN(nn.Module):
         self.projection_batch_norm = nn.BatchNorm1d(hp.projection_out_size)
         self.projection_fc_1 = nn.Linear(hp.projection_out_size, hp.projection_out_size)
         dec_layers = hp.standard_decoder_layers
-        self.lstm = nn.LSTM(hp.projection_out_size, hp.standard_decoder_nodes,
+        self.lstm = LSTM(hp.projection_out_size, hp.standard_decoder_nodes,
                             bidirectional=hp.standard_decoder_bidirectional, num_layers=dec_layers,
                             dropout=hp.dropout if dec_layers > 1 else 0.0)
         self.dropout = nn.Dropout(hp.dropout)
