@@ -406,13 +406,14 @@ int cfm_ctc_greedy_decode(const float* logits, long sb, long st, const int32_t* 
  *   gx (L, ndir*4H) fp32, whh (ndir, 4H, H) fp32, y (L, ndir*H) = torch's output layout,
  *   gates (L, ndir*4H) post-activation, c (L, ndir*H) cell states (both saved for the backward),
  *   dg (L, ndir*4H) pre-activation gate gradients.  H % 8 == 0, H <= 1024, ndir 1 or 2.
- * ws: cfm_lstm_ws_bytes(L, ndir) of device scratch (step counters + error flags: after a pass,
- * ws[2*ndir*L] (fwd) / ws[2*ndir*L+1] (bwd) != 0 means a step wait hit its 2-s limit). */
-size_t cfm_lstm_ws_bytes(int L, int ndir);
+ * ws: cfm_lstm_ws_bytes(H, ndir) of 16-B aligned device scratch (two error flags + the tagged-word
+ * exchange rings; one workspace serves a forward and its backward): after a pass, ((int*)ws)[0] (fwd) /
+ * ((int*)ws)[1] (bwd) != 0 means a step wait hit its 2-s limit. */
+size_t cfm_lstm_ws_bytes(int H, int ndir);
 int cfm_lstm_fwd(const float* gx, const float* whh, float* y, float* gates, float* c, int L, int H,
-                 int ndir, int* ws, void* stream);
+                 int ndir, void* ws, void* stream);
 int cfm_lstm_bwd(const float* dy, const float* whh, const float* gates, const float* c, float* dg,
-                 int L, int H, int ndir, int* ws, void* stream);
+                 int L, int H, int ndir, void* ws, void* stream);
 
 #ifdef __cplusplus
 }

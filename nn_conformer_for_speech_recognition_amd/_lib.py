@@ -151,7 +151,7 @@ _SIGS = {
                                  c_long, c_void_p]),
     "cfm_ctc_greedy_decode": (c_int, [c_void_p, c_long, c_long, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                       c_void_p, c_void_p, c_void_p, c_void_p]),
-    "cfm_lstm_ws_bytes": (c_size_t, [c_int, c_int]),
+    "cfm_lstm_ws_bytes": (c_size_t, [c_int, c_int]),   # (H, ndir)
     "cfm_lstm_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                              c_void_p]),
     "cfm_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,

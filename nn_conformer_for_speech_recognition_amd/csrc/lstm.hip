@@ -6,10 +6,12 @@
 // The recurrence is latency bound (L serial mat-vecs of 4H x H), so it runs as ONE cooperative launch per
 // pass: each workgroup owns 8 hidden units of one direction, keeps its 32 rows of W_hh (forward) or its 8
 // columns of W_hh (backward) in registers for the whole sequence, and the workgroups of a direction
-// exchange h_t (forward) / dgates_t (backward) through HBM with one agent-scope counter per step.  Both
+// exchange h_t (forward) / dgates_t (backward) through HBM as tagged 64-bit words (value + step tag, polled
+// directly: no counters or cache-maintenance fences on the per-step path).  Both
 // directions run concurrently in the same grid.  Co-residency is guaranteed by the cooperative launch
 // (it fails instead of over-subscribing); every wait is bounded by a wall-clock limit that raises a device
-// error flag and releases all other waiters, so a fault can never leave waves spinning.
+// error flag and releases all other waiters, so a fault can never leave waves spinning.  The outputs y /
+// gates / c / dg are plain stores: they are read only by later launches.
 #include "cfm_common.h"
 
 namespace {
@@ -27,33 +29,39 @@ __device__ __forceinline__ float tanh_f(float x) {
   return copysignf(r, x);
 }
 
-__device__ __forceinline__ float ld_coherent(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Exchange words: (tag << 32) | float bits, written with one 64-bit agent-scope store, so a reader
+// polls the data itself -- no counters, no L2 write-back / invalidate fences on the per-step path.
+__device__ __forceinline__ void put_word(unsigned long long* p, unsigned tag, float v) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// thread 0 only: wait until *cnt reaches `want` (or the error flag is raised / the limit expires)
-__device__ __forceinline__ void wait_count(const int* cnt, int want, int* err) {
-  const long long t0 = wall_clock64();
-  while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) {
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-    if (wall_clock64() - t0 > kSpinTicks) {
-      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
+// wait until word p carries `tag`; bounded by the wall-clock limit (then raises *err and returns 0)
+__device__ __forceinline__ float get_word(const unsigned long long* p, unsigned tag, int* err) {
+  unsigned long long w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((unsigned)(w >> 32) != tag) {
+    const long long t0 = wall_clock64();
+    for (;;) {
+      __builtin_amdgcn_s_sleep(1);
+      w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((unsigned)(w >> 32) == tag) break;
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return 0.f;
+      if (wall_clock64() - t0 > kSpinTicks) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0.f;
+      }
     }
-    __builtin_amdgcn_s_sleep(1);
   }
+  return __uint_as_float((unsigned)w);
 }
 
-__device__ __forceinline__ void signal_count(int* cnt) {
-  __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// gx: (L, ndir*4H) input gates incl. both biases; whh: (ndir, 4H, H); y: (L, ndir*H) outputs, also the h
-// exchange buffer; gates_out: (L, ndir*4H) post-activation i,f,g,o; c_out: (L, ndir*H); cnt: ndir*L zeros.
+// gx: (L, ndir*4H) input gates incl. both biases; whh: (ndir, 4H, H); y: (L, ndir*H) outputs; gates_out:
+// (L, ndir*4H) post-activation i,f,g,o; c_out: (L, ndir*H); xch: (ndir, 2, H) zeroed tagged words (a ring of
+// two steps: a workgroup writes step s+2 only after every workgroup has read step s).  Step s carries tag s+1.
 __global__ __launch_bounds__(kThreads) void lstm_fwd_rec(const float* __restrict__ gx, const float* __restrict__ whh,
-                                                        float* y, float* __restrict__ gates_out,
-                                                        float* __restrict__ c_out, int* cnt, int* err, int L, int H,
-                                                        int nwg, int ndir) {
+                                                        float* __restrict__ y, float* __restrict__ gates_out,
+                                                        float* __restrict__ c_out, unsigned long long* xch, int* err,
+                                                        int L, int H, int nwg, int ndir) {
   __shared__ float hl[kMaxH];
   __shared__ float gl[4 * kUnits];
   const int tid = threadIdx.x;
@@ -68,17 +76,14 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_rec(const float* __restrict
 #pragma unroll
   for (int j = 0; j < kMaxK; ++j) w[j] = j < kpt ? wr[q + 8 * j] : 0.f;
   float c = 0.f;
-  int* cn = cnt + (long)dir * L;
+  unsigned long long* xd = xch + (long)dir * 2 * H;
   for (int s = 0; s < L; ++s) {
     const int t = dir ? L - 1 - s : s;
     const float gxv = q == 0 ? gx[t * ldg + (long)dir * 4 * H + grow] : 0.f;
     float acc = 0.f;
     if (s > 0) {
-      if (tid == 0) wait_count(cn + s - 1, nwg, err);
-      __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const int tp = dir ? t + 1 : t - 1;
-      for (int k = tid; k < H; k += kThreads) hl[k] = ld_coherent(y + tp * ldy + (long)dir * H + k);
+      const unsigned long long* src = xd + (long)((s - 1) & 1) * H;
+      for (int k = tid; k < H; k += kThreads) hl[k] = get_word(src + k, (unsigned)s, err);
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < kMaxK; ++j)
@@ -94,28 +99,26 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_rec(const float* __restrict
       const float gg = tanh_f(gl[2 * kUnits + tid]), og = sigm(gl[3 * kUnits + tid]);
       c = fg * c + ig * gg;
       const float h = og * tanh_f(c);
+      put_word(xd + (long)(s & 1) * H + u0 + tid, (unsigned)(s + 1), h);
       const long gb = t * ldg + (long)dir * 4 * H + u0 + tid;
       gates_out[gb] = ig;
       gates_out[gb + H] = fg;
       gates_out[gb + 2 * H] = gg;
       gates_out[gb + 3 * H] = og;
       c_out[t * ldy + (long)dir * H + u0 + tid] = c;
-      __hip_atomic_store(y + t * ldy + (long)dir * H + u0 + tid, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      y[t * ldy + (long)dir * H + u0 + tid] = h;
     }
-    __syncthreads();
-    if (tid == 0) signal_count(cn + s);
   }
 }
 
 // Backward through time.  dy: (L, ndir*H) gradient of y; gates/c: the forward's saved values; dg: (L, ndir*4H)
-// pre-activation gate gradients (output, and the exchange buffer); cnt: ndir*L zeros.
+// pre-activation gate gradients; xch: (ndir, 2, 4H) zeroed tagged words; step s (descending) carries tag L-s.
 //   dh_t = dy_t + dgates_{t+1} W_hh,  dc_t = dh_t o (1 - tanh^2 c_t) + dc_{t+1} f_{t+1}
 //   di = dc g i(1-i), df = dc c_{t-1} f(1-f), dg = dc i (1-g^2), do = dh tanh(c_t) o(1-o)
 __global__ __launch_bounds__(kThreads) void lstm_bwd_rec(const float* __restrict__ dy, const float* __restrict__ whh,
                                                         const float* __restrict__ gates, const float* __restrict__ cst,
-                                                        float* dg, int* cnt, int* err, int L, int H, int nwg,
-                                                        int ndir) {
+                                                        float* __restrict__ dg, unsigned long long* xch, int* err,
+                                                        int L, int H, int nwg, int ndir) {
   __shared__ float dl[4 * kMaxH];
   const int tid = threadIdx.x;
   const int dir = blockIdx.x / nwg;
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_rec(const float* __restrict
 #pragma unroll
   for (int j = 0; j < kMaxK; ++j) w[j] = j < kpt ? wc[(long)(p + 32 * j) * H] : 0.f;
   float dc_carry = 0.f;
-  int* cn = cnt + (long)dir * L;
+  unsigned long long* xd = xch + (long)dir * 2 * H4;
   const long col = (long)dir * H + u0 + u;
   const long gcol = (long)dir * H4 + u0 + u;
   for (int s = L - 1; s >= 0; --s) {
@@ -146,11 +149,8 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_rec(const float* __restrict
     }
     float acc = 0.f;
     if (s < L - 1) {
-      if (tid == 0) wait_count(cn + s + 1, nwg, err);
-      __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const int tn = dir ? t - 1 : t + 1;
-      for (int k = tid; k < H4; k += kThreads) dl[k] = ld_coherent(dg + tn * ldg + (long)dir * H4 + k);
+      const unsigned long long* src = xd + (long)((s + 1) & 1) * H4;
+      for (int k = tid; k < H4; k += kThreads) dl[k] = get_word(src + k, (unsigned)(L - s - 1), err);
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < kMaxK; ++j)
@@ -170,15 +170,20 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_rec(const float* __restrict
       const float d_f = dc * cp * fg * (1.f - fg);
       const float d_g = dc * ig * (1.f - gg * gg);
       dc_carry = dc * fg;
-      float* o = dg + t * ldg + gcol;
-      __hip_atomic_store(o, d_i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o + H, d_f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o + 2 * H, d_g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o + 3 * H, d_o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned tag = (unsigned)(L - s);
+      unsigned long long* o = xd + (long)(s & 1) * H4 + u0 + u;
+      put_word(o, tag, d_i);
+      put_word(o + H, tag, d_f);
+      put_word(o + 2 * H, tag, d_g);
+      put_word(o + 3 * H, tag, d_o);
+      float* og_ = dg + t * ldg + gcol;
+      og_[0] = d_i;
+      og_[H] = d_f;
+      og_[2 * H] = d_g;
+      og_[3 * H] = d_o;
     }
+    // dl is rewritten by the next step's poll only after every thread passed this barrier
     __syncthreads();
-    if (tid == 0) signal_count(cn + s);
   }
 }
 
@@ -190,40 +195,44 @@ int launch_coop(const void* fn, int grid, void** args, hipStream_t s, const char
 
 }  // namespace
 
-CFM_EXPORT size_t cfm_lstm_ws_bytes(int L, int ndir) { return (size_t)(2L * ndir * L + 64) * sizeof(int); }
+// ws layout: [2 error flags, padded to 16 B][fwd ring (ndir, 2, H) u64][bwd ring (ndir, 2, 4H) u64]
+CFM_EXPORT size_t cfm_lstm_ws_bytes(int H, int ndir) { return 16 + (size_t)ndir * 2 * 5 * H * 8; }
 
 // Forward recurrence of one LSTM layer over one unbatched sequence (nn.LSTM on a 2-D input).
 CFM_EXPORT int cfm_lstm_fwd(const float* gx, const float* whh, float* y, float* gates, float* c, int L, int H,
-                            int ndir, int* ws, void* stream) {
+                            int ndir, void* ws, void* stream) {
   CFM_REQUIRE(gx && whh && y && gates && c && ws, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(L > 0 && (ndir == 1 || ndir == 2), CFM_ERR_ARG, "L > 0, ndir 1 or 2");
   CFM_REQUIRE(H >= kUnits && H % kUnits == 0 && H <= kMaxH, CFM_ERR_SHAPE, "hidden size: multiple of 8, <= 1024");
+  CFM_REQUIRE(((uintptr_t)ws & 15) == 0, CFM_ERR_ALIGN, "ws 16-B aligned");
   hipStream_t s = cfm::as_stream(stream);
-  int* cnt = ws;
-  int* err = ws + 2L * ndir * L;
-  if (hipMemsetAsync(ws, 0, cfm_lstm_ws_bytes(L, ndir), s) != hipSuccess)
+  int* err = (int*)ws;
+  unsigned long long* xch = (unsigned long long*)((char*)ws + 16);
+  if (hipMemsetAsync(err, 0, sizeof(int), s) != hipSuccess ||
+      hipMemsetAsync(xch, 0, (size_t)ndir * 2 * H * 8, s) != hipSuccess)
     return cfm::fail(CFM_ERR_LAUNCH, "cfm_lstm_fwd: memset");
   int nwg = H / kUnits;
-  void* args[] = {(void*)&gx, (void*)&whh, (void*)&y, (void*)&gates, (void*)&c, (void*)&cnt, (void*)&err,
+  void* args[] = {(void*)&gx, (void*)&whh, (void*)&y, (void*)&gates, (void*)&c, (void*)&xch, (void*)&err,
                   (void*)&L, (void*)&H, (void*)&nwg, (void*)&ndir};
   return launch_coop((const void*)lstm_fwd_rec, nwg * ndir, args, s, "cfm_lstm_fwd");
 }
 
-// Backward recurrence: dg (L, ndir*4H) <- pre-activation gate gradients.  ws: the same layout as the forward
-// (its second counter half is used, so one workspace serves a forward and its backward).
+// Backward recurrence: dg (L, ndir*4H) <- pre-activation gate gradients.  ws: the forward's workspace layout
+// (its backward ring and second flag are used, so one workspace serves a forward and its backward).
 CFM_EXPORT int cfm_lstm_bwd(const float* dy, const float* whh, const float* gates, const float* c, float* dg, int L,
-                            int H, int ndir, int* ws, void* stream) {
+                            int H, int ndir, void* ws, void* stream) {
   CFM_REQUIRE(dy && whh && gates && c && dg && ws, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(L > 0 && (ndir == 1 || ndir == 2), CFM_ERR_ARG, "L > 0, ndir 1 or 2");
   CFM_REQUIRE(H >= kUnits && H % kUnits == 0 && H <= kMaxH, CFM_ERR_SHAPE, "hidden size: multiple of 8, <= 1024");
+  CFM_REQUIRE(((uintptr_t)ws & 15) == 0, CFM_ERR_ALIGN, "ws 16-B aligned");
   hipStream_t s = cfm::as_stream(stream);
-  int* cnt = ws + (long)ndir * L;
-  int* err = ws + 2L * ndir * L + 1;
-  if (hipMemsetAsync(cnt, 0, (size_t)ndir * L * sizeof(int), s) != hipSuccess ||
-      hipMemsetAsync(err, 0, sizeof(int), s) != hipSuccess)
+  int* err = (int*)ws + 1;
+  unsigned long long* xch = (unsigned long long*)((char*)ws + 16) + (long)ndir * 2 * H;
+  if (hipMemsetAsync(err, 0, sizeof(int), s) != hipSuccess ||
+      hipMemsetAsync(xch, 0, (size_t)ndir * 2 * 4 * H * 8, s) != hipSuccess)
     return cfm::fail(CFM_ERR_LAUNCH, "cfm_lstm_bwd: memset");
   int nwg = H / kUnits;
-  void* args[] = {(void*)&dy, (void*)&whh, (void*)&gates, (void*)&c, (void*)&dg, (void*)&cnt, (void*)&err,
+  void* args[] = {(void*)&dy, (void*)&whh, (void*)&gates, (void*)&c, (void*)&dg, (void*)&xch, (void*)&err,
                   (void*)&L, (void*)&H, (void*)&nwg, (void*)&ndir};
   return launch_coop((const void*)lstm_bwd_rec, nwg * ndir, args, s, "cfm_lstm_bwd");
 }

@@ -9,7 +9,7 @@ weight_hh_l0, bias_ih_l0, bias_hh_l0 and the `_reverse` set) so checkpoints load
 
 Per layer: gx = x W_ih^T + b_ih + b_hh for both directions in one fp32 cfm_gemm; the recurrence in one
 cooperative launch (cfm_lstm_fwd, csrc/lstm.hip: W_hh held in registers across the whole sequence,
-h_t exchanged through HBM with one counter per step, both directions concurrently).  Backward: the
+h_t exchanged through HBM as tagged 64-bit words polled directly, both directions concurrently).  Backward: the
 reverse-time recurrence (cfm_lstm_bwd) produces the pre-activation gate gradients dG (L, ndir*4H); dx,
 dW_ih, dW_hh (time-shifted views of dG and y, no copies) and the bias gradient are cfm_gemm / cfm_colsum.
 Everything computes in fp32, like the reference.
@@ -54,10 +54,10 @@ class _LSTMLayer(torch.autograd.Function):
         y = torch.empty(Lseq, ndir * H, device=dev, dtype=torch.float32)
         gates = torch.empty(Lseq, ndir * 4 * H, device=dev, dtype=torch.float32)
         c = torch.empty(Lseq, ndir * H, device=dev, dtype=torch.float32)
-        ws = torch.empty(L.size_call("cfm_lstm_ws_bytes", Lseq, ndir) // 4, device=dev, dtype=torch.int32)
+        ws = torch.empty(L.size_call("cfm_lstm_ws_bytes", H, ndir) // 4, device=dev, dtype=torch.int32)
         L.call("cfm_lstm_fwd", L.ptr(gx), L.ptr(w_hh), L.ptr(y), L.ptr(gates), L.ptr(c), Lseq, H, ndir, L.ptr(ws),
                L.stream())
-        _check_flag(ws, 2 * ndir * Lseq, "cfm_lstm_fwd")
+        _check_flag(ws, 0, "cfm_lstm_fwd")
         ctx.save_for_backward(x, w_ih, w_hh, y, gates, c)
         ctx.H, ctx.ndir, ctx.ws = H, ndir, ws
         ctx.mark_non_differentiable(c)
@@ -73,7 +73,7 @@ class _LSTMLayer(torch.autograd.Function):
         dg = torch.empty(Lseq, ndir * H4, device=x.device, dtype=torch.float32)
         L.call("cfm_lstm_bwd", L.ptr(dy), L.ptr(w_hh), L.ptr(gates), L.ptr(c), L.ptr(dg), Lseq, H, ndir, L.ptr(ws),
                L.stream())
-        _check_flag(ws, 2 * ndir * Lseq + 1, "cfm_lstm_bwd")
+        _check_flag(ws, 1, "cfm_lstm_bwd")
         dx = ops.linear_dgrad(dg, w_ih) if ctx.needs_input_grad[0] else None
         dw_ih = ops.linear_wgrad(dg, x)
         db = ops.colsum(dg)
