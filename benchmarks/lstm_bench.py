@@ -25,6 +25,7 @@ def timeit(fn, n):
 
 def main():
     dev = "cuda"
+    only = sys.argv[1] if len(sys.argv) > 1 else None          # "libcfm": skip the MIOpen leg (profiling)
     for L in (1280, 11936):
         torch.manual_seed(0)
         ref = torch.nn.LSTM(256, 512, bidirectional=True).to(dev)
@@ -34,6 +35,8 @@ def main():
         dy = torch.randn(L, 1024, device=dev)
         n = 5 if L < 5000 else 2
         for name, m in (("libcfm", mine), ("torch_miopen", ref)):
+            if only and name != only:
+                continue
             def fwd():
                 with torch.no_grad():
                     m(x)

@@ -85,9 +85,11 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_rec(const float* __restrict
       const unsigned long long* src = xd + (long)((s - 1) & 1) * H;
       for (int k = tid; k < H; k += kThreads) hl[k] = get_word(src + k, (unsigned)s, err);
       __syncthreads();
+      float a4[4] = {0.f, 0.f, 0.f, 0.f};   // four independent FMA chains
 #pragma unroll
       for (int j = 0; j < kMaxK; ++j)
-        if (j < kpt) acc = fmaf(w[j], hl[q + 8 * j], acc);
+        if (j < kpt) a4[j & 3] = fmaf(w[j], hl[q + 8 * j], a4[j & 3]);
+      acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
       acc += __shfl_xor(acc, 1);
       acc += __shfl_xor(acc, 2);
       acc += __shfl_xor(acc, 4);
@@ -152,9 +154,11 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_rec(const float* __restrict
       const unsigned long long* src = xd + (long)((s + 1) & 1) * H4;
       for (int k = tid; k < H4; k += kThreads) dl[k] = get_word(src + k, (unsigned)(L - s - 1), err);
       __syncthreads();
+      float a4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < kMaxK; ++j)
-        if (j < kpt) acc = fmaf(w[j], dl[p + 32 * j], acc);
+        if (j < kpt) a4[j & 3] = fmaf(w[j], dl[p + 32 * j], a4[j & 3]);
+      acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
       acc += __shfl_xor(acc, 1);
       acc += __shfl_xor(acc, 2);
       acc += __shfl_xor(acc, 4);
