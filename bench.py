@@ -281,6 +281,167 @@ def cpu_baseline_s10(threads, steps=2):
                       f"front-end + frame projection + 16 layers, mean of {steps} after 1 warm-up"}
 
 
+class Harness:
+    """One training configuration of the bench, reusable by tests (tests/test_gpu_bench_harness.py) and the
+    NaN hunt (benchmarks/nan_hunt.py): model + synthetic batch + GradAllReducer + Adafactor, the step as
+    fwd_bwd() (captured into a HIP graph unless eager) + post() (all-reduce + optimizer, eager).
+
+    Every step also adds (loss is not finite) to a device counter (`bad`, read once at the end, no host
+    sync per step): the bench reports it as `nonfinite_steps` and exits non-zero when it is not 0."""
+
+    def __init__(self, cfg, dev, rank=0, world=1, *, dropout=0.1, fp8=False, specaug=False, dp_overlap=False,
+                 eager=False, no_optimizer=False, probe_inline=False, lr=2e-5, seed=1234):
+        self.cfg = cfg
+        name, L, d, H, ffn, K, B, secs, pos_enc = cfg
+        self.dev, self.rank, self.world = dev, rank, world
+        self.eager = bool(eager or dp_overlap)
+        self.no_optimizer, self.probe_inline = no_optimizer, probe_inline
+        self.T_in, self.Fb, self.V = 100 * secs + 1, 80, 1024
+        self.B, self.L, self.d, self.ffn = B, L, d, ffn
+        self.cd = torch.bfloat16
+        torch.manual_seed(seed)                      # identical init on every rank (then broadcast)
+        self.model = EncoderCTC(L, d, H, ffn, K, self.V, self.Fb, self.T_in, dropout, self.cd, pos_enc,
+                                fp8).to(dev).train()
+        cdist.broadcast_parameters(self.model)
+        self.params = [p for p in self.model.parameters() if p.requires_grad]
+        # DP: the Conformer's grouped weight gradients are written straight into flat all-reduce buckets; with
+        # dp_overlap (eager) each chunk's bucket is reduced while the lower layers' backward still runs
+        self.reducer = cdist.GradAllReducer(self.params, model=self.model, overlap=bool(dp_overlap))
+        self.opt = Adafactor(self.params, lr=lr, beta1=0.9, scale_parameter=False, relative_step=False)
+        # synthetic data (SURVEY.md §8d): per-utterance min-max-normalised uniform mels, full lengths
+        g = torch.Generator(device="cpu").manual_seed(seed + rank)
+        x = torch.rand(B, self.Fb, self.T_in, generator=g)
+        x = (x - x.amin((1, 2), keepdim=True)) / (x.amax((1, 2), keepdim=True) - x.amin((1, 2), keepdim=True))
+        self.x = x.to(dev)
+        self.T2 = T2 = self.model.T2
+        self.lens_i32 = torch.full((B,), T2, dtype=torch.int32, device=dev)
+        U = T2 // 4
+        targets = torch.randint(1, self.V, (B, U), generator=g).to(dev)
+        self.rng = torch.zeros(1, dtype=torch.int64, device=dev)     # device dropout step counter
+        _lib.call("cfm_rng_bind", _lib.ptr(self.rng))
+        self.tgt_i32 = targets.to(torch.int32).contiguous()
+        self.tlen_i32 = torch.full((B,), U, dtype=torch.int32, device=dev)
+        self.seed0 = 17 * rank + 1
+        self.bad = torch.zeros(1, dtype=torch.int32, device=dev)     # steps whose loss was not finite
+        self.steps_run = 0
+        # SpecAugment (configs[2]): the global batch's draws on the host in the reference's order
+        # (specaugment.draw, python random seeded as speechcommands.py:18), this rank's slice packed into
+        # a STATIC device block that the captured step reads; refreshed before every step
+        self.sa_params = None
+        if specaug:
+            import random as _random
+            self._sa_rng = _random.Random(42)
+            self._sa_hp = HParams(None)
+            self._tau_glob = [self.T_in] * (B * world)
+            self.sa_params = self.specaug_refresh()
+        self.graph = self.probe_graph = None
+        self.static_loss = None
+        self.host_t = []
+
+    def specaug_refresh(self):
+        B = self.B
+        dr = specaugment.draw(B * self.world, self.Fb, self._tau_glob, self._sa_hp, self._sa_rng)
+        blk = specaugment.pack(dr, self._tau_glob, self.rank * B, (self.rank + 1) * B)
+        if self.sa_params is None:
+            return blk.to(self.dev)
+        self.sa_params.copy_(blk.pin_memory(), non_blocking=True)
+        return self.sa_params
+
+    def fwd_bwd(self):
+        self.rng.add_(1)
+        loss, _ = self.model(self.x, self.lens_i32, self.tgt_i32, self.tlen_i32, seed=self.seed0,
+                             specaug_params=self.sa_params)
+        loss.backward()
+        self.bad.add_((~torch.isfinite(loss.detach())).to(torch.int32))
+        return loss
+
+    def post(self):
+        self.reducer.allreduce()
+        if not self.no_optimizer:
+            self.opt.step()
+
+    def setup(self, warmup, probes=()):
+        """Eager: `warmup` steps.  Graph: warm up on a side stream (allocator + autotuned state settle), then
+        capture ONE training step's forward + backward into a HIP graph (all-reduce + optimizer stay eager:
+        few launches).  probes: KernelProbe objects -- a second capture of the same step carries their slot
+        kernels and is replayed only after the timed region (probe_replays)."""
+        opt = self.opt
+        if self.eager:
+            for _ in range(warmup):
+                self.step()
+            torch.cuda.synchronize()
+            return
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(warmup, 1)):
+                opt.zero_grad(set_to_none=True)
+                self.fwd_bwd()
+                self.post()
+                self.steps_run += 1
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        opt.zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        if self.probe_inline:                 # legacy: probes inside the timed graph
+            for p in probes:
+                p.active = True
+        with torch.cuda.graph(self.graph):
+            self.static_loss = self.fwd_bwd()
+        for p in probes:
+            p.active = False
+        grads_timed = [p.grad for p in self.params]
+        if probes and not self.probe_inline:
+            # a second capture of the same step carries the probe's slot kernels (68 one-lane launches per
+            # step); it is replayed after the timed region, so the probes never sit inside `value`'s clock
+            opt.zero_grad(set_to_none=True)
+            self.probe_graph = torch.cuda.CUDAGraph()
+            for p in probes:
+                p.active = True
+            with torch.cuda.graph(self.probe_graph):
+                self.fwd_bwd()
+            for p in probes:
+                p.active = False
+            for p, g in zip(self.params, grads_timed):
+                p.grad = g           # the timed replays' optimizer steps read the timed graph's grads
+        self.step()                  # one replay outside the timed region
+        torch.cuda.synchronize()
+
+    def step(self):
+        if self.graph is None:
+            self.opt.zero_grad(set_to_none=True)
+            if self.sa_params is not None:
+                self.specaug_refresh()
+            loss = self.fwd_bwd()
+            self.post()
+            self.static_loss = loss
+        else:
+            t_a = time.perf_counter()
+            if self.sa_params is not None:
+                self.specaug_refresh()
+            self.graph.replay()
+            t_b = time.perf_counter()
+            self.post()
+            self.host_t.append((t_b - t_a, time.perf_counter() - t_b))
+        self.steps_run += 1
+        return self.static_loss
+
+    def probe_replays(self, n):
+        if self.probe_graph is not None:
+            for _ in range(n):
+                self.probe_graph.replay()
+
+    def nonfinite_steps(self):
+        return int(self.bad.item())
+
+    def params_finite(self):
+        """All parameters finite (one pass over the weights; after the timed region)."""
+        ok = torch.ones(1, dtype=torch.bool, device=self.dev)
+        for p in self.params:
+            ok &= torch.isfinite(p.detach()).all()
+        return bool(ok.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -299,6 +460,7 @@ def main():
     ap.add_argument("--specaug", action="store_true",
                     help="SpecAugment inside the step (host draws in the reference order, one warp+mask kernel)")
     ap.add_argument("--pos-enc", choices=("none", "rel"), default=None, help="override the config's pos encoding")
+    ap.add_argument("--layers", type=int, default=None, help="override the config's layer count (debug runs)")
     ap.add_argument("--nst", action="store_true", help="configs[3]: the NST pseudo-label pass (eval fwd + decode)")
     ap.add_argument("--fp8", action="store_true",
                     help="configs[4]: forward FFN / QKV / out-projection GEMMs on fp8 e4m3 MFMA (backward bf16)")
@@ -306,9 +468,12 @@ def main():
                     help="N>1: eager backward with bucket all-reduces overlapped (default: graph + reduce after)")
     ap.add_argument("--probe-inline", action="store_true",
                     help="put the roofline probe kernels inside the timed graph (default: a separate probed graph)")
+    ap.add_argument("--poison", action="store_true",
+                    help="debug: NaN-fill every torch.empty (deterministic algorithms + fill_uninitialized_memory)")
     args = ap.parse_args()
-    if args.dp_overlap:
-        args.eager = True
+    if args.poison:
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        torch.utils.deterministic.fill_uninitialized_memory = True
     if args.gemm_mode is not None:
         _lib.call("cfm_gemm_set_mode", args.gemm_mode)
     if args.attn_mode:
@@ -320,70 +485,26 @@ def main():
     cfg = CONFIGS[args.config]
     if args.pos_enc is not None:
         cfg = cfg[:8] + (args.pos_enc,)
+    if args.layers is not None:
+        cfg = cfg[:1] + (args.layers,) + cfg[2:]
     name, L, d, H, ffn, K, B, secs, pos_enc = cfg
-    T_in, Fb, V = 100 * secs + 1, 80, 1024
-    cd = torch.bfloat16
 
-    torch.manual_seed(1234)                      # identical init on every rank (then broadcast)
-    model = EncoderCTC(L, d, H, ffn, K, V, Fb, T_in, args.dropout, cd, pos_enc, args.fp8).to(dev).train()
-    cdist.broadcast_parameters(model)
     if args.nst:
+        torch.manual_seed(1234)
+        T_in, Fb = 100 * secs + 1, 80
+        model = EncoderCTC(L, d, H, ffn, K, 1024, Fb, T_in, args.dropout, torch.bfloat16, pos_enc,
+                           args.fp8).to(dev).train()
+        cdist.broadcast_parameters(model)
         gx = torch.Generator(device="cpu").manual_seed(1234 + rank)
         xs = torch.rand(B, Fb, T_in, generator=gx)
         xs = (xs - xs.amin((1, 2), keepdim=True)) / (xs.amax((1, 2), keepdim=True) - xs.amin((1, 2), keepdim=True))
         return run_nst(args, model, xs.to(dev), torch.full((B,), model.T2, dtype=torch.int32, device=dev), dev, cfg,
                        rank, world)
-    params = [p for p in model.parameters() if p.requires_grad]
-    # DP: the Conformer's grouped weight gradients are written straight into flat all-reduce buckets; with
-    # --dp-overlap (eager) each chunk's bucket is reduced while the lower layers' backward still runs
-    reducer = cdist.GradAllReducer(params, model=model, overlap=bool(args.dp_overlap))
-    opt = Adafactor(params, lr=2e-5, beta1=0.9, scale_parameter=False, relative_step=False)
 
-    # synthetic data: per-utterance min-max-normalised uniform mels, full lengths
-    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
-    x = torch.rand(B, Fb, T_in, generator=g)
-    x = (x - x.amin((1, 2), keepdim=True)) / (x.amax((1, 2), keepdim=True) - x.amin((1, 2), keepdim=True))
-    x = x.to(dev)
-    T2 = model.T2
-    lens_i32 = torch.full((B,), T2, dtype=torch.int32, device=dev)
-    U = T2 // 4
-    targets = torch.randint(1, V, (B, U), generator=g).to(dev)
-
-    rng = torch.zeros(1, dtype=torch.int64, device=dev)     # device dropout step counter
-    _lib.call("cfm_rng_bind", _lib.ptr(rng))
-    tgt_i32 = targets.to(torch.int32).contiguous()
-    tlen_i32 = torch.full((B,), U, dtype=torch.int32, device=dev)
-    seed0 = 17 * rank + 1
-
-    # SpecAugment (configs[2]): the global batch's draws on the host in the reference's order
-    # (specaugment.draw, python random seeded as speechcommands.py:18), this rank's slice packed into
-    # a STATIC device block that the captured step reads; refreshed before every step
-    sa_params = None
-    if args.specaug:
-        import random as _random
-        sa_rng = _random.Random(42)
-        sa_hp = HParams(None)
-        tau_glob = [T_in] * (B * world)
-
-        def specaug_refresh():
-            dr = specaugment.draw(B * world, Fb, tau_glob, sa_hp, sa_rng)
-            blk = specaugment.pack(dr, tau_glob, rank * B, (rank + 1) * B)
-            if sa_params is None:
-                return blk.to(dev)
-            sa_params.copy_(blk.pin_memory(), non_blocking=True)
-            return sa_params
-        sa_params = specaug_refresh()
-
-    def fwd_bwd():
-        rng.add_(1)
-        loss, _ = model(x, lens_i32, tgt_i32, tlen_i32, seed=seed0, specaug_params=sa_params)
-        loss.backward()
-        return loss
-
-    def post():
-        reducer.allreduce()
-        if not args.no_optimizer:
-            opt.step()
+    h = Harness(cfg, dev, rank, world, dropout=args.dropout, fp8=args.fp8, specaug=args.specaug,
+                dp_overlap=args.dp_overlap, eager=args.eager, no_optimizer=args.no_optimizer,
+                probe_inline=args.probe_inline)
+    model, T2, T_in = h.model, h.T2, h.T_in
 
     # dominant kernel: the FFN up-projection GEMM (M=B*T2, N=ffn, K=d, bf16, SiLU epilogue)
     M_ffn = B * T2
@@ -394,110 +515,56 @@ def main():
     # second probed family: the grouped weight-gradient launch (one per step)
     wprobe = KernelProbe(lambda kind, shape, dsc: kind == "wgroup", dev)
     ops.PROBE = lambda kind, shape, dsc, launch: probe(kind, shape, dsc, lambda: wprobe(kind, shape, dsc, launch))
-    graph = probe_graph = None
-    if args.eager:
-        def step(i):
-            opt.zero_grad(set_to_none=True)
-            if sa_params is not None:
-                specaug_refresh()
-            loss = fwd_bwd()
-            post()
-            return loss
-        for i in range(args.warmup):
-            step(i)
-        torch.cuda.synchronize()
-    else:
-        # warm up on a side stream (allocator + autotuned state settle), then capture ONE training
-        # step's forward + backward into a HIP graph; all-reduce + optimizer stay eager (few launches)
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for i in range(max(args.warmup, 1)):
-                opt.zero_grad(set_to_none=True)
-                fwd_bwd()
-                post()
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        opt.zero_grad(set_to_none=True)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            static_loss = fwd_bwd()
-        grads_timed = [p.grad for p in params]
-        # a second capture of the same step carries the probe's slot kernels (68 one-lane launches per
-        # step); it is replayed after the timed region, so the probes never sit inside `value`'s clock
-        probe_graph = None
-        if not args.probe_inline:
-            opt.zero_grad(set_to_none=True)
-            probe_graph = torch.cuda.CUDAGraph()
-            probe.active = wprobe.active = True
-            with torch.cuda.graph(probe_graph):
-                fwd_bwd()
-            probe.active = wprobe.active = False
-            for p, g in zip(params, grads_timed):
-                p.grad = g           # the timed replays' optimizer steps read the timed graph's grads
-        else:
-            graph = torch.cuda.CUDAGraph()    # legacy: probes inside the timed graph
-            opt.zero_grad(set_to_none=True)
-            probe.active = wprobe.active = True
-            with torch.cuda.graph(graph):
-                static_loss = fwd_bwd()
-            probe.active = wprobe.active = False
-
-        host_t = []
-
-        def step(i):
-            t_a = time.perf_counter()
-            if sa_params is not None:
-                specaug_refresh()
-            graph.replay()
-            t_b = time.perf_counter()
-            post()
-            host_t.append((t_b - t_a, time.perf_counter() - t_b))
-            return static_loss
-        step(0)                      # one replay outside the timed region
-        torch.cuda.synchronize()
-        probe.reset()
-        wprobe.reset()
+    h.setup(args.warmup, probes=(probe, wprobe))
+    probe.reset()
+    wprobe.reset()
+    bad_before = h.nonfinite_steps()
 
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    if graph is None:
+    if h.graph is None:
         probe.active = wprobe.active = True
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(args.warmup + i)
+    for _ in range(args.steps):
+        loss = h.step()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
     probe.active = wprobe.active = False
-    ops.PROBE = None
     elapsed = t1 - t0
     if world > 1:
         tt = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = tt.item()
     ms_step = 1000.0 * elapsed / args.steps
-    if graph is not None and os.environ.get("BENCH_HOST_TIMING"):
-        print("host ms per step (replay, post):", [(round(1e3 * a, 2), round(1e3 * b, 2)) for a, b in host_t],
+    if h.graph is not None and os.environ.get("BENCH_HOST_TIMING"):
+        print("host ms per step (replay, post):", [(round(1e3 * a, 2), round(1e3 * b, 2)) for a, b in h.host_t],
               file=sys.stderr)
     frames_total = B * T_in * world * args.steps
     value = frames_total / elapsed
+    # numerics of the timed steps: non-finite losses over every step run (warm-up included) and the final weights
+    loss_val = float(loss.item())
+    nonfinite = h.nonfinite_steps()
+    params_ok = h.params_finite()
+    if world > 1:
+        tt = torch.tensor([nonfinite, 0 if params_ok else 1], device=dev, dtype=torch.int64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.SUM)
+        nonfinite, params_ok = int(tt[0].item()), int(tt[1].item()) == 0
 
-    if graph is not None and probe_graph is not None:
-        for _ in range(args.steps):
-            probe_graph.replay()
+    h.probe_replays(args.steps)
+    ops.PROBE = None
     gemm_ms, n_launch = probe.mean_ms()
     if os.environ.get("BENCH_PROBE_DUMP"):
         torch.save(probe.slots.cpu(), os.environ["BENCH_PROBE_DUMP"])
-    if probe_graph is not None:
+    if h.probe_graph is not None:
         timing = ("in-kernel s_memrealtime first-start / last-end of every matching launch over --steps replays "
                   "of a second capture of the same step that carries the probe kernels, run right after the timed "
                   "region (the timed graph carries no probes)")
     else:
         timing = ("in-kernel s_memrealtime first-start / last-end of every matching launch in the timed "
-                  "region" + (" (graph replays)" if graph is not None else ""))
+                  "region" + (" (graph replays)" if h.graph is not None else ""))
     gemm_flops = 2.0 * M_ffn * ffn * d
     # algorithmic bytes of one FFN up-projection launch: A (M x d) + W (ffn x d) bf16 reads, bias fp32,
     # y and the saved pre-activation (M x ffn each, bf16) written
@@ -525,15 +592,19 @@ def main():
              "intensity_flop_per_byte": round(intensity, 1), "machine_balance_flop_per_byte": round(balance, 1),
              "avg_launch_ms": round(ms, 4), "launches_timed": n_launch, "timing": timing,
              "flops_per_launch": flops, "algorithmic_bytes": nbytes}
-        path = os.path.join(REPO, "profiles", "r02", pmc_file)
-        if os.path.exists(path):
+        for rnd in ("r03", "r02"):
+            path = os.path.join(REPO, "profiles", rnd, pmc_file)
+            if not os.path.exists(path):
+                continue
             with open(path) as f:
                 rec = json.load(f)
             if rec.get("shape_key") == [M_ffn, d, ffn, L] and rec.get("hbm_bytes_per_launch"):
                 e["traffic"] = rec["hbm_bytes_per_launch"]
-                e["traffic_source"] = f"profiles/r02/{pmc_file} ({rec.get('kernel', '?')[:80]})"
+                e["traffic_source"] = f"profiles/{rnd}/{pmc_file} ({rec.get('kernel', '?')[:80]})"
+                break
         return e
 
+    valid = nonfinite == 0 and params_ok
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
@@ -544,11 +615,13 @@ def main():
                    "pos_enc": pos_enc, "specaug": bool(args.specaug),
                    "global_batch": B * world, "seq_len": T_in, "enc_frames": T2, "frontend": "frame",
                    "dropout": args.dropout, "optimizer": None if args.no_optimizer else "adafactor",
-                   "parallelism": f"dp{world}", "launch": "eager" if args.eager else "hip-graph (fwd+bwd)"},
+                   "parallelism": f"dp{world}", "launch": "eager" if h.eager else "hip-graph (fwd+bwd)"},
         "per_gpu_value": round(value / world, 1),
         "step_algorithmic_tflops": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
-        "loss": float(loss.item()),
+        "loss": loss_val,
+        "steps_checked": h.steps_run, "nonfinite_steps": nonfinite, "nonfinite_before_timing": bad_before,
+        "params_finite": params_ok, "valid": valid,
         "roofline": roofline_entry(f"gemm_pipe FFN up-projection M={M_ffn} N={ffn} K={d} (+bias+SiLU+dropout, "
                                    f"y and pre-activation stored)", gemm_flops, gemm_bytes, gemm_ms, n_launch,
                                    "gemm_ffn_up_pmc.json"),
@@ -556,6 +629,8 @@ def main():
                                          f"M={M_ffn} tokens", wg_flops, wg_bytes, wg_ms, wg_n,
                                          "wgrad_group_pmc.json"),
     }
+    if args.poison:
+        result["poison"] = True
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
         result["cpu_baseline_configs0"] = cpu_baseline_s10(args.cpu_threads)
@@ -563,6 +638,10 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+    if not valid:
+        print(f"bench: INVALID step numerics: {nonfinite} of {h.steps_run} steps had a non-finite loss, "
+              f"parameters finite: {params_ok}", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
+from .debug import check as _chk
 from ._lib import ACT_SILU
 
 _EPS = 1e-5
@@ -97,7 +98,7 @@ _REL_PNAMES = ["self_attn.linear_pos.weight", "self_attn.pos_bias_u", "self_attn
 class _Cfg:
     __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
                  "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t", "group_wgrad", "layer_index",
-                 "grad_dest", "flush_here", "on_flushed", "sync_bn", "shadow8")
+                 "grad_dest", "flush_here", "on_flushed", "on_routed", "sync_bn", "shadow8")
 
 
 # the 2-D (and pointwise-conv) weight matrices of _PNAMES: cast to the compute dtype once per step
@@ -127,6 +128,7 @@ class _Side:
         self.group = None      # ops.WgradGroup when this layer's weight gradients are deferred
         self.dest = None       # {weight index: (dW view, db view)} in a data-parallel gradient bucket
         self.rgroup = None     # ops.ReduceGroup: this layer's small column reductions, deferred likewise
+        self.routed = 0        # grouped weight gradients written straight into their bucket views
 
     def run(self, fn, *inputs):
         self.side.wait_stream(self.main)
@@ -161,6 +163,8 @@ def _wgrad_bias(side, dy, x, widx=None):
     grouped launch writes straight into the bucket (autograd adopts the returned views as .grad)."""
     if side.group is not None and ops.wgrad_group_ok(dy, x):
         dest = side.dest.get(widx) if (side.dest and widx is not None) else None
+        if dest is not None:
+            side.routed += 1
         return side.group.add(dy, x, dest)
     dw = torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=torch.float32)
     db = torch.empty(dy.shape[1], device=dy.device, dtype=torch.float32)
@@ -202,6 +206,7 @@ def _ffn_fwd(x, P, o, cfg, seed):
     if y is None:
         y = ops.linear(h, w2, P[o + 5], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, out_scale=0.5,
                        residual=x)
+    _chk(f"ffn{o}_fwd", xn, mu, rs, pre, h, y)
     return y, (xn, mu, rs, pre, h, w1, w2)
 
 
@@ -238,6 +243,7 @@ def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads, side, g2=None, nxt=None):
     grads[o + 2], grads[o + 3] = _wgrad_bias(side, da, xn, o + 2)
     dxn = ops.linear_dgrad(da, w1, wt=_wt(cfg, o + 2))
     dx, grads[o], grads[o + 1], g2n = _ln_bwd(dxn, x, P, o, mu, rs, g, side, nxt)
+    _chk(f"ffn{o}_bwd", g2, da, dxn, dx, g2n)
     return dx, g2n
 
 
@@ -259,6 +265,7 @@ def _mha_fwd(x, P, R, cfg, seed, lens):
     y = _fp8_linear(o, cfg, 10, bias=P[11], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, residual=x)
     if y is None:
         y = ops.linear(o, wout, P[11], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, residual=x)
+    _chk("mha_fwd", xn, mu, rs, qkv, pos, o, lse, y)
     return y, (xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv)
 
 
@@ -285,6 +292,7 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
     grads[8], grads[9] = _wgrad_bias(side, dqkv, xn, 8)
     dxn = ops.linear_dgrad(dqkv, win, wt=_wt(cfg, 8))
     dx, grads[6], grads[7], g2n = _ln_bwd(dxn, x, P, 6, mu, rs, g, side, nxt)
+    _chk("mha_bwd", g4, do, Dh, dqkv, dpos, dxn, dx, g2n)
     return dx, g2n
 
 
@@ -304,6 +312,7 @@ def _conv_fwd(x, P, cfg, seed):
         z, bmean, binv = ops.bn_silu_fwd(yv, P[18], P[19], cfg.bn_rm, cfg.bn_rv, cfg.bn_mom, _EPS, cfg.training, B,
                                          T, d, ws, cd)
     y = ops.linear(z, wp2, P[21], out_dtype=torch.float32, drop_p=cfg.p, seed=seed, residual=x)
+    _chk("conv_fwd", xn, mu, rs, a, yv, bmean, binv, z, y)
     return y, (xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw)
 
 
@@ -327,6 +336,7 @@ def _conv_bwd(g, x, sv, P, cfg, seed, grads, side, g2=None, nxt=None):
     grads[14] = dw.view(2 * d, d, 1)
     dxn = ops.linear_dgrad(da, wp1, wt=_wt(cfg, 14))
     dx, grads[12], grads[13], g2n = _ln_bwd(dxn, x, P, 12, mu, rs, g, side, nxt)
+    _chk("conv_bwd", g3, dz, dy, grads[18], grads[19], da, dxn, dx, g2n)
     return dx, g2n
 
 
@@ -359,6 +369,7 @@ class _ConformerLayerFn(torch.autograd.Function):
             x3 = xc
         x4, sv4 = _ffn_fwd(x3, P, 22, cfg, s + 30)
         out, mu5, rs5 = ops.layernorm_fwd(x4, P[28], P[29], _EPS, out_dtype=torch.float32)
+        _chk(f"layer{cfg.layer_index}_fwd_out", out, mu5, rs5)
         ctx.cfg = cfg
         ctx.sv = (sv1, sva, svc, sv4)
         ctx.save_for_backward(x0, chain[0], chain[1], x3, x4, mu5, rs5, lens, *params)
@@ -407,6 +418,8 @@ class _ConformerLayerFn(torch.autograd.Function):
             g, g2 = _mha_bwd(g, c0, sva, P, R, cfg, s + 20, lens, grads, rgrads, side, g2, ffn1_in)
         g, _ = _ffn_bwd(g, x0, sv1, P, 0, cfg, s, grads, side, g2, None)
         side.join()
+        if cfg.on_routed is not None and side.dest and side.routed == len(side.dest):
+            cfg.on_routed(cfg.layer_index)       # (data-parallel reducer: this layer's buckets are final at flush)
         if cfg.layer_index == 0 or cfg.flush_here:
             # layer 0 runs backward last: everything deferred is flushed; data-parallel runs also flush at
             # bucket boundaries so the bucket's all-reduce (on_flushed) overlaps the remaining backward
@@ -418,6 +431,7 @@ class _ConformerLayerFn(torch.autograd.Function):
                 rgrp.flush()
             if cfg.on_flushed is not None:
                 cfg.on_flushed(cfg.layer_index)
+        _chk(f"layer{cfg.layer_index}_bwd_dx", g)
         ctx.sv = None
         return (g, None, None, *grads, *rgrads)
 
@@ -451,7 +465,7 @@ class ConformerLayer(nn.Module):
 
     def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None, shadow=None, layer_index=0,
                        group_wgrad=False, grad_dest=None, flush_here=False, on_flushed=None, sync_bn=None,
-                       count_batches=True):
+                       count_batches=True, on_routed=None):
         """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device; shadow: optional
         ({param index: compute-dtype copy}, {param index: its transposed K-major copy}) of this
         layer's weight matrices (see Conformer._shadows)."""
@@ -470,7 +484,7 @@ class ConformerLayer(nn.Module):
         cfg.pe = pe
         cfg.layer_index = layer_index
         cfg.group_wgrad = bool(group_wgrad) and "wgroup" not in ops.DISABLED
-        cfg.grad_dest, cfg.flush_here, cfg.on_flushed = grad_dest, flush_here, on_flushed
+        cfg.grad_dest, cfg.flush_here, cfg.on_flushed, cfg.on_routed = grad_dest, flush_here, on_flushed, on_routed
         cfg.sync_bn = sync_bn
         if count_batches and self.training and bn.track_running_stats:
             bn.num_batches_tracked.add_(1)
@@ -512,6 +526,7 @@ class Conformer(nn.Module):
         self.grad_dest = None
         self.flush_layers = frozenset()
         self.on_flushed = None
+        self.on_routed = None
         self.sync_bn = None     # (reduce_sums(t) in-place all-reduce, world) -> cross-replica BatchNorm
 
     def _pe(self, T, device):
@@ -574,7 +589,7 @@ class Conformer(nn.Module):
                                      layer_index=i, group_wgrad=group,
                                      grad_dest=self.grad_dest[i] if self.grad_dest else None,
                                      flush_here=i in self.flush_layers, on_flushed=self.on_flushed,
-                                     sync_bn=self.sync_bn, count_batches=False)
+                                     sync_bn=self.sync_bn, count_batches=False, on_routed=self.on_routed)
         # every layer's BatchNorm num_batches_tracked += 1 in one multi-tensor launch (not one per layer)
         counters = [ly.conv_module.sequential[3].num_batches_tracked for ly in self.conformer_layers
                     if self.training and ly.conv_module.sequential[3].track_running_stats]

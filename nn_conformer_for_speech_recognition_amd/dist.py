@@ -11,6 +11,7 @@ averaged gradients equal the single-process gradients of the global batch (tests
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -78,6 +79,8 @@ class GradAllReducer:
         self.flat = []            # chunk buckets: (flat tensor, lo_layer, hi_layer)
         self.pending = []         # async work handles of this step
         self.launched = set()
+        self.routed = set()       # Conformer layers whose grouped gradients all landed in the buckets
+        self._no_sync = False
         self.conformer = None
         owned = set()
         if model is not None:
@@ -134,6 +137,7 @@ class GradAllReducer:
         if self.overlap:
             conf.flush_layers = frozenset(flush)
             conf.on_flushed = self._on_flushed
+            conf.on_routed = self._on_routed
         return owned
 
     def _world(self):
@@ -153,33 +157,68 @@ class GradAllReducer:
 
     def _on_flushed(self, layer_index):
         """Called by the Conformer right after it flushed the grouped launch at `layer_index`: every chunk
-        whose layers are all >= layer_index is final -> issue its all-reduce now (async)."""
-        if self._world() == 1:
+        whose layers are all >= layer_index is final -> issue its all-reduce now (async).  Only chunks whose
+        every grouped weight/bias gradient was WRITTEN into its bucket view by this backward's grouped launch
+        (on_routed) qualify: a layer that accumulated into an existing .grad, or skipped the grouped launch
+        (gradient hooks, unsupported operand shapes), finishes its gradients through AccumulateGrad AFTER
+        this call, so its chunk waits for allreduce().  Nothing launches under no_sync()."""
+        if self._world() == 1 or self._no_sync:
             return
         for i, (flat, lo, hi) in enumerate(self.flat):
-            if i not in self.launched and lo >= layer_index:
-                self.launched.add(i)
-                w = self._reduce(flat, True)
-                if w is not None:
-                    self.pending.append(w)
+            if i in self.launched or lo < layer_index:
+                continue
+            if not all(li in self.routed for li in range(lo, hi)):
+                continue
+            self.launched.add(i)
+            w = self._reduce(flat, True)
+            if w is not None:
+                self.pending.append(w)
 
-    def _check_adopted(self):
-        """The grouped gradients must be the bucket views (else the reduction would miss them)."""
-        if self.conformer is None:
-            return
-        for li, layer in enumerate(self.conformer.conformer_layers):
-            ps = layer.params()
+    def _on_routed(self, layer_index):
+        """The Conformer's layer `layer_index` routed all its grouped gradients into the bucket views."""
+        self.routed.add(layer_index)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation over micro-batches (DDP's no_sync): backward passes inside the context issue
+        no bucket all-reduce; the allreduce() after the last micro-batch reduces the accumulated gradients."""
+        prev = self._no_sync
+        self._no_sync = True
+        try:
+            yield
+        finally:
+            self._no_sync = prev
+            self.routed = set()
+
+    def _chunk_views(self, chunk):
+        """(param, bucket view) pairs of one chunk's grouped gradients."""
+        _, lo, hi = self.flat[chunk]
+        out = []
+        for li in range(lo, hi):
+            ps = self.conformer.conformer_layers[li].params()
             for wi, (dw, db) in self.conformer.grad_dest[li].items():
-                for p, v in ((ps[wi], dw), (ps[wi + 1], db)):
-                    if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
-                        v.copy_(p.grad.reshape(v.shape))
-                        p.grad = v.view(p.shape)
+                out += [(ps[wi], dw), (ps[wi + 1], db)]
+        return out
+
+    def _adopt(self, chunk, copy):
+        """Make every grouped gradient of `chunk` its bucket view.  copy=True (chunk not yet reduced): a
+        gradient living elsewhere is copied in first.  copy=False (chunk reduced during backward, only from
+        fully routed layers): the bucket already holds the reduced gradient, so .grad is just re-pointed."""
+        for p, v in self._chunk_views(chunk):
+            if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                if copy:
+                    v.copy_(p.grad.reshape(v.shape))
+                p.grad = v.view(p.shape)
 
     def allreduce(self):
         if self._world() == 1:
             self.launched.clear()
+            self.routed = set()
             return
-        self._check_adopted()
+        if self.conformer is not None:
+            for i in range(len(self.flat)):
+                if i not in self.launched:
+                    self._adopt(i, copy=True)      # before any of those chunks' reductions starts
         for i, (flat, lo, hi) in enumerate(self.flat):
             if i not in self.launched:
                 w = self._reduce(flat, True)
@@ -205,8 +244,12 @@ class GradAllReducer:
                 off += g.numel()
         for w in self.pending:
             w.wait()
+        if self.conformer is not None:
+            for i in self.launched:
+                self._adopt(i, copy=False)
         self.pending = []
         self.launched = set()
+        self.routed = set()
 
 
 def global_batch_slice(global_batch, rank, world):

@@ -31,6 +31,14 @@ class Vocab:
         self.pad_idx = self.stoi[pad_token]
         self.blank_idx = self.stoi[blank_token]
 
+    @classmethod
+    def from_file(cls, path, ntokens=None, **kw):
+        """myVocab.read_vocab (myvocab.py:163-176): one token per line in id order (the file save_vocab
+        writes), the first `ntokens` kept."""
+        with open(path, "r", encoding="utf-8") as f:
+            toks = f.read().split("\n")
+        return cls(toks[:ntokens], **kw)
+
     def __len__(self):
         return len(self.itos)
 

@@ -38,9 +38,53 @@ def _wgrad_strided(a, lda, b, ldb, M, N, K, out):
                     workspace=ws)
 
 
-def _check_flag(ws, idx, what):
-    if int(ws[idx].item()) != 0:
-        raise L.CfmError(f"{what}: a step wait exceeded its limit (workgroups not co-resident?)")
+class _ErrorFlags:
+    """Sticky device-side record of the recurrence kernels' wait-limit flags, checked WITHOUT a host sync per
+    launch (a per-layer .item() would stall the host queue every pass and cannot run inside a HIP-graph
+    capture).  note() folds a launch's flag into a persistent device word (stream-ordered max, capturable);
+    poll() copies that word to pinned host memory behind an event and raises once a completed copy shows a
+    set flag -- at the next forward, i.e. one step late, never blocking; sync_check() waits and raises now."""
+
+    def __init__(self):
+        self.dev = {}
+        self.host = {}
+        self.event = {}
+
+    def _word(self, device):
+        key = str(device)
+        if key not in self.dev:
+            self.dev[key] = torch.zeros(1, dtype=torch.int32, device=device)
+        return self.dev[key]
+
+    def note(self, ws, idx):
+        w = self._word(ws.device)
+        torch.maximum(w, ws[idx:idx + 1], out=w)
+
+    def poll(self, device):
+        """Raise if a finished earlier copy saw a set flag; then (outside capture) start a fresh async copy."""
+        key = str(device)
+        ev = self.event.get(key)
+        if ev is not None and ev.query() and int(self.host[key][0]) != 0:
+            self.host[key][0] = 0
+            self.dev[key].zero_()
+            raise L.CfmError("cfm_lstm_fwd/bwd: a step wait exceeded its limit (workgroups not co-resident?)")
+        if torch.cuda.is_current_stream_capturing() or key not in self.dev:
+            return
+        if key not in self.host:
+            self.host[key] = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self.host[key].copy_(self.dev[key], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.event[key] = ev
+
+    def sync_check(self, device):
+        key = str(device)
+        if key in self.dev and int(self.dev[key].item()) != 0:
+            self.dev[key].zero_()
+            raise L.CfmError("cfm_lstm_fwd/bwd: a step wait exceeded its limit (workgroups not co-resident?)")
+
+
+ERRORS = _ErrorFlags()
 
 
 class _LSTMLayer(torch.autograd.Function):
@@ -57,7 +101,7 @@ class _LSTMLayer(torch.autograd.Function):
         ws = torch.empty(L.size_call("cfm_lstm_ws_bytes", H, ndir) // 4, device=dev, dtype=torch.int32)
         L.call("cfm_lstm_fwd", L.ptr(gx), L.ptr(w_hh), L.ptr(y), L.ptr(gates), L.ptr(c), Lseq, H, ndir, L.ptr(ws),
                L.stream())
-        _check_flag(ws, 0, "cfm_lstm_fwd")
+        ERRORS.note(ws, 0)
         ctx.save_for_backward(x, w_ih, w_hh, y, gates, c)
         ctx.H, ctx.ndir, ctx.ws = H, ndir, ws
         ctx.mark_non_differentiable(c)
@@ -73,7 +117,7 @@ class _LSTMLayer(torch.autograd.Function):
         dg = torch.empty(Lseq, ndir * H4, device=x.device, dtype=torch.float32)
         L.call("cfm_lstm_bwd", L.ptr(dy), L.ptr(w_hh), L.ptr(gates), L.ptr(c), L.ptr(dg), Lseq, H, ndir, L.ptr(ws),
                L.stream())
-        _check_flag(ws, 1, "cfm_lstm_bwd")
+        ERRORS.note(ws, 1)
         dx = ops.linear_dgrad(dg, w_ih) if ctx.needs_input_grad[0] else None
         dw_ih = ops.linear_wgrad(dg, x)
         db = ops.colsum(dg)
@@ -127,6 +171,7 @@ class LSTM(nn.Module):
         if input.dim() != 2:
             raise NotImplementedError("LSTM: only the unbatched 2-D (L, input_size) form (asrnn.py:252) is supported")
         H, ndir = self.hidden_size, 2 if self.bidirectional else 1
+        ERRORS.poll(input.device)            # earlier passes' wait-limit flags (no host sync)
         x = input.float().contiguous()
         hn, cn = [], []
         for layer in range(self.num_layers):
@@ -149,6 +194,11 @@ class LSTM(nn.Module):
                 x = F.dropout(x, self.dropout, True)
         out = x.to(input.dtype) if input.dtype != torch.float32 else x
         return out, (torch.stack(hn), torch.stack(cn))
+
+    @staticmethod
+    def check_errors(device=None):
+        """Synchronising check of every recurrence launched so far on `device` (raises CfmError)."""
+        ERRORS.sync_check(device or torch.device("cuda", torch.cuda.current_device()))
 
     def extra_repr(self):
         return (f"{self.input_size}, {self.hidden_size}, num_layers={self.num_layers}, "

@@ -364,6 +364,184 @@ def gen_asrnn(tmp):
     print("asrnn_small.npz")
 
 
+class _TTVocab:
+    """torchtext.vocab.Vocab as the reference uses it (torchtext is absent from this image; its published
+    semantics): `vocab(ordered_dict, min_freq=1)` keeps the dict's tokens in insertion order, insert_token()
+    shifts later ids, lookup by token falls back to the default index once set."""
+
+    def __init__(self, ordered_dict, min_freq=1):
+        self.itos = [t for t, f in ordered_dict.items() if f >= min_freq]
+        self.default = None
+
+    def insert_token(self, token, index):
+        self.itos.insert(index, token)
+
+    def set_default_index(self, i):
+        self.default = i
+
+    def __contains__(self, t):
+        return t in self.itos
+
+    def __getitem__(self, t):
+        if t in self.itos:
+            return self.itos.index(t)
+        if self.default is None:
+            raise RuntimeError(f"token {t!r} not found and default index is not set")
+        return self.default
+
+    def __len__(self):
+        return len(self.itos)
+
+    def lookup_tokens(self, ids):
+        return [self.itos[i] for i in ids]
+
+
+def _install_runner_stubs(calls):
+    """Recording stubs for the Runner / myVocab imports absent from this image (jiwer, torchtext, tqdm,
+    colorama) and the plotting module lib.evals (matplotlib): jiwer.wer records the word lists it gets."""
+    import importlib.machinery
+    import transformers  # noqa: F401  (loads torch's import-time probes of tqdm before the stub replaces it)
+    _mod = types.ModuleType
+
+    def mod(name):
+        m = _mod(name)
+        m.__spec__ = importlib.machinery.ModuleSpec(name, None)
+        return m
+    tt = mod("torchtext")
+    ttv = mod("torchtext.vocab")
+    ttv.vocab = lambda od, min_freq=1: _TTVocab(od, min_freq)
+    tt.vocab = ttv
+    sys.modules["torchtext"] = tt
+    sys.modules["torchtext.vocab"] = ttv
+    jw = mod("jiwer")
+
+    def wer(t, p):
+        calls.append((list(t), list(p)))
+        return 0.25
+    jw.wer = wer
+    sys.modules["jiwer"] = jw
+
+    class _Bar:
+        def __init__(self, *a, **k):
+            self.postfix = ""
+            self.bar_format = ""
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+        def set_description(self, *a):
+            pass
+
+        def update(self, *a):
+            pass
+    tq = mod("tqdm")
+    tq.tqdm = _Bar
+    sys.modules["tqdm"] = tq
+    co = mod("colorama")
+    co.Fore = types.SimpleNamespace(MAGENTA="", RESET="", CYAN="", GREEN="", RED="", BLUE="", YELLOW="")
+    sys.modules["colorama"] = co
+    ev = mod("lib.evals")
+
+    class Evals:
+        def __init__(self, *a, **k):
+            pass
+
+        def plot(self, *a, **k):
+            pass
+
+        def heatmap(self, *a, **k):
+            pass
+    ev.Evals = Evals
+    sys.modules["lib.evals"] = ev
+
+
+def gen_runner_vocab(tmp):
+    """The Runner / vocabulary surface around the hot path: the reference's own
+    myVocab (reading its shipped vocabs/myvocab.txt, and building from sentences), myVocab.decode on fixed
+    id rows (myvocab.py:211-231), and Runner.train / test / generate_labels (runner.py:102-281) driven by a
+    stub model that returns fixed logits -- the word lists the reference hands to jiwer.wer are recorded."""
+    calls = []
+    _install_runner_stubs(calls)
+    from lib.standard.myvocab import myVocab
+    from lib.standard.runner import Runner
+    vocab_file = os.path.join(REF, "vocabs", "myvocab.txt")
+    voc = myVocab(tmp, vocab_path=vocab_file)
+    itos = voc.vocab.lookup_tokens(list(range(len(voc))))
+    sents = ["yes no yes", "up down", "left yes", "no no no go", "stop"]
+    data = [(None, None, s) for s in sents]
+    built = myVocab(tmp, data=data, vocab_path=os.path.join(tmp, "built.txt"))
+    built_itos = built.vocab.lookup_tokens(list(range(len(built))))
+    parsed = [voc.parse(s) for s in ["yes no", "up unknownword down"]]
+    g = torch.Generator().manual_seed(11)
+    V = len(itos)
+    rows = torch.randint(0, V, (6, 9), generator=g)
+    rows[0, :] = 1                              # all <pad>
+    rows[1, :] = torch.tensor([0, 0, 5, 5, 0, 1, 7, 7, 2])   # blanks, repeats (not collapsed), <unk>
+    decoded = voc.decode(rows)
+
+    hp = _hparams(tmp)
+    hp.batch_size = 4
+    hp.set_blank_index(voc.vocab[voc.blank_token])
+    hp.plots_dir = tmp
+    hp.standard_model_path = os.path.join(tmp, "std.pth")
+    hp.finetuning_model_path = os.path.join(tmp, "ft.pth")
+    B, T = 4, 12
+    logits = torch.randn(5, B, T, V, generator=g) * 3.0      # train x2, validation x1, pretrain x2
+    logits[0, 2] = -10.0
+    logits[0, 2, :, 0] = 10.0                   # an all-blank prediction -> '_' in the word lists
+    out_lens = torch.tensor([T, T, T - 3, T])
+    tgts = torch.randint(3, V, (3, B, 2), generator=g)
+    tgt_lens = torch.tensor([[1, 2, 1, 0], [2, 1, 1, 1], [1, 1, 0, 2]])
+    for j in range(3):
+        for b in range(B):
+            tgts[j, b, tgt_lens[j, b]:] = voc.vocab[voc.pad_token]    # padded with <pad>, as get_batch does
+
+    class StubModel(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.zeros(1))
+            self.i = 0
+
+        def forward(self, x, input_lens, SpecAugment=False, lm=None, finetuning=False):
+            k = int(x.reshape(-1)[0].item())
+            return torch.log_softmax(logits[k] + self.w, -1), out_lens.clone()
+
+        def predict(self, lg):
+            return torch.argmax(lg, dim=-1)
+
+    class StubData:
+        idxes = {"train": list(range(8)), "validation": list(range(4)), "pretrain": list(range(8))}
+        vocab = voc
+
+        def shuffle(self, kind):
+            pass
+
+        def get_batch(self, i, kind):
+            k = {"train": i, "validation": 2, "pretrain": 3 + i}[kind]
+            x = torch.full((B, 1, 4, 4), float(k))
+            j = min(k, 2)
+            return {"input": {"mels": x, "tau": torch.full((B,), T)},
+                    "target": {"transcripts": tgts[j].clone(), "lens": tgt_lens[j].clone()}, "unpadded_len": B}
+
+    model = StubModel()
+    runner = Runner(model, hp)
+    runner.train(StubData(), 1)
+    train_calls = [list(c) for c in calls]
+    labels = runner.generate_labels(StubData())
+    rec = {"itos": itos, "built_from": sents, "built_itos": built_itos, "parsed": parsed,
+           "decode_rows": rows.tolist(), "decoded": decoded, "batch": B, "T": T,
+           "logits": logits.tolist(), "out_lens": out_lens.tolist(), "targets": tgts.tolist(),
+           "target_lens": tgt_lens.tolist(), "wer_calls": train_calls, "labels": labels,
+           "note": "wer_calls: (target words, predicted words) the reference's Runner.train passes to jiwer.wer: "
+                   "2 train batches then 1 validation batch; labels: Runner.generate_labels over 2 pretrain batches"}
+    with open(os.path.join(HERE, "runner_vocab.json"), "w") as f:
+        json.dump(rec, f)
+    print("runner_vocab.json", len(train_calls), "wer calls,", len(labels), "labels")
+
+
 def main():
     import tempfile
     _install_stubs()
@@ -373,6 +551,7 @@ def main():
         gen_conformer_layers()
         gen_conformer_L()
         gen_asrnn(tmp)
+        gen_runner_vocab(tmp)
 
 
 if __name__ == "__main__":

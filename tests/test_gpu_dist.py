@@ -53,7 +53,7 @@ def _grads(m, x, lens, tgt, tl, reducer=None):
     return {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()}
 
 
-def _worker(rank, world, port, cd, q, bn="eval"):
+def _worker(rank, world, port, cd, q, bn="eval", accum=False):
     import faulthandler
     faulthandler.dump_traceback_later(100, exit=True)     # a stuck rank reports where, then exits
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -67,7 +67,16 @@ def _worker(rank, world, port, cd, q, bn="eval"):
         m.conformers.set_sync_batchnorm()
     red = cdist.GradAllReducer([p for p in m.parameters()], model=m, chunk_layers=1, overlap=True)
     sl = slice(2 * rank, 2 * rank + 2)
-    g = _grads(m, x[sl].contiguous(), lens[sl].contiguous(), tgt[sl].contiguous(), tl[sl].contiguous(), red)
+    mb = (x[sl].contiguous(), lens[sl].contiguous(), tgt[sl].contiguous(), tl[sl].contiguous())
+    if accum:
+        # gradient accumulation over two micro-batches (the same slice twice): the first backward runs under
+        # no_sync (no bucket all-reduce), the second accumulates into the bucket views in place (no grouped
+        # launch: .grad exists) and its chunks are reduced by allreduce(), never mid-backward
+        with red.no_sync():
+            loss, _ = m(*mb, seed=3)
+            loss.backward()
+        assert not red.launched
+    g = _grads(m, *mb, red)
     # the grouped gradients really are the bucket views (no copy-in)
     ok = None
     if m.conformers.grad_dest is not None:
@@ -79,9 +88,10 @@ def _worker(rank, world, port, cd, q, bn="eval"):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("cd,bn", [(torch.bfloat16, "eval"), (torch.float32, "eval"), (torch.bfloat16, "sync"),
-                                   (torch.float32, "sync")])
-def test_two_rank_grads_equal_one_rank_full_batch(cd, bn):
+@pytest.mark.parametrize("cd,bn,accum", [(torch.bfloat16, "eval", False), (torch.float32, "eval", False),
+                                         (torch.bfloat16, "sync", False), (torch.float32, "sync", False),
+                                         (torch.bfloat16, "eval", True), (torch.float32, "eval", True)])
+def test_two_rank_grads_equal_one_rank_full_batch(cd, bn, accum):
     """bn='eval': BatchNorm on running statistics; bn='sync': train-mode BatchNorm with
     Conformer.set_sync_batchnorm() (cross-replica statistics) -- the running statistics must then
     also equal the single-process ones."""
@@ -89,7 +99,7 @@ def test_two_rank_grads_equal_one_rank_full_batch(cd, bn):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cd, q, bn)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cd, q, bn, accum)) for r in range(world)]
     for p in procs:
         p.start()
     import queue
@@ -107,11 +117,14 @@ def test_two_rank_grads_equal_one_rank_full_batch(cd, bn):
         p.join(timeout=60)
         assert p.exitcode == 0
     m1, *data = _setup(cd, bn)
+    if accum:                       # the single process accumulates the same two micro-batches
+        loss, _ = m1(*data, seed=3)
+        loss.backward()
     ref = _grads(m1, *data)
     ref.update({"buf." + n: b.detach().cpu().clone() for n, b in m1.named_buffers() if "running" in n})
     (_, g0, ok0), (_, g1, _) = out
     if cd == torch.bfloat16:
-        assert ok0
+        assert ok0                  # (accum: the second micro-batch added in place into the bucket views)
     # train-mode BN in bf16: the replicas' fp32 partial sums are added in another order than the single
     # process's, which flips a few bf16 roundings of the normalised activations -> bf16-level noise
     tol = 2e-2 if (bn == "sync" and cd == torch.bfloat16) else 1e-4

@@ -55,6 +55,7 @@ def test_lstm_fwd_bwd_vs_torch(L, In, H, layers, bidir):
     pr = dict(ref.named_parameters())
     for name, p in mine.named_parameters():
         assert _rel(p.grad, pr[name].grad) < 2e-4, name
+    LSTM.check_errors()      # the recurrences' wait-limit flags (kept on the device, no per-launch sync)
 
 
 def test_lstm_long_sequence_direction_symmetry():
@@ -74,6 +75,25 @@ def test_lstm_long_sequence_direction_symmetry():
     y_uni, _ = uni(x.flip(0))
     assert (y_bi[:, H:] - y_uni.flip(0)).abs().amax().item() < 1e-5
     assert torch.isfinite(y_bi).all()
+    LSTM.check_errors()
+
+
+def test_lstm_no_host_sync_per_layer():
+    """The forward / backward issue no blocking device read (a per-layer .item() stalled the host
+    queue): with torch's sync debug mode set to error, a 2-layer bidirectional pass runs through."""
+    torch.manual_seed(5)
+    m = LSTM(64, 128, num_layers=2, bidirectional=True).to(DEV)
+    x = torch.randn(50, 64, device=DEV, requires_grad=True)
+    m(x)        # first call: lazily allocates the flag word and its pinned host copy
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        y, _ = m(x)
+        y.sum().backward()
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    LSTM.check_errors()
+    assert torch.isfinite(x.grad).all()
 
 
 def test_lstm_state_dict_matches_torch_names():
