@@ -59,6 +59,43 @@ def main():
         probes = (pr, wp)
     report = {"config": cfg, "eager": args.eager, "poison": args.poison, "probe": args.probe, "steps": []}
 
+    def snapshot():
+        snap = {}
+        for p in h.params:
+            st = h.opt.state.get(p, {})
+            snap[id(p)] = (p.detach().clone(), None if p.grad is None else p.grad.detach().clone(),
+                           {k: v.clone() for k, v in st.items() if torch.is_tensor(v)}, int(st.get("step", 0)))
+        return snap
+
+    def diagnose(snap):
+        """After a post() that left non-finite weights: which parameters, and what a plain torch Adafactor
+        (transformers' formulas, fp32) computes from the same pre-step weights / gradients / state."""
+        out = []
+        for p in h.params:
+            if bool(torch.isfinite(p.detach()).all()):
+                continue
+            p0, g0, st0, step0 = snap[id(p)]
+            rec = {"name": names[id(p)], "shape": list(p.shape), "grad_finite": bool(torch.isfinite(g0).all()),
+                   "p0_finite": bool(torch.isfinite(p0).all()), "state_finite": {k: bool(torch.isfinite(v).all())
+                                                                                 for k, v in st0.items()},
+                   "step_before": step0, "grad_ptr": p.grad.data_ptr(), "n_bad": int((~torch.isfinite(p)).sum())}
+            try:
+                from transformers.optimization import Adafactor as HFA
+                q = torch.nn.Parameter(p0.clone())
+                q.grad = g0.clone()
+                o = HFA([q], lr=2e-5, beta1=0.9, scale_parameter=False, relative_step=False)
+                if step0:
+                    o.state[q] = {"step": step0, **{k: v.clone() for k, v in st0.items()}}
+                    o.state[q]["RMS"] = 0
+                o.step()
+                rec["hf_finite"] = bool(torch.isfinite(q.detach()).all())
+            except Exception as e:        # noqa: BLE001
+                rec["hf_error"] = repr(e)[:200]
+            out.append(rec)
+            if len(out) >= 6:
+                break
+        return out
+
     def inspect(i, loss):
         torch.cuda.synchronize()
         lv = float(loss.item())
@@ -88,9 +125,15 @@ def main():
         for i in range(args.steps):
             h.graph.replay()
             rec = inspect(i, h.static_loss)
+            snap = snapshot()
+            rec["fast_path_key_hit"] = any(v[0] == h.opt._ptrkey([p for p in g["params"] if p.grad is not None])
+                                           for g in h.opt.param_groups for v in [h.opt._fast.get((id(g), dev))]
+                                           if v is not None)
             h.post()
             torch.cuda.synchronize()
             rec["params_finite_after"] = h.params_finite()
+            if not rec["params_finite_after"]:
+                rec["diagnose"] = diagnose(snap)
             report["steps"].append(rec)
             print(json.dumps(rec), flush=True)
             if args.probe and i % 3 == 2:

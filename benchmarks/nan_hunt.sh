@@ -2,7 +2,7 @@
 # NaN hunt driver for one gpurun call: every scenario under its own time limit; exit 1 (= NaN found) lets the
 # chain continue, anything else (fault, abort, timeout) stops it.
 set -u
-OUT=${OUT:-gpurun_out/nan3}
+OUT=${OUT:-gpurun_out/nan5}
 mkdir -p "$OUT"
 run() {
   local tag=$1; shift
@@ -23,6 +23,10 @@ for sc in "$@"; do
     S15ep)  CFM_NANCHECK=1 run S15ep python -u benchmarks/nan_hunt.py --config S15 --eager --poison --steps 3 ;;
     L60g)   run L60g python -u benchmarks/nan_hunt.py --config L60 --probe --steps 10 ;;
     L60gp)  run L60gp python -u benchmarks/nan_hunt.py --config L60 --probe --poison --steps 6 ;;
+    L15gn)  run L15gn python -u benchmarks/nan_hunt.py --config L15 --steps 6 ;;
+    L15gd)  run L15gd python -u benchmarks/nan_hunt.py --config L15 --probe --steps 3 ;;
+    S15gnp) run S15gnp python -u benchmarks/nan_hunt.py --config S15 --poison --steps 6 ;;
+    S15gpd) run S15gpd python -u benchmarks/nan_hunt.py --config S15 --probe --poison --steps 3 ;;
     bench)  run bench python -u bench.py --no-cpu-baseline ;;
   esac
 done

@@ -336,6 +336,12 @@ int cfm_conv2_bwd_data_ws(const void* dh2, const void* w2r, void* dh1, int dtype
                           int T1, int C1, int C2, void* ws, void* stream);
 int cfm_conv2_bwd_weight(const void* dh2, const void* h1, float* dw2r, int dtype, int B, int F1,
                          int T1, int C1, int C2, void* stream);
+/* conv2 weight gradient with deterministic split-K slabs in `ws` (cfm_conv2_bwd_weight_ws_bytes bytes; NULL ->
+ * one K slice): no atomics, no memset (graph-replay safe).  Replaces Conv2d.backward's weight gradient of
+ * lib/convsubsampling.py:37. */
+size_t cfm_conv2_bwd_weight_ws_bytes(int B, int F1, int T1, int C1, int C2);
+int cfm_conv2_bwd_weight_ws(const void* dh2, const void* h1, float* dw2r, int dtype, int B, int F1,
+                            int T1, int C1, int C2, float* ws, void* stream);
 size_t cfm_conv1_bwd_ws_bytes(int B, int F, int T, int C1);
 int cfm_conv1_bwd_weight(const void* dh1, int dtype_h, const float* x, float* dw1, float* db1,
                          int B, int F, int T, int C1, float* ws, void* stream);

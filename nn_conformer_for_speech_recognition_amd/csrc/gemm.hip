@@ -1653,21 +1653,43 @@ CFM_EXPORT int cfm_conv2_fwd(const void* h1, const void* w2r, const float* b2, v
   return cfm::check_launch("cfm_conv2_fwd");
 }
 
-CFM_EXPORT int cfm_conv2_bwd_weight(const void* dh2, const void* h1, float* dw2r, int dtype, int B, int F1, int T1,
-                                    int C1, int C2, void* stream) {
+// conv2 weight gradient dW2r (C2 x 9*C1, fp32) = dh2^T im2col(h1) over M = B*T2*F2 tokens.  Split-K over the
+// tokens into DETERMINISTIC slabs (ws: split x C2 x 9*C1 floats, each slab written whole by its K slice) summed in
+// slice order by splitk_reduce_kernel -- no atomics and no memset: the round-2 form zeroed dW with
+// hipMemsetAsync and accumulated with atomics, and inside a replayed HIP graph that left part of dW unzeroed /
+// stale (the round-2 NaN losses: nan_hunt showed this gradient alone going non-finite under poisoned memory).
+static int conv2_wgrad_split(int B, int F1, int T1, int C1, int C2) {
+  const Conv2Geo g = conv2_geo(B, F1, T1, C1, C2);
+  const int Mrows = B * g.T2 * g.F2;
+  const int tiles = cdiv(C2, BM) * cdiv(9 * C1, BN);
+  int split = 512 / (tiles > 0 ? tiles : 1);
+  split = split < 1 ? 1 : (split > 16 ? 16 : split);
+  if (Mrows / 1024 < split) split = Mrows / 1024 > 1 ? Mrows / 1024 : 1;
+  return split;
+}
+
+CFM_EXPORT size_t cfm_conv2_bwd_weight_ws_bytes(int B, int F1, int T1, int C1, int C2) {
+  const int split = conv2_wgrad_split(B, F1, T1, C1, C2);
+  return split > 1 ? (size_t)split * C2 * 9 * C1 * sizeof(float) : 0;
+}
+
+CFM_EXPORT int cfm_conv2_bwd_weight_ws(const void* dh2, const void* h1, float* dw2r, int dtype, int B, int F1, int T1,
+                                       int C1, int C2, float* ws, void* stream) {
   CFM_REQUIRE(dh2 && h1 && dw2r, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(C1 % 8 == 0 && C2 % 8 == 0, CFM_ERR_SHAPE, "conv2: C1 and C2 must be multiples of 8");
   const Conv2Geo g = conv2_geo(B, F1, T1, C1, C2);
   const int Mrows = B * g.T2 * g.F2;
   GemmP p = plain_params(C2, 9 * C1, Mrows, dw2r, 9L * C1, CFM_F32);
-  const int tiles = cdiv(C2, BM) * cdiv(9 * C1, BN);
-  int split = 1024 / (tiles > 0 ? tiles : 1);
-  split = split < 1 ? 1 : (split > 64 ? 64 : split);
-  if (Mrows / 512 < split) split = Mrows / 512 > 1 ? Mrows / 512 : 1;
+  const int split = ws ? conv2_wgrad_split(B, F1, T1, C1, C2) : 1;
   p.split_k = split;
   p.k_per_split = split_k_for(p, dtype == CFM_BF16 ? BK16 : BK32);
+  const int used = cdiv(Mrows, p.k_per_split);       // slices that hold tokens (each writes its whole slab)
+  p.split_k = used;
+  if (used > 1) {
+    CFM_REQUIRE((long)C2 * 9 * C1 < (1L << 31), CFM_ERR_SHAPE, "conv2 wgrad: slab too large");
+    p.slab = ws;
+  }
   hipStream_t s = cfm::as_stream(stream);
-  if (split > 1) (void)hipMemsetAsync(dw2r, 0, sizeof(float) * C2 * 9 * C1, s);
   int rc;
   if (dtype == CFM_BF16)
     rc = launch_typed<false, false>(dtype, p, StridedOp<bf16>{(const bf16*)dh2, C2, 0, C2 % 8 == 0},
@@ -1676,7 +1698,18 @@ CFM_EXPORT int cfm_conv2_bwd_weight(const void* dh2, const void* h1, float* dw2r
     rc = launch_typed<false, false>(dtype, p, StridedOp<float>{(const float*)dh2, C2, 0, C2 % 4 == 0},
                                     Conv2WgradB<float>{(const float*)h1, g}, 1, s);
   if (rc != CFM_OK) return rc;
+  if (used > 1) {
+    const long n4 = (long)C2 * 9 * C1 / 4;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n4 + 255) / 256), 1), dim3(256), 0, s, p.slab, used, C2,
+                       9 * C1, dw2r, 9L * C1, 0L, (const float*)nullptr, (const float*)nullptr, (float*)nullptr);
+  }
   return cfm::check_launch("cfm_conv2_bwd_weight");
+}
+
+// (workspace-free form: one K slice, no split -- kept for the C ABI; the host path passes a workspace)
+CFM_EXPORT int cfm_conv2_bwd_weight(const void* dh2, const void* h1, float* dw2r, int dtype, int B, int F1, int T1,
+                                    int C1, int C2, void* stream) {
+  return cfm_conv2_bwd_weight_ws(dh2, h1, dw2r, dtype, B, F1, T1, C1, C2, nullptr, stream);
 }
 
 namespace {

@@ -650,7 +650,10 @@ def conv2_bwd_weight(dh2, h1):
     B, F1, T1, C1 = h1.shape
     C2 = dh2.shape[-1]
     dw2r = torch.empty(C2, 9 * C1, device=h1.device, dtype=torch.float32)
-    L.call("cfm_conv2_bwd_weight", L.ptr(dh2), L.ptr(h1), L.ptr(dw2r), L.dt(h1), B, F1, T1, C1, C2, L.stream())
+    nb = L.size_call("cfm_conv2_bwd_weight_ws_bytes", B, F1, T1, C1, C2)
+    ws = workspace(nb, h1.device) if nb else None     # deterministic split-K slabs (no atomics / memset)
+    L.call("cfm_conv2_bwd_weight_ws", L.ptr(dh2), L.ptr(h1), L.ptr(dw2r), L.dt(h1), B, F1, T1, C1, C2, L.ptr(ws),
+           L.stream())
     return dw2r
 
 

@@ -1,0 +1,99 @@
+"""The bench's own training step, many steps, under poisoned memory.
+
+Round 2's bench lines sometimes reported a NaN loss.  benchmarks/nan_hunt.py (bench.Harness + per-step
+checks, every torch.empty NaN-filled) traced it to the conv2 weight gradient (lib/convsubsampling.py:37's
+Conv2d backward): it was zeroed with hipMemsetAsync and accumulated with split-K atomics, and inside a
+replayed HIP graph part of dW was left unzeroed / stale (half of dW non-finite under poisoning, huge finite
+garbage otherwise, which Adafactor turned into NaN weights).  It now uses deterministic split-K slabs.
+
+These tests run the real bench harness -- HIP-graph capture of fwd+bwd, the probe-carrying second capture,
+GradAllReducer, Adafactor -- at small dims for >= 10 steps with torch's fill_uninitialized_memory on, and
+assert a finite loss, finite gradient norms and finite weights after every step."""
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+@pytest.fixture
+def poisoned():
+    prev_det = torch.are_deterministic_algorithms_enabled()
+    prev_warn = torch.is_deterministic_algorithms_warn_only_enabled()
+    prev_fill = torch.utils.deterministic.fill_uninitialized_memory
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    torch.utils.deterministic.fill_uninitialized_memory = True
+    yield
+    torch.utils.deterministic.fill_uninitialized_memory = prev_fill
+    torch.use_deterministic_algorithms(prev_det, warn_only=prev_warn)
+
+
+def _grad_norm(params):
+    gs = [p.grad for p in params if p.grad is not None]
+    return torch.stack(torch._foreach_norm(gs)).norm().item()
+
+
+@pytest.mark.parametrize("pos", ["none", "rel"])
+def test_bench_harness_graph_steps_finite(poisoned, pos):
+    import bench
+    dev = torch.device("cuda", 0)
+    # (name, layers, d, heads, ffn, K, batch, seconds, pos): small Conformer, full front-end (80 mels)
+    cfg = ("tiny", 2, 256, 4, 1024, 15, 6, 3, pos)
+    h = bench.Harness(cfg, dev, dropout=0.1)
+    M = h.B * h.T2
+    pr = bench.KernelProbe(lambda kind, shape, dsc: kind == "gemm" and shape == (M, h.ffn, h.d), dev)
+    wp = bench.KernelProbe(lambda kind, shape, dsc: kind == "wgroup", dev)
+    bench.ops.PROBE = lambda kind, shape, dsc, launch: pr(kind, shape, dsc, lambda: wp(kind, shape, dsc, launch))
+    try:
+        h.setup(2, probes=(pr, wp))
+        assert h.graph is not None and h.probe_graph is not None
+        losses = []
+        for i in range(12):
+            h.graph.replay()
+            torch.cuda.synchronize()
+            loss = h.static_loss.item()
+            gn = _grad_norm(h.params)
+            assert loss == loss and abs(loss) < 1e30, (i, loss)
+            assert gn == gn and gn < 1e30, (i, gn)
+            h.post()
+            if i % 4 == 3:
+                h.probe_replays(1)      # the bench replays the probe graph after its timed loop
+            assert h.params_finite(), i
+            losses.append(loss)
+        assert h.nonfinite_steps() == 0
+        assert pr.mean_ms()[1] > 0 and wp.mean_ms()[1] > 0      # the probe graph really ran its probes
+    finally:
+        bench.ops.PROBE = None
+
+
+def test_conv2_wgrad_graph_replay_matches_eager(poisoned):
+    """The conv2 weight gradient captured into a HIP graph and replayed: equal to the eager result every
+    replay (the round-2 memset + atomics form was not, under replay)."""
+    from nn_conformer_for_speech_recognition_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(3)
+    B, F1, T1, C1, C2 = 4, 37, 148, 512, 128
+    F2, T2 = (F1 - 3) // 2 + 1, (T1 - 3) // 2 + 1
+    h1 = (torch.randn(B, F1, T1, C1, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    dh2 = (torch.randn(B, T2, F2, C2, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    want = ops.conv2_bwd_weight(dh2, h1).clone()
+    ref = torch.einsum("btfo,btfkc->okc", dh2.float(),
+                       torch.stack([h1.float()[:, 2 * f:2 * f + 3].unfold(2, 3, 2)[:, :, :T2].permute(0, 2, 1, 4, 3)
+                                    for f in range(F2)], dim=2).reshape(B, T2, F2, 9, C1)).reshape(C2, 9 * C1)
+    assert ((want - ref).norm() / ref.norm()).item() < 1e-4
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.conv2_bwd_weight(dh2, h1)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = ops.conv2_bwd_weight(dh2, h1)
+    for _ in range(3):
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all()
+        assert torch.equal(out, want)            # deterministic slab order: bit-identical to eager
