@@ -434,6 +434,11 @@ class Harness:
     def nonfinite_steps(self):
         return int(self.bad.item())
 
+    def close(self):
+        """Unbind the device dropout counter (libcfm keeps its address; it dies with this harness)."""
+        torch.cuda.synchronize()
+        _lib.call("cfm_rng_bind", None)
+
     def params_finite(self):
         """All parameters finite (one pass over the weights; after the timed region)."""
         ok = torch.ones(1, dtype=torch.bool, device=self.dev)

@@ -697,7 +697,7 @@ __device__ __forceinline__ void wait_stages(int younger) {
 // 64x64 per wave; (192, 8, 4) -> 96x32 per wave (192-row tiles: 63 x N/128 tiles of the encoder's
 // M = 11,936 fill the 256 CUs in whole rounds); (128, 4, 2) -> 64x64.
 struct WgTask;   // grouped weight-gradient task (below)
-__device__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn);
+__device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn);
 
 // F8: A and B are fp8 e4m3 (OCP), K-major, viewed as bf16 PAIRS by everything up to the LDS image (K, ld and
 // the tile geometry in 2-byte units, so DMA, swizzle and ring are byte-identical to the bf16 kernel); each
@@ -1122,7 +1122,7 @@ struct WgTask {
 };
 static_assert(sizeof(WgTask) % 4 == 0, "word-copied task");
 
-__device__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn) {
+__device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn) {
   const WgTask* tab = reinterpret_cast<const WgTask*>(ga.group_tab);
   const int nwg = gridDim.x, L = blockIdx.x;
   int id = L;

@@ -43,7 +43,7 @@ def test_bench_harness_graph_steps_finite(poisoned, pos):
     dev = torch.device("cuda", 0)
     # (name, layers, d, heads, ffn, K, batch, seconds, pos): small Conformer, full front-end (80 mels)
     cfg = ("tiny", 2, 256, 4, 1024, 15, 6, 3, pos)
-    h = bench.Harness(cfg, dev, dropout=0.1)
+    h = bench.Harness(cfg, dev, dropout=0.1)      # binds its device dropout counter (cfm_rng_bind)
     M = h.B * h.T2
     pr = bench.KernelProbe(lambda kind, shape, dsc: kind == "gemm" and shape == (M, h.ffn, h.d), dev)
     wp = bench.KernelProbe(lambda kind, shape, dsc: kind == "wgroup", dev)
@@ -68,6 +68,7 @@ def test_bench_harness_graph_steps_finite(poisoned, pos):
         assert pr.mean_ms()[1] > 0 and wp.mean_ms()[1] > 0      # the probe graph really ran its probes
     finally:
         bench.ops.PROBE = None
+        h.close()        # libcfm holds the address of the harness's dropout counter: unbind before it is freed
 
 
 def test_conv2_wgrad_graph_replay_matches_eager(poisoned):
