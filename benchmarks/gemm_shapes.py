@@ -30,7 +30,12 @@ def timeit(fn, n=20, warm=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--torch", action="store_true", help="also time torch (hipBLASLt) on the bare GEMMs")
+    ap.add_argument("--mode", type=int, default=None, help="cfm_gemm_set_mode value")
     a = ap.parse_args()
+    if a.mode is not None:
+        from nn_conformer_for_speech_recognition_amd import _lib
+        _lib.call("cfm_gemm_set_mode", a.mode)
     M, d, F = 32 * 373, 512, 2048
     bf = torch.bfloat16
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -69,6 +74,20 @@ def main():
         t = sorted(res_t[k])[len(res_t[k]) // 2]
         out[k] = round(t, 2)
         print(f"{k:48s} {t:8.2f} us {fl / t / 1e6:7.0f} TF/s")
+    if a.torch:
+        import torch.nn.functional as tF
+        tc = {"torch ffn_up fwd (bias only)": (2 * M * F * d, lambda: tF.linear(x512, w_up)),
+              "torch ffn_down fwd (bf16 out)": (2 * M * F * d, lambda: tF.linear(x2048, w_dn)),
+              "torch qkv fwd": (2 * M * 3 * d * d, lambda: tF.linear(x512, w_qkv)),
+              "torch out fwd": (2 * M * d * d, lambda: tF.linear(x512, w_o)),
+              "torch ffn_down dgrad (da = g2 W2)": (2 * M * F * d, lambda: torch.mm(g2, w_dn)),
+              "torch ffn_up dgrad (dx = da W1)": (2 * M * F * d, lambda: torch.mm(da, w_up)),
+              "torch wgrad ffn_up (dW1 = da^T x)": (2 * M * F * d, lambda: torch.mm(da.t(), x512)),
+              "torch wgrad ffn_down (dW2 = g2^T h)": (2 * M * F * d, lambda: torch.mm(g2.t(), x2048))}
+        for k, (fl, fn) in tc.items():
+            t = sorted(timeit(fn) for _ in range(a.reps))[a.reps // 2]
+            out[k] = round(t, 2)
+            print(f"{k:48s} {t:8.2f} us {fl / t / 1e6:7.0f} TF/s")
     # grouped weight gradients of one layer (8 GEMMs) as the step launches them
     grp = ops.WgradGroup()
     pairs = [(g2, x2048), (da, x512), (g2, x2048), (da, x512), (qkv, x512), (g2, x512), (rn(M, 2 * d), x512),
@@ -82,7 +101,7 @@ def main():
     t = sorted(timeit(wg, n=10) for _ in range(a.reps))[a.reps // 2]
     out["wgrad group (1 layer, 8 GEMMs)"] = round(t, 2)
     print(f"{'wgrad group (1 layer, 8 GEMMs)':48s} {t:8.2f} us {fl / t / 1e6:7.0f} TF/s")
-    print(json.dumps({"lib": os.environ.get("CFM_LIB", "default"), "us": out}))
+    print(json.dumps({"lib": os.environ.get("CFM_LIB", "default"), "mode": a.mode, "us": out}))
 
 
 if __name__ == "__main__":

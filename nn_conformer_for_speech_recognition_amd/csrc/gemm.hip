@@ -493,7 +493,16 @@ __device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2
 // rows).  Rows are staged through LDS in chunks of CHB bands (<= 128 rows), then every thread
 // finishes 8 consecutive columns of a row (16-B / 32-B vector stores).  The caller guarantees every
 // wave is done reading the staging LDS (`st`, >= 128 x EP_STRIDE floats).
-template <int FM, int FN, int WM, int WN, int NTt, int BNt = BN>
+// (row, col) inside a 32x32 accumulator block of register r: the 32x32x16 MFMA layout, or (M16) four 16x16x32
+// blocks packed as r = 4 (2a + b) + q -> block (a, b) of the 32x32, register q
+template <bool M16> __device__ __forceinline__ int accr(int r, int lane) {
+  return M16 ? 16 * ((r >> 3) & 1) + 4 * (lane >> 4) + (r & 3) : (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+template <bool M16> __device__ __forceinline__ int accc(int r, int lane) {
+  return M16 ? 16 * ((r >> 2) & 1) + (lane & 15) : (lane & 31);
+}
+
+template <int FM, int FN, int WM, int WN, int NTt, int BNt = BN, bool M16 = false>
 __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM][FN], float* st, int z, int zs,
                                                 int m0, int n0, int wm, int wn, int lane, int tid) {
   constexpr int BAND = FM * 32, CHB = (128 / BAND) >= 1 && WM % (128 / BAND) == 0 ? 128 / BAND : 1;
@@ -508,8 +517,8 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * BAND + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const int n = n0 + wn * FN * 32 + j * 32 + (lane & 31);
+          const int m = m0 + wm * BAND + i * 32 + accr<M16>(r, lane);
+          const int n = n0 + wn * FN * 32 + j * 32 + accc<M16>(r, lane);
           epilogue_store(p, z, zs, m, n, acc[i][j][r]);
         }
     return;
@@ -523,8 +532,8 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int row = (wm % CHB) * BAND + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            const int col = wn * FN * 32 + j * 32 + (lane & 31);
+            const int row = (wm % CHB) * BAND + i * 32 + accr<M16>(r, lane);
+            const int col = wn * FN * 32 + j * 32 + accc<M16>(r, lane);
             st[row * EPS + col] = acc[i][j][r];
           }
     }
@@ -632,9 +641,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pipe_rsrc(const PipeOp& o, int
                                            __builtin_amdgcn_readfirstlane((int)o.bytes), 0x00020000);
 }
 
-// one wave-instruction of LDS-DMA: lane l's 16 B from rsrc + voff land at lds_base + 16 l
+// one wave-instruction of LDS-DMA: lane l's 16 B from rsrc + voff land at lds_base + 16 l.
+// Issued through inline asm: the compiler then does not know that it writes LDS, and does not put a
+// conservative `s_waitcnt vmcnt(0)` in front of the next LDS read it cannot prove disjoint (it did so in the
+// grouped weight-gradient loop, where every K step then waited for the DMA it had just issued).  Every
+// consumer waits with its own counted vmcnt + barrier, so no compiler-inserted wait is needed.
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 16, voff, 0, 0, 0);
+  const unsigned l = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_base);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(l), "v"(voff), "s"(r) : "memory", "m0");
 }
 
 // K-major [R][BKt] image: BKt*2-B rows, RPB rows per 256-B bank row, CPR 16-B chunks per row;
@@ -683,6 +699,15 @@ __device__ __forceinline__ bf16x8 pipe_frag(const char* img, int row0, int kk, i
   }
 }
 
+// one 16x16x32 operand fragment (rows row0 .. row0+15, k = kk + 8 (lane >> 4) .. +7) from a K-major swizzled
+// stage image: conflict-free ds_read_b128 on the 64-deep images (kk a multiple of 16)
+template <int BKt>
+__device__ __forceinline__ bf16x8 pipe_frag16k(const char* img, int row0, int kk, int lane) {
+  typedef KmSw<BKt> S;
+  const int r = row0 + (lane & 15), c = (kk >> 3) + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(img + r * S::RB + 16 * S::slot(r, c));
+}
+
 // wait until at most `younger` stages (of PER DMA instructions each) are still in flight
 template <int PER>
 __device__ __forceinline__ void wait_stages(int younger) {
@@ -704,11 +729,15 @@ __device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& 
 // 64-fp8 k-step (4 16-B chunks of a row) feeds one v_mfma_scale_f32_32x32x64_f8f6f4: lane (r, h) holds the
 // 32 bytes k = 32h .. 32h+31 (chunks 2h, 2h+1).  Unit block scales; the per-tensor dequantisation
 // (alpha_a * alpha_b) is applied in the epilogue.
+// M16: the main loop on v_mfma_f32_16x16x32_bf16 (each 32x32 block of a wave's tile as four 16x16 blocks; same
+// LDS images, fragments per k and accumulator registers) -- K-major plain operands only.  On random data the
+// chip holds a higher clock under the 16x16 shape than under 32x32x16 (MI355X_MICROARCH.md, DVFS item 7).
 template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2, bool GA = false,
-          bool GROUP = false, bool F8 = false, int BNt = BN>
+          bool GROUP = false, bool F8 = false, int BNt = BN, bool M16 = false>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(OCC * NWV / 4)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   static_assert(!F8 || (AK && BKM && !GA && !GROUP && BKt % 32 == 0), "fp8: K-major plain operands");
+  static_assert(!M16 || (AK && BKM && !GA && !GROUP && !F8 && BKt % 32 == 0), "16x16x32: K-major plain bf16");
   typedef PipeGeo<BMt, BKt, NST, NWV, BNt> G;
   constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BNt / WN / 32;
   static_assert(WM * FM * 32 == BMt && WN * FN * 32 == BNt, "wave tiling");
@@ -796,6 +825,11 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x16){0};
+  f32x4 acc4[M16 ? 2 * FM : 1][M16 ? 2 * FN : 1];
+#pragma unroll
+  for (int i = 0; i < (M16 ? 2 * FM : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < (M16 ? 2 * FN : 1); ++j) acc4[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   // bias gradient of a weight-gradient GEMM: column sums of the staged MN-major A tile ([k][BMt],
   // chunk c of k-row k at slot c ^ 4(k&3)); thread = one 8-column chunk x every RGth k-row
   constexpr int ACH = BMt / 8, RG = G::NTt / ACH;
@@ -848,6 +882,26 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
                                                                         127, 0, 127);
       continue;
     }
+    if constexpr (M16) {
+      constexpr int KS32 = BKt / 32;
+      bf16x8 a16[KS32][2 * FM], b16[KS32][2 * FN];
+#pragma unroll
+      for (int q = 0; q < KS32; ++q) {
+#pragma unroll
+        for (int j = 0; j < 2 * FN; ++j) b16[q][j] = pipe_frag16k<BKt>(sb, wn * FN * 32 + 16 * j, 32 * q, lane);
+#pragma unroll
+        for (int i = 0; i < 2 * FM; ++i) a16[q][i] = pipe_frag16k<BKt>(sa, wm * FM * 32 + 16 * i, 32 * q, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < KS32; ++q)
+#pragma unroll
+        for (int i = 0; i < 2 * FM; ++i)
+#pragma unroll
+          for (int j = 0; j < 2 * FN; ++j)
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a16[q][i], b16[q][j], acc4[i][j], 0, 0, 0);
+      continue;
+    }
     // every fragment of the stage is read up front (the stage is complete after the barrier), so the
     // LDS latency of later k-steps hides under the MFMAs of earlier ones
     constexpr int KST = BKt / 16;
@@ -892,6 +946,14 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
       }
     }
   }
+  if constexpr (M16) {   // pack the 16x16 blocks into the 32x32 accumulator registers (accr / accc<true>)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = acc4[2 * i + ((r >> 3) & 1)][2 * j + ((r >> 2) & 1)][r & 3];
+  }
   if (p.dbg & 1) {   // timing experiment: keep the accumulators live, store nothing
     float t = 0.f;
 #pragma unroll
@@ -908,8 +970,203 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     if (p.alpha_a) p.alpha *= p.alpha_a[0];
     if (p.alpha_b) p.alpha *= p.alpha_b[0];
   }
-  tile_epilogue_g<FM, FN, WM, WN, G::NTt, BNt>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane, tid);
+  tile_epilogue_g<FM, FN, WM, WN, G::NTt, BNt, M16>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane,
+                                                      tid);
   probe_end(p.probe);
+}
+
+extern int g_gemm_mode;
+// ---------------------------------------------------------------- persistent, register-deferred epilogue
+// For the encoder's wide-output, short-reduction GEMMs (K = 512; N = 1024-2048: FFN up-projection with its
+// bias + SiLU + dropout + pre-activation epilogue, QKV and pointwise-conv-1 forward), whose store traffic
+// (up to 98 MB per launch) left the MFMAs idle through every tile's epilogue.  One workgroup per CU walks
+// a contiguous, XCD-local range of 256 x 128 tiles and the K steps of ALL its tiles form one continuous
+// LDS-DMA stage stream (3-deep ring, BK 64: the next tile's first stages load during the current tile's
+// last steps).  The product is computed TRANSPOSED (16x16x32 MFMA with the weight rows as the A operand),
+// so each lane holds 4 consecutive output columns of one row: a finished tile's accumulators are copied to
+// a second register set and its epilogue -- bias from LDS, SiLU, dropout, bf16 packing, 8-byte range-
+// checked buffer stores -- runs two 16x16 blocks per K step INSIDE the next tile's main loop.  Every K step
+// issues the same number of vector-memory ops (dummy out-of-range DMA / stores where there is nothing to
+// move), so each wait is one compile-time `vmcnt`.  No LDS staging, no barrier for the epilogue.
+constexpr int PS_BM = 256, PS_BN = 128, PS_BK = 64, PS_NK = 8, PS_NST = 3;
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+template <bool PRE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+void gemm_pers_kernel(GemmP p, PipeOp oa, PipeOp ob, int ntm, int ntn, int tper) {
+  constexpr int BMt = PS_BM, BNt = PS_BN, BKt = PS_BK, NK = PS_NK, NST = PS_NST, NWV = 8;
+  constexpr int ABYTES = BMt * BKt * 2, BBYTES = BNt * BKt * 2, STAGE = ABYTES + BBYTES;
+  constexpr int AP = ABYTES / 1024 / NWV, BP = BBYTES / 1024 / NWV;     // DMA pieces per wave per stage (4, 2)
+  constexpr int P = AP + BP;
+  constexpr int SB = PRE ? 2 : 1;       // stores per epilogue block
+  constexpr int S = 2 * SB;             // stores per K step (two 16x16 blocks)
+  static_assert(AP * NWV * 1024 == ABYTES && BP * NWV * 1024 == BBYTES, "whole DMA pieces per wave");
+  constexpr int RING = NST * STAGE;
+  __shared__ __attribute__((aligned(1024))) char lds[RING + 2048 * 4];
+  float* sbias = reinterpret_cast<float*>(lds + RING);
+  probe_begin(p.probe);
+  gemm_drop_prep(p);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;            // 4 x 2 waves of 64 (m) x 64 (n)
+  const int ntiles = ntm * ntn, GW = gridDim.x, Lb = blockIdx.x;
+  const int pos = (GW % 8 == 0) ? (Lb & 7) * (GW / 8) + (Lb >> 3) : Lb;   // XCD-contiguous tile ranges
+  const int t_begin = min(pos * tper, ntiles), t_end = min(t_begin + tper, ntiles);
+  const int ntl = t_end - t_begin;
+  // bias of every output column in LDS for the whole launch (N <= 2048)
+  for (int c = tid; c < p.N; c += 512) sbias[c] = p.bias ? p.bias[c] : 0.f;
+  __syncthreads();
+  if (ntl <= 0) return;
+  const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, 0), rb = pipe_rsrc(ob, 0);
+  const int crec = __builtin_amdgcn_readfirstlane((int)((long)p.M * p.ldc * 2));
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, crec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(PRE ? p.pre : p.C, (short)0, crec, 0x00020000);
+
+  // per-lane DMA source offsets of a tile's stage 0 (later stages add kt * 128 B)
+  auto tile_offs = [&](int t, unsigned (&oA)[AP], unsigned (&oB)[BP]) {
+    const int tm = t / ntn, tn = t % ntn;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) oA[i] = pipe_src<true, BMt, BKt>(oa, (i * NWV + wid) * 64 + lane, tm * BMt, 0);
+#pragma unroll
+    for (int i = 0; i < BP; ++i) oB[i] = pipe_src<true, BNt, BKt>(ob, (i * NWV + wid) * 64 + lane, tn * BNt, 0);
+  };
+  auto issue = [&](int slot, const unsigned (&oA)[AP], const unsigned (&oB)[BP], int kt, bool real) {
+    char* sa = lds + slot * STAGE;
+    char* sb = sa + ABYTES;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) dma16(ra, sa + (i * NWV + wid) * 1024, real ? oA[i] + kt * (BKt * 2) : 0xFFFFFF00u);
+#pragma unroll
+    for (int i = 0; i < BP; ++i) dma16(rb, sb + (i * NWV + wid) * 1024, real ? oB[i] + kt * (BKt * 2) : 0xFFFFFF00u);
+  };
+
+  // epilogue of block b (0..15: jn = b >> 2 over n, im = b & 3 over m) of a finished tile held in `a`
+  // (transposed 16x16 layout: register q <-> column n0w + 16 jn + 4 (lane >> 4) + q, row m0w + 16 im + (lane & 15))
+  auto epi_block = [&](const f32x4& a, int m0w, int n0w, int jn, int im, bool real) {
+    const int n = n0w + 16 * jn + 4 * (lane >> 4), m = m0w + 16 * im + (lane & 15);
+    float v[4] = {a[0], a[1], a[2], a[3]};
+    const float4 bs = *reinterpret_cast<const float4*>(sbias + n);
+    v[0] = v[0] * p.alpha + bs.x; v[1] = v[1] * p.alpha + bs.y; v[2] = v[2] * p.alpha + bs.z; v[3] = v[3] * p.alpha + bs.w;
+    const unsigned off = (real && !(p.dbg & 16)) ? (unsigned)(((long)m * p.ldc + n) * 2) : 0xFFFFFFF0u;
+    if constexpr (PRE) {
+      bf16x4 pv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pv[e] = (bf16)v[e];
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, pv), rp, off, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
+    }
+    if (p.drop_p > 0.f) {   // the epilogue_store8 keying: pair (n, n+1) of row m shares one 32-bit hash
+      const uint32_t j0 = (uint32_t)((p.doff + (uint64_t)((long)m * p.N + n)) >> 1);
+      const uint32_t h0 = cfm_mix32(j0 ^ p.dkey0), h1 = cfm_mix32((j0 + 1) ^ p.dkey0);
+      v[0] *= (h0 & 0xFFFFu) >= p.dthr ? p.dkeep : 0.f;
+      v[1] *= (h0 >> 16) >= p.dthr ? p.dkeep : 0.f;
+      v[2] *= (h1 & 0xFFFFu) >= p.dthr ? p.dkeep : 0.f;
+      v[3] *= (h1 >> 16) >= p.dthr ? p.dkeep : 0.f;
+    }
+    bf16x4 cv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cv[e] = (bf16)(v[e] * p.out_scale);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, cv), rc, off, 0, 0);
+  };
+
+  f32x4 acc[4][4], prv[4][4];   // [jn][im]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = prv[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  int pm0w = 0, pn0w = 0;
+  bool pend = false;
+  unsigned cA[AP], cB[BP], nA[AP], nB[BP];
+  tile_offs(t_begin, cA, cB);
+  if (ntl > 1) tile_offs(t_begin + 1, nA, nB);
+  else {
+#pragma unroll
+    for (int i = 0; i < AP; ++i) nA[i] = cA[i];
+#pragma unroll
+    for (int i = 0; i < BP; ++i) nB[i] = cB[i];
+  }
+  // prologue: stages 0, 1 of the first tile, each followed by S dropped stores (uniform vmcnt accounting)
+  const u32x2_t zero2 = {0u, 0u};
+  issue(0, cA, cB, 0, true);
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int s2 = 0; s2 < S; ++s2) __builtin_amdgcn_raw_buffer_store_b64(zero2, rc, 0xFFFFFFF0u, 0, 0);
+  asm volatile("" ::: "memory");
+  issue(1, cA, cB, 1, true);
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int s2 = 0; s2 < S; ++s2) __builtin_amdgcn_raw_buffer_store_b64(zero2, rc, 0xFFFFFFF0u, 0, 0);
+  asm volatile("" ::: "memory");
+
+  int g = 0;    // global stage index of this workgroup (slot = g % NST)
+  for (int lt = 0; lt < ntl; ++lt) {
+    const int t = t_begin + lt;
+    const int m0w = (t / ntn) * BMt + wm * 64, n0w = (t % ntn) * BNt + wn * 64;
+    const bool has_next = lt + 1 < ntl;
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt, ++g) {
+      // stage g landed once only stores(g-2), DMA(g+1), stores(g-1) are younger than it
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * S + P) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // DMA of stage g+2: this tile's kt+2, or the next tile's first stages (dropped past the last tile)
+      if (kt + 2 < NK) issue((g + 2) % NST, cA, cB, kt + 2, true);
+      else issue((g + 2) % NST, nA, nB, kt + 2 - NK, has_next);
+      asm volatile("" ::: "memory");   // (issue order = the vmcnt accounting: DMA(g+2) before this step's stores)
+      // two 16x16 epilogue blocks of the previous tile (dropped stores when there is none)
+      epi_block(prv[(2 * kt) >> 2][(2 * kt) & 3], pm0w, pn0w, (2 * kt) >> 2, (2 * kt) & 3, pend);
+      epi_block(prv[(2 * kt + 1) >> 2][(2 * kt + 1) & 3], pm0w, pn0w, (2 * kt + 1) >> 2, (2 * kt + 1) & 3, pend);
+      asm volatile("" ::: "memory");
+      const char* sa = lds + (g % NST) * STAGE;
+      const char* sb = sa + ABYTES;
+#pragma unroll
+      for (int q = 0; q < BKt / 32; ++q) {
+        bf16x8 fa[4], fb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = pipe_frag16k<BKt>(sb, wn * 64 + 16 * j, 32 * q, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = pipe_frag16k<BKt>(sa, wm * 64 + 16 * i, 32 * q, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
+      }
+    }
+    // this tile becomes the pending one; the next tile's offsets move up
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        prv[j][i] = acc[j][i];
+        acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    pm0w = m0w;
+    pn0w = n0w;
+    pend = true;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) cA[i] = nA[i];
+#pragma unroll
+    for (int i = 0; i < BP; ++i) cB[i] = nB[i];
+    if (lt + 2 < ntl) tile_offs(t_begin + lt + 2, nA, nB);
+  }
+  // the last tile's epilogue
+#pragma unroll
+  for (int b = 0; b < 16; ++b) epi_block(prv[b >> 2][b & 3], pm0w, pn0w, b >> 2, b & 3, true);
+  probe_end(p.probe);
+}
+
+// the persistent kernel serves K-major bf16 GEMMs with K == 512, N a multiple of 128 (<= 2048), bf16 output and
+// an epilogue of bias / alpha / (SiLU + pre) / dropout / out_scale only.  Opt-in (cfm_gemm_set_mode bit 15):
+// same-box A/B, FFN up-projection 63.7 -> 56.7 us but QKV 37.8 -> 39.9 us and the L15 step 24.0 -> 24.3 ms
+// (the epilogue's stores and the stage waits share one in-order vmcnt, so a K step that waits for its stage
+// also waits for the previous tile's stores)
+bool pers_ok(const cfm_gemm_desc& d, const GemmP& p) {
+  return (g_gemm_mode & 32768) && d.a_kmajor && d.b_kmajor && d.batch == 1 && p.split_k == 1 && d.K == 512 &&
+         p.N % PS_BN == 0 && p.N <= 2048 && p.N >= 1024 && !p.res && !p.act_grad && !p.cmap && !p.rd_out &&
+         !p.acs_slab && !p.slab && p.dtc == CFM_BF16 && p.ldc % 4 == 0 && (p.act == 0 || (p.act == CFM_ACT_SILU &&
+         p.pre && p.dtpre == CFM_BF16)) && (long)p.M * p.ldc * 2 < (1L << 31) - 64 && !p.dbg &&
+         p.alpha_a == nullptr && p.alpha_b == nullptr && ((uintptr_t)p.C % 8) == 0 &&
+         (p.pre == nullptr || ((uintptr_t)p.pre % 8) == 0) && d.lda == 512 && d.ldb == 512;
 }
 
 // ---------------------------------------------------------------- persistent, interleaved epilogue
@@ -1351,7 +1608,7 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 //   V128: 128x128 tile, BK 64, 3-stage ring (96 KiB, 4 waves)
 //   V128S: 128x128 tile, BK 32, 3-stage ring (68 KiB incl. the aliased epilogue staging: two
 //          workgroups of 4 waves per CU) -- narrow outputs (N = 512) fill the chip
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, bool M16 = false>
 void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
   const int sel = (g_gemm_mode >> 4) & 7;   // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S, 5 V192, 6 V192S, 7 V192S8
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k), g128(cdiv(p.N, BN), cdiv(p.M, 128), batch * p.split_k);
@@ -1361,7 +1618,14 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
     // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
     if (v == 5 || (v == 0 && p.N <= 512 && p.split_k == 1 && p.M >= 4096)) {
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
-      hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob, GatherA{});
+      // 4-deep ring (4 x 40 KiB = the whole 160 KiB LDS): FFN-up data gradient 34.2 -> 32.5 us same-box;
+      // cfm_gemm_set_mode bit 14 keeps the 3-deep ring (A/B)
+      if (!(g_gemm_mode & 16384))
+        hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 4, 1, AK, BKM, 8, 4, false, false, false, BN, M16>), g192,
+                           dim3(512), 0, s, p, oa, ob, GatherA{});
+      else
+        hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, AK, BKM, 8, 4, false, false, false, BN, M16>), g192,
+                           dim3(512), 0, s, p, oa, ob, GatherA{});
       return;
     }
     // auto: 1024- / 1536-wide outputs of short reductions (QKV, pointwise-conv-1 forward) take 192-row tiles
@@ -1373,7 +1637,8 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
       v = 7;
     if (v == 7) {   // 192 x 128 tiles, 8 waves of 96 x 32, BK 32 (uneven A DMA split): two per CU
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
-      hipLaunchKernelGGL((gemm_pipe_kernel<192, 32, 3, 2, AK, BKM, 8, 4>), g192, dim3(512), 0, s, p, oa, ob, GatherA{});
+      hipLaunchKernelGGL((gemm_pipe_kernel<192, 32, 3, 2, AK, BKM, 8, 4, false, false, false, BN, M16>), g192, dim3(512),
+                         0, s, p, oa, ob, GatherA{});
       return;
     }
     if (v == 6) {   // 192 x 128 tiles, 4 waves of 96x64, BK 32: two workgroups per CU
@@ -1388,8 +1653,12 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
     // 256-row workgroups per CU so one's epilogue hides under the other's MFMAs; long ones keep BK 64
     v = p.k_per_split <= 512 ? 2 : 1;      // (V128S measured no faster for N = 512 outputs)
   }
-  if (v == 1) hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob, GatherA{});
-  else if (v == 2) hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, AK, BKM>), g256, dim3(512), 0, s, p, oa, ob, GatherA{});
+  if (v == 1)
+    hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, AK, BKM, 8, 2, false, false, false, BN, M16>), g256, dim3(512), 0,
+                       s, p, oa, ob, GatherA{});
+  else if (v == 2)
+    hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, AK, BKM, 8, 2, false, false, false, BN, M16>), g256, dim3(512), 0,
+                       s, p, oa, ob, GatherA{});
   else if (v == 4) hipLaunchKernelGGL((gemm_pipe_kernel<128, 32, 3, 2, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob, GatherA{});
   else hipLaunchKernelGGL((gemm_pipe_kernel<128, 64, 3, 1, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob, GatherA{});
 }
@@ -1422,6 +1691,17 @@ int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   const PipeOp oa{(const bf16*)d.A, d.lda, d.stride_a, d.M, (unsigned)(ea * 2)};
   const PipeOp ob{(const bf16*)d.B, d.ldb, d.stride_b, d.N, (unsigned)(eb * 2)};
   const bool ak = d.a_kmajor != 0, bkm = d.b_kmajor != 0;
+  if (pers_ok(d, p)) {
+    const int ntm = cdiv(p.M, PS_BM), ntn = p.N / PS_BN, ntiles = ntm * ntn;
+    const int grid = min(ntiles, num_cus());
+    const int tper = cdiv(ntiles, grid);
+    if (g_gemm_mode & 65536) p.dbg |= 16;   // timing experiment: every epilogue store dropped (range check)
+    if (p.act == CFM_ACT_SILU)
+      hipLaunchKernelGGL((gemm_pers_kernel<true>), dim3(grid), dim3(512), 0, s, p, oa, ob, ntm, ntn, tper);
+    else
+      hipLaunchKernelGGL((gemm_pers_kernel<false>), dim3(grid), dim3(512), 0, s, p, oa, ob, ntm, ntn, tper);
+    return CFM_OK;
+  }
   if (ie_ok(d, p)) {
     const int ntm = cdiv(p.M, IE_BM), ntn = p.N / BN;
     const int grid = min(ntm * ntn, num_cus());
@@ -1431,7 +1711,10 @@ int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
       hipLaunchKernelGGL((gemm_pipe_ie_kernel<false>), dim3(grid), dim3(IE_NWV * 64), 0, s, p, oa, ob, ntm, ntn);
     return CFM_OK;
   }
-  if (ak && bkm) launch_pipe_t<true, true>(p, oa, ob, d.batch, s);
+  // the K-major x K-major GEMMs (forward and data-gradient) run 16x16x32 MFMA main loops (L15 step 25.0 -> 24.7 ms
+  // same-box A/B); cfm_gemm_set_mode bit 13 selects the 32x32x16 form
+  if (ak && bkm && !(g_gemm_mode & 8192)) launch_pipe_t<true, true, true>(p, oa, ob, d.batch, s);
+  else if (ak && bkm) launch_pipe_t<true, true>(p, oa, ob, d.batch, s);
   else if (ak) launch_pipe_t<true, false>(p, oa, ob, d.batch, s);
   else if (bkm) launch_pipe_t<false, true>(p, oa, ob, d.batch, s);
   else launch_pipe_t<false, false>(p, oa, ob, d.batch, s);

@@ -46,7 +46,9 @@ def gemm_mode():
     _lib.call("cfm_gemm_set_mode", 3)
 
 
-@pytest.mark.parametrize("mode", [1, 18, 34, 50, 82, 98, 114])   # register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128 / 192x128 BK64, BK32 4 waves, BK32 8 waves (AK only)
+# register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128 / 192x128 BK64, BK32 4 waves, BK32 8 waves (AK only);
+# K-major x K-major run 16x16x32 MFMA main loops by default, + 8192 the 32x32x16 form; + 16384: 4-deep ring (192 rows)
+@pytest.mark.parametrize("mode", [1, 18, 34, 50, 82, 98, 114, 8192 | 18, 8192 | 34, 8192 | 82, 8192 | 114, 16384 | 82])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(1000, 512, 512), (264, 136, 192), (520, 264, 1000), (8, 8, 64)])
 def test_gemm_kernel_variants(gemm_mode, mode, ak, bk, M, N, K):
@@ -421,3 +423,36 @@ def test_wgrad_group_wide_tiles_match_per_gemm(gemm_mode):
         ref = d.float().T @ x.float()
         assert _rel(b, ref) < 1e-5 and _rel(a, ref) < 1e-5
         assert _rel(bb, d.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("M,N", [(11936, 2048), (1000, 1536), (300, 1024), (11936, 1024)])
+@pytest.mark.parametrize("epi", ["bias", "silu_pre_drop", "scaled"])
+def test_gemm_persistent_deferred_epilogue_matches_pipeline(gemm_mode, M, N, epi):
+    """The persistent register-deferred-epilogue kernel (K = 512, N 1024-2048, bf16 out; opt-in with
+    cfm_gemm_set_mode bit 15) against the tiled LDS-DMA pipeline (the default) on the same inputs:
+    fp32 pre-activations within accumulation-order noise, bf16 outputs within one rounding step, and the
+    dropout masks identical (same element keying)."""
+    K = 512
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    outs = []
+    for mode in (3 | 32768, 3):
+        gemm_mode(mode)
+        y = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+        pre = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+        if epi == "bias":
+            ops.linear(x, w, b, out=y)
+        elif epi == "silu_pre_drop":
+            ops.linear(x, w, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=5, out=y)
+        else:
+            ops.gemm(x, w, y, M, N, K, a_kmajor=True, b_kmajor=True, alpha=0.5, bias=b, out_scale=2.0)
+        torch.cuda.synchronize()
+        outs.append((y.float().clone(), pre.float().clone()))
+    (y0, p0), (y1, p1) = outs
+    assert torch.isfinite(y0).all() and (y0 != 7.0).float().mean() > 0.99       # every element written
+    assert _rel(y0, y1) < 4e-3
+    if epi == "silu_pre_drop":
+        assert _rel(p0, p1) < 4e-3
+        assert torch.equal(y0 == 0, y1 == 0)          # identical dropout masks
