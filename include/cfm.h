@@ -290,6 +290,16 @@ int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dtype_a, const float*
 /* With dw == NULL, cfm_glu_dwconv_bwd leaves the depthwise weight/bias partial sums in ws; this
    reduces them (deterministically) into dw (C x K) and db (C) -- on any stream ordered after it. */
 int cfm_glu_dwconv_bwd_wgrad(float* ws, int B, int T, int C, int K, float* dw, float* db, void* stream);
+/* cfm_bn_silu_bwd_apply folded into cfm_glu_dwconv_bwd: the BatchNorm1d + SiLU input gradient
+ *   dy = gamma*invstd*(du - dbeta*invM - yhat*dgamma*invM)   (training; eval: gamma*invstd*du)
+ * is formed inside the depthwise backward from dz, y and the stats, never stored (torchaudio
+ * ConformerLayer conv_module BatchNorm1d -> SiLU -> depthwise).  dbeta / dgamma:
+ * from cfm_bn_silu_bwd_sums (or their SyncBatchNorm all-reduced totals with invM = 1 / rows summed
+ * over).  K must be one of 3, 5, 7, 15, 31, 33.  dw == NULL: partials left in ws as above. */
+int cfm_glu_dwconv_bwd_bn(const void* dz, int dtype_dz, const float* y, const float* gamma, const float* beta,
+                          const float* mean, const float* invstd, const float* dbeta, const float* dgamma,
+                          float invM, int training, const void* a, int dtype_a, const float* w_dw, void* da,
+                          int dtype_da, float* dw, float* db, int B, int T, int C, int K, float* ws, void* stream);
 
 /* ---------------------------------------------------------------- Attention
  * nn.MultiheadAttention(need_weights=False, key_padding_mask) core (torchaudio ConformerLayer

@@ -121,6 +121,9 @@ _SIGS = {
                            c_void_p, c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_void_p]),
     "cfm_bn_bwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                            c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p]),
+    "cfm_glu_dwconv_bwd_bn": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_float, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                      c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "cfm_glu_dwconv_bwd_wgrad": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "cfm_glu_dwconv_bwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                    c_int, c_int, c_int, c_int, c_void_p, c_void_p]),

@@ -325,12 +325,19 @@ def _conv_bwd(g, x, sv, P, cfg, seed, grads, side, g2=None, nxt=None):
     grads[20] = dw.view(d, d, 1)
     dz = ops.linear_dgrad(g3, wp2, wt=_wt(cfg, 20))
     ws = ops.convmod_ws(B, T, d, K, x.device)
-    if cfg.sync_bn is not None and cfg.training:
-        dy, grads[18], grads[19] = ops.bn_silu_bwd_sync(dz, yv, P[18], P[19], bmean, binv, ws, cfg.sync_bn[0],
-                                                        cfg.sync_bn[1])
+    sync = cfg.sync_bn is not None and cfg.training
+    dy = None
+    if K in ops.BN_FOLD_K and "bnfold" not in ops.DISABLED:     # (CFM_DISABLE=bnfold: separate BN backward, A/B)
+        da, dwdw, grads[17], grads[18], grads[19] = ops.bn_silu_glu_dwconv_bwd(
+            dz, yv, P[18], P[19], bmean, binv, cfg.training, a, wdw, B, T, d, K, ws, cd, side=side,
+            reduce_sums=cfg.sync_bn[0] if sync else None, world=cfg.sync_bn[1] if sync else 1)
     else:
-        dy, grads[18], grads[19] = ops.bn_silu_bwd(dz, yv, P[18], P[19], bmean, binv, cfg.training, ws)
-    da, dwdw, grads[17] = ops.glu_dwconv_bwd(dy, a, wdw, B, T, d, K, ws, cd, side=side)
+        if sync:
+            dy, grads[18], grads[19] = ops.bn_silu_bwd_sync(dz, yv, P[18], P[19], bmean, binv, ws, cfg.sync_bn[0],
+                                                            cfg.sync_bn[1])
+        else:
+            dy, grads[18], grads[19] = ops.bn_silu_bwd(dz, yv, P[18], P[19], bmean, binv, cfg.training, ws)
+        da, dwdw, grads[17] = ops.glu_dwconv_bwd(dy, a, wdw, B, T, d, K, ws, cd, side=side)
     grads[16] = dwdw.view(d, 1, K)
     dw, grads[15] = _wgrad_bias(side, da, xn, 14)
     grads[14] = dw.view(2 * d, d, 1)

@@ -9,6 +9,8 @@
 // padded frames — exactly what torchaudio/transformers do (padding is not masked there).
 // Per-workgroup partial sums go to a workspace and are combined by cfm::colreduce
 // (deterministic two-level reduction; no atomics).
+#include <cstdlib>
+
 #include "cfm_common.h"
 
 namespace {
@@ -116,6 +118,88 @@ __global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const void* __restr
   if (wv == 0 && c < C) {
     const float a1 = sg[lane] + sg[CT + lane] + sg[2 * CT + lane] + sg[3 * CT + lane];
     const float a2 = sg[4 * CT + lane] + sg[5 * CT + lane] + sg[6 * CT + lane] + sg[7 * CT + lane];
+    const long part_idx = (long)b * gridDim.y + blockIdx.y;
+    const long nparts = (long)gridDim.z * gridDim.y;
+    part[part_idx * C + c] = a1;
+    part[(nparts + part_idx) * C + c] = a2;
+  }
+}
+
+// Vectorised forward (bf16 a, C % 4 == 0, compiled K): staging loads and the y stores move 4 channels per lane
+// (8- / 16-byte accesses) through LDS; the taps run lane = channel as above.  Same partial-sum layout.
+template <int KT>
+__global__ __launch_bounds__(256) void glu_dwconv_fwd_vec_kernel(const bf16* __restrict__ a,
+                                                                 const float* __restrict__ w,
+                                                                 const float* __restrict__ bias,
+                                                                 float* __restrict__ y, int T, int C,
+                                                                 float* __restrict__ part) {
+  constexpr int PAD = (KT - 1) / 2, ROWS = TT + KT - 1, NP = (ROWS + 15) / 16;
+  constexpr int FB = TT / 4, WN = FB + KT - 1;
+  constexpr int L_OUT = TT * CT + 8 * CT;
+  __shared__ __attribute__((aligned(16))) float sm[ROWS * CT > L_OUT ? ROWS * CT : L_OUT];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int q = tid & 15, rs = tid >> 4;
+  const int c0 = blockIdx.x * CT, t0 = blockIdx.y * TT, b = blockIdx.z;
+  const int cq = c0 + 4 * q;
+  const bool cok = cq < C;
+  const int cqc = cok ? cq : C - 4;
+  const int c = c0 + lane, cw = c < C ? c : C - 1;
+  float wr[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) wr[k] = w[cw * KT + k];
+  const float bb = bias[cw];
+  bf16x4 x4[NP], g4[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int t = min(max(t0 - PAD + rs + 16 * p, 0), T - 1);
+    const long row = (long)b * T + t;
+    x4[p] = *reinterpret_cast<const bf16x4*>(a + row * 2 * C + cqc);
+    g4[p] = *reinterpret_cast<const bf16x4*>(a + row * 2 * C + C + cqc);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int r = rs + 16 * p, t = t0 - PAD + r;
+    if (r < ROWS) {
+      const bool ok = cok && t >= 0 && t < T;
+      f32x4 g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = ok ? (float)x4[p][j] * sigmoid_f((float)g4[p][j]) : 0.f;
+      *reinterpret_cast<f32x4*>(sm + r * CT + 4 * q) = g;
+    }
+  }
+  __syncthreads();
+  const int tb = wv * FB;
+  float win[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) win[j] = sm[(tb + j) * CT + lane];
+  float acc[FB], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int f = 0; f < FB; ++f) {
+    float v = bb;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) v += wr[k] * win[f + k];
+    acc[f] = v;
+    if (c < C && t0 + tb + f < T) {
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < FB; ++f) sm[(tb + f) * CT + lane] = acc[f];
+  sm[TT * CT + wv * CT + lane] = s1;
+  sm[TT * CT + (4 + wv) * CT + lane] = s2;
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int f = rs + 16 * p - PAD, t = t0 + f;
+    if (f >= 0 && f < TT && t < T && cok)
+      *reinterpret_cast<f32x4*>(y + ((long)b * T + t) * C + cq) = *reinterpret_cast<const f32x4*>(sm + f * CT + 4 * q);
+  }
+  if (wv == 0 && c < C) {
+    const float* r = sm + TT * CT;
+    const float a1 = r[lane] + r[CT + lane] + r[2 * CT + lane] + r[3 * CT + lane];
+    const float a2 = r[4 * CT + lane] + r[5 * CT + lane] + r[6 * CT + lane] + r[7 * CT + lane];
     const long part_idx = (long)b * gridDim.y + blockIdx.y;
     const long nparts = (long)gridDim.z * gridDim.y;
     part[part_idx * C + c] = a1;
@@ -249,14 +333,27 @@ __global__ void bn_bwd_apply_total_kernel(const void* __restrict__ dz, int dtdz,
   }
 }
 
+// BatchNorm1d + SiLU backward folded into the depthwise-conv backward (BN=true): the kernel reads dz (the
+// pointwise-conv-2 data gradient) and the BN input y and forms the BN input gradient
+//   dy = gamma * invstd * (du - dbeta / M - yhat * dgamma / M)   (train; eval: gamma * invstd * du)
+//   du = dz * silu'(yhat * gamma + beta),  yhat = (y - mean) * invstd
+// on the fly, so the fp32 dy never goes through HBM (one write + one read of B*T*C floats and a launch saved).
+struct BnBwd {
+  const void* dz; int dtdz;
+  const float* y;
+  const float *gamma, *beta, *mean, *invstd, *dgamma, *dbeta;
+  float invM;
+  int training;
+};
+
 // backward of y = dwconv(GLU(a)).  grid (ceil(C/CT), ceil(T/TT), B)
 // part: [nparts][K+1][C] per-block partial dw (K taps) and db (tap K).
-template <int KT, typename TA>
+template <int KT, typename TA, bool BN = false>
 __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const float* __restrict__ dy,
                                                              const void* __restrict__ a, int dta,
                                                              const float* __restrict__ w, void* __restrict__ da,
                                                              int dtda, int T, int C, int Krt,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part, BnBwd bn) {
   const int K = KT > 0 ? KT : Krt;
   extern __shared__ float sm[];                  // sdy [(TT+K-1)][CT], sg [(TT+K-1)][CT]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -271,11 +368,23 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const float* __rest
     const int cc = c < C ? c : C - 1;
     const TA* ap = reinterpret_cast<const TA*>(a) + cc;
     float dv[NR], xv[NR], gv[NR];
+    float bg = 0.f, bis = 0.f, bmu = 0.f, bbt = 0.f, bk1 = 0.f, bk2 = 0.f;
+    if constexpr (BN) {
+      bg = bn.gamma[cc]; bis = bn.invstd[cc]; bmu = bn.mean[cc]; bbt = bn.beta[cc];
+      bk1 = bn.training ? bn.dbeta[cc] * bn.invM : 0.f;
+      bk2 = bn.training ? bn.dgamma[cc] * bn.invM : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const int t = min(max(t0 - pad + wv + 4 * i, 0), T - 1);
       const long row = (long)b * T + t;
-      dv[i] = dy[row * C + cc];
+      if constexpr (BN) {
+        const float yh = (bn.y[row * C + cc] - bmu) * bis;
+        const float du = ld_dyn(bn.dz, bn.dtdz, row * C + cc) * silu_grad_f(yh * bg + bbt);
+        dv[i] = bg * bis * (du - bk1 - yh * bk2);
+      } else {
+        dv[i] = dy[row * C + cc];
+      }
       xv[i] = to_f32(ap[row * 2 * C]);
       gv[i] = to_f32(ap[row * 2 * C + C]);
     }
@@ -289,6 +398,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const float* __rest
       }
     }
   } else {
+    static_assert(!BN || KT > 0, "BN folding: compiled kernel sizes only");
     for (int r = wv; r < rows; r += 4) {
       const int t = t0 - pad + r;
       float vd = 0.f, vg = 0.f;
@@ -401,6 +511,155 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_kernel(const float* __rest
   }
 }
 
+// Vectorised backward (bf16 a / da, C % 4 == 0, compiled K): the staging loads and the da stores move 4 channels
+// per lane (8- and 16-byte accesses: the scalar kernel above issues one 2-byte load per lane per row) while the
+// depthwise math stays lane = channel out of LDS.  The GLU-input gradient goes back through LDS so the lane that
+// staged a row's GLU inputs also writes that row's da from its registers (no second read of a).
+// Staging map: thread = (row group rs = tid / 16, channel quad q = tid % 16); pass p covers rows rs + 16 p.
+template <int KT, bool BN, bool DZ16>
+__global__ __launch_bounds__(256) void glu_dwconv_bwd_vec_kernel(const float* __restrict__ dy,
+                                                                 const bf16* __restrict__ a,
+                                                                 const float* __restrict__ w, bf16* __restrict__ da,
+                                                                 int T, int C, float* __restrict__ part, BnBwd bn) {
+  constexpr int PAD = (KT - 1) / 2, ROWS = TT + KT - 1, NP = (ROWS + 15) / 16;
+  constexpr int FB = TT / 4, WN = FB + KT - 1;
+  constexpr int L_STAGE = 2 * ROWS * CT, L_OUT = TT * CT + 4 * (KT + 1) * CT;
+  __shared__ __attribute__((aligned(16))) float sm[L_STAGE > L_OUT ? L_STAGE : L_OUT];
+  float* sdy = sm;                 // [ROWS][CT] dy (staging)      | [TT][CT] dg (output)
+  float* sg = sm + ROWS * CT;      // [ROWS][CT] GLU output        | red [4][KT+1][CT] after TT*CT
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int q = tid & 15, rs = tid >> 4;
+  const int c0 = blockIdx.x * CT, t0 = blockIdx.y * TT, b = blockIdx.z;
+  const int cq = c0 + 4 * q;
+  const bool cok = cq < C;
+  const int cqc = cok ? cq : C - 4;
+  const int c = c0 + lane, cw = c < C ? c : C - 1;
+  float wr[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) wr[k] = w[cw * KT + k];
+  f32x4 bg, bis, bmu, bbt, bk1, bk2;
+  if constexpr (BN) {
+    bg = *reinterpret_cast<const f32x4*>(bn.gamma + cqc);
+    bis = *reinterpret_cast<const f32x4*>(bn.invstd + cqc);
+    bmu = *reinterpret_cast<const f32x4*>(bn.mean + cqc);
+    bbt = *reinterpret_cast<const f32x4*>(bn.beta + cqc);
+    if (bn.training) {
+      bk1 = *reinterpret_cast<const f32x4*>(bn.dbeta + cqc) * bn.invM;
+      bk2 = *reinterpret_cast<const f32x4*>(bn.dgamma + cqc) * bn.invM;
+    } else {
+      bk1 = f32x4{0.f, 0.f, 0.f, 0.f};
+      bk2 = bk1;
+    }
+  }
+  f32x4 v4[NP];
+  bf16x4 z4[NP];
+  bf16x4 x4[NP], g4[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int t = min(max(t0 - PAD + rs + 16 * p, 0), T - 1);
+    const long row = (long)b * T + t;
+    if constexpr (BN) {
+      v4[p] = *reinterpret_cast<const f32x4*>(bn.y + row * C + cqc);
+      if constexpr (DZ16) z4[p] = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const bf16*>(bn.dz) + row * C + cqc);
+    } else {
+      v4[p] = *reinterpret_cast<const f32x4*>(dy + row * C + cqc);
+    }
+    x4[p] = *reinterpret_cast<const bf16x4*>(a + row * 2 * C + cqc);
+    g4[p] = *reinterpret_cast<const bf16x4*>(a + row * 2 * C + C + cqc);
+  }
+  f32x4 zf[NP];
+  if constexpr (BN && !DZ16) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int t = min(max(t0 - PAD + rs + 16 * p, 0), T - 1);
+      zf[p] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(bn.dz) + ((long)b * T + t) * C + cqc);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int r = rs + 16 * p, t = t0 - PAD + r;
+    if (r < ROWS) {
+      const bool ok = cok && t >= 0 && t < T;
+      f32x4 d, g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float dv;
+        if constexpr (BN) {
+          const float yh = (v4[p][j] - bmu[j]) * bis[j];
+          float dzv;
+          if constexpr (DZ16) dzv = (float)z4[p][j];
+          else dzv = zf[p][j];
+          const float du = dzv * silu_grad_f(yh * bg[j] + bbt[j]);
+          dv = bg[j] * bis[j] * (du - bk1[j] - yh * bk2[j]);
+        } else {
+          dv = v4[p][j];
+        }
+        d[j] = ok ? dv : 0.f;
+        g[j] = ok ? (float)x4[p][j] * sigmoid_f((float)g4[p][j]) : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(sdy + r * CT + 4 * q) = d;
+      *reinterpret_cast<f32x4*>(sg + r * CT + 4 * q) = g;
+    }
+  }
+  __syncthreads();
+  // wave w: frames 16w .. 16w+15; the dy and GLU values they touch (16+K-1 each) in registers
+  const int tb = wv * FB;
+  float wd[WN], wg[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    wd[j] = sdy[(tb + j) * CT + lane];
+    wg[j] = sg[(tb + j) * CT + lane];
+  }
+  float dw[KT + 1], dg[FB];
+#pragma unroll
+  for (int k = 0; k <= KT; ++k) dw[k] = 0.f;
+#pragma unroll
+  for (int f = 0; f < FB; ++f) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) s += wr[k] * wd[f - k + 2 * PAD];
+    dg[f] = s;
+    const float dyt = wd[f + PAD];
+#pragma unroll
+    for (int k = 0; k < KT; ++k) dw[k] += dyt * wg[f + k];
+    dw[KT] += dyt;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < FB; ++f) sm[(tb + f) * CT + lane] = dg[f];
+  float* red = sm + TT * CT;
+#pragma unroll
+  for (int k = 0; k <= KT; ++k) red[(wv * (KT + 1) + k) * CT + lane] = dw[k];
+  __syncthreads();
+  // da of the tile's own rows, from the staging registers of the thread that loaded them
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int r = rs + 16 * p, f = r - PAD, t = t0 + f;
+    if (f >= 0 && f < TT && t < T && cok) {
+      const f32x4 d = *reinterpret_cast<const f32x4*>(sm + f * CT + 4 * q);
+      bf16x4 o1, o2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float sg1 = sigmoid_f((float)g4[p][j]);
+        o1[j] = (bf16)(d[j] * sg1);
+        o2[j] = (bf16)(d[j] * (float)x4[p][j] * sg1 * (1.f - sg1));
+      }
+      const long row = (long)b * T + t;
+      *reinterpret_cast<bf16x4*>(da + row * 2 * C + cq) = o1;
+      *reinterpret_cast<bf16x4*>(da + row * 2 * C + C + cq) = o2;
+    }
+  }
+  const long part_idx = (long)b * gridDim.y + blockIdx.y;
+  for (int i = tid; i < (KT + 1) * CT; i += 256) {
+    const int k = i / CT, l = i % CT;
+    const int cc = c0 + l;
+    if (cc < C)
+      part[(part_idx * (KT + 1) + k) * C + cc] =
+          red[k * CT + l] + red[((KT + 1) + k) * CT + l] + red[(2 * (KT + 1) + k) * CT + l] +
+          red[(3 * (KT + 1) + k) * CT + l];
+  }
+}
+
 // sums[k][c] (k <= K) -> dw[c][k], db[c]
 __global__ void dwconv_scatter_kernel(const float* __restrict__ sums, int C, int K, float* __restrict__ dw,
                                       float* __restrict__ db) {
@@ -440,6 +699,7 @@ int bn_bwd_impl(const void* dz, int dtdz, const float* y, const float* gamma, co
 }
 
 #define CFM_K_CASES(X) X(3) X(5) X(7) X(15) X(31) X(33)
+bool g_dwconv_scalar = getenv("CFM_DWCONV_SCALAR") != nullptr;   // A/B: the one-channel-per-lane kernels
 }  // namespace
 
 CFM_EXPORT size_t cfm_convmod_ws_bytes(int B, int T, int C, int K) {
@@ -465,6 +725,15 @@ CFM_EXPORT int cfm_glu_dwconv_fwd(const void* a, int dta, const float* w, const 
   dim3 grid(cdiv(C, CT), cdiv(T, TT), B);
   const size_t lds = (size_t)(TT + K - 1) * CT * sizeof(float);
   hipStream_t s = cfm::as_stream(stream);
+  if (dta == CFM_BF16 && (C % 4) == 0 && !g_dwconv_scalar) {
+    switch (K) {
+#define X(k) case k: hipLaunchKernelGGL((glu_dwconv_fwd_vec_kernel<k>), grid, dim3(256), 0, s, reinterpret_cast<const bf16*>(a), w, bias, y, T, C, ws); \
+                     return cfm::check_launch("cfm_glu_dwconv_fwd");
+      CFM_K_CASES(X)
+#undef X
+      default: break;
+    }
+  }
   switch (K) {
 #define X(k) case k: if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_fwd_kernel<k, bf16>), grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws); \
                     else hipLaunchKernelGGL((glu_dwconv_fwd_kernel<k, float>), grid, dim3(256), lds, s, a, dta, w, bias, y, T, C, K, ws); break;
@@ -539,6 +808,29 @@ CFM_EXPORT int cfm_bn_bwd(const void* dz, int dtdz, const float* y, const float*
   return cfm::check_launch("cfm_bn_bwd");
 }
 
+namespace {
+
+// the vectorised backward for bf16 a/da, C % 4 == 0 and a compiled K; false if not eligible
+bool dwconv_bwd_vec(const float* dy, const void* a, int dta, const float* w, void* da, int dtda, int B, int T, int C,
+                    int K, float* ws, const BnBwd& bn, bool use_bn, hipStream_t s) {
+  if (g_dwconv_scalar || dta != CFM_BF16 || dtda != CFM_BF16 || (C % 4) != 0) return false;
+  const bool dz16 = use_bn && bn.dtdz == CFM_BF16;
+  dim3 grid(cdiv(C, CT), cdiv(T, TT), B);
+  const bf16* ab = reinterpret_cast<const bf16*>(a);
+  bf16* dab = reinterpret_cast<bf16*>(da);
+  switch (K) {
+#define X(k) case k:                                                                                             \
+    if (!use_bn) hipLaunchKernelGGL((glu_dwconv_bwd_vec_kernel<k, false, false>), grid, dim3(256), 0, s, dy, ab, w, dab, T, C, ws, bn); \
+    else if (dz16) hipLaunchKernelGGL((glu_dwconv_bwd_vec_kernel<k, true, true>), grid, dim3(256), 0, s, dy, ab, w, dab, T, C, ws, bn); \
+    else hipLaunchKernelGGL((glu_dwconv_bwd_vec_kernel<k, true, false>), grid, dim3(256), 0, s, dy, ab, w, dab, T, C, ws, bn); \
+    return true;
+    CFM_K_CASES(X)
+#undef X
+    default: return false;
+  }
+}
+}  // namespace
+
 CFM_EXPORT int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dta, const float* w, void* da, int dtda,
                                   float* dw, float* db, int B, int T, int C, int K, float* ws, void* stream) {
   CFM_REQUIRE(dy && a && w && da && ws, CFM_ERR_ARG, "null pointer");
@@ -549,14 +841,14 @@ CFM_EXPORT int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dta, const
   const size_t red = (size_t)4 * (K + 1) * CT * sizeof(float);
   if (red > lds) lds = red;
   hipStream_t s = cfm::as_stream(stream);
-  switch (K) {
-#define X(k) case k: if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_bwd_kernel<k, bf16>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws); \
-                    else hipLaunchKernelGGL((glu_dwconv_bwd_kernel<k, float>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws); break;
+  if (!dwconv_bwd_vec(dy, a, dta, w, da, dtda, B, T, C, K, ws, BnBwd{}, false, s)) switch (K) {
+#define X(k) case k: if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_bwd_kernel<k, bf16>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws, BnBwd{}); \
+                    else hipLaunchKernelGGL((glu_dwconv_bwd_kernel<k, float>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws, BnBwd{}); break;
     CFM_K_CASES(X)
 #undef X
     default:
-      if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_bwd_kernel<0, bf16>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws);
-      else hipLaunchKernelGGL((glu_dwconv_bwd_kernel<0, float>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws);
+      if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_bwd_kernel<0, bf16>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws, BnBwd{});
+      else hipLaunchKernelGGL((glu_dwconv_bwd_kernel<0, float>), grid, dim3(256), lds, s, dy, a, dta, w, da, dtda, T, C, K, ws, BnBwd{});
   }
   if (!dw) return cfm::check_launch("cfm_glu_dwconv_bwd");   // weight grads later: cfm_glu_dwconv_bwd_wgrad
   const long np = conv_nparts(B, T);
@@ -564,6 +856,40 @@ CFM_EXPORT int cfm_glu_dwconv_bwd(const float* dy, const void* a, int dta, const
   cfm::colreduce(ws, (int)np, (long)C * (K + 1), sums, 0, s);
   hipLaunchKernelGGL(dwconv_scatter_kernel, dim3(cdiv((long)C * (K + 1), 256)), dim3(256), 0, s, sums, C, K, dw, db);
   return cfm::check_launch("cfm_glu_dwconv_bwd");
+}
+
+// the BatchNorm1d + SiLU input gradient folded into the depthwise-conv backward (BnBwd above); dbeta / dgamma are
+// the BN parameter gradients of this pass (cfm_bn_silu_bwd_sums, or their all-reduced totals under SyncBN, with
+// invM = 1 / rows summed over).  Weight partials as cfm_glu_dwconv_bwd (dw == NULL: deferred).
+CFM_EXPORT int cfm_glu_dwconv_bwd_bn(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta,
+                                     const float* mean, const float* invstd, const float* dbeta, const float* dgamma,
+                                     float invM, int training, const void* a, int dta, const float* w, void* da,
+                                     int dtda, float* dw, float* db, int B, int T, int C, int K, float* ws,
+                                     void* stream) {
+  CFM_REQUIRE(dz && y && gamma && beta && mean && invstd && a && w && da && ws, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(!training || (dbeta && dgamma), CFM_ERR_ARG, "training mode needs dbeta / dgamma");
+  CFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, CFM_ERR_UNSUPPORTED, "depthwise kernel must be odd and <= 63");
+  CFM_REQUIRE(B > 0 && T > 0 && C > 0, CFM_ERR_SHAPE, "bad shape");
+  dim3 grid(cdiv(C, CT), cdiv(T, TT), B);
+  size_t lds = (size_t)2 * (TT + K - 1) * CT * sizeof(float);
+  const size_t red = (size_t)4 * (K + 1) * CT * sizeof(float);
+  if (red > lds) lds = red;
+  hipStream_t s = cfm::as_stream(stream);
+  const BnBwd bn{dz, dtdz, y, gamma, beta, mean, invstd, dgamma, dbeta, invM, training};
+  if (!dwconv_bwd_vec(nullptr, a, dta, w, da, dtda, B, T, C, K, ws, bn, true, s)) switch (K) {
+#define X(k) case k: if (dta == CFM_BF16) hipLaunchKernelGGL((glu_dwconv_bwd_kernel<k, bf16, true>), grid, dim3(256), lds, s, nullptr, a, dta, w, da, dtda, T, C, K, ws, bn); \
+                    else hipLaunchKernelGGL((glu_dwconv_bwd_kernel<k, float, true>), grid, dim3(256), lds, s, nullptr, a, dta, w, da, dtda, T, C, K, ws, bn); break;
+    CFM_K_CASES(X)
+#undef X
+    default:
+      return cfm::fail(CFM_ERR_UNSUPPORTED, "cfm_glu_dwconv_bwd_bn: kernel size without a compiled variant");
+  }
+  if (!dw) return cfm::check_launch("cfm_glu_dwconv_bwd_bn");
+  const long np = conv_nparts(B, T);
+  float* sums = ws + np * (long)C * (K + 1);
+  cfm::colreduce(ws, (int)np, (long)C * (K + 1), sums, 0, s);
+  hipLaunchKernelGGL(dwconv_scatter_kernel, dim3(cdiv((long)C * (K + 1), 256)), dim3(256), 0, s, sums, C, K, dw, db);
+  return cfm::check_launch("cfm_glu_dwconv_bwd_bn");
 }
 
 CFM_EXPORT int cfm_glu_dwconv_bwd_wgrad(float* ws, int B, int T, int C, int K, float* dw, float* db, void* stream) {

@@ -556,6 +556,10 @@ def bn_silu_bwd(dz, y, gamma, beta, mean, invstd, training, ws):
     return dy, dgamma, dbeta
 
 
+# kernel sizes with a compiled depthwise variant (convmod.hip CFM_K_CASES); the BN-folded backward needs one
+BN_FOLD_K = (3, 5, 7, 15, 31, 33)
+
+
 def glu_dwconv_bwd(dy, a, w_dw, B, T, C, K, ws, da_dtype, side=None):
     """side: optional conformer._Side -- the depthwise weight/bias reduction then runs there."""
     da = torch.empty(B * T, 2 * C, device=a.device, dtype=da_dtype)
@@ -564,6 +568,38 @@ def glu_dwconv_bwd(dy, a, w_dw, B, T, C, K, ws, da_dtype, side=None):
     defer = side is not None
     L.call("cfm_glu_dwconv_bwd", L.ptr(dy), L.ptr(a), L.dt(a), L.ptr(w_dw), L.ptr(da), L.dt(da),
            None if defer else L.ptr(dw), None if defer else L.ptr(db), B, T, C, K, L.ptr(ws), L.stream())
+    return _dwconv_wgrad(ws, B, T, C, K, da, dw, db, side)
+
+
+def bn_silu_glu_dwconv_bwd(dz, y, gamma, beta, mean, invstd, training, a, w_dw, B, T, C, K, ws, da_dtype,
+                           side=None, reduce_sums=None, world=1):
+    """BatchNorm1d + SiLU backward folded into the GLU + depthwise-conv backward (cfm_glu_dwconv_bwd_bn): the
+    BN parameter gradients come from cfm_bn_silu_bwd_sums, the BN input gradient is formed inside the depthwise
+    kernel and never stored.  reduce_sums / world: SyncBatchNorm (as bn_silu_bwd_sync).
+    Returns (da, dw_dw, db_dw, dgamma, dbeta)."""
+    M = B * T
+    dbg = torch.empty(2, C, device=y.device, dtype=torch.float32)     # [dbeta; dgamma] of this rank
+    L.call("cfm_bn_silu_bwd_sums", L.ptr(dz), L.dt(dz), L.ptr(y), L.ptr(gamma), L.ptr(beta), L.ptr(mean),
+           L.ptr(invstd), M, C, L.ptr(ws), L.ptr(dbg[0]), L.ptr(dbg[1]), L.stream())
+    tot, rows = dbg, M
+    if reduce_sums is not None and training:
+        tot = dbg.clone()
+        reduce_sums(tot)
+        rows = int(world) * M
+    da = torch.empty(M, 2 * C, device=a.device, dtype=da_dtype)
+    dw = torch.empty(C, K, device=a.device, dtype=torch.float32)
+    db = torch.empty(C, device=a.device, dtype=torch.float32)
+    defer = side is not None
+    L.call("cfm_glu_dwconv_bwd_bn", L.ptr(dz), L.dt(dz), L.ptr(y), L.ptr(gamma), L.ptr(beta), L.ptr(mean),
+           L.ptr(invstd), L.ptr(tot[0]), L.ptr(tot[1]), 1.0 / rows, int(bool(training)), L.ptr(a), L.dt(a),
+           L.ptr(w_dw), L.ptr(da), L.dt(da), None if defer else L.ptr(dw), None if defer else L.ptr(db), B, T, C, K,
+           L.ptr(ws), L.stream())
+    da, dw, db = _dwconv_wgrad(ws, B, T, C, K, da, dw, db, side)
+    return da, dw, db, dbg[1], dbg[0]
+
+
+def _dwconv_wgrad(ws, B, T, C, K, da, dw, db, side):
+    defer = side is not None
     if defer:
         if getattr(side, "rgroup", None) is not None:
             np_ = L.load().cfm_convmod_nparts(B, T)

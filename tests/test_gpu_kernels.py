@@ -456,3 +456,63 @@ def test_gemm_persistent_deferred_epilogue_matches_pipeline(gemm_mode, M, N, epi
     if epi == "silu_pre_drop":
         assert _rel(p0, p1) < 4e-3
         assert torch.equal(y0 == 0, y1 == 0)          # identical dropout masks
+
+
+@pytest.mark.parametrize("training", [True, False])
+@pytest.mark.parametrize("sync", [False, True])
+@pytest.mark.parametrize("B,T,C,K,dt", [(2, 37, 64, 31, torch.bfloat16), (3, 100, 96, 3, torch.float32),
+                                        (1, 129, 200, 33, torch.bfloat16), (2, 64, 512, 15, torch.bfloat16),
+                                        (2, 50, 66, 31, torch.bfloat16)])
+def test_bn_folded_dwconv_bwd(training, sync, B, T, C, K, dt):
+    """cfm_glu_dwconv_bwd_bn (BatchNorm1d + SiLU input gradient formed inside the depthwise backward) vs a
+    torch fp64 autograd reference of GLU -> depthwise conv -> BatchNorm1d -> SiLU, and vs the unfused
+    bn_silu_bwd + glu_dwconv_bwd pair.  sync: the SyncBatchNorm route with an identity all-reduce."""
+    if sync and not training:
+        pytest.skip("SyncBatchNorm backward is a training-mode path")
+    g = torch.Generator().manual_seed(B * 1000 + T + C + K)
+    a = torch.randn(B * T, 2 * C, generator=g)
+    w = torch.randn(C, K, generator=g) * 0.3
+    bias = torch.randn(C, generator=g) * 0.1
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.1
+    dz = torch.randn(B * T, C, generator=g)
+    rm, rv = torch.randn(C, generator=g) * 0.1, torch.rand(C, generator=g) + 0.5
+
+    # reference (fp64, CPU autograd)
+    ad = a.double().requires_grad_()
+    wd, bd = w.double().requires_grad_(), bias.double().requires_grad_()
+    gd, btd = gamma.double().requires_grad_(), beta.double().requires_grad_()
+    u = torch.nn.functional.glu(ad.view(B, T, 2 * C), dim=-1).transpose(1, 2)
+    y = torch.nn.functional.conv1d(u, wd.view(C, 1, K), bd, padding=(K - 1) // 2, groups=C)
+    if training:
+        mu, var = y.mean(dim=(0, 2)), y.var(dim=(0, 2), unbiased=False)
+    else:
+        mu, var = rm.double(), rv.double()
+    yh = (y - mu[None, :, None]) / torch.sqrt(var[None, :, None] + 1e-5)
+    z = torch.nn.functional.silu(yh * gd[None, :, None] + btd[None, :, None])
+    (z.transpose(1, 2).reshape(B * T, C) * dz.double()).sum().backward()
+
+    ad_, wd_, bd_ = a.to(DEV, dt), w.to(DEV), bias.to(DEV)
+    gam, bet = gamma.to(DEV), beta.to(DEV)
+    ws = ops.convmod_ws(B, T, C, K, DEV)
+    yv = ops.glu_dwconv_fwd(ad_, wd_, bd_, B, T, C, K, ws)
+    _, mean, invstd = ops.bn_silu_fwd(yv, gam, bet, rm.to(DEV), rv.to(DEV), 0.1, 1e-5, training, B, T, C, ws, dt)
+    dzd = dz.to(DEV, dt)
+    red = (lambda t: None) if sync else None
+    da, dw, db, dg, dbt = ops.bn_silu_glu_dwconv_bwd(dzd, yv, gam, bet, mean, invstd, training, ad_, wd_, B, T, C,
+                                                     K, ws, dt, reduce_sums=red, world=1)
+    dy, dg2, dbt2 = ops.bn_silu_bwd(dzd, yv, gam, bet, mean, invstd, training, ws)
+    da2, dw2, db2 = ops.glu_dwconv_bwd(dy, ad_, wd_, B, T, C, K, ws, dt)
+    torch.cuda.synchronize()
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+    assert _rel(da.float(), ad.grad) < tol
+    assert _rel(dw, wd.grad) < tol
+    if training:    # batch-stat BN cancels the depthwise bias: its true gradient is 0, ours is rounding noise
+        assert (db.double().cpu() - bd.grad).norm() < tol * wd.grad.norm()
+    else:
+        assert _rel(db, bd.grad) < tol
+    assert _rel(dg, gd.grad) < tol and _rel(dbt, btd.grad) < tol
+    # same formula, same summation order as the unfused pair
+    assert _rel(da.float(), da2.float()) < 1e-5
+    assert _rel(dw, dw2) < 1e-5 and (db - db2).norm() < 1e-5 * dw.norm()
+    assert torch.equal(dg, dg2) and torch.equal(dbt, dbt2)
