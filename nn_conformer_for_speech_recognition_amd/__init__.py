@@ -6,3 +6,5 @@ reference's ConvSubSampling / SpecAugment); the hot path runs on hand-written HI
 libcfm.so behind the C ABI in include/cfm.h.
 """
 __version__ = "0.1.0"
+
+from . import library  # noqa: E402,F401  (registers torch.ops.cfm.*)

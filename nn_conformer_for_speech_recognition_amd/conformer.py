@@ -583,6 +583,8 @@ class Conformer(nn.Module):
         return self
 
     def forward_tokens(self, x, lens_i32, B, T, seed=None):
+        if torch.compiler.is_compiling():
+            return self._forward_tokens_ops(x, lens_i32, B, T, seed)
         if seed is None:
             seed = (self._step * 1000003 + 12345) & 0x7FFFFFFF
             self._step += 1
@@ -602,6 +604,21 @@ class Conformer(nn.Module):
                     if self.training and ly.conv_module.sequential[3].track_running_stats]
         if counters:
             torch._foreach_add_(counters, 1)
+        return x
+
+    def _forward_tokens_ops(self, x, lens_i32, B, T, seed):
+        """The encoder as torch.ops.cfm.* calls (library.layer_forward): the route torch.compile traces
+        (fullgraph=True).  Same kernels as the fused layer node; dropout seeds are fixed per call site unless
+        `seed` is given (a device step counter bound with cfm_rng_bind salts them per step, as in HIP-graph
+        replay), so no Python-side step counter is mutated inside the traced region."""
+        from . import library
+        base = 12345 if seed is None else seed
+        for i, layer in enumerate(self.conformer_layers):
+            x = library.layer_forward(layer, x, lens_i32, B, T, self.compute_dtype, base + 100 * i)
+        for ly in self.conformer_layers:
+            bn = ly.conv_module.sequential[3]
+            if self.training and bn.track_running_stats:
+                bn.num_batches_tracked.add_(1)
         return x
 
     def forward(self, input, lengths):
