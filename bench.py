@@ -290,11 +290,12 @@ class Harness:
     sync per step): the bench reports it as `nonfinite_steps` and exits non-zero when it is not 0."""
 
     def __init__(self, cfg, dev, rank=0, world=1, *, dropout=0.1, fp8=False, specaug=False, dp_overlap=False,
-                 eager=False, no_optimizer=False, probe_inline=False, lr=2e-5, seed=1234):
+                 eager=False, no_optimizer=False, probe_inline=False, lr=2e-5, seed=1234, grad_bf16=False):
         self.cfg = cfg
         name, L, d, H, ffn, K, B, secs, pos_enc = cfg
         self.dev, self.rank, self.world = dev, rank, world
-        self.eager = bool(eager or dp_overlap)
+        self.eager = bool(eager)
+        self.dp_overlap = bool(dp_overlap)
         self.no_optimizer, self.probe_inline = no_optimizer, probe_inline
         self.T_in, self.Fb, self.V = 100 * secs + 1, 80, 1024
         self.B, self.L, self.d, self.ffn = B, L, d, ffn
@@ -305,8 +306,12 @@ class Harness:
         cdist.broadcast_parameters(self.model)
         self.params = [p for p in self.model.parameters() if p.requires_grad]
         # DP: the Conformer's grouped weight gradients are written straight into flat all-reduce buckets; with
-        # dp_overlap (eager) each chunk's bucket is reduced while the lower layers' backward still runs
-        self.reducer = cdist.GradAllReducer(self.params, model=self.model, overlap=bool(dp_overlap))
+        # dp_overlap each chunk's bucket is reduced while the lower layers' backward still runs (eager: from the
+        # backward itself; graph: the step is captured as a chain of graphs cut at the chunk boundaries and the
+        # reduces are issued between replays, cdist.SegmentedStepGraph).  grad_bf16: bf16 reduce copies
+        self.reducer = cdist.GradAllReducer(self.params, model=self.model, overlap=bool(dp_overlap),
+                                            grad_dtype=torch.bfloat16 if grad_bf16 else torch.float32)
+        self.seg = None
         self.opt = Adafactor(self.params, lr=lr, beta1=0.9, scale_parameter=False, relative_step=False)
         # synthetic data: per-utterance min-max-normalised uniform mels, full lengths
         g = torch.Generator(device="cpu").manual_seed(seed + rank)
@@ -386,8 +391,12 @@ class Harness:
         if self.probe_inline:                 # legacy: probes inside the timed graph
             for p in probes:
                 p.active = True
-        with torch.cuda.graph(self.graph):
-            self.static_loss = self.fwd_bwd()
+        if self.dp_overlap:
+            self.seg = cdist.SegmentedStepGraph(self.reducer)
+            self.static_loss = self.seg.capture(self.fwd_bwd)
+        else:
+            with torch.cuda.graph(self.graph):
+                self.static_loss = self.fwd_bwd()
         for p in probes:
             p.active = False
         grads_timed = [p.grad for p in self.params]
@@ -398,7 +407,7 @@ class Harness:
             self.probe_graph = torch.cuda.CUDAGraph()
             for p in probes:
                 p.active = True
-            with torch.cuda.graph(self.probe_graph):
+            with self.reducer.no_sync(), torch.cuda.graph(self.probe_graph):    # (no reduce / cut inside)
                 self.fwd_bwd()
             for p in probes:
                 p.active = False
@@ -419,7 +428,10 @@ class Harness:
             t_a = time.perf_counter()
             if self.sa_params is not None:
                 self.specaug_refresh()
-            self.graph.replay()
+            if self.seg is not None:
+                self.seg.replay()
+            else:
+                self.graph.replay()
             t_b = time.perf_counter()
             self.post()
             self.host_t.append((t_b - t_a, time.perf_counter() - t_b))
@@ -470,7 +482,13 @@ def main():
     ap.add_argument("--fp8", action="store_true",
                     help="configs[4]: forward FFN / QKV / out-projection GEMMs on fp8 e4m3 MFMA (backward bf16)")
     ap.add_argument("--dp-overlap", action="store_true",
-                    help="N>1: eager backward with bucket all-reduces overlapped (default: graph + reduce after)")
+                    help="bucket all-reduces overlapped with the backward (default when N>1): graph mode captures "
+                         "the step as a chain of graphs cut at the gradient-chunk boundaries; with --eager the "
+                         "reduces are issued from the backward itself")
+    ap.add_argument("--no-dp-overlap", action="store_true",
+                    help="N>1: one graph for fwd+bwd, every bucket reduced after the replay")
+    ap.add_argument("--grad-bf16", action="store_true",
+                    help="N>1: reduce the gradient buckets through bf16 copies (half the xGMI bytes)")
     ap.add_argument("--probe-inline", action="store_true",
                     help="put the roofline probe kernels inside the timed graph (default: a separate probed graph)")
     ap.add_argument("--poison", action="store_true",
@@ -507,8 +525,8 @@ def main():
                        rank, world)
 
     h = Harness(cfg, dev, rank, world, dropout=args.dropout, fp8=args.fp8, specaug=args.specaug,
-                dp_overlap=args.dp_overlap, eager=args.eager, no_optimizer=args.no_optimizer,
-                probe_inline=args.probe_inline)
+                dp_overlap=args.dp_overlap or (world > 1 and not args.no_dp_overlap), eager=args.eager,
+                no_optimizer=args.no_optimizer, probe_inline=args.probe_inline, grad_bf16=args.grad_bf16)
     model, T2, T_in = h.model, h.T2, h.T_in
 
     # dominant kernel: the FFN up-projection GEMM (M=B*T2, N=ffn, K=d, bf16, SiLU epilogue)
@@ -620,7 +638,11 @@ def main():
                    "pos_enc": pos_enc, "specaug": bool(args.specaug),
                    "global_batch": B * world, "seq_len": T_in, "enc_frames": T2, "frontend": "frame",
                    "dropout": args.dropout, "optimizer": None if args.no_optimizer else "adafactor",
-                   "parallelism": f"dp{world}", "launch": "eager" if h.eager else "hip-graph (fwd+bwd)"},
+                   "parallelism": f"dp{world}",
+                   "launch": "eager" if h.eager else (f"hip-graph chain ({len(h.seg)} segments, bucket all-reduce "
+                                                      "between replays)" if h.seg is not None
+                                                      else "hip-graph (fwd+bwd)"),
+                   "grad_reduce_dtype": "bf16" if h.reducer.grad_dtype == torch.bfloat16 else "fp32"},
         "per_gpu_value": round(value / world, 1),
         "step_algorithmic_tflops": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),

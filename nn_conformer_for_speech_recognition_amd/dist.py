@@ -70,12 +70,24 @@ class GradAllReducer:
     boundary and calls back here; the chunk's bucket all-reduce is then issued asynchronously (RCCL runs
     it on its own stream, ordered after the flush) while the lower layers' backward continues.
     allreduce() issues whatever is left (all buckets when not overlapping) and waits for everything.
-    Inside a captured HIP graph use overlap=False and call allreduce() after the replay."""
+    HIP graphs: SegmentedStepGraph captures the step as a chain of graphs cut at those same flush points and
+    issues each finished chunk's all-reduce between two replays (the collectives themselves are never
+    captured); a single captured graph (overlap=False) reduces everything in allreduce() after the replay.
 
-    def __init__(self, params, bucket_bytes=64 << 20, model=None, chunk_layers=4, overlap=False):
+    grad_dtype=torch.bfloat16: the buckets are reduced through bf16 copies (half the xGMI bytes; each rank's
+    fp32 bucket is cast down, summed/averaged in bf16 by the collective, cast back into the fp32 bucket).
+    The optimizer still reads fp32 gradients and updates fp32 master weights."""
+
+    def __init__(self, params, bucket_bytes=64 << 20, model=None, chunk_layers=4, overlap=False,
+                 grad_dtype=torch.float32):
+        if grad_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"grad_dtype must be float32 or bfloat16, got {grad_dtype}")
         self.params = [p for p in params if p.requires_grad]
         self.bucket_bytes = bucket_bytes
         self.overlap = overlap
+        self.grad_dtype = grad_dtype
+        self._low = {}            # id(fp32 bucket) -> its bf16 staging copy
+        self.segmenter = None     # SegmentedStepGraph while it captures (cuts instead of reduces)
         self.flat = []            # chunk buckets: (flat tensor, lo_layer, hi_layer)
         self.pending = []         # async work handles of this step
         self.launched = set()
@@ -146,6 +158,21 @@ class GradAllReducer:
         return dist.get_world_size()
 
     def _reduce(self, t, async_op):
+        """All-reduce (average) the fp32 bucket t; returns a waitable handle or None (already done)."""
+        if self.grad_dtype == torch.bfloat16:
+            low = self._low.get(id(t))
+            if low is None or low.numel() != t.numel():
+                low = torch.empty(t.numel(), device=t.device, dtype=torch.bfloat16)
+                self._low[id(t)] = low
+            _cast_into(t, low)
+            w = self._reduce_raw(low, async_op)
+            if w is None:
+                _cast_into(low, t)
+                return None
+            return _CastBack(w, low, t)
+        return self._reduce_raw(t, async_op)
+
+    def _reduce_raw(self, t, async_op):
         op = _avg_op()
         if op is not None:
             return dist.all_reduce(t, op=op, async_op=async_op)
@@ -155,6 +182,23 @@ class GradAllReducer:
         t.mul_(1.0 / dist.get_world_size())
         return None
 
+    def final_chunks(self, layer_index):
+        """Chunks whose all-reduce may start once the grouped launch flushed at `layer_index` (see
+        _on_flushed), not yet launched."""
+        return [i for i, (flat, lo, hi) in enumerate(self.flat)
+                if i not in self.launched and lo >= layer_index and all(li in self.routed for li in range(lo, hi))]
+
+    def launch_chunk(self, i):
+        """Issue chunk i's bucket all-reduce now (async; allreduce() waits for it)."""
+        if i in self.launched:
+            return
+        self.launched.add(i)
+        if self._world() == 1:
+            return
+        w = self._reduce(self.flat[i][0], True)
+        if w is not None:
+            self.pending.append(w)
+
     def _on_flushed(self, layer_index):
         """Called by the Conformer right after it flushed the grouped launch at `layer_index`: every chunk
         whose layers are all >= layer_index is final -> issue its all-reduce now (async).  Only chunks whose
@@ -162,17 +206,15 @@ class GradAllReducer:
         (on_routed) qualify: a layer that accumulated into an existing .grad, or skipped the grouped launch
         (gradient hooks, unsupported operand shapes), finishes its gradients through AccumulateGrad AFTER
         this call, so its chunk waits for allreduce().  Nothing launches under no_sync()."""
-        if self._world() == 1 or self._no_sync:
+        if self._no_sync:
             return
-        for i, (flat, lo, hi) in enumerate(self.flat):
-            if i in self.launched or lo < layer_index:
-                continue
-            if not all(li in self.routed for li in range(lo, hi)):
-                continue
-            self.launched.add(i)
-            w = self._reduce(flat, True)
-            if w is not None:
-                self.pending.append(w)
+        if self.segmenter is not None:           # capturing a segmented step graph: cut, reduce at replay
+            self.segmenter.cut(self.final_chunks(layer_index))
+            return
+        if self._world() == 1:
+            return
+        for i in self.final_chunks(layer_index):
+            self.launch_chunk(i)
 
     def _on_routed(self, layer_index):
         """The Conformer's layer `layer_index` routed all its grouped gradients into the bucket views."""
@@ -250,6 +292,88 @@ class GradAllReducer:
         self.pending = []
         self.launched = set()
         self.routed = set()
+
+
+def _cast_into(src, dst):
+    if src.is_cuda:
+        from . import ops
+        ops.cast_into(src, dst)
+    else:
+        dst.copy_(src)
+
+
+class _CastBack:
+    """Handle of an async bf16 bucket reduce: wait() orders the stream after the collective, then casts the
+    reduced bf16 copy back into the fp32 bucket."""
+
+    def __init__(self, work, low, dst):
+        self.work, self.low, self.dst = work, low, dst
+
+    def wait(self):
+        self.work.wait()
+        _cast_into(self.low, self.dst)
+
+
+class SegmentedStepGraph:
+    """A training step's forward + backward captured as a CHAIN of HIP graphs cut where the Conformer flushes
+    a gradient chunk (GradAllReducer(overlap=True) flush points, in backward order), all in ONE private memory
+    pool and replayed in capture order.  After replaying segment i, the chunks that became final in it are
+    all-reduced (async, RCCL's stream) while segment i+1's backward runs on the compute stream -- the
+    data-parallel overlap of the eager path, with graph launch costs.  The collectives are launched from the
+    host between replays, never captured.
+
+    Usage (after one eager warm-up step, so allocator / staging tables exist):
+        seg = SegmentedStepGraph(reducer); out = seg.capture(step_fn)   # step_fn: forward + backward
+        loop: seg.replay(); reducer.allreduce(); optimizer.step()"""
+
+    def __init__(self, reducer):
+        if not reducer.overlap:
+            raise ValueError("SegmentedStepGraph needs GradAllReducer(overlap=True) (its flush points)")
+        self.reducer = reducer
+        self.graphs = []          # [(CUDAGraph, [chunk indices final after it])]
+        self._g = None
+        self._pool = None
+
+    def cut(self, chunks):
+        """Called (through the reducer) at a flush point inside the captured backward."""
+        self._g.capture_end()
+        self.graphs.append((self._g, list(chunks)))
+        self._g = torch.cuda.CUDAGraph()
+        self._g.capture_begin(pool=self._pool, capture_error_mode="relaxed")
+
+    def capture(self, fn):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        self._pool = torch.cuda.graph_pool_handle()
+        self.graphs = []
+        red = self.reducer
+        red.routed = set()
+        with torch.cuda.stream(s):
+            # relaxed capture mode: the cuts run on autograd's device thread, not the thread that began the
+            # capture (thread-local / global capture sequences must end on the thread that started them)
+            self._g = torch.cuda.CUDAGraph()
+            self._g.capture_begin(pool=self._pool, capture_error_mode="relaxed")
+            red.segmenter = self
+            try:
+                out = fn()
+            finally:
+                red.segmenter = None
+            self._g.capture_end()
+            self.graphs.append((self._g, []))
+            self._g = None
+        torch.cuda.current_stream().wait_stream(s)
+        red.launched = set()
+        return out
+
+    def replay(self):
+        red = self.reducer
+        for g, chunks in self.graphs:
+            g.replay()
+            for i in chunks:
+                red.launch_chunk(i)
+
+    def __len__(self):
+        return len(self.graphs)
 
 
 def global_batch_slice(global_batch, rank, world):

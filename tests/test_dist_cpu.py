@@ -36,13 +36,19 @@ def _worker(rank, world, port, q):
     red = cdist.GradAllReducer(model.parameters(), bucket_bytes=64)   # tiny buckets: several calls
     red.allreduce()
     grads = [p.grad.clone() for p in model.parameters()]
+    # bf16 reduce copies of the fp32 buckets (GradAllReducer(grad_dtype=bf16)): 1.25 and 2.5 average to
+    # 1.875, exact in bf16
+    for p in model.parameters():
+        p.grad = torch.full_like(p, 1.25 * (r + 1))
+    cdist.GradAllReducer(model.parameters(), bucket_bytes=64, grad_dtype=torch.bfloat16).allreduce()
+    grads16 = [p.grad.clone() for p in model.parameters()]
     lo, hi = cdist.global_batch_slice(8, r, w)
     hp = HParams(None)
     tau = [40, 38, 37, 30, 25, 20, 12, 9]
     random.seed(42)
     draws = psa.draw(8, 40, tau, hp)
     local = psa.pack(draws, tau, lo, hi)
-    q.put((r, w0, grads, (lo, hi), local, len(red.buckets)))
+    q.put((r, w0, grads, (lo, hi), local, len(red.buckets), grads16))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -60,7 +66,9 @@ def test_dp_allreduce_broadcast_and_slicing():
         p.join(timeout=60)
         assert p.exitcode == 0
     out.sort(key=lambda t: t[0])
-    (_, w0a, ga, sa, la, nb), (_, w0b, gb, sb, lb, _) = out
+    (_, w0a, ga, sa, la, nb, g16a), (_, w0b, gb, sb, lb, _, g16b) = out
+    for x, y in zip(g16a, g16b):
+        assert x.dtype == torch.float32 and torch.equal(x, torch.full_like(x, 1.875)) and torch.equal(x, y)
     assert torch.equal(w0a, w0b)                                  # broadcast from rank 0
     for x, y in zip(ga, gb):
         assert torch.allclose(x, torch.full_like(x, 1.5)) and torch.equal(x, y)   # mean of 1 and 2
