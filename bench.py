@@ -34,7 +34,7 @@ from nn_conformer_for_speech_recognition_amd import ops  # noqa: E402
 from nn_conformer_for_speech_recognition_amd import specaugment  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.ctc import ctc_head_loss  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.conformer import Conformer  # noqa: E402
-from nn_conformer_for_speech_recognition_amd.frontend import linear  # noqa: E402
+from nn_conformer_for_speech_recognition_amd.frontend import frame_frontend, linear  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.lib.convsubsampling import ConvSubSampling  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.lib.hparams import HParams  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.optim import Adafactor  # noqa: E402
@@ -97,10 +97,8 @@ class EncoderCTC(torch.nn.Module):
         B = x.shape[0]
         if specaug_params is not None:
             x = specaugment.apply(x, specaug_params, intended=True)
-        h2 = self.conv_sub_sampling.forward_frames(x, self.cd)
         p = self.dropout if self.training else 0.0
-        h = linear(h2.view(B * self.T2, -1), self.standard_linear.weight, self.standard_linear.bias, cd=self.cd,
-                   drop_p=p, seed=seed)
+        h = frame_frontend(self.conv_sub_sampling, self.standard_linear, x, self.cd, drop_p=p, seed=seed)
         y = self.conformers.forward_tokens(h, lens_i32, B, self.T2, seed=seed + 7)
         return ctc_head_loss(y, self.ctc_fc.weight, self.ctc_fc.bias, targets_i32, lens_i32, tgt_lens_i32, B,
                              self.T2, blank=0, reduction="mean", zero_infinity=True, compute_dtype=self.cd)
@@ -119,9 +117,7 @@ def run_nst(args, model, x, lens_i32, dev, cfg, rank, world):
 
     def label_pass():
         with torch.no_grad():
-            h2 = model.conv_sub_sampling.forward_frames(x, model.cd)
-            h = linear(h2.view(B * model.T2, -1), model.standard_linear.weight, model.standard_linear.bias,
-                       cd=model.cd)
+            h = frame_frontend(model.conv_sub_sampling, model.standard_linear, x, model.cd)
             y = model.conformers.forward_tokens(h, lens_i32, B, model.T2, seed=1)
             logits = linear(y, model.ctc_fc.weight, model.ctc_fc.bias, cd=model.cd).view(B, model.T2, -1)
             return greedy_decode(logits, lens_i32, blank=0, pad=-1, collapse=False)

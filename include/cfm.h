@@ -124,6 +124,7 @@ int cfm_logmel_fwd(const float* wave, long ld_wave, const int32_t* lens, int B, 
  * (asrnn.py:208 / frame projection) and the projection block (asrnn.py:73-89).
  *   A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]
  *   B(n,k) = B[n*ldb + k] if b_kmajor else B[k*ldb + n]
+ * (A / B rows may overlap, ld below the row length: read-only windowed views, cfm_ffold_*.)
  * Epilogue, in order: v = alpha*acc + bias[n];  v *= act'(pre[m,n]) if act_grad;
  *   if act == SILU { pre[m,n] = v (if pre != NULL); v = silu(v) };  v *= dropout(seed, idx);
  *   v *= out_scale;  v += residual[m,n];  C = v  (or atomically C += v when split_k > 1).
@@ -355,6 +356,49 @@ int cfm_conv2_bwd_weight_ws(const void* dh2, const void* h1, float* dw2r, int dt
 size_t cfm_conv1_bwd_ws_bytes(int B, int F, int T, int C1);
 int cfm_conv1_bwd_weight(const void* dh1, int dtype_h, const float* x, float* dw1, float* db1,
                          int B, int F, int T, int C1, float* ws, void* stream);
+
+/* ---------------------------------------------------------------- folded front-end ('frame' projection)
+ * ConvSubSampling is two biased Conv2d with NO nonlinearity between them (lib/convsubsampling.py:41-43),
+ * and in the 'frame' projection mode it feeds the per-frame Linear (the standard_linear of
+ * asrnn.py:28,208 applied to every subsampled frame) before any dropout: the three are ONE linear map
+ * of an Ke x Ke window of the mels, Ke = k1 + (k2 - 1) s1 (11), stride Se = s1 s2 (4):
+ *   h[b, t2, o] = bfull[o] + sum_{f < Ke, r < F} Wfull[o][f][r] x[b, r, Se t2 + f]
+ *   W_eff[c2][e][f] = sum_{c1, a, b} W2[c2][c1][a][b] W1[c1][e - s1 a][f - s1 b]       (the 11x11 conv)
+ *   Wfull[o][f][r]  = sum_{f2, c2} Wp[o][f2 C2 + c2] W_eff[c2][r - Se f2][f]
+ * so the step computes a (B*T2) x D x (Ke F) GEMM instead of conv1 -> conv2 -> Linear (~280 GFLOP
+ * forward at Conformer-L / 15 s; the folded GEMM is 22 GFLOP with the hi + lo bf16 split of x).  The
+ * GEMM reads x through a strided view: the packed input xt holds each utterance's frames as rows of Cx
+ * channels (time-major; bf16 hi then lo rows of Fp, or fp32), row t2 of the view starts at frame Se t2
+ * and spans Ke frames (lda = Se Cx < K: overlapping rows).  Utterance slots are Tslot = Se T2p frames
+ * (T2p = T2 + padding rows), so the weight-gradient GEMM H = G^T X over all B*T2p padded rows (G zero
+ * on the padding rows) is one single-stride product; the parameter gradients then follow from
+ * H (D x Kp) and S = sum_rows G by the transposed contractions (cfm_ffold_bwd_weights).
+ * Replaces Conv2d.forward/backward x2 and nn.Linear.forward/backward of that sequence. */
+typedef struct {
+  int B, F, T;        /* mels (B, F, T) fp32 */
+  int C1, C2, D;      /* conv1 / conv2 channels, projection width */
+  int k1, s1, k2, s2; /* square kernels, the same stride on both axes (nn.Conv2d, no padding) */
+  int dtype;          /* GEMM operand type: CFM_BF16 or CFM_F32 */
+  int hilo;           /* bf16: 1 = x as hi + lo bf16 rows (K doubles, ~16-bit x), 0 = hi only */
+  /* filled by cfm_ffold_geometry: */
+  int F2, T2, Ke, Se, Fp, Cx, Kp, lda, T2p, Tslot;
+  long xt_elems;      /* elements of the packed input (B * Tslot * Cx + tail slack) */
+  long ws_floats;     /* floats of the composed-weight workspace */
+} cfm_ffold_geo;
+int cfm_ffold_geometry(cfm_ffold_geo* g);
+/* x (B, F, T) fp32 -> xt (xt_elems, dtype): frame t of utterance b at row b*Tslot + t (zero past T). */
+int cfm_ffold_pack(const float* x, void* xt, const cfm_ffold_geo* g, void* stream);
+/* w1 (C1, 1, k1, k1), b1 (C1), w2 (C2, C1, k2, k2), b2 (C2), wp (D, F2*C2) (features (f2, c2)), bp (D)
+ * -> wfull (D, Kp) dtype (columns f*Cx + h*Fp + r, zero past Ke*Cx), bfull (D) fp32; ws (ws_floats) keeps
+ * W_eff / b_eff for the backward. */
+int cfm_ffold_compose(const float* w1, const float* b1, const float* w2, const float* b2, const float* wp,
+                      const float* bp, void* wfull, float* bfull, float* ws, const cfm_ffold_geo* g,
+                      void* stream);
+/* H (D, Kp) fp32 = G^T X over the padded rows, S (D) = column sums of G (G: the gradient of h after the
+ * dropout backward) -> dw1, db1, dw2, db2, dwp (same shapes as the weights; fp32, overwritten).  dbp = S. */
+int cfm_ffold_bwd_weights(const float* H, const float* S, const float* w1, const float* b1, const float* w2,
+                          const float* wp, float* ws, float* dw1, float* db1, float* dw2, float* db2, float* dwp,
+                          const cfm_ffold_geo* g, void* stream);
 
 /* ---------------------------------------------------------------- Adafactor (runner.py:36)
  * transformers.Adafactor(lr, beta1, scale_parameter=False, relative_step=False) as one

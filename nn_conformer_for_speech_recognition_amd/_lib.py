@@ -46,6 +46,13 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class FfoldGeo(ctypes.Structure):
+    """cfm_ffold_geo (include/cfm.h): the folded front-end geometry; cfm_ffold_geometry fills the derived fields."""
+    _fields_ = [(n, c_int) for n in ("B", "F", "T", "C1", "C2", "D", "k1", "s1", "k2", "s2", "dtype", "hilo",
+                                     "F2", "T2", "Ke", "Se", "Fp", "Cx", "Kp", "lda", "T2p", "Tslot")] + [
+        ("xt_elems", c_long), ("ws_floats", c_long)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "cfm_version": (c_int, []),
@@ -162,6 +169,10 @@ _SIGS = {
                              c_void_p]),
     "cfm_lstm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                              c_void_p]),
+    "cfm_ffold_geometry": (c_int, [c_void_p]),
+    "cfm_ffold_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cfm_ffold_compose": (c_int, [c_void_p] * 11),
+    "cfm_ffold_bwd_weights": (c_int, [c_void_p] * 14),
     "cfm_conv1_bwd_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "cfm_conv1_bwd_weight": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                      c_void_p, c_void_p]),

@@ -133,4 +133,60 @@ __device__ void store_transposed(float* stage, const f32x16& a0, const f32x16& a
   __builtin_amdgcn_wave_barrier();
 }
 
+// ------------------------------------------------------------------------------------ LDS-DMA head images
+// A head operand slice (rows of dk = 64 bf16 = 128 B at row stride ld) staged with `buffer_load ... lds`
+// into an unpadded [rows][128 B] image whose 16-B chunk c of row r sits in slot c ^ ((r >> 1) & 7): the
+// 32 rows x one chunk of an MFMA operand fragment then hit 16 distinct bank groups per 16 lanes
+// (conflict-free ds_read_b128).  One wave-instruction moves one 1-KiB piece = 8 rows; no VGPR round trip,
+// so a whole head can be in flight while the first tiles are already being consumed (counted vmcnt +
+// s_barrier per tile).  Rows past the operand's `nrows` clamp to its last row (finite data; masked).
+__device__ __forceinline__ int himg(int r, int c) { return r * 128 + 16 * (c ^ ((r >> 1) & 7)); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const bf16* base, long bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
+}
+
+// piece `pc` (rows 8 pc .. 8 pc + 7) of the image at `img`: lane l's 16 B from row 8 pc + l / 8
+__device__ __forceinline__ void head_dma_piece(__amdgpu_buffer_rsrc_t r, char* img, int pc, long ld, int nrows,
+                                               int lane) {
+  const int row = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+  const unsigned voff = (unsigned)(((long)min(row, nrows - 1) * ld + 8 * c) * 2);
+  const unsigned l = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(img + 1024 * pc));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(l), "v"(voff), "s"(r) : "memory", "m0");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+#define W(k) case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(k) : "memory"); break;
+    W(0) W(1) W(2) W(3) W(4) W(5) W(6) W(7) W(8) W(9) W(10) W(11) W(12) W(13) W(14) W(15) W(16)
+#undef W
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// fragments from a head image: A-operand rows r0 + (lane & 31), k = k0 + 8 (lane >> 5) .. +7 (natural order)
+__device__ __forceinline__ bf16x8 hfrag(const char* img, int r0, int k0, int lane) {
+  const int r = r0 + (lane & 31);
+  return *reinterpret_cast<const bf16x8*>(img + himg(r, (k0 >> 3) + (lane >> 5)));
+}
+// trfrag_perm on a head image (transposed, k order matching an accumulator used as the B operand)
+__device__ __forceinline__ bf16x8 htrfrag(const char* img, int r0, int c0, int lane) {
+  const int hh = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int row = r0 + 4 * hh + q, col = c0 + 16 * g1 + 4 * p4;
+  const char* a0 = img + himg(row, col >> 3) + (col & 7) * 2;
+  const char* a1 = img + himg(row + 8, col >> 3) + (col & 7) * 2;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 }  // namespace

@@ -1586,6 +1586,13 @@ int launch_typed(int /*dtype: implied by the loaders' element type*/, GemmP p, O
   return CFM_OK;
 }
 
+// elements one batch of a strided operand spans: (rows - 1) * ld + row length.  Rows may overlap (ld < row
+// length: the folded front-end's windowed view of the packed mels, frontfold.hip); reads past the extent
+// return zero through the buffer range check
+long pipe_extent(int kmajor, long mn, long K, long ld) {
+  return kmajor ? (mn - 1) * ld + K : (K - 1) * ld + mn;
+}
+
 // The LDS-DMA kernel takes plain strided bf16 operands whose 16-B chunks never straddle the
 // reduction edge: K-major operands need K % 64 == 0, MN-major ones M (N) % 8 == 0, and every
 // batch must fit the 32-bit range of a buffer resource.
@@ -1593,8 +1600,7 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
   if (!va || !vb || p.cmap) return false;
   if (p.k_per_split % BK16) return false;
   auto fits = [](long bytes) { return bytes > 0 && bytes < (1L << 31); };
-  const long ea = d.a_kmajor ? (long)d.M * d.lda : (long)d.K * d.lda;
-  const long eb = d.b_kmajor ? (long)d.N * d.ldb : (long)d.K * d.ldb;
+  const long ea = pipe_extent(d.a_kmajor, d.M, d.K, d.lda), eb = pipe_extent(d.b_kmajor, d.N, d.K, d.ldb);
   if (!fits(ea * 2) || !fits(eb * 2)) return false;
   if (d.a_kmajor ? d.K % BK16 != 0 : d.M % 8 != 0) return false;
   if (d.b_kmajor ? d.K % BK16 != 0 : d.N % 8 != 0) return false;
@@ -1616,7 +1622,7 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
   if constexpr (AK) {
     // auto: outputs <= 512 columns (the encoder's d-wide outputs) take the 192-row tiles: 63 x 4 = 252
     // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
-    if (v == 5 || (v == 0 && p.N <= 512 && p.split_k == 1 && p.M >= 4096)) {
+    if (v == 5 || (v == 0 && p.N <= 512 && p.split_k == 1 && (long)p.M * batch >= 4096)) {
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
       // 4-deep ring (4 x 40 KiB = the whole 160 KiB LDS): FFN-up data gradient 34.2 -> 32.5 us same-box;
       // cfm_gemm_set_mode bit 14 keeps the 3-deep ring (A/B)
@@ -1686,8 +1692,7 @@ int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   p.vec_c = vec_epilogue_ok(p);
   p.dbg = ((g_gemm_mode & 8) ? 1 : 0) | ((g_gemm_mode & 1024) ? 2 : 0);   // bit 10: generic dropout path (A/B)
   if (cdiv(p.M, 128) > 65535 || (long)d.batch * p.split_k > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
-  const long ea = d.a_kmajor ? (long)d.M * d.lda : (long)d.K * d.lda;
-  const long eb = d.b_kmajor ? (long)d.N * d.ldb : (long)d.K * d.ldb;
+  const long ea = pipe_extent(d.a_kmajor, d.M, d.K, d.lda), eb = pipe_extent(d.b_kmajor, d.N, d.K, d.ldb);
   const PipeOp oa{(const bf16*)d.A, d.lda, d.stride_a, d.M, (unsigned)(ea * 2)};
   const PipeOp ob{(const bf16*)d.B, d.ldb, d.stride_b, d.N, (unsigned)(eb * 2)};
   const bool ak = d.a_kmajor != 0, bkm = d.b_kmajor != 0;
@@ -1762,8 +1767,9 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   CFM_REQUIRE(split == 1 || (d->dtype_c == CFM_F32 && d->act == CFM_ACT_NONE && !d->act_grad &&
                              !d->residual && d->drop_p <= 0.f),
               CFM_ERR_ARG, "split_k needs a plain fp32 epilogue");
-  CFM_REQUIRE(d->a_kmajor ? d->lda >= d->K : d->lda >= d->M, CFM_ERR_SHAPE, "lda");
-  CFM_REQUIRE(d->b_kmajor ? d->ldb >= d->K : d->ldb >= d->N, CFM_ERR_SHAPE, "ldb");
+  // A and B are read-only: rows may overlap (ld below the row length -- the folded front-end's windowed view
+  // of the packed mels, frontfold.hip); C rows may not
+  CFM_REQUIRE(d->lda >= 1 && d->ldb >= 1, CFM_ERR_SHAPE, "lda / ldb");
   CFM_REQUIRE(d->ldc >= d->N, CFM_ERR_SHAPE, "ldc");
   if (d->M == 0 || d->N == 0) return CFM_OK;
 

@@ -5,9 +5,13 @@
                    an implicit GEMM on MFMA that writes (B, T2, F2, C2) "frame-major" rows.
   linear           torch.nn.Linear (+ fused SiLU / dropout epilogue) — standard_linear (asrnn.py:208),
                    the per-frame projection, projection_fc.
+  frame_frontend   'frame' projection mode: conv_subsample + the per-frame Linear folded into ONE GEMM over a
+                   strided view of the packed mels (the three maps are linear with nothing between them).
   projection_block asrnn.py:73-89 — Linear -> SiLU -> BatchNorm1d (train: batch statistics).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -50,6 +54,73 @@ class _ConvSubFn(torch.autograd.Function):
 
 def conv_subsample(x, w1, b1, w2, b2, cd):
     return _ConvSubFn.apply(x, w1, b1, w2, b2, cd)
+
+
+class _FrameFoldFn(torch.autograd.Function):
+    """x (B, F, T) fp32 -> drop(Linear(flatten_frames(ConvSubSampling(x)))) (B*T2, D) fp32 as ONE GEMM over
+    a strided view of the packed mels (frontfold.hip; the fold of convsubsampling.py:41-43 + asrnn.py:208).
+    No input gradient (mels are data)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, wp, bp, cd, s1, s2, drop_p, seed, hilo):
+        B, F, T = x.shape
+        D = wp.shape[0]
+        g = ops.ffold_geometry(B, F, T, w1.shape[0], w2.shape[0], D, w1.shape[-1], s1, w2.shape[-1], s2, cd, hilo)
+        if wp.shape[1] != g.F2 * g.C2:
+            raise ValueError(f"projection expects {wp.shape[1]} features, the front-end gives {g.F2 * g.C2}")
+        xt = ops.ffold_pack(x, g, cd)
+        wfull, bfull, ws = ops.ffold_compose(w1, b1, w2, b2, wp, bp, g, cd)
+        h = torch.empty(B * g.T2, D, device=x.device, dtype=torch.float32)
+        ops.gemm(xt, wfull, h, g.T2, D, g.Kp, lda=g.lda, stride_a=g.Tslot * g.Cx, batch=B, stride_c=g.T2 * D,
+                 bias=bfull, drop_p=drop_p, seed=seed)
+        ctx.save_for_backward(xt, ws, w1, b1, w2, wp)
+        ctx.g = g
+        ctx.cfg = (cd, drop_p, seed)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        xt, ws, w1, b1, w2, wp = ctx.saved_tensors
+        g = ctx.g
+        cd, drop_p, seed = ctx.cfg
+        B, T2, T2p, D = g.B, g.T2, g.T2p, g.D
+        dh = dh.contiguous()
+        gr = ops.scale_dropout(dh, 1.0, drop_p, seed, 0, out_dtype=cd) if drop_p > 0 else _cd(dh, cd)
+        gpad = torch.zeros(B, T2p, D, device=dh.device, dtype=cd)    # zero rows past T2: the view's padding
+        gpad[:, :T2].copy_(gr.view(B, T2, D))
+        K = B * T2p
+        H = torch.empty(D, g.Kp, device=dh.device, dtype=torch.float32)
+        split = max(2, min(16, K // 512))      # >= 2: the slab path (deterministic) also yields S = colsum(G)
+        if cd == torch.bfloat16:
+            S = torch.empty(D, device=dh.device, dtype=torch.float32)
+            wsk = ops.workspace(4 * (split * D * g.Kp + split * D), dh.device)
+            ops.gemm(gpad.view(K, D), xt, H, D, g.Kp, K, a_kmajor=False, lda=D, b_kmajor=False, ldb=g.lda,
+                     split_k=split, workspace=wsk, a_colsum=S)
+        else:
+            wsk = ops.workspace(4 * split * D * g.Kp, dh.device)
+            ops.gemm(gpad.view(K, D), xt, H, D, g.Kp, K, a_kmajor=False, lda=D, b_kmajor=False, ldb=g.lda,
+                     split_k=split, workspace=wsk)
+            S = ops.colsum(gpad.view(K, D))
+        dw1, db1, dw2, db2, dwp = ops.ffold_bwd_weights(H, S, w1, b1, w2, wp, ws, g)
+        return None, dw1, db1, dw2, db2, dwp, S, None, None, None, None, None, None
+
+
+def frame_frontend(convsub, proj, x, cd, drop_p=0.0, seed=0, hilo=True):
+    """The 'frame'-mode encoder input: dropout(proj(ConvSubSampling(x) per frame)) -> (B*T2, D) fp32.
+    convsub: lib.convsubsampling.ConvSubSampling; proj: the nn.Linear(F2*C2, D) (features (f2, c2)).
+    x (B, 1, F, T) or (B, F, T) mels.  Folded into one GEMM (frontfold.hip) unless CFM_FFOLD=0 (the unfolded
+    conv1 -> conv2 -> Linear kernels, for A/B)."""
+    if x.dim() == 4:
+        x = x.reshape(x.shape[0], x.shape[2], x.shape[3])
+    x = x.float().contiguous()
+    c1, c2 = convsub.conv_sub_1, convsub.conv_sub_2
+    if os.environ.get("CFM_FFOLD", "1") == "0":
+        h2 = convsub.forward_frames(x, cd)
+        B, T2 = h2.shape[0], h2.shape[1]
+        return linear(h2.reshape(B * T2, -1), proj.weight, proj.bias, cd=cd, drop_p=drop_p, seed=seed)
+    convsub._check()
+    return _FrameFoldFn.apply(x, c1.weight, c1.bias, c2.weight, c2.bias, proj.weight, proj.bias, cd,
+                              int(c1.stride[0]), int(c2.stride[0]), float(drop_p), int(seed), bool(hilo))
 
 
 class _LinearFn(torch.autograd.Function):

@@ -23,7 +23,7 @@ import torch.nn as nn
 from ... import specaugment as _sa
 from ...conformer import Conformer
 from ...ctc import greedy_decode as _greedy_decode
-from ...frontend import linear as _linear, projection_block as _projection_block
+from ...frontend import frame_frontend as _frame_frontend, linear as _linear, projection_block as _projection_block
 from ...lstm import LSTM
 from ..convsubsampling import ConvSubSampling
 
@@ -134,10 +134,10 @@ class ASRNN(nn.Module):
         B = x.shape[0]
         p = hp.dropout if self.training else 0.0
         if self.frontend_proj == "frame":
-            h2 = self.conv_sub_sampling.forward_frames(x, cd)                    # (B, T2, F2, C2)
-            _, T2, F2, C2 = h2.shape
-            h = _linear(h2.reshape(B * T2, F2 * C2), self.standard_linear.weight, self.standard_linear.bias, cd=cd,
-                        drop_p=p, seed=random.getrandbits(31))
+            # ConvSubSampling -> per-frame Linear -> dropout as ONE folded GEMM (frontend.frame_frontend)
+            h = _frame_frontend(self.conv_sub_sampling, self.standard_linear, x, cd, drop_p=p,
+                                seed=random.getrandbits(31))
+            T2 = h.shape[0] // B
             lens = subsampled_lengths(input_lens.to(h.device).long(), hp)
             lens_i32 = lens.clamp(min=1).to(torch.int32)
             y = self.conformers.forward_tokens(h, lens_i32, B, T2)

@@ -693,6 +693,39 @@ def conv2_bwd_weight(dh2, h1):
     return dw2r
 
 
+# ----------------------------------------------------------------------------- folded front-end
+def ffold_geometry(B, F, T, C1, C2, D, k1, s1, k2, s2, dtype, hilo=True):
+    """cfm_ffold_geometry (host only): the folded 'frame'-mode front-end's packed-input / GEMM geometry."""
+    g = L.FfoldGeo(B=B, F=F, T=T, C1=C1, C2=C2, D=D, k1=k1, s1=s1, k2=k2, s2=s2,
+                   dtype=BF16 if dtype == torch.bfloat16 else F32, hilo=int(bool(hilo)))
+    L.call("cfm_ffold_geometry", L.ctypes.byref(g))
+    return g
+
+
+def ffold_pack(x, g, dtype):
+    xt = torch.empty(g.xt_elems, device=x.device, dtype=dtype)
+    L.call("cfm_ffold_pack", L.ptr(x), L.ptr(xt), L.ctypes.byref(g), L.stream())
+    return xt
+
+
+def ffold_compose(w1, b1, w2, b2, wp, bp, g, dtype):
+    """-> (wfull (D, Kp) dtype, bfull (D) fp32, ws) -- ws keeps W_eff / b_eff for ffold_bwd_weights."""
+    dev = w1.device
+    wfull = torch.empty(g.D, g.Kp, device=dev, dtype=dtype)
+    bfull = torch.empty(g.D, device=dev, dtype=torch.float32)
+    ws = torch.empty(g.ws_floats, device=dev, dtype=torch.float32)
+    L.call("cfm_ffold_compose", L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(wp), L.ptr(bp), L.ptr(wfull),
+           L.ptr(bfull), L.ptr(ws), L.ctypes.byref(g), L.stream())
+    return wfull, bfull, ws
+
+
+def ffold_bwd_weights(H, S, w1, b1, w2, wp, ws, g):
+    dw1, db1, dw2, db2, dwp = (torch.empty_like(t) for t in (w1, b1, w2, torch.empty(g.C2, device=w1.device), wp))
+    L.call("cfm_ffold_bwd_weights", L.ptr(H), L.ptr(S), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(wp), L.ptr(ws),
+           L.ptr(dw1), L.ptr(db1), L.ptr(dw2), L.ptr(db2), L.ptr(dwp), L.ctypes.byref(g), L.stream())
+    return dw1, db1, dw2, db2, dwp
+
+
 # ----------------------------------------------------------------------------- CTC head
 def _rows(x, batch_first):
     """(B, T, sb, st) of a (B, T, V) / (T, B, V) tensor with contiguous classes."""

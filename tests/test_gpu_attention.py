@@ -34,7 +34,7 @@ def _ref(qkv, lens, B, T, H, dk, do):
     return o.detach(), x.grad.view(B * T, 3 * H * dk)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 8])
+@pytest.mark.parametrize("mode", [0, 1, 8, 32])
 @pytest.mark.parametrize("B,T,H", [(3, 373, 2), (2, 64, 4), (2, 97, 1)])
 def test_attention_vs_torch(attn_mode, mode, B, T, H):
     attn_mode(mode)
@@ -67,6 +67,24 @@ def test_attention_kernels_agree_under_dropout(attn_mode):
         assert _rel(o, outs[0][0]) < 1e-2
         for sl in range(3):      # dQ, dK, dV: a mask that differs on ~10 % of the entries fails these
             assert _rel(d[:, sl * HD:(sl + 1) * HD], outs[0][1][:, sl * HD:(sl + 1) * HD]) < 1e-2
+
+
+@pytest.mark.parametrize("B,T,H", [(3, 373, 2), (2, 384, 1), (2, 64, 3), (3, 97, 2), (2, 33, 1), (1, 1, 2)])
+def test_forward_dma_staging_bit_identical(attn_mode, B, T, H):
+    """The LDS-DMA-staged whole-head forward (default) and the register-staged one (cfm_attn_set_mode bit 5)
+    run the same arithmetic in the same order: outputs and lse bit-identical, ragged lengths, dropout."""
+    dk = 64
+    g = torch.Generator().manual_seed(T + H)
+    qkv = torch.randn(B * T, 3 * H * dk, generator=g).to(DEV, torch.bfloat16)
+    lens = torch.tensor([T] + [max(1, T - 17 * (i + 1)) for i in range(B - 1)], dtype=torch.int32, device=DEV)
+    res = []
+    for mode in (0, 32):
+        attn_mode(mode)
+        o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=0.1, seed=13)
+        torch.cuda.synchronize()
+        res.append((o.clone(), lse.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
 
 
 def test_rowdot_epilogue_feeds_attention_bwd():
