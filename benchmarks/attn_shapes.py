@@ -46,8 +46,7 @@ def main():
         tb = timeit(lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=p, seed=3))
         out[f"fwd_p{p}"], out[f"bwd_p{p}"] = round(tf, 2), round(tb, 2)
         print(f"libcfm p={p}: fwd {tf:7.1f} us {fl / tf / 1e6:6.0f} TF/s | bwd {tb:7.1f} us {2.5 * fl / tb / 1e6:6.0f} TF/s")
-    for mode, tag in ((32, "register-staged (A/B)"), (34, "register-staged, staging only"),
-                      (36, "register-staged, no epilogue stores")):
+    for mode, tag in ((32, "LDS-DMA staged (A/B)"), (2, "staging only"), (4, "no epilogue stores")):
         _lib.call("cfm_attn_set_mode", mode)
         t = timeit(lambda: ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=0.1, seed=3))
         out[f"fwd_mode{mode}"] = round(t, 2)

@@ -3,7 +3,7 @@
 # (DMA vs register staging), bench A/B (fold vs CFM_FFOLD=0) and a kernel summary.
 set -o pipefail
 O=gpurun_out/ff1; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_frontfold.py tests/test_gpu_frontend.py tests/test_gpu_attention.py -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|error" $O/pytest.log | head -20; tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_frontfold.py tests/test_gpu_frontend.py tests/test_gpu_attention.py tests/test_gpu_conformer.py -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|error" $O/pytest.log | head -20; tail -30 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 timeout -k 10 120 python benchmarks/attn_shapes.py > $O/attn_shapes.txt 2>&1 || { echo attn_shapes failed; tail $O/attn_shapes.txt; exit 1; }
 grep libcfm $O/attn_shapes.txt

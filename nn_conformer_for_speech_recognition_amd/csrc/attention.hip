@@ -192,6 +192,57 @@ __device__ __forceinline__ void head_stage(const AttnM& p, const bf16* base0, co
   }
 }
 
+// One key tile of the forward's online softmax for a wave (queries on the lanes, keys k0 + acc_row(r, hh)
+// [+ 32] in s0 / s1, raw unscaled scores): masking only on the utterance's last tile (`tail`, uniform), the
+// running max kept in scaled log2 units (c = scale * log2 e > 0, so max(c s) = c max(s)), p = 2^(c s - m) as
+// one FMA + v_exp; rescales o0/o1 and l; attention dropout applied to p (the returned P is dropped/scaled,
+// l stays the undropped sum, as nn.MultiheadAttention: dropout after the softmax).
+__device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16& s1, f32x16& o0, f32x16& o1,
+                                             float& m, float& l, float c, int kbase, int len, bool tail, int b,
+                                             int h, int qi, int hh, uint32_t dthr, float dkeep, uint32_t dkey) {
+  if (tail && kbase + TILE > len) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k0 = kbase + acc_row(r, hh);
+      s0[r] = (k0 < len) ? s0[r] : -INFINITY;
+      s1[r] = (k0 + 32 < len) ? s1[r] : -INFINITY;
+    }
+  }
+  float mloc = fmaxf(s0[0], s1[0]);
+#pragma unroll
+  for (int r = 1; r < 16; ++r) mloc = fmaxf(mloc, fmaxf(s0[r], s1[r]));
+  mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+  const float mn = fmaxf(m, mloc * c);
+  const float alpha = fast_exp2(m - mn);
+  float ls = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    s0[r] = fast_exp2(__builtin_fmaf(s0[r], c, -mn));
+    s1[r] = fast_exp2(__builtin_fmaf(s1[r], c, -mn));
+    ls += s0[r] + s1[r];
+  }
+  ls += __shfl_xor(ls, 32, 64);
+  l = l * alpha + ls;
+  m = mn;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    o0[r] *= alpha;
+    o1[r] *= alpha;
+  }
+  if (p.drop_p > 0.f) {
+    const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kbase) >> 1);   // even: 32-bit pair indices
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
+      const int k0 = acc_row(r, hh);
+      float m0, m1, m2, m3;
+      dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
+      dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
+      s0[r] *= m0; s0[r + 1] *= m1;
+      s1[r] *= m2; s1[r + 1] *= m3;
+    }
+  }
+}
+
 // forward: grid (B*H), block 64 * ceil(T/32); dynamic LDS head_lds_bytes(T)
 __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(AttnM p, bf16* __restrict__ o,
                                                                             float* __restrict__ lse) {
@@ -229,44 +280,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
       s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
       s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
     }
-    float mloc = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int k0 = kt * TILE + acc_row(r, hh);
-      s0[r] = (k0 < len) ? s0[r] * c : -INFINITY;
-      s1[r] = (k0 + 32 < len) ? s1[r] * c : -INFINITY;
-      mloc = fmaxf(mloc, fmaxf(s0[r], s1[r]));
-    }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float mn = fmaxf(m, mloc);
-    const float alpha = fast_exp2(m - mn);
-    float ls = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = fast_exp2(s0[r] - mn);
-      s1[r] = fast_exp2(s1[r] - mn);
-      ls += s0[r] + s1[r];
-    }
-    ls += __shfl_xor(ls, 32, 64);
-    l = l * alpha + ls;
-    m = mn;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      o0[r] *= alpha;
-      o1[r] *= alpha;
-    }
-    if (p.drop_p > 0.f) {
-      const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
-        const int k0 = acc_row(r, hh);
-        float m0, m1, m2, m3;
-        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
-        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
-        s0[r] *= m0; s0[r + 1] *= m1;
-        s1[r] *= m2; s1[r + 1] *= m3;
-      }
-    }
+    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -349,44 +363,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_dma_kernel(
       s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hfrag(tK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
       s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hfrag(tK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
     }
-    float mloc = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int k0 = kt * TILE + acc_row(r, hh);
-      s0[r] = (k0 < len) ? s0[r] * c : -INFINITY;
-      s1[r] = (k0 + 32 < len) ? s1[r] * c : -INFINITY;
-      mloc = fmaxf(mloc, fmaxf(s0[r], s1[r]));
-    }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float mn = fmaxf(m, mloc);
-    const float alpha = fast_exp2(m - mn);
-    float ls = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = fast_exp2(s0[r] - mn);
-      s1[r] = fast_exp2(s1[r] - mn);
-      ls += s0[r] + s1[r];
-    }
-    ls += __shfl_xor(ls, 32, 64);
-    l = l * alpha + ls;
-    m = mn;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      o0[r] *= alpha;
-      o1[r] *= alpha;
-    }
-    if (p.drop_p > 0.f) {
-      const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int k0 = acc_row(r, hh);
-        float m0, m1, m2, m3;
-        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
-        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
-        s0[r] *= m0; s0[r + 1] *= m1;
-        s1[r] *= m2; s1[r + 1] *= m3;
-      }
-    }
+    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -431,7 +408,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
   load_bfrags(p, kvbase + h * p.dk, p.D3, qi, p.T, qf, lane);
   load_bfrags(p, dout + (long)b * p.T * p.HD + h * p.dk, p.HD, qi, p.T, gf, lane);
   const bool qvalid = qi < p.T;
-  const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : 0.f;
+  const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : INFINITY;   // rows past T: P = 0
   const float Dq = qvalid ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
   const float c = p.scale * LOG2E;
   __syncthreads();
@@ -460,10 +437,13 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
         d0[r + 1] *= (hsh >> 16) >= dthr ? dkeep : 0.f;
       }
     }
+    if (k0 + 32 > len) {     // the last (partial) key step only: masked keys
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s0[r] = k0 + acc_row(r, hh) < len ? s0[r] : -INFINITY;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int kk = k0 + acc_row(r, hh);
-      const float p0 = fast_exp2(kk < len && qvalid ? s0[r] * c - L2 : -INFINITY);
+      const float p0 = fast_exp2(__builtin_fmaf(s0[r], c, -L2));
       s0[r] = p0 * (d0[r] - Dq);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -683,7 +663,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e;
-          const float pa = fast_exp2(sa[r] * c - Lr[e]);   // lse = +inf for q >= T
+          const float pa = fast_exp2(__builtin_fmaf(sa[r], c, -Lr[e]));   // lse = +inf for q >= T
           pf[r >> 3][r & 7] = (bf16)(pa * mk[e]);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -723,7 +703,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e;
-          const float pa = fast_exp2(sa[r] * c - Lr[e]);
+          const float pa = fast_exp2(__builtin_fmaf(sa[r], c, -Lr[e]));
           const float m = (bits >> r) & 1u ? keep : 0.f;
           sf[r >> 3][r & 7] = (bf16)(pa * (ga[r] * m - Dr[e]));
         }
@@ -1011,8 +991,9 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 6,
           cfm::g_rng_salt};
-  if (use_head(T) && p.vec && dk == DKP && (g_attn_mode & 32) == 0) {
-    // LDS-DMA staging (cfm_attn_set_mode bit 5 selects the register-staged kernel for A/B)
+  if (use_head(T) && p.vec && dk == DKP && (g_attn_mode & 32)) {
+    // LDS-DMA staging (cfm_attn_set_mode bit 5; measured no faster than register staging at T = 373:
+    // profiles/r03/attn_fwd_dma_ab.txt)
     hipLaunchKernelGGL(attn_fwd_head_dma_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), head_dma_lds_bytes(T), s, p,
                        (bf16*)o, lse);
     return cfm::check_launch("cfm_attn_fwd");

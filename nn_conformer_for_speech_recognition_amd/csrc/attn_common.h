@@ -126,9 +126,25 @@ __device__ void store_transposed(float* stage, const f32x16& a0, const f32x16& a
     stage[c * 65 + 32 + acc_row(r, hh)] = a1[r] * mulc;
   }
   __builtin_amdgcn_wave_barrier();
-  for (int idx = lane; idx < 32 * 64; idx += 64) {
-    const int cc = idx >> 6, d = idx & 63;
-    if (cc < nvalid && d < dk) out[(long)(row0 + cc) * ld + d] = (bf16)stage[cc * 65 + d];
+  if (dk == 64 && ((uintptr_t)out & 15) == 0 && (ld & 7) == 0) {
+    // 16-B stores: lane = (row cc = 8 it + lane / 8, 8-column group lane % 8), whole 128-B rows per 8 lanes
+    const int g8 = lane & 7;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int cc = 8 * it + (lane >> 3);
+      if (cc < nvalid) {
+        const float* src = stage + cc * 65 + 8 * g8;
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)src[e];
+        *reinterpret_cast<bf16x8*>(out + (long)(row0 + cc) * ld + 8 * g8) = v;
+      }
+    }
+  } else {
+    for (int idx = lane; idx < 32 * 64; idx += 64) {
+      const int cc = idx >> 6, d = idx & 63;
+      if (cc < nvalid && d < dk) out[(long)(row0 + cc) * ld + d] = (bf16)stage[cc * 65 + d];
+    }
   }
   __builtin_amdgcn_wave_barrier();
 }

@@ -16,8 +16,8 @@
 //   dW2[c2][c1][a][b] = sum_{kh,kw} W1[c1][kh][kw] dW_eff[c2][s1 a + kh][s1 b + kw] + b1[c1] db_eff[c2]
 //   dW1[c1][kh][kw]   = sum_{c2,a,b} W2[c2][c1][a][b] dW_eff[c2][s1 a + kh][s1 b + kw]
 //   db1[c1] = sum_{c2,a,b} W2[c2][c1][a][b] db_eff[c2]                                          db2 = db_eff
-// These contractions are 0.03-0.2 GMAC each: plain fp32 SIMT kernels with LDS-staged operands, every
-// reduction done in a fixed order (deterministic, no atomics).
+// These contractions are 0.03-0.2 GMAC each: fp32 GEMMs on cfm_gemm's exact-f32 MFMA path (deterministic
+// split-K slabs, no atomics) over re-indexed views, with elementwise gathers between them.
 #include "cfm_common.h"
 
 namespace {
@@ -25,11 +25,13 @@ namespace {
 struct FG {   // device copy of the geometry
   int B, F, T, C1, C2, D, k1, s1, k2, s2;
   int F2, T2, Ke, Se, Fp, Cx, Kp, nh, Tslot, Ke2;
+  int n1, n2;   // padded row lengths (multiples of 4) of the tap + bias tables: k1^2 + 1 -> n1, Ke^2 + 1 -> n2
 };
+inline int pad4(int n) { return (n + 3) / 4 * 4; }
 
 FG dev_geo(const cfm_ffold_geo& g) {
   return FG{g.B, g.F, g.T, g.C1, g.C2, g.D, g.k1, g.s1, g.k2, g.s2, g.F2, g.T2, g.Ke, g.Se, g.Fp, g.Cx, g.Kp,
-            g.Cx / g.Fp, g.Tslot, g.Ke * g.Ke};
+            g.Cx / g.Fp, g.Tslot, g.Ke * g.Ke, pad4(g.k1 * g.k1 + 1), pad4(g.Ke * g.Ke + 1)};
 }
 
 // ------------------------------------------------------------------------------------------- pack
@@ -61,275 +63,187 @@ __global__ __launch_bounds__(256) void ffold_pack_kernel(const float* __restrict
 }
 
 // ------------------------------------------------------------------------------------------- compose
-// W_eff partials over 64-channel chunks of conv1: grid (C2, ceil(C1/64)); thread j < Ke^2 -> tap (e, f),
-// thread Ke^2 -> the b1 term of b_eff
-constexpr int CCH = 64;
-__global__ __launch_bounds__(256) void ffold_weff_part_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
-                                                              const float* __restrict__ w2, float* __restrict__ part,
-                                                              FG g) {
-  extern __shared__ float sm[];
-  const int k1k1 = g.k1 * g.k1, k2k2 = g.k2 * g.k2;
-  float* w2s = sm;                      // [CCH][k2k2]
-  float* w1s = w2s + CCH * k2k2;        // [CCH][k1k1]
-  float* b1s = w1s + CCH * k1k1;        // [CCH]
-  const int c2 = blockIdx.x, c10 = blockIdx.y * CCH, nc = min(CCH, g.C1 - c10);
-  for (int i = threadIdx.x; i < nc * k2k2; i += blockDim.x) w2s[i] = w2[((long)c2 * g.C1 + c10) * k2k2 + i];
-  for (int i = threadIdx.x; i < nc * k1k1; i += blockDim.x) w1s[i] = w1[(long)c10 * k1k1 + i];
-  for (int i = threadIdx.x; i < nc; i += blockDim.x) b1s[i] = b1[c10 + i];
-  __syncthreads();
-  const int j = threadIdx.x;
-  if (j > g.Ke2) return;
+// The contractions run as fp32 GEMMs on the exact-f32 MFMA path of cfm_gemm over re-indexed views, with
+// elementwise gathers between them (n1 = 52 columns: the k1^2 = 49 conv1 taps, the bias, zero padding to a
+// multiple of 4 for the split-K reduction; n2 = 124: the Ke^2 = 121 taps, the bias, padding):
+//   P    (C2*k2^2 x n1)    = W2t^T W1e            W2t = W2 as (C1 x C2 k2^2), W1e = [W1 | b1] (C1 x n1)
+//   Weff (C2 x n2)         = gather(P) (+ b2)     the conv composition; column Ke^2 = b_eff
+//   Q    (D*F2 x n2)       = Wp' Weff^T            Wp' = Wp viewed as (D F2 x C2)
+//   Wfull, bfull           = gather(Q) (+ bp)
+// backward:
+//   Hg   (D*F2 x n2)       = gather(H) | S        Hg[(o,f2)][(e,f)] = H[o][f][Se f2 + e], column Ke^2 = S[o]
+//   dWeff (C2 x n2)        = Wp'^T Hg             (split-K slabs; column Ke^2 = db_eff)
+//   dWp  (D*F2 x C2)       = Hg Weff^T            (= dWp (D x F2 C2) in its own layout)
+//   Gd   (C2*k2^2 x n1)    = gather(dWeff)        Gd[(c2,a,b)][(kh,kw)] = dWeff[c2][s1 a + kh][s1 b + kw], | db_eff
+//   dW2  (C2 x C1 x k2^2)  = per c2: W1e Gd_c2^T  (written in the reference layout)
+//   W1o  (C1 x n1)         = W2t Gd               -> dW1 = W1o[:, :49], db1 = W1o[:, 49]
+
+// W2 (C2, C1, k2^2) -> W2t (C1, C2 k2^2); W1 (C1, k1^2), b1 -> W1e (C1, n1)
+__global__ __launch_bounds__(256) void ffold_prep_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
+                                                         const float* __restrict__ w2, float* __restrict__ w2t,
+                                                         float* __restrict__ w1e, FG g) {
+  const int k1k1 = g.k1 * g.k1, k2k2 = g.k2 * g.k2, n1 = g.n1, n2t = g.C2 * k2k2;
+  const long nt = (long)g.C1 * n2t, ne = (long)g.C1 * n1;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nt + ne; i += (long)gridDim.x * 256) {
+    if (i < nt) {
+      const int c1 = (int)(i / n2t), rem = (int)(i - (long)c1 * n2t), c2 = rem / k2k2, ab = rem - c2 * k2k2;
+      w2t[i] = w2[((long)c2 * g.C1 + c1) * k2k2 + ab];
+    } else {
+      const long j = i - nt;
+      const int c1 = (int)(j / n1), t = (int)(j - (long)c1 * n1);
+      w1e[j] = t < k1k1 ? w1[(long)c1 * k1k1 + t] : (t == k1k1 ? b1[c1] : 0.f);
+    }
+  }
+}
+
+// Weff[c2][(e,f)] = sum_{a,b valid} P[(c2,a,b)][(e - s1 a) k1 + f - s1 b];  Weff[c2][Ke^2] = b2 + sum_ab P[.][k1^2]
+__global__ __launch_bounds__(256) void ffold_weff_kernel(const float* __restrict__ P, const float* __restrict__ b2,
+                                                         float* __restrict__ weff, FG g) {
+  const int n1 = g.n1, n2 = g.n2, k2k2 = g.k2 * g.k2, k1k1 = g.k1 * g.k1;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g.C2 * n2) return;
+  const int c2 = i / n2, j = i - c2 * n2;
+  const float* pc = P + (long)c2 * k2k2 * n1;
   float acc = 0.f;
   if (j < g.Ke2) {
     const int e = j / g.Ke, f = j - e * g.Ke;
-    for (int c = 0; c < nc; ++c)
-      for (int a = 0; a < g.k2; ++a) {
-        const int kh = e - g.s1 * a;
-        if (kh < 0 || kh >= g.k1) continue;
-        for (int bb = 0; bb < g.k2; ++bb) {
-          const int kw = f - g.s1 * bb;
-          if (kw < 0 || kw >= g.k1) continue;
-          acc += w2s[c * k2k2 + a * g.k2 + bb] * w1s[c * k1k1 + kh * g.k1 + kw];
-        }
+    for (int a = 0; a < g.k2; ++a) {
+      const int kh = e - g.s1 * a;
+      if (kh < 0 || kh >= g.k1) continue;
+      for (int bb = 0; bb < g.k2; ++bb) {
+        const int kw = f - g.s1 * bb;
+        if (kw >= 0 && kw < g.k1) acc += pc[(a * g.k2 + bb) * n1 + kh * g.k1 + kw];
       }
-  } else {
-    for (int c = 0; c < nc; ++c) {
-      float s = 0.f;
-      for (int q = 0; q < k2k2; ++q) s += w2s[c * k2k2 + q];
-      acc += s * b1s[c];
     }
+  } else if (j == g.Ke2) {
+    acc = b2[c2];
+    for (int ab = 0; ab < k2k2; ++ab) acc += pc[ab * n1 + k1k1];
   }
-  part[((long)blockIdx.y * g.C2 + c2) * (g.Ke2 + 1) + j] = acc;
+  weff[i] = acc;
 }
 
-// out[i] = sum_p part[p n + i] in order (+ add[i / (Ke^2+1)] on the bias slots)
-__global__ __launch_bounds__(256) void ffold_reduce_kernel(const float* __restrict__ part, int np, int n,
-                                                           const float* __restrict__ add, int row,
-                                                           float* __restrict__ out) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  float s = 0.f;
-  for (int p = 0; p < np; ++p) s += part[(long)p * n + i];
-  if (add && i % row == row - 1) s += add[i / row];
-  out[i] = s;
-}
-
-// Wfull / bfull: two output rows o per block; W_eff (+ b_eff column) and the two Wp rows in LDS.  Output
-// (f, r): the (f2, e = r - Se f2) pairs with 0 <= e < Ke are f2 = r/Se - jj, jj < ceil(Ke/Se) (a uniform
-// trip count; invalid pairs read a clamped address and are discarded)
+// Wfull[o][f Cx + h Fp + r] = sum_{f2: 0 <= r - Se f2 < Ke} Q[(o,f2)][(r - Se f2) Ke + f] (zero past Ke Cx);
+// bfull[o] = bp[o] + sum_f2 Q[(o,f2)][Ke^2].  One thread per (o, column < Kp)
 template <typename TW>
-__global__ __launch_bounds__(256) void ffold_wfull_kernel(const float* __restrict__ wp, const float* __restrict__ bp,
-                                                          const float* __restrict__ weff, TW* __restrict__ wfull,
-                                                          float* __restrict__ bfull, FG g) {
-  extern __shared__ float sm[];
-  const int R = g.Ke2 + 1, NF = g.F2 * g.C2;
-  float* ws = sm;               // [C2][Ke^2 + 1]
-  float* wps = ws + g.C2 * R;   // [2][F2 * C2]
-  __shared__ float red[2][4];
-  const int o0 = blockIdx.x * 2;
-  const int nro = min(2, g.D - o0);
-  for (int i = threadIdx.x; i < g.C2 * R; i += 256) ws[i] = weff[i];
-  for (int i = threadIdx.x; i < 2 * NF; i += 256) {
-    const int q = i / NF;
-    wps[i] = q < nro ? wp[(long)(o0 + q) * NF + (i - q * NF)] : 0.f;
+__global__ __launch_bounds__(256) void ffold_wfull_kernel(const float* __restrict__ Q, const float* __restrict__ bp,
+                                                          TW* __restrict__ wfull, float* __restrict__ bfull, FG g) {
+  const int n2 = g.n2;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)g.D * g.Kp) return;
+  const int o = (int)(i / g.Kp), col = (int)(i - (long)o * g.Kp);
+  const float* qo = Q + (long)o * g.F2 * n2;
+  if (col == 0) {
+    float s = bp[o];
+    for (int f2 = 0; f2 < g.F2; ++f2) s += qo[f2 * n2 + g.Ke2];
+    bfull[o] = s;
   }
-  __syncthreads();
-  const int JJ = (g.Ke + g.Se - 1) / g.Se;
-  for (int idx = threadIdx.x; idx < g.Ke * g.Fp; idx += 256) {
-    const int f = idx / g.Fp, r = idx - f * g.Fp;
-    float a0 = 0.f, a1 = 0.f;
-    for (int jj = 0; jj < JJ; ++jj) {
-      const int f2 = r / g.Se - jj, e = r - g.Se * f2;
-      const bool ok = f2 >= 0 && f2 < g.F2 && e < g.Ke && r < g.F;
-      const int f2c = ok ? f2 : 0, ec = ok ? e : 0;
-      const float* wcol = ws + ec * g.Ke + f;
-      const float* p0 = wps + f2c * g.C2;
-      const float* p1 = p0 + NF;
-      float t0 = 0.f, t1 = 0.f;
-      for (int c2 = 0; c2 < g.C2; ++c2) {
-        const float w = wcol[c2 * R];
-        t0 += p0[c2] * w;
-        t1 += p1[c2] * w;
-      }
-      if (ok) { a0 += t0; a1 += t1; }
-    }
-    for (int q = 0; q < nro; ++q)
-      for (int h = 0; h < g.nh; ++h)
-        wfull[(long)(o0 + q) * g.Kp + f * g.Cx + h * g.Fp + r] = from_f32<TW>(q ? a1 : a0);
-  }
-  for (int c = g.Ke * g.Cx + threadIdx.x; c < g.Kp; c += 256)
-    for (int q = 0; q < nro; ++q) wfull[(long)(o0 + q) * g.Kp + c] = from_f32<TW>(0.f);
-  // bfull[o] = bp[o] + sum_{f2,c2} Wp[o][f2 C2 + c2] b_eff[c2]
-  float s0 = 0.f, s1 = 0.f;
-  for (int i = threadIdx.x; i < NF; i += 256) {
-    const float be = ws[(i % g.C2) * R + g.Ke2];
-    s0 += wps[i] * be;
-    s1 += wps[NF + i] * be;
-  }
-  s0 = wave_sum(s0);
-  s1 = wave_sum(s1);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane == 0) { red[0][wv] = s0; red[1][wv] = s1; }
-  __syncthreads();
-  if (threadIdx.x < nro) {
-    const int q = threadIdx.x;
-    bfull[o0 + q] = bp[o0 + q] + ((red[q][0] + red[q][1]) + (red[q][2] + red[q][3]));
-  }
-}
-
-// ------------------------------------------------------------------------------------------- backward
-// H row o as Hs[f * F + r] = sum_h H[o][f Cx + h Fp + r]
-__device__ __forceinline__ void load_hrow(const float* __restrict__ H, const FG& g, int o, float* hs, int tid, int nt) {
-  for (int i = tid; i < g.Ke * g.F; i += nt) {
-    const int f = i / g.F, r = i - f * g.F;
-    float v = 0.f;
-    if (o < g.D)
-      for (int h = 0; h < g.nh; ++h) v += H[(long)o * g.Kp + f * g.Cx + h * g.Fp + r];
-    hs[i] = v;
-  }
-}
-
-// dW_eff / db_eff partials over 16-row chunks of o: grid (ceil(D/16), ceil(C2/16))
-constexpr int OB = 16, CB = 16;
-__global__ __launch_bounds__(256) void ffold_bwd_part_kernel(const float* __restrict__ H, const float* __restrict__ S,
-                                                             const float* __restrict__ wp, float* __restrict__ part,
-                                                             FG g) {
-  extern __shared__ float sm[];
-  const int KF = g.Ke * g.F, R = g.Ke2 + 1, NF = g.F2 * g.C2;
-  float* hs = sm;                     // [OB][Ke * F]
-  float* wps = hs + OB * KF;          // [OB][F2][CB]
-  float* ss = wps + OB * g.F2 * CB;   // [OB]
-  const int o0 = blockIdx.x * OB, c0 = blockIdx.y * CB;
-  for (int q = 0; q < OB; ++q) load_hrow(H, g, o0 + q, hs + q * KF, threadIdx.x, 256);
-  for (int i = threadIdx.x; i < OB * g.F2 * CB; i += 256) {
-    const int q = i / (g.F2 * CB), rem = i - q * g.F2 * CB, f2 = rem / CB, cl = rem - f2 * CB;
-    const int o = o0 + q, c2 = c0 + cl;
-    wps[i] = (o < g.D && c2 < g.C2) ? wp[(long)o * NF + f2 * g.C2 + c2] : 0.f;
-  }
-  for (int i = threadIdx.x; i < OB; i += 256) ss[i] = o0 + i < g.D ? S[o0 + i] : 0.f;
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < CB * R; idx += 256) {
-    const int cl = idx / R, j = idx - cl * R, c2 = c0 + cl;
-    if (c2 >= g.C2) continue;
-    float acc = 0.f;
-    if (j < g.Ke2) {
-      const int e = j / g.Ke, f = j - e * g.Ke;
-      for (int q = 0; q < OB; ++q) {
-        const float* hrow = hs + q * KF + f * g.F + e;
-        const float* wrow = wps + q * g.F2 * CB + cl;
-        for (int f2 = 0; f2 < g.F2; ++f2) acc += wrow[f2 * CB] * hrow[g.Se * f2];
-      }
-    } else {
-      for (int q = 0; q < OB; ++q) {
-        float t = 0.f;
-        for (int f2 = 0; f2 < g.F2; ++f2) t += wps[q * g.F2 * CB + f2 * CB + cl];
-        acc += t * ss[q];
-      }
-    }
-    part[((long)blockIdx.x * g.C2 + c2) * R + j] = acc;
-  }
-}
-
-// dWp rows o0, o0+1 per block (W_eff and the two H rows in LDS); dWp[o][f2 C2 + c2]
-__global__ __launch_bounds__(256) void ffold_bwd_wp_kernel(const float* __restrict__ H, const float* __restrict__ S,
-                                                           const float* __restrict__ weff, float* __restrict__ dwp,
-                                                           FG g) {
-  extern __shared__ float sm[];
-  const int KF = g.Ke * g.F, R = g.Ke2 + 1, NF = g.F2 * g.C2;
-  float* ws = sm;               // [C2][R]
-  float* hs = ws + g.C2 * R;    // [2][Ke * F]
-  const int o0 = blockIdx.x * 2, nro = min(2, g.D - o0);
-  for (int i = threadIdx.x; i < g.C2 * R; i += 256) ws[i] = weff[i];
-  load_hrow(H, g, o0, hs, threadIdx.x, 256);
-  load_hrow(H, g, o0 + 1, hs + KF, threadIdx.x, 256);
-  __syncthreads();
-  const float S0 = S[o0], S1 = nro > 1 ? S[o0 + 1] : 0.f;
-  for (int idx = threadIdx.x; idx < NF; idx += 256) {
-    const int f2 = idx / g.C2, c2 = idx - f2 * g.C2;
-    const float* wrow = ws + c2 * R;
-    float a0 = 0.f, a1 = 0.f;
-    for (int e = 0; e < g.Ke; ++e) {
-      const float* h0 = hs + g.Se * f2 + e;
-      for (int f = 0; f < g.Ke; ++f) {
-        const float w = wrow[e * g.Ke + f];
-        a0 += w * h0[f * g.F];
-        a1 += w * h0[KF + f * g.F];
-      }
-    }
-    const float be = wrow[g.Ke2];
-    dwp[(long)o0 * NF + idx] = a0 + be * S0;
-    if (nro > 1) dwp[(long)(o0 + 1) * NF + idx] = a1 + be * S1;
-  }
-}
-
-// dW2 / db2: one block per c2 (dW_eff row in LDS)
-__global__ __launch_bounds__(256) void ffold_bwd_w2_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
-                                                           const float* __restrict__ dweff, float* __restrict__ dw2,
-                                                           float* __restrict__ db2, FG g) {
-  __shared__ float dws[256];
-  const int R = g.Ke2 + 1, c2 = blockIdx.x, k1k1 = g.k1 * g.k1, k2k2 = g.k2 * g.k2;
-  for (int i = threadIdx.x; i < R; i += 256) dws[i] = dweff[(long)c2 * R + i];
-  __syncthreads();
-  const float dbe = dws[g.Ke2];
-  if (threadIdx.x == 0) db2[c2] = dbe;
-  for (int idx = threadIdx.x; idx < g.C1 * k2k2; idx += 256) {
-    const int c1 = idx / k2k2, ab = idx - c1 * k2k2, a = ab / g.k2, bb = ab - a * g.k2;
-    const float* w1r = w1 + (long)c1 * k1k1;
-    float acc = 0.f;
-    for (int kh = 0; kh < g.k1; ++kh)
-      for (int kw = 0; kw < g.k1; ++kw)
-        acc += w1r[kh * g.k1 + kw] * dws[(g.s1 * a + kh) * g.Ke + g.s1 * bb + kw];
-    dw2[((long)c2 * g.C1 + c1) * k2k2 + ab] = acc + b1[c1] * dbe;
-  }
-}
-
-// dW1 / db1: four conv1 channels per block (one wave each); all of dW_eff and the four channels' W2 taps in LDS
-__global__ __launch_bounds__(256) void ffold_bwd_w1_kernel(const float* __restrict__ w2, const float* __restrict__ dweff,
-                                                           float* __restrict__ dw1, float* __restrict__ db1, FG g) {
-  extern __shared__ float sm[];
-  const int R = g.Ke2 + 1, k1k1 = g.k1 * g.k1, k2k2 = g.k2 * g.k2;
-  float* dws = sm;              // [C2][R]
-  float* w2s = dws + g.C2 * R;  // [4][C2][k2k2]
-  const int c10 = blockIdx.x * 4;
-  for (int i = threadIdx.x; i < g.C2 * R; i += 256) dws[i] = dweff[i];
-  for (int i = threadIdx.x; i < 4 * g.C2 * k2k2; i += 256) {
-    const int q = i / (g.C2 * k2k2), rem = i - q * g.C2 * k2k2, c2 = rem / k2k2, ab = rem - c2 * k2k2;
-    const int c1 = c10 + q;
-    w2s[i] = c1 < g.C1 ? w2[((long)c2 * g.C1 + c1) * k2k2 + ab] : 0.f;
-  }
-  __syncthreads();
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, c1 = c10 + wv;
-  if (c1 >= g.C1 || lane > k1k1) return;
-  const float* w2c = w2s + wv * g.C2 * k2k2;
   float acc = 0.f;
-  if (lane < k1k1) {
-    const int kh = lane / g.k1, kw = lane - kh * g.k1;
-    for (int c2 = 0; c2 < g.C2; ++c2)
-      for (int a = 0; a < g.k2; ++a)
-        for (int bb = 0; bb < g.k2; ++bb)
-          acc += w2c[c2 * k2k2 + a * g.k2 + bb] * dws[c2 * R + (g.s1 * a + kh) * g.Ke + g.s1 * bb + kw];
-    dw1[(long)c1 * k1k1 + lane] = acc;
-  } else {
-    for (int c2 = 0; c2 < g.C2; ++c2) {
-      float t = 0.f;
-      for (int q = 0; q < k2k2; ++q) t += w2c[c2 * k2k2 + q];
-      acc += t * dws[c2 * R + g.Ke2];
+  if (col < g.Ke * g.Cx) {
+    const int f = col / g.Cx, r = (col - f * g.Cx) % g.Fp;
+    if (r < g.F) {
+      const int f2hi = min(r / g.Se, g.F2 - 1);
+      for (int f2 = f2hi; f2 >= 0 && r - g.Se * f2 < g.Ke; --f2) acc += qo[f2 * n2 + (r - g.Se * f2) * g.Ke + f];
     }
-    db1[c1] = acc;
+  }
+  wfull[i] = from_f32<TW>(acc);
+}
+
+// ------------------------------------------------------------------------------------------- backward gathers
+// Hg[(o,f2)][(e,f)] = sum_h H[o][f Cx + h Fp + Se f2 + e];  Hg[(o,f2)][Ke^2] = S[o]
+__global__ __launch_bounds__(256) void ffold_hg_kernel(const float* __restrict__ H, const float* __restrict__ S,
+                                                       float* __restrict__ hg, FG g) {
+  const int n2 = g.n2;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)g.D * g.F2 * n2) return;
+  const int row = (int)(i / n2), j = (int)(i - (long)row * n2), o = row / g.F2, f2 = row - o * g.F2;
+  float v;
+  if (j < g.Ke2) {
+    const int e = j / g.Ke, f = j - e * g.Ke;
+    const float* h = H + (long)o * g.Kp + f * g.Cx + g.Se * f2 + e;
+    v = 0.f;
+    for (int q = 0; q < g.nh; ++q) v += h[q * g.Fp];
+  } else {
+    v = j == g.Ke2 ? S[o] : 0.f;
+  }
+  hg[i] = v;
+}
+
+// Gd[(c2,a,b)][(kh,kw)] = dWeff[c2][(s1 a + kh) Ke + s1 b + kw];  Gd[.][k1^2] = db_eff[c2] (= db2)
+__global__ __launch_bounds__(256) void ffold_gd_kernel(const float* __restrict__ dweff, float* __restrict__ gd,
+                                                       float* __restrict__ db2, FG g) {
+  const int n1 = g.n1, n2 = g.n2, k2k2 = g.k2 * g.k2, k1k1 = g.k1 * g.k1;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g.C2 * k2k2 * n1) return;
+  const int row = i / n1, t = i - row * n1, c2 = row / k2k2, ab = row - c2 * k2k2, a = ab / g.k2, bb = ab - a * g.k2;
+  const float* dw = dweff + (long)c2 * n2;
+  if (t < k1k1) {
+    const int kh = t / g.k1, kw = t - kh * g.k1;
+    gd[i] = dw[(g.s1 * a + kh) * g.Ke + g.s1 * bb + kw];
+  } else if (t == k1k1) {
+    gd[i] = dw[g.Ke2];
+    if (ab == 0) db2[c2] = dw[g.Ke2];
+  } else {
+    gd[i] = 0.f;
   }
 }
 
-constexpr size_t LDS_MAX = 160 * 1024;
+// dW2[c2][c1][ab] = dW2t[c1][c2 k2^2 + ab]
+__global__ __launch_bounds__(256) void ffold_dw2_kernel(const float* __restrict__ w2g, float* __restrict__ dw2, FG g) {
+  const int k2k2 = g.k2 * g.k2;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)g.C1 * g.C2 * k2k2) return;
+  const int c2 = (int)(i / ((long)g.C1 * k2k2)), rem = (int)(i - (long)c2 * g.C1 * k2k2), c1 = rem / k2k2,
+            ab = rem - c1 * k2k2;
+  dw2[i] = w2g[(long)c1 * g.C2 * k2k2 + c2 * k2k2 + ab];
+}
 
-size_t wfull_lds(const cfm_ffold_geo& g) { return ((size_t)g.C2 * (g.Ke * g.Ke + 1) + 2 * (size_t)g.F2 * g.C2) * 4; }
-size_t part_lds(const cfm_ffold_geo& g) {
-  return ((size_t)OB * g.Ke * g.F + (size_t)OB * g.F2 * CB + OB) * 4;
+// W1o (C1 x n1) -> dw1 (C1 x k1^2), db1 (C1)
+__global__ __launch_bounds__(256) void ffold_w1_split_kernel(const float* __restrict__ w1o, float* __restrict__ dw1,
+                                                             float* __restrict__ db1, FG g) {
+  const int n1 = g.n1, k1k1 = g.k1 * g.k1;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g.C1 * n1) return;
+  const int c1 = i / n1, t = i - c1 * n1;
+  if (t < k1k1) dw1[(long)c1 * k1k1 + t] = w1o[i];
+  else if (t == k1k1) db1[c1] = w1o[i];
 }
-size_t wp_lds(const cfm_ffold_geo& g) { return ((size_t)g.C2 * (g.Ke * g.Ke + 1) + 2 * (size_t)g.Ke * g.F) * 4; }
-size_t w1_lds(const cfm_ffold_geo& g) {
-  return ((size_t)g.C2 * (g.Ke * g.Ke + 1) + 4 * (size_t)g.C2 * g.k2 * g.k2) * 4;
+
+// workspace layout (floats), shared by compose and the backward (W2t, W1e and Weff persist in between)
+struct WsLayout {
+  long w2t, w1e, P, weff, Q, dweff, gd, w1o, w2g, slab, total;
+};
+WsLayout ws_layout(const cfm_ffold_geo& g) {
+  const long n1 = pad4(g.k1 * g.k1 + 1), n2 = pad4(g.Ke * g.Ke + 1), k2k2 = (long)g.k2 * g.k2;
+  WsLayout L;
+  long o = 0;
+  auto take = [&](long n) { const long r = o; o += (n + 63) / 64 * 64; return r; };
+  L.w2t = take((long)g.C1 * g.C2 * k2k2);
+  L.w1e = take((long)g.C1 * n1);
+  L.P = take((long)g.C2 * k2k2 * n1);
+  L.weff = take((long)g.C2 * n2);
+  L.Q = take((long)g.D * g.F2 * n2);            // forward Q / backward Hg
+  L.dweff = take((long)g.C2 * n2);
+  L.gd = take((long)g.C2 * k2k2 * n1);
+  L.w1o = take((long)g.C1 * n1);
+  L.w2g = take((long)g.C1 * g.C2 * k2k2);
+  const long sC = 64L * g.C2 * n2, sF = 16L * g.C1 * n1, sP = 8L * g.C2 * k2k2 * n1;
+  L.slab = take(std::max(sC, std::max(sF, sP)));
+  L.total = o;
+  return L;
 }
-int nparts(const cfm_ffold_geo& g) { return cdiv(g.C1, CCH) > cdiv(g.D, OB) ? cdiv(g.C1, CCH) : cdiv(g.D, OB); }
+
+// fp32 GEMM through the C ABI (exact-f32 MFMA path)
+int f32gemm(int M, int N, int K, const float* A, long lda, int akm, const float* B, long ldb, int bkm, float* C,
+            long ldc, int batch, long sa, long sb, long sc, int split, float* slab, hipStream_t s) {
+  cfm_gemm_desc d{};
+  d.M = M; d.N = N; d.K = K; d.batch = batch; d.dtype_ab = CFM_F32;
+  d.A = A; d.lda = lda; d.stride_a = sa; d.a_kmajor = akm;
+  d.B = B; d.ldb = ldb; d.stride_b = sb; d.b_kmajor = bkm;
+  d.C = C; d.ldc = ldc; d.stride_c = sc; d.dtype_c = CFM_F32;
+  d.alpha = 1.f; d.out_scale = 1.f; d.ldr = N; d.dtype_pre = CFM_F32; d.dtype_r = CFM_F32;
+  d.split_k = split; d.workspace = split > 1 ? slab : nullptr;
+  return cfm_gemm(&d, (void*)s);
+}
 
 }  // namespace
 
@@ -354,10 +268,7 @@ CFM_EXPORT int cfm_ffold_geometry(cfm_ffold_geo* g) {
   g->Tslot = g->Se * g->T2p;
   const long slack = (g->Kp + g->Cx - 1) / g->Cx;
   g->xt_elems = ((long)g->B * g->Tslot + slack) * g->Cx;
-  const long R = (long)g->C2 * (g->Ke * g->Ke + 1);
-  g->ws_floats = R * (2 + nparts(*g));
-  CFM_REQUIRE(wfull_lds(*g) <= LDS_MAX && part_lds(*g) <= LDS_MAX && wp_lds(*g) <= LDS_MAX && w1_lds(*g) <= LDS_MAX,
-              CFM_ERR_UNSUPPORTED, "front-end fold: LDS staging exceeds 160 KiB");
+  g->ws_floats = ws_layout(*g).total;
   CFM_REQUIRE((long)g->B * g->Tslot * g->Cx * (g->dtype == CFM_BF16 ? 2 : 4) < (1L << 31), CFM_ERR_SHAPE,
               "packed input >= 2 GiB");
   return CFM_OK;
@@ -383,18 +294,26 @@ CFM_EXPORT int cfm_ffold_compose(const float* w1, const float* b1, const float* 
   CFM_REQUIRE(w1 && b1 && w2 && b2 && wp && bp && wfull && bfull && ws && g, CFM_ERR_ARG, "null pointer");
   const FG d = dev_geo(*g);
   hipStream_t s = cfm::as_stream(stream);
-  const int R = g->Ke * g->Ke + 1, n = g->C2 * R;
-  float* weff = ws;
-  float* part = ws + 2 * (long)n;
-  const int ns = cdiv(g->C1, CCH);
-  const size_t lds1 = ((size_t)CCH * (g->k2 * g->k2 + g->k1 * g->k1) + CCH) * 4;
-  hipLaunchKernelGGL(ffold_weff_part_kernel, dim3(g->C2, ns), dim3(R <= 128 ? 128 : 256), lds1, s, w1, b1, w2, part, d);
-  hipLaunchKernelGGL(ffold_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, part, ns, n, b2, R, weff);
+  const WsLayout L = ws_layout(*g);
+  const int n1 = d.n1, n2 = d.n2, k2k2 = g->k2 * g->k2;
+  const long nprep = (long)g->C1 * (g->C2 * k2k2 + n1);
+  hipLaunchKernelGGL(ffold_prep_kernel, dim3((unsigned)std::min<long>(cdiv(nprep, 256), 2048)), dim3(256), 0, s, w1,
+                     b1, w2, ws + L.w2t, ws + L.w1e, d);
+  // P (C2 k2^2 x n1) = sum_c1 W2t[c1][(c2,ab)] W1e[c1][t]: A, B MN-major over k = c1
+  const int splitP = std::max(1, std::min(8, g->C1 / 64));
+  int rc = f32gemm(g->C2 * k2k2, n1, g->C1, ws + L.w2t, (long)g->C2 * k2k2, 0, ws + L.w1e, n1, 0, ws + L.P, n1, 1, 0,
+                   0, 0, splitP, ws + L.slab, s);
+  if (rc != CFM_OK) return rc;
+  hipLaunchKernelGGL(ffold_weff_kernel, dim3(cdiv(g->C2 * n2, 256)), dim3(256), 0, s, ws + L.P, b2, ws + L.weff, d);
+  // Q (D F2 x n2) = Wp' (D F2 x C2, K-major) Weff (C2 x n2: MN-major B over k = c2)
+  rc = f32gemm(g->D * g->F2, n2, g->C2, wp, g->C2, 1, ws + L.weff, n2, 0, ws + L.Q, n2, 1, 0, 0, 0, 1, nullptr, s);
+  if (rc != CFM_OK) return rc;
+  const long nw = (long)g->D * g->Kp;
   if (g->dtype == CFM_BF16)
-    hipLaunchKernelGGL(ffold_wfull_kernel<bf16>, dim3(cdiv(g->D, 2)), dim3(256), wfull_lds(*g), s, wp, bp, weff,
+    hipLaunchKernelGGL(ffold_wfull_kernel<bf16>, dim3((unsigned)cdiv(nw, 256)), dim3(256), 0, s, ws + L.Q, bp,
                        (bf16*)wfull, bfull, d);
   else
-    hipLaunchKernelGGL(ffold_wfull_kernel<float>, dim3(cdiv(g->D, 2)), dim3(256), wfull_lds(*g), s, wp, bp, weff,
+    hipLaunchKernelGGL(ffold_wfull_kernel<float>, dim3((unsigned)cdiv(nw, 256)), dim3(256), 0, s, ws + L.Q, bp,
                        (float*)wfull, bfull, d);
   return cfm::check_launch("cfm_ffold_compose");
 }
@@ -406,15 +325,31 @@ CFM_EXPORT int cfm_ffold_bwd_weights(const float* H, const float* S, const float
               "null pointer");
   const FG d = dev_geo(*g);
   hipStream_t s = cfm::as_stream(stream);
-  const int R = g->Ke * g->Ke + 1, n = g->C2 * R;
-  const float* weff = ws;
-  float* dweff = ws + n;
-  float* part = ws + 2 * (long)n;
-  const int nob = cdiv(g->D, OB);
-  hipLaunchKernelGGL(ffold_bwd_part_kernel, dim3(nob, cdiv(g->C2, CB)), dim3(256), part_lds(*g), s, H, S, wp, part, d);
-  hipLaunchKernelGGL(ffold_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, part, nob, n, nullptr, R, dweff);
-  hipLaunchKernelGGL(ffold_bwd_wp_kernel, dim3(cdiv(g->D, 2)), dim3(256), wp_lds(*g), s, H, S, weff, dwp, d);
-  hipLaunchKernelGGL(ffold_bwd_w2_kernel, dim3(g->C2), dim3(256), 0, s, w1, b1, dweff, dw2, db2, d);
-  hipLaunchKernelGGL(ffold_bwd_w1_kernel, dim3(cdiv(g->C1, 4)), dim3(256), w1_lds(*g), s, w2, dweff, dw1, db1, d);
+  const WsLayout L = ws_layout(*g);
+  const int n1 = d.n1, n2 = d.n2, k2k2 = g->k2 * g->k2;
+  const long nhg = (long)g->D * g->F2 * n2;
+  float* hg = ws + L.Q;
+  hipLaunchKernelGGL(ffold_hg_kernel, dim3((unsigned)cdiv(nhg, 256)), dim3(256), 0, s, H, S, hg, d);
+  // dWeff (C2 x n2) = sum_{(o,f2)} Wp'[(o,f2)][c2] Hg[(o,f2)][n]: both MN-major over k = (o, f2), split-K slabs
+  const int KC = g->D * g->F2;
+  const int splitC = std::max(1, std::min(64, KC / 256));
+  int rc = f32gemm(g->C2, n2, KC, wp, g->C2, 0, hg, n2, 0, ws + L.dweff, n2, 1, 0, 0, 0, splitC, ws + L.slab, s);
+  if (rc != CFM_OK) return rc;
+  // dWp (D F2 x C2) = Hg (K-major, k = n) Weff^T (K-major)
+  rc = f32gemm(KC, g->C2, n2, hg, n2, 1, ws + L.weff, n2, 1, dwp, g->C2, 1, 0, 0, 0, 1, nullptr, s);
+  if (rc != CFM_OK) return rc;
+  hipLaunchKernelGGL(ffold_gd_kernel, dim3(cdiv(g->C2 * k2k2 * n1, 256)), dim3(256), 0, s, ws + L.dweff, ws + L.gd,
+                     db2, d);
+  // dW2t (C1 x C2 k2^2) = W1e (C1 x n1, K-major) Gd^T (Gd: (C2 k2^2) x n1, K-major); then dW2 = its permute
+  rc = f32gemm(g->C1, g->C2 * k2k2, n1, ws + L.w1e, n1, 1, ws + L.gd, n1, 1, ws + L.w2g, (long)g->C2 * k2k2, 1, 0, 0,
+               0, 1, nullptr, s);
+  if (rc != CFM_OK) return rc;
+  hipLaunchKernelGGL(ffold_dw2_kernel, dim3(cdiv((long)g->C1 * g->C2 * k2k2, 256)), dim3(256), 0, s, ws + L.w2g, dw2, d);
+  // W1o (C1 x n1) = W2t (C1 x C2 k2^2, K-major) Gd ((C2 k2^2) x n1: MN-major B over k = (c2, ab))
+  const int KF = g->C2 * k2k2;
+  const int splitF = std::max(1, std::min(16, KF / 64));
+  rc = f32gemm(g->C1, n1, KF, ws + L.w2t, KF, 1, ws + L.gd, n1, 0, ws + L.w1o, n1, 1, 0, 0, 0, splitF, ws + L.slab, s);
+  if (rc != CFM_OK) return rc;
+  hipLaunchKernelGGL(ffold_w1_split_kernel, dim3(cdiv(g->C1 * n1, 256)), dim3(256), 0, s, ws + L.w1o, dw1, db1, d);
   return cfm::check_launch("cfm_ffold_bwd_weights");
 }

@@ -1409,13 +1409,17 @@ __device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& 
 }
 
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
-template <bool AK, bool BKM, class OA, class OB>
+// exact-f32 MFMA GEMM (v_mfma_f32_32x32x2f32), register-staged K tiles of 16; TBM x TBM output tile, 4 waves
+// of (TBM/2)^2: TBM = 128 for the large shapes, 64 (4x the workgroups) when the 128-tile grid would leave the
+// chip mostly idle (the folded front-end's small contractions, frontfold.hip)
+template <bool AK, bool BKM, class OA, class OB, int TBM = 128>
 __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p, OA oa, OB ob) {
+  constexpr int FR = TBM / 64, FS = TBM + 4, TT = BK32 * FS, NV = TBM / 64;
   gemm_drop_prep(p);
-  __shared__ __attribute__((aligned(16))) float lds[4 * TILE32];
+  __shared__ __attribute__((aligned(16))) float lds[4 * TT];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int m0 = blockIdx.y * TBM, n0 = blockIdx.x * TBM;
   const int z = blockIdx.z / p.split_k, ks = blockIdx.z % p.split_k;
   oa.batch(z);
   ob.batch(z);
@@ -1423,41 +1427,41 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p, OA oa, OB ob) {
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg + BK32 - 1) / BK32 : 0;
 
-  f32x16 acc[2][2];
+  f32x16 acc[FR][FR];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FR; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+    for (int j = 0; j < FR; ++j) acc[i][j] = (f32x16){0};
 
-  float4 ra[2], rb[2];
-  // tile = 16 k x 128 rows = 512 float4
+  float4 ra[NV], rb[NV];
+  // tile = 16 k x TBM rows = 4 * TBM float4
   auto gload = [&](int kt) {
     const int k0 = kbeg + kt * BK32;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = tid + NT * i;
       if constexpr (AK) ra[i] = oa.load(m0 + (v >> 2), k0 + (v & 3) * 4, p.M, kend);
-      else ra[i] = oa.load(k0 + (v >> 5), m0 + (v & 31) * 4, kend, p.M);
+      else ra[i] = oa.load(k0 + v / (TBM / 4), m0 + (v % (TBM / 4)) * 4, kend, p.M);
       if constexpr (BKM) rb[i] = ob.load(n0 + (v >> 2), k0 + (v & 3) * 4, p.N, kend);
-      else rb[i] = ob.load(k0 + (v >> 5), n0 + (v & 31) * 4, kend, p.N);
+      else rb[i] = ob.load(k0 + v / (TBM / 4), n0 + (v % (TBM / 4)) * 4, kend, p.N);
     }
   };
   auto put = [&](float* t, bool kmaj, int v, float4 r) {
     if (kmaj) {
       const int row = v >> 2, kc = (v & 3) * 4;
-      t[(kc + 0) * F_STRIDE + row] = r.x;
-      t[(kc + 1) * F_STRIDE + row] = r.y;
-      t[(kc + 2) * F_STRIDE + row] = r.z;
-      t[(kc + 3) * F_STRIDE + row] = r.w;
+      t[(kc + 0) * FS + row] = r.x;
+      t[(kc + 1) * FS + row] = r.y;
+      t[(kc + 2) * FS + row] = r.z;
+      t[(kc + 3) * FS + row] = r.w;
     } else {
-      *reinterpret_cast<float4*>(t + (v >> 5) * F_STRIDE + (v & 31) * 4) = r;
+      *reinterpret_cast<float4*>(t + (v / (TBM / 4)) * FS + (v % (TBM / 4)) * 4) = r;
     }
   };
   auto sstore = [&](int buf) {
-    float* ta = lds + buf * 2 * TILE32;
-    float* tb = ta + TILE32;
+    float* ta = lds + buf * 2 * TT;
+    float* tb = ta + TT;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int v = tid + NT * i;
       put(ta, AK, v, ra[i]);
       put(tb, BKM, v, rb[i]);
@@ -1472,20 +1476,20 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p, OA oa, OB ob) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const float* ta = lds + cur * 2 * TILE32;
-    const float* tb = ta + TILE32;
+    const float* ta = lds + cur * 2 * TT;
+    const float* tb = ta + TT;
 #pragma unroll
     for (int kk = 0; kk < BK32; kk += 2) {
       const int kr = kk + (lane >> 5);
-      float af[2], bfr[2];
+      float af[FR], bfr[FR];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = ta[kr * F_STRIDE + wm * 64 + i * 32 + (lane & 31)];
+      for (int i = 0; i < FR; ++i) af[i] = ta[kr * FS + wm * (TBM / 2) + i * 32 + (lane & 31)];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = tb[kr * F_STRIDE + wn * 64 + j * 32 + (lane & 31)];
+      for (int j = 0; j < FR; ++j) bfr[j] = tb[kr * FS + wn * (TBM / 2) + j * 32 + (lane & 31)];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FR; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FR; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < nk) sstore(cur ^ 1);
@@ -1493,13 +1497,13 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p, OA oa, OB ob) {
   }
 
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FR; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FR; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int n = n0 + wn * 64 + j * 32 + (lane & 31);
+        const int m = m0 + wm * (TBM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn * (TBM / 2) + j * 32 + (lane & 31);
         epilogue_store(p, z, blockIdx.z, m, n, acc[i][j][r]);
       }
 }
@@ -1579,9 +1583,16 @@ int launch_typed(int /*dtype: implied by the loaders' element type*/, GemmP p, O
       hipLaunchKernelGGL((gemm_bf16_kernel<128, AK, BKM, OA, OB>), grid, dim3(256), 0, s, p, oa, ob);
     }
   } else {
-    dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
-    if (grid.y > 65535 || grid.z > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
-    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, OA, OB>), grid, dim3(NT), 0, s, p, oa, ob);
+    // 64-row tiles when 128-row tiles would give fewer workgroups than CUs (small fp32 contractions)
+    if ((long)cdiv(p.N, BN) * cdiv(p.M, BM) * batch * p.split_k < 256) {
+      dim3 grid(cdiv(p.N, 64), cdiv(p.M, 64), batch * p.split_k);
+      if (grid.y > 65535 || grid.z > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, OA, OB, 64>), grid, dim3(NT), 0, s, p, oa, ob);
+    } else {
+      dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
+      if (grid.y > 65535 || grid.z > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, OA, OB>), grid, dim3(NT), 0, s, p, oa, ob);
+    }
   }
   return CFM_OK;
 }

@@ -71,7 +71,7 @@ def test_attention_kernels_agree_under_dropout(attn_mode):
 
 @pytest.mark.parametrize("B,T,H", [(3, 373, 2), (2, 384, 1), (2, 64, 3), (3, 97, 2), (2, 33, 1), (1, 1, 2)])
 def test_forward_dma_staging_bit_identical(attn_mode, B, T, H):
-    """The LDS-DMA-staged whole-head forward (default) and the register-staged one (cfm_attn_set_mode bit 5)
+    """The register-staged whole-head forward (default) and the LDS-DMA-staged one (cfm_attn_set_mode bit 5)
     run the same arithmetic in the same order: outputs and lse bit-identical, ragged lengths, dropout."""
     dk = 64
     g = torch.Generator().manual_seed(T + H)
