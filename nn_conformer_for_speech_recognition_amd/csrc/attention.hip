@@ -24,10 +24,11 @@ int attn_simt_fwd_launch(const void*, void*, float*, const int32_t*, const void*
 size_t attn_simt_ws_bytes(int B, int T, int H);
 size_t attn_rel_ws_bytes(int B, int T, int H, int dk);
 int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len, const void* pos, const float* pu,
-                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s);
+                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s,
+                        const void* mask);
 int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, const int32_t* len, const void* pos,
                         const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
-                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s);
+                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s, const void* mask);
 int attn_simt_bwd_launch(const void*, const void*, const void*, const float*, const int32_t*, const void*,
                          const float*, const float*, void*, float*, float*, float*, int, int, int, int, int, float,
                          uint64_t, float*, hipStream_t);
@@ -199,7 +200,8 @@ __device__ __forceinline__ void head_stage(const AttnM& p, const bf16* base0, co
 // l stays the undropped sum, as nn.MultiheadAttention: dropout after the softmax).
 __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16& s1, f32x16& o0, f32x16& o1,
                                              float& m, float& l, float c, int kbase, int len, bool tail, int b,
-                                             int h, int qi, int hh, uint32_t dthr, float dkeep, uint32_t dkey) {
+                                             int h, int qi, int hh, uint32_t dthr, float dkeep, uint32_t dkey,
+                                             uint32_t w) {
   if (tail && kbase + TILE > len) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -229,7 +231,13 @@ __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16&
     o0[r] *= alpha;
     o1[r] *= alpha;
   }
-  if (p.drop_p > 0.f) {
+  if (p.drop_p > 0.f && p.qm) {     // precomputed keep bits (cfm_attn_dropmask), w loaded a tile ahead
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] *= mbit(w, r, dkeep);
+      s1[r] *= mbit(w, 16 + r, dkeep);
+    }
+  } else if (p.drop_p > 0.f) {
     const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kbase) >> 1);   // even: 32-bit pair indices
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
@@ -271,16 +279,20 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
   float m = -INFINITY, l = 0.f;
   const float c = p.scale * LOG2E;
   const int qi = q0 + (lane & 31);
+  const bool pm = p.drop_p > 0.f && p.qm;
+  uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int kt = 0; kt < nkt; ++kt) {
     const bf16* sK = sKall + kt * TILE * KS;
     const bf16* sV = sVall + kt * TILE * KS;
+    const uint32_t wcur = wnext;
+    if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
     f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
       s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
     }
-    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
+    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey, wcur);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -349,7 +361,11 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_dma_kernel(
   float m = -INFINITY, l = 0.f;
   const float c = p.scale * LOG2E;
   const int qi = q0 + (lane & 31);
+  const bool pm = p.drop_p > 0.f && p.qm;
+  uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int kt = 0; kt < nkt; ++kt) {
+    const uint32_t wcur = wnext;
+    if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
     const int last = 16 * kt + 15;         // this wave's pieces of tiles <= kt: P = wv + j nw <= last
     const int done = last >= wv ? min(issued, (last - wv) / nw + 1) : 0;
     wait_vm_n(issued - done);
@@ -363,7 +379,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_dma_kernel(
       s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hfrag(tK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
       s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hfrag(tK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
     }
-    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
+    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey, wcur);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -418,8 +434,14 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
   const int nks = (len + 31) / 32;
   const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
   const uint32_t hq = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)qi) * T2 + (uint32_t)(2 * hh);
+  const bool pm = p.drop_p > 0.f && p.qm;
+  uint32_t wcur = 0u, wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int ks = 0; ks < nks; ++ks) {
     const int k0 = ks * 32;
+    if (pm && (ks & 1) == 0) {       // a new 64-key tile: its word was loaded a tile ahead
+      wcur = wnext;
+      if (2 * ((ks >> 1) + 1) < nks) wnext = qm_word(p, b, h, (ks >> 1) + 1, qi, hh);
+    }
     f32x16 s0 = (f32x16){0}, d0 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -428,7 +450,11 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
       if (s == 1) __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (p.drop_p > 0.f) {
+    if (pm) {
+      const uint32_t w = wcur >> (16 * (ks & 1));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d0[r] *= mbit(w, r, dkeep);
+    } else if (p.drop_p > 0.f) {
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
         const uint32_t hsh = cfm_mix32(
@@ -639,13 +665,17 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
         sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, q0, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       bf16x8 pf[2];
-      unsigned bits = 0;
+      const bool pre = drop && p.km != nullptr;     // precomputed keep bits: this lane's 16 bits of the step
+      unsigned bits = pre ? (km_word(p, b, h, qt, kj) >> (16 * hh)) & 0xFFFFu : 0u;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {          // registers 4g .. 4g+3 = queries q0 + 8g + 4hh + 0..3
         const float4 Lg = *reinterpret_cast<const float4*>(sL + q0 + 8 * g + 4 * hh);
         const float Lr[4] = {Lg.x, Lg.y, Lg.z, Lg.w};
         float mk[4] = {1.f, 1.f, 1.f, 1.f};
-        if (drop) {
+        if (pre) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) mk[e] = mbit(bits, 4 * g + e, dkeep);
+        } else if (drop) {
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
             // (the wave-uniform offset through readfirstlane: otherwise the per-register bases are
@@ -966,6 +996,32 @@ size_t head_lds_bytes(int T) {
   return img > stage ? img : stage;
 }
 
+// ------------------------------------------------------------------------------------ dropout keep bits
+// The query-major keep bits (AttnM::qm) from the same counter-based hash as the per-element path (didx pairs,
+// cfm_mix32 with the step-salted key, 16 bits per element).  grid (ceil(2 Tq / 256), nkt, B*H): one thread per
+// word, 16 pair hashes, 32-bit index math.  (The dK/dV kernels keep hashing in-kernel: their DPP-shared hash
+// costs less than a second, key-major layout would.)
+__global__ __launch_bounds__(256) void attn_dropmask_kernel(AttnM p, uint32_t* __restrict__ qm, MaskGeo g) {
+  const uint64_t seed = salted_seed(p.seed, p.salt);
+  const uint32_t key = drop_key(seed, 0), thr = drop_thr(p.drop_p);
+  const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= 2 * g.Tq) return;
+  const int q = f >> 1, hh = f & 1, kt = blockIdx.y;
+  const uint32_t bh = blockIdx.z;
+  const uint32_t rowj = (bh * (uint32_t)p.T + (uint32_t)q) * T2 + (uint32_t)(32 * kt);
+  uint32_t w = 0;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const uint32_t hs = cfm_mix32((rowj + (uint32_t)((32 * t + acc_row(r, hh)) >> 1)) ^ key);
+      w |= ((hs & 0xFFFFu) >= thr ? 1u : 0u) << (16 * t + r);
+      w |= ((hs >> 16) >= thr ? 1u : 0u) << (16 * t + r + 1);
+    }
+  qm[((long)(bh * g.nkt + kt) * g.Tq) * 2 + f] = w;
+}
+
 // Q rows of every wave + K and V of the padded length; the epilogue staging aliases them
 size_t head_dma_lds_bytes(int T) {
   const size_t img = ((size_t)cdiv(T, 32) * 32 + 2 * (size_t)cdiv(T, TILE) * TILE) * 128;
@@ -975,9 +1031,43 @@ size_t head_dma_lds_bytes(int T) {
 
 }  // namespace
 
+CFM_EXPORT size_t cfm_attn_dropmask_bytes(int B, int T, int H) {
+  const MaskGeo g = mask_geo(B, T, H);
+  return (size_t)(g.qwords + g.kwords) * sizeof(uint32_t);
+}
+
+CFM_EXPORT int cfm_attn_dropmask(void* mask, int B, int T, int H, float drop_p, uint64_t seed, void* stream) {
+  CFM_REQUIRE(mask, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(B > 0 && T > 0 && H > 0, CFM_ERR_SHAPE, "bad shape");
+  CFM_REQUIRE((double)B * H * T * (T + 1) < 8589934592.0, CFM_ERR_SHAPE, "attention dropout index space (2^33)");
+  if (drop_p <= 0.f) return CFM_OK;
+  const MaskGeo g = mask_geo(B, T, H);
+  AttnM p{};
+  p.B = B; p.T = T; p.H = H; p.drop_p = drop_p; p.seed = seed; p.salt = cfm::g_rng_salt;
+  hipLaunchKernelGGL(attn_dropmask_kernel, dim3((unsigned)cdiv(2 * g.Tq, 256), g.nkt, B * H), dim3(256), 0,
+                     cfm::as_stream(stream), p, (uint32_t*)mask, g);
+  return cfm::check_launch("cfm_attn_dropmask");
+}
+
+static int attn_fwd_impl(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
+                         const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
+                         float drop_p, uint64_t seed, void* stream, const void* mask);
+
 CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
                             const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
                             float drop_p, uint64_t seed, void* stream) {
+  return attn_fwd_impl(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, stream, nullptr);
+}
+
+CFM_EXPORT int cfm_attn_fwd_m(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
+                              const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
+                              float drop_p, uint64_t seed, const void* mask, void* stream) {
+  return attn_fwd_impl(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, stream, mask);
+}
+
+static int attn_fwd_impl(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
+                         const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
+                         float drop_p, uint64_t seed, void* stream, const void* mask) {
   CFM_REQUIRE(qkv && o && lse && lengths, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0 && dk <= 1024, CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(!pos || (pos_u && pos_v), CFM_ERR_ARG, "rel-pos needs pos_u and pos_v");
@@ -987,10 +1077,12 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   hipStream_t s = cfm::as_stream(stream);
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, s);
-  if (pos) return cfm::attn_rel_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, drop_p, seed, s);
+  if (pos)
+    return cfm::attn_rel_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, drop_p, seed, s, mask);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 6,
           cfm::g_rng_salt};
+  if (use_head(T)) set_mask(p, mask);     // the whole-head kernels read the bits; the tiled ones hash
   if (use_head(T) && p.vec && dk == DKP && (g_attn_mode & 32)) {
     // LDS-DMA staging (cfm_attn_set_mode bit 5; measured no faster than register staging at T = 373:
     // profiles/r03/attn_fwd_dma_ab.txt)
@@ -1017,7 +1109,8 @@ CFM_EXPORT size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel, in
 static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const float* lse,
                          const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                          void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
-                         int dtype, float drop_p, uint64_t seed, float* ws, void* stream, bool d_ready) {
+                         int dtype, float drop_p, uint64_t seed, float* ws, void* stream, bool d_ready,
+                         const void* mask = nullptr) {
   CFM_REQUIRE(qkv && o && dout && lse && lengths && dqkv && ws, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0, CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(!pos || (pos_u && pos_v && dpos && dpos_u && dpos_v), CFM_ERR_ARG, "rel-pos grads need buffers");
@@ -1038,7 +1131,8 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
                        (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
   if (pos)
     return cfm::attn_rel_bwd_launch(qkv, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H,
-                                    dk, drop_p, seed, ws, s);
+                                    dk, drop_p, seed, ws, s, mask);
+  if (use_head(T) && (g_attn_mode & 8) == 0) set_mask(p, mask);   // whole-head dQ + wave dK/dV read the bits
   if (use_head(T) && (g_attn_mode & 8) == 0)
     hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), dkdv_wave_lds_bytes(T), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);
@@ -1071,6 +1165,15 @@ CFM_EXPORT int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* d
                                    int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
   return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H, dk, dtype,
                        drop_p, seed, ws, stream, true);
+}
+
+CFM_EXPORT int cfm_attn_bwd_m(const void* qkv, const void* o, const void* dout, const float* lse,
+                              const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
+                              void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
+                              int dtype, float drop_p, uint64_t seed, float* ws, int d_ready, const void* mask,
+                              void* stream) {
+  return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H, dk, dtype,
+                       drop_p, seed, ws, stream, d_ready != 0, mask);
 }
 
 CFM_EXPORT int cfm_attn_set_mode(int mode) {

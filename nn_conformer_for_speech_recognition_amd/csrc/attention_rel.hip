@@ -182,9 +182,13 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
     }
     __syncthreads();
   }
+  const bool pm = p.drop_p > 0.f && p.qm;
+  uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int kt = 0; kt < nkt; ++kt) {
     const bf16* sK = skv + (kt & 1) * 2 * TILE * KS;
     const bf16* sV = sK + TILE * KS;
+    const uint32_t wcur = wnext;
+    if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
     if (kt + 1 < nkt) {
       tile_load(p, b, (kt + 1) * TILE, kcol, rk, tid);
       tile_load(p, b, (kt + 1) * TILE, vcol, rv, tid);
@@ -219,7 +223,14 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
       o0[r] *= alpha;
       o1[r] *= alpha;
     }
-    if (p.drop_p > 0.f) {
+    if (p.drop_p > 0.f && p.qm) {      // precomputed keep bits (cfm_attn_dropmask)
+      const uint32_t w = wcur;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] *= mbit(w, r, dkeep);
+        s1[r] *= mbit(w, 16 + r, dkeep);
+      }
+    } else if (p.drop_p > 0.f) {
       const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
@@ -299,9 +310,13 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
     }
     __syncthreads();
   }
+  const bool pm = p.drop_p > 0.f && p.qm;
+  uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int kt = 0; kt < nkt; ++kt) {
     const bf16* sK = skv + (kt & 1) * 2 * TILE * KS;
     const bf16* sV = sK + TILE * KS;
+    const uint32_t wcur = wnext;
+    if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
     if (kt + 1 < nkt) {
       tile_load(p, b, (kt + 1) * TILE, kcol, rk, tid);
       tile_load(p, b, (kt + 1) * TILE, vcol, rv, tid);
@@ -317,7 +332,14 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
       d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 0, 16 * s, lane), gf[s], d0, 0, 0, 0);
       d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32, 16 * s, lane), gf[s], d1, 0, 0, 0);
     }
-    if (p.drop_p > 0.f) {
+    if (p.drop_p > 0.f && p.qm) {
+      const uint32_t w = wcur;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        d0[r] *= mbit(w, r, dkeep);
+        d1[r] *= mbit(w, 16 + r, dkeep);
+      }
+    } else if (p.drop_p > 0.f) {
       const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
@@ -535,13 +557,17 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
       const float* tL = sLD[cur][0] + 32 * t;
       const float* tD = sLD[cur][1] + 32 * t;
       f32x16 pd;
+      const uint32_t wkm = (drop && p.km) ? km_word(p, b, h, 2 * qt + t, kj) >> (16 * hh) : 0u;
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         // dropout of (query of register r / r+1, key kj): lanes kj, kj^1 share one 32-bit hash per query
         // (index (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2); the even lane hashes register r's query,
         // the odd lane register r+1's, and a DPP swap hands each lane its partner's
         float m0 = 1.f, m1 = 1.f;
-        if (drop) {
+        if (drop && p.km) {
+          m0 = mbit(wkm, r, dkeep);
+          m1 = mbit(wkm, r + 1, dkeep);
+        } else if (drop) {
           const uint32_t hm = cfm_mix32(
               (hbase + __builtin_amdgcn_readfirstlane((qt * TILE + 32 * t + (r & 3) + 8 * (r >> 2)) * (int)T2)) ^ dkey);
           const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
@@ -697,16 +723,18 @@ static RelP make_relp(const void* pos, const float* pu, const float* pv, int dk)
 }
 
 static AttnM make_attnm(const void* qkv, const void* dout, const int32_t* len, int B, int T, int H, int dk,
-                        float drop_p, uint64_t seed) {
+                        float drop_p, uint64_t seed, const void* mask) {
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, len, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), 0,
           g_rng_salt};
+  set_mask(p, mask);
   return p;
 }
 
 int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len, const void* pos, const float* pu,
-                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s) {
-  const AttnM p = make_attnm(qkv, qkv, len, B, T, H, dk, drop_p, seed);
+                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s,
+                        const void* mask) {
+  const AttnM p = make_attnm(qkv, qkv, len, B, T, H, dk, drop_p, seed, mask);
   hipLaunchKernelGGL(attn_rel_fwd_kernel, dim3(cdiv(p.T, 128), p.H, p.B), dim3(256), 0, s, p,
                      make_relp(pos, pu, pv, p.dk), (bf16*)o, lse);
   return check_launch("cfm_attn_fwd(rel)");
@@ -715,8 +743,9 @@ int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len
 // D (rowsum dO*O per head) must already be in ws[0 .. B*H*T)
 int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, const int32_t* len, const void* pos,
                         const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
-                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s) {
-  const AttnM p = make_attnm(qkv, dout, len, B, T, H, dk, drop_p, seed);
+                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s,
+                        const void* mask) {
+  const AttnM p = make_attnm(qkv, dout, len, B, T, H, dk, drop_p, seed, mask);
   const RelP rp = make_relp(pos, pu, pv, p.dk);
   const size_t d_bytes = ((size_t)p.B * p.H * p.T * sizeof(float) + 255) & ~(size_t)255;
   float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + d_bytes);

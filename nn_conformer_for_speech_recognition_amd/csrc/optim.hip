@@ -65,7 +65,13 @@ __global__ __launch_bounds__(EB) void ada_colpart(const AdaP* __restrict__ t, in
   float cacc[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) cacc[k] = 0.f;
-  for (int r = r0 + wv; r < r1; r += 4) {
+  // the wave's RB/4 rows: their sums stay in registers (lane j keeps row j's) and the row EMAs are updated
+  // once after the loop -- a read-modify-write per row inside it serialised every row on a memory round trip
+  float rsum = 0.f;
+#pragma unroll 2
+  for (int j = 0; j < RB / 4; ++j) {
+    const int r = r0 + wv + 4 * j;
+    if (r >= r1) break;
     const float* g = q.g + ((long)b * q.R + r) * q.C;
     float s = 0.f;
 #pragma unroll
@@ -79,7 +85,11 @@ __global__ __launch_bounds__(EB) void ada_colpart(const AdaP* __restrict__ t, in
       }
     }
     s = wave_sum(s);
-    if (lane == 0) row_update(q, (long)b * q.R + r, s, b2t);
+    rsum = lane == j ? s : rsum;
+  }
+  {
+    const int r = r0 + wv + 4 * lane;
+    if (lane < RB / 4 && r < r1) row_update(q, (long)b * q.R + r, rsum, b2t);
   }
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
@@ -218,10 +228,15 @@ __global__ __launch_bounds__(EB) void ada_sumsq(const AdaP* __restrict__ t, int 
   const long end = min(q.numel, start + CHUNK);
   float s = 0.f;
   if (vec4_ok(q)) {
-    for (long i = start + 4 * threadIdx.x; i < end; i += 4 * EB) {
-      float u[4];
-      ada_u<4>(q, rowmean, (unsigned)i, b2t, eps1, true, u);
-      s += u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3];
+    // CHUNK / (4 EB) = 4 float4 steps per thread, unrolled: their loads are in flight together
+#pragma unroll
+    for (int j = 0; j < CHUNK / (4 * EB); ++j) {
+      const long i = start + 4 * threadIdx.x + (long)j * 4 * EB;
+      if (i < end) {
+        float u[4];
+        ada_u<4>(q, rowmean, (unsigned)i, b2t, eps1, true, u);
+        s += u[0] * u[0] + u[1] * u[1] + u[2] * u[2] + u[3] * u[3];
+      }
     }
   } else {
     for (long i = start + threadIdx.x; i < end; i += EB) {

@@ -3,6 +3,7 @@ nn.MultiheadAttention's core: softmax(q k^T / sqrt(dk) + key_padding_mask) v, ra
 Every kernel family is checked: whole-head with the wave-per-key-block dK/dV (default), tiled (mode 1),
 four-wave whole-head dK/dV (mode 8); and the three must agree with each other under dropout (same
 counter-based masks; the dQ, dK and dV slices compared separately)."""
+import numpy as np
 import pytest
 import torch
 
@@ -182,3 +183,96 @@ def test_rel_attention_mfma_matches_simt_under_dropout(attn_mode):
         outs.append((o.float(), g[0].float(), g[1], g[2], g[3]))
     for a, b in zip(outs[0], outs[1]):
         assert _rel(a, b) < 3e-2
+
+
+# ------------------------------------------------------------------------------------ precomputed dropout bits
+def _mix32(x):
+    x = x.astype(np.uint64) & 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def _acc_row(r, hh):
+    return (r & 3) + 8 * (r >> 2) + 4 * hh
+
+
+def _mask_words(B, T, H, p, seed):
+    """numpy restatement of cfm_attn_dropmask (attention.hip attn_dropmask_kernel): query-major words (and, for the
+    layout cross-check, key-major ones) from the per-element-pair hash the attention kernels use (cfm_common.h
+    cfm_mix32 / drop_key)."""
+    key = int(_mix32(np.array([(seed & 0xFFFFFFFF) ^ int(_mix32(np.array([((seed >> 32) + 0x9E3779B9) & 0xFFFFFFFF]))[0])]))[0])
+    thr = int(np.float32(p) * np.float32(65536.0) + np.float32(0.5))
+    T2 = (T + (T & 1)) >> 1
+    nkt, Tq = (T + 63) // 64, (T + 127) // 128 * 128
+    nqs, Tk = 2 * nkt, Tq
+    bh = np.arange(B * H, dtype=np.uint64)[:, None, None, None]
+    kt = np.arange(nkt, dtype=np.uint64)[None, :, None, None]
+    q = np.arange(Tq, dtype=np.uint64)[None, None, :, None]
+    hh = np.arange(2)[None, None, None, :]
+    qm = np.zeros((B * H, nkt, Tq, 2), dtype=np.uint64)
+    for t in range(2):
+        for r in range(0, 16, 2):
+            k = 64 * kt + 32 * t + _acc_row(r, hh).astype(np.uint64)
+            hs = _mix32((((bh * T + q) * T2 + k // 2) & 0xFFFFFFFF) ^ key)
+            qm |= ((hs & 0xFFFF) >= thr).astype(np.uint64) << (16 * t + r)
+            qm |= ((hs >> 16) >= thr).astype(np.uint64) << (16 * t + r + 1)
+    bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
+    qs = np.arange(nqs, dtype=np.uint64)[None, :, None]
+    kp = np.arange(Tk // 2, dtype=np.uint64)[None, None, :]
+    w0 = np.zeros((B * H, nqs, Tk // 2), dtype=np.uint64)
+    w1 = np.zeros_like(w0)
+    for h2 in range(2):
+        for r in range(16):
+            qq = 32 * qs + _acc_row(r, h2)
+            hs = _mix32((((bh * T + qq) * T2 + kp) & 0xFFFFFFFF) ^ key)
+            w0 |= ((hs & 0xFFFF) >= thr).astype(np.uint64) << (16 * h2 + r)
+            w1 |= ((hs >> 16) >= thr).astype(np.uint64) << (16 * h2 + r)
+    km = np.stack([w0, w1], -1).reshape(B * H, nqs, Tk)
+    return qm.reshape(-1).astype(np.uint32), km.reshape(-1).astype(np.uint32)
+
+
+@pytest.mark.parametrize("B,T,H,seed", [(2, 373, 2, 9), (1, 97, 3, (1 << 40) + 5), (2, 64, 1, 77)])
+def test_dropmask_bits_match_hash(B, T, H, seed):
+    m = ops.attn_dropmask(B, T, H, 0.1, seed, DEV)
+    torch.cuda.synchronize()
+    got = m.cpu().numpy().view(np.uint32)
+    qm, _ = _mask_words(B, T, H, 0.1, seed)
+    assert got.size == qm.size           # query-major words only (the dK/dV kernels hash in-kernel)
+    np.testing.assert_array_equal(got, qm)
+    keep = np.unpackbits(got.view(np.uint8)).mean()
+    assert 0.88 < keep < 0.92
+
+
+@pytest.mark.parametrize("rel", [False, True])
+@pytest.mark.parametrize("T", [373, 97])
+def test_dropmask_path_matches_hash_path(rel, T):
+    """Forward + every gradient with the precomputed bits == the per-element hash path (same masks; only the
+    bf16 rounding order differs), ragged lengths, relative positions on and off."""
+    B, H, dk = 2, 2, 64
+    g = torch.Generator().manual_seed(T + 3 * rel)
+    qkv = torch.randn(B * T, 3 * H * dk, generator=g).to(DEV, torch.bfloat16)
+    lens = torch.tensor([T, T - 31], dtype=torch.int32, device=DEV)
+    do = torch.randn(B * T, H * dk, generator=g).to(DEV, torch.bfloat16)
+    pos = pu = pv = None
+    if rel:
+        pos = (0.5 * torch.randn(2 * T - 1, H * dk, generator=g)).to(DEV, torch.bfloat16)
+        pu = (0.3 * torch.randn(H * dk, generator=g)).to(DEV)
+        pv = (0.3 * torch.randn(H * dk, generator=g)).to(DEV)
+    outs = []
+    for use_mask in (False, True):
+        mask = ops.attn_dropmask(B, T, H, 0.1, 21, DEV) if use_mask else None
+        o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, pos, pu, pv, drop_p=0.1, seed=21, mask=mask)
+        dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, pos, pu, pv, drop_p=0.1, seed=21,
+                                            mask=mask)
+        outs.append((o.float(), dqkv.float(), dpos, dpu))
+    HD = H * dk
+    assert _rel(outs[1][0], outs[0][0]) < 3e-3
+    for sl in range(3):
+        assert _rel(outs[1][1][:, sl * HD:(sl + 1) * HD], outs[0][1][:, sl * HD:(sl + 1) * HD]) < 5e-3, sl
+    if rel:
+        assert _rel(outs[1][2], outs[0][2]) < 5e-3
+        assert _rel(outs[1][3], outs[0][3]) < 5e-3
