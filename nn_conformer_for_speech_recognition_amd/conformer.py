@@ -261,9 +261,10 @@ def _mha_fwd(x, P, R, cfg, seed, lens):
         pos = ops.linear(_w(cfg.pe, cd), wpos)          # (2T-1, d) projected table (no bias)
         pu = R[1].reshape(-1).float().contiguous()
         pv = R[2].reshape(-1).float().contiguous()
-    # attention-dropout keep bits once per step (cfm_attn_dropmask), read by the forward and both backward kernels
+    # attention-dropout keep bits once per step (cfm_attn_dropmask; opt-in CFM_ENABLE=dropmask: measured no faster
+    # than the in-kernel hashes at L15 / L60, profiles/r03/dropmask_ab.txt)
     mask = (ops.attn_dropmask(B, T, H, cfg.p, seed, qkv.device)
-            if cfg.p > 0 and cd == torch.bfloat16 and "dropmask" not in ops.DISABLED else None)
+            if cfg.p > 0 and cd == torch.bfloat16 and "dropmask" in ops.ENABLED else None)
     o, lse = ops.attn_fwd(qkv, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed, mask=mask)
     y = _fp8_linear(o, cfg, 10, bias=P[11], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, residual=x)
     if y is None:

@@ -1626,8 +1626,9 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 //   V128S: 128x128 tile, BK 32, 3-stage ring (68 KiB incl. the aliased epilogue staging: two
 //          workgroups of 4 waves per CU) -- narrow outputs (N = 512) fill the chip
 template <bool AK, bool BKM, bool M16 = false>
-void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
-  const int sel = (g_gemm_mode >> 4) & 7;   // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S, 5 V192, 6 V192S, 7 V192S8
+void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s, int force = 0) {
+  // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S, 5 V192, 6 V192S, 7 V192S8
+  const int sel = force ? force : (g_gemm_mode >> 4) & 7;
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k), g128(cdiv(p.N, BN), cdiv(p.M, 128), batch * p.split_k);
   int v = sel;
   if constexpr (AK) {
@@ -1726,6 +1727,47 @@ int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
     else
       hipLaunchKernelGGL((gemm_pipe_ie_kernel<false>), dim3(grid), dim3(IE_NWV * 64), 0, s, p, oa, ob, ntm, ntn);
     return CFM_OK;
+  }
+  // Tail-balanced row split for wide, short-reduction K-major GEMMs that would run on 256 x 128 tiles two per CU
+  // (FFN up-projection forward, FFN down-projection data gradient: M 11,936, N 2048, K 512 -> 752 tiles on 512
+  // slots, the second round 47 % full): the first full rounds on 256-row tiles, the remaining rows on 128-row
+  // tiles in ONE round (half-height tiles: the tail costs half a round).  Epilogue indices stay global (C / pre /
+  // residual row offsets, dropout index offset).  Opt-in (cfm_gemm_set_mode bit 17): measured SLOWER at L15 (step
+  // 21.61 -> 22.01 ms, profiles/r03/gemm_tail_split_ab.txt) -- one 512-tile round takes 46 us vs 68 us for all 752
+  // tiles, i.e. the kernel's time follows its tile count (store-bound epilogues), not its rounds.
+  if (ak && bkm && d.batch == 1 && p.split_k == 1 && !p.cmap && !p.rd_out && !p.acs_slab && (g_gemm_mode & 131072) &&
+      ((g_gemm_mode >> 4) & 7) == 0 && p.N > 1536 && p.k_per_split <= 512) {
+    const long slots = 2L * num_cus();
+    const int ntn = cdiv(p.N, BN);
+    const long tiles = (long)cdiv(p.M, 256) * ntn;
+    const long per_round = slots / ntn;                 // 256-row panels per full round
+    const int rows_big = (int)((tiles / slots) * per_round * 256);
+    const int rest = p.M - rows_big;
+    if (tiles > slots && rows_big > 0 && rest > 0 && (long)cdiv(rest, 128) * ntn <= slots) {
+      GemmP p1 = p, p2 = p;
+      p1.M = rows_big;
+      p2.M = rest;
+      const int ec = p.dtc == CFM_BF16 ? 2 : 4;
+      p2.C = (char*)p.C + (long)rows_big * p.ldc * ec;
+      if (p.pre) p2.pre = (char*)p.pre + (long)rows_big * p.ldc * (p.dtpre == CFM_BF16 ? 2 : 4);
+      if (p.res) p2.res = (const char*)p.res + (long)rows_big * p.ldr * (p.dtr == CFM_BF16 ? 2 : 4);
+      p2.doff = p.doff + (uint64_t)rows_big * (uint64_t)p.N;
+      PipeOp oa1 = oa, oa2 = oa;
+      oa1.lim = rows_big;
+      oa2.base = oa.base + (long)rows_big * oa.ld;
+      oa2.lim = rest;
+      oa2.bytes = (unsigned)(pipe_extent(1, rest, p.K, oa.ld) * 2);
+      p1.vec_c = vec_epilogue_ok(p1);
+      p2.vec_c = vec_epilogue_ok(p2);
+      if (!(g_gemm_mode & 8192)) {
+        launch_pipe_t<true, true, true>(p1, oa1, ob, 1, s, 2);
+        launch_pipe_t<true, true, true>(p2, oa2, ob, 1, s, 4);
+      } else {
+        launch_pipe_t<true, true>(p1, oa1, ob, 1, s, 2);
+        launch_pipe_t<true, true>(p2, oa2, ob, 1, s, 4);
+      }
+      return CFM_OK;
+    }
   }
   // the K-major x K-major GEMMs (forward and data-gradient) run 16x16x32 MFMA main loops (L15 step 25.0 -> 24.7 ms
   // same-box A/B); cfm_gemm_set_mode bit 13 selects the 32x32x16 form

@@ -94,6 +94,7 @@ def linear_dgrad(dy, w, out_dtype=None, pre=None, act_grad=False, drop_p=0.0, se
 
 # fusions that can be switched off for same-box A/B timing: CFM_DISABLE="rowdot,lndrop,wgbias"
 DISABLED = frozenset(x for x in os.environ.get("CFM_DISABLE", "").split(",") if x)
+ENABLED = frozenset(x for x in os.environ.get("CFM_ENABLE", "").split(",") if x)   # opt-in variants (A/B)
 
 # target workgroup count (in 128x128-tile units) of the split-K weight-gradient GEMMs
 _WGRAD_WGS = int(os.environ.get("CFM_WGRAD_WGS", "512"))

@@ -516,3 +516,34 @@ def test_bn_folded_dwconv_bwd(training, sync, B, T, C, K, dt):
     assert _rel(da.float(), da2.float()) < 1e-5
     assert _rel(dw, dw2) < 1e-5 and (db - db2).norm() < 1e-5 * dw.norm()
     assert torch.equal(dg, dg2) and torch.equal(dbt, dbt2)
+
+
+@pytest.mark.parametrize("M", [11936, 9000])
+def test_gemm_tail_split_matches_single_launch(gemm_mode, M):
+    """The tail-balanced row split of wide short-K K-major GEMMs (256-row tiles for whole rounds, 128-row tiles
+    for the rest; opt-in cfm_gemm_set_mode bit 17) against one launch: FFN up-projection forward (bias +
+    SiLU + pre-activation + dropout) and FFN down-projection data gradient (silu'(pre) + dropout) epilogues.
+    Same dropout masks (global element index), values within the two MFMA shapes' fp32 summation order."""
+    N, K = 2048, 512
+    g = torch.Generator().manual_seed(M)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g)).to(DEV, torch.bfloat16)
+    b = (0.1 * torch.randn(N, generator=g)).to(DEV)
+    dz = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w2t = (0.05 * torch.randn(N, K, generator=g)).to(DEV, torch.bfloat16)
+    outs = []
+    for mode in (3 | 131072, 3):
+        gemm_mode(mode)
+        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        y = ops.linear(x, w, b, out_dtype=torch.bfloat16, act=1, pre=pre, drop_p=0.1, seed=5)
+        gd = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.gemm(dz, w2t, gd, M, N, K, act_grad=True, pre=pre, drop_p=0.1, seed=6)
+        torch.cuda.synchronize()
+        outs.append((y.float(), pre.float(), gd.float()))
+    (y1, p1, g1), (y0, p0, g0) = outs
+    assert _rel(p1, p0) < 2e-3
+    assert _rel(y1, y0) < 2e-3
+    assert _rel(g1, g0) < 2e-3
+    drop1, drop0 = (y1 == 0) & (p1 != 0), (y0 == 0) & (p0 != 0)
+    assert (drop1 != drop0).float().mean().item() < 1e-4
+    assert 0.08 < drop0.float().mean().item() < 0.12
