@@ -23,6 +23,7 @@ int attn_simt_fwd_launch(const void*, void*, float*, const int32_t*, const void*
                          int, int, int, int, float, uint64_t, hipStream_t);
 size_t attn_simt_ws_bytes(int B, int T, int H);
 size_t attn_rel_ws_bytes(int B, int T, int H, int dk);
+extern int g_rel_mode;   // attention_rel.hip: cfm_attn_set_mode's bits for the rel-pos kernels
 int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len, const void* pos, const float* pu,
                         const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s,
                         const void* mask);
@@ -1178,5 +1179,6 @@ CFM_EXPORT int cfm_attn_bwd_m(const void* qkv, const void* o, const void* dout, 
 
 CFM_EXPORT int cfm_attn_set_mode(int mode) {
   g_attn_mode = mode;
+  cfm::g_rel_mode = mode;
   return CFM_OK;
 }

@@ -63,9 +63,19 @@ __device__ __forceinline__ void load_q_uv(const AttnM& p, const RelP& rp, int b,
   }
 }
 
-// 16-B chunk `v` (0..511) of a 64-row chunk of the band: row v>>3, columns (v&7)*8
+// s_waitcnt vmcnt(0) as a real instruction the compiler's wait insertion accounts for (inline asm is opaque to
+// it): issued once after a kernel's prologue loads (q fragments, K/V of the head) so that their first use inside
+// the tile loop does not make the compiler wait for everything outstanding -- the prefetch just issued included --
+// on every iteration.  gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15.
+__device__ __forceinline__ void wait_prologue_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// 16-B chunk `v` (0..511) of a 64-row chunk of the band: row v>>3, columns (v&7)*8.  VEC: relative rows
+// outside [0, 2T-1) clamp to the nearest valid row instead of reading zero (branch-free prefetch, ld8c):
+// such rows only ever meet (query, key) pairs outside the valid range, whose probabilities are zero
+template <bool VEC>
 __device__ __forceinline__ uint4 ring_chunk_load(const AttnM& p, const RelP& rp, int h, int row0, int v) {
-  return ld8p(p, rp, h, row0 + (v >> 3), (v & 7) * 8);
+  if constexpr (VEC) return ld8c(rp.pos + h * p.dk, p.HD, row0 + (v >> 3), 2 * p.T - 1, (v & 7) * 8);
+  else return ld8p(p, rp, h, row0 + (v >> 3), (v & 7) * 8);
 }
 __device__ __forceinline__ void ring_chunk_store(bf16* slot, const uint4 (&reg)[2], int tid) {
 #pragma unroll
@@ -146,6 +156,7 @@ __device__ __forceinline__ BandRows band_rows_q(const bf16* ring, int kt, int wv
 
 // ------------------------------------------------------------------------------------ forward
 // grid (ceil(T/128), H, B), 4 waves x 32 queries; K/V tiles of 64 keys double-buffered, band ring.
+template <bool VEC>
 __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf16* __restrict__ o,
                                                            float* __restrict__ lse) {
   if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
@@ -170,18 +181,19 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
   uint4 rk[2], rv[2], rq[2];
   const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
   if (nkt > 0) {
-    tile_load(p, b, 0, kcol, rk, tid);
-    tile_load(p, b, 0, vcol, rv, tid);
+    tile_load<VEC>(p, b, 0, kcol, rk, tid);
+    tile_load<VEC>(p, b, 0, vcol, rv, tid);
     tile_store(skv, rk, tid);
     tile_store(skv + TILE * KS, rv, tid);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load(p, rp, h, rbase + ch * TILE, tid + 256 * i);
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
       ring_chunk_store(sring + ch * TILE * KS, rq, tid);
     }
     __syncthreads();
   }
+  wait_prologue_loads();
   const bool pm = p.drop_p > 0.f && p.qm;
   uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int kt = 0; kt < nkt; ++kt) {
@@ -190,10 +202,10 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
     const uint32_t wcur = wnext;
     if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
     if (kt + 1 < nkt) {
-      tile_load(p, b, (kt + 1) * TILE, kcol, rk, tid);
-      tile_load(p, b, (kt + 1) * TILE, vcol, rv, tid);
+      tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
+      tile_load<VEC>(p, b, (kt + 1) * TILE, vcol, rv, tid);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
     }
     f32x16 s0, s1;
     scores_qlanes(sK, band_rows_q(sring, kt, wv), qu, qv, st, s0, s1, lane);
@@ -268,6 +280,7 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
 // ------------------------------------------------------------------------------------ dQ (+ du, dv partials)
 // grid (ceil(T/128), H, B).  part: (B * 4*gridDim.x, 2*H*dk) fp32 -- row (b, 32-query block): per-column
 // sums over the block's queries of scale * sum_j dS k_j (u half) and scale * sum_j dS p_r (v half).
+template <bool VEC>
 __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, const bf16* __restrict__ dout,
                                                               const float* __restrict__ lse,
                                                               const float* __restrict__ Dg, bf16* __restrict__ dqkv,
@@ -298,18 +311,19 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
   uint4 rk[2], rv[2], rq[2];
   const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
   if (nkt > 0) {
-    tile_load(p, b, 0, kcol, rk, tid);
-    tile_load(p, b, 0, vcol, rv, tid);
+    tile_load<VEC>(p, b, 0, kcol, rk, tid);
+    tile_load<VEC>(p, b, 0, vcol, rv, tid);
     tile_store(skv, rk, tid);
     tile_store(skv + TILE * KS, rv, tid);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load(p, rp, h, rbase + ch * TILE, tid + 256 * i);
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
       ring_chunk_store(sring + ch * TILE * KS, rq, tid);
     }
     __syncthreads();
   }
+  wait_prologue_loads();
   const bool pm = p.drop_p > 0.f && p.qm;
   uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int kt = 0; kt < nkt; ++kt) {
@@ -318,10 +332,10 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
     const uint32_t wcur = wnext;
     if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
     if (kt + 1 < nkt) {
-      tile_load(p, b, (kt + 1) * TILE, kcol, rk, tid);
-      tile_load(p, b, (kt + 1) * TILE, vcol, rv, tid);
+      tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
+      tile_load<VEC>(p, b, (kt + 1) * TILE, vcol, rv, tid);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
     }
     const BandRows br = band_rows_q(sring, kt, wv);
     f32x16 s0, s1;
@@ -424,6 +438,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
 // starting at relative row T-64-64qt+J0; it moves DOWN one chunk per query tile (ring chunk kc holds
 // rows T-64+J0-64(kc-2) ..+63, tile qt uses chunks qt, qt+1, qt+2).
 // dsbuf: (B, H, T, ldS) bf16, scale * dS, query-major.
+template <bool VEC>
 __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp, const bf16* __restrict__ dout,
                                                                 const float* __restrict__ lse,
                                                                 const float* __restrict__ Dg,
@@ -458,22 +473,41 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
   float* st = sst + wv * 32 * SS2;
   uint4 rq[2], rg[2], rr[2];
   float rl = 0.f, rd = 0.f;
+  bool rlv = false;
   const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
   const bf16* gbase = dout + (long)b * p.T * p.HD + h * p.dk;
+  // next query tile into registers; VEC: branch-free (clamped rows, raw lse / D -- validity and the log2 e
+  // scaling applied at the LDS store, so no wait lands here)
   auto gload = [&](int qt) {
     const int r0 = qt * TILE;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int v = tid + 256 * i;
-      rq[i] = ld8(qbase, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
-      rg[i] = ld8(gbase, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+      if constexpr (VEC) {
+        rq[i] = ld8c(qbase, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8);
+        rg[i] = ld8c(gbase, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8);
+      } else {
+        rq[i] = ld8(qbase, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+        rg[i] = ld8(gbase, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+      }
     }
     if (tid < TILE) {
       const int qi = r0 + tid;
-      rl = qi < p.T ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : INFINITY;
-      rd = qi < p.T ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
+      rlv = qi < p.T;
+      const long li = ((long)b * p.H + h) * p.T + min(qi, p.T - 1);
+      rl = lse[li];
+      rd = Dg[li];
     }
   };
+  // pos_bias_u / pos_bias_v of this thread's 8 staging columns ((tid + 256 i) & 7 == tid & 7 for both
+  // chunks), loaded once instead of per query tile
+  float pu8[8], pv8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int d = (tid & 7) * 8 + e;
+    pu8[e] = d < p.dk ? rp.pu[h * p.dk + d] : 0.f;
+    pv8[e] = d < p.dk ? rp.pv[h * p.dk + d] : 0.f;
+  }
   auto sstore = [&](int buf) {
     bf16* t = sq + buf * 3 * TILE * KS;
 #pragma unroll
@@ -484,19 +518,16 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
       bf16x8 qu, qv;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int d = c8 + e;
-        const float u = d < p.dk ? rp.pu[h * p.dk + d] : 0.f;
-        const float w = d < p.dk ? rp.pv[h * p.dk + d] : 0.f;
-        qu[e] = (bf16)((float)q[e] + u);
-        qv[e] = (bf16)((float)q[e] + w);
+        qu[e] = (bf16)((float)q[e] + pu8[e]);
+        qv[e] = (bf16)((float)q[e] + pv8[e]);
       }
       *reinterpret_cast<bf16x8*>(t + row * KS + c8) = qu;
       *reinterpret_cast<bf16x8*>(t + TILE * KS + row * KS + c8) = qv;
       *reinterpret_cast<uint4*>(t + 2 * TILE * KS + row * KS + c8) = rg[i];
     }
     if (tid < TILE) {
-      sLD[buf][0][tid] = rl;
-      sLD[buf][1][tid] = rd;
+      sLD[buf][0][tid] = rlv ? rl * LOG2E : INFINITY;   // lse = +inf for q >= T: P = 0
+      sLD[buf][1][tid] = rlv ? rd : 0.f;
     }
   };
   if (nqt > 0) {
@@ -505,11 +536,12 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load(p, rp, h, cb - 64 * (ch - 2), tid + 256 * i);
+      for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load<VEC>(p, rp, h, cb - 64 * (ch - 2), tid + 256 * i);
       ring_chunk_store(sring + ch * TILE * KS, rr, tid);
     }
     __syncthreads();
   }
+  wait_prologue_loads();
   bf16* dsb = dsbuf + ((long)b * p.H + h) * p.T * (long)ldS;
   for (int qt = 0; qt < nqt; ++qt) {
     const int cur = qt & 1;
@@ -519,7 +551,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
     if (qt + 1 < nqt) {
       gload(qt + 1);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load(p, rp, h, cb - 64 * (qt + 1), tid + 256 * i);
+      for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load<VEC>(p, rp, h, cb - 64 * (qt + 1), tid + 256 * i);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -584,13 +616,22 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
           sa[r + e] = pa * (ga[r + e] * ma - tD[qa]);
         }
       }
-      // scale * dS -> dsbuf[i][j] (query-major: lanes = consecutive keys)
-      if (kj < p.T) {
+      // scale * dS -> dsbuf[i][j] (query-major): the 32 x 32 block goes through the wave's stage (free after
+      // the skew reads) as bf16 [query][40] and out as 16-B row chunks, 2 stores per lane instead of 16
+      // 2-byte ones.  Keys >= T (zero dS) land in the row's padding [T, ldS); chunks past ldS are skipped.
+      {
+        bf16* sd = reinterpret_cast<bf16*>(st);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qia = qt * TILE + 32 * t + acc_row(r, hh);
-          if (qia < p.T) dsb[(long)qia * ldS + kj] = (bf16)(sa[r] * p.scale);
+        for (int r = 0; r < 16; ++r) sd[acc_row(r, hh) * 40 + jj] = (bf16)(sa[r] * p.scale);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int idx = 64 * it + lane, qr = idx >> 2, kc = k0w + 8 * (idx & 3);
+          const int qia = qt * TILE + 32 * t + qr;
+          const uint4 v = *reinterpret_cast<const uint4*>(sd + qr * 40 + 8 * (idx & 3));
+          if (qia < p.T && kc < ldS) *reinterpret_cast<uint4*>(dsb + (long)qia * ldS + kc) = v;
         }
+        __builtin_amdgcn_wave_barrier();
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -722,6 +763,11 @@ static RelP make_relp(const void* pos, const float* pu, const float* pv, int dk)
   return RelP{(const bf16*)pos, pu, pv, ((uintptr_t)pos % 16 == 0) && (dk % 8 == 0)};
 }
 
+// branch-free prefetch kernels (ld8c): dk = 64 with 16-B aligned rows of qkv / dout / pos.  cfm_attn_set_mode
+// bit 6 keeps the zero-filling loads (A/B)
+int g_rel_mode = 0;
+static bool rel_vec(const AttnM& p, const RelP& rp) { return p.vec && rp.pvec && p.dk == 64 && !(g_rel_mode & 64); }
+
 static AttnM make_attnm(const void* qkv, const void* dout, const int32_t* len, int B, int T, int H, int dk,
                         float drop_p, uint64_t seed, const void* mask) {
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, len, 1.f / sqrtf((float)dk), drop_p, seed,
@@ -735,8 +781,11 @@ int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len
                         const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s,
                         const void* mask) {
   const AttnM p = make_attnm(qkv, qkv, len, B, T, H, dk, drop_p, seed, mask);
-  hipLaunchKernelGGL(attn_rel_fwd_kernel, dim3(cdiv(p.T, 128), p.H, p.B), dim3(256), 0, s, p,
-                     make_relp(pos, pu, pv, p.dk), (bf16*)o, lse);
+  const RelP rp = make_relp(pos, pu, pv, p.dk);
+  if (rel_vec(p, rp))
+    hipLaunchKernelGGL(attn_rel_fwd_kernel<true>, dim3(cdiv(p.T, 128), p.H, p.B), dim3(256), 0, s, p, rp, (bf16*)o, lse);
+  else
+    hipLaunchKernelGGL(attn_rel_fwd_kernel<false>, dim3(cdiv(p.T, 128), p.H, p.B), dim3(256), 0, s, p, rp, (bf16*)o, lse);
   return check_launch("cfm_attn_fwd(rel)");
 }
 
@@ -753,10 +802,17 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
   bf16* dsbuf = reinterpret_cast<bf16*>(reinterpret_cast<char*>(part) + part_bytes);
   const int ldS = rel_ldS(p.T);
   const dim3 grid(cdiv(p.T, 128), p.H, p.B);
-  hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws, (bf16*)dqkv,
-                     dsbuf, ldS);
-  hipLaunchKernelGGL(attn_rel_bwd_dq_kernel, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws, (bf16*)dqkv,
-                     part);
+  if (rel_vec(p, rp)) {
+    hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                       (bf16*)dqkv, dsbuf, ldS);
+    hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                       (bf16*)dqkv, part);
+  } else {
+    hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                       (bf16*)dqkv, dsbuf, ldS);
+    hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                       (bf16*)dqkv, part);
+  }
   const size_t ds_bytes = ((size_t)p.B * p.H * p.T * ldS * sizeof(bf16) + 255) & ~(size_t)255;
   float* dpos_part = reinterpret_cast<float*>(reinterpret_cast<char*>(dsbuf) + ds_bytes);
   hipLaunchKernelGGL(attn_rel_bwd_dpos_kernel, dim3(cdiv(2 * p.T - 1, TILE), p.H, p.B), dim3(256), 0, s, p, rp,

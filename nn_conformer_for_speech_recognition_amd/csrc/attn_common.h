@@ -125,12 +125,25 @@ __device__ __forceinline__ bf16x8 acc2frag(const f32x16& a, int s) {
 // accumulator row of register r for lane half hh
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
 
+// 16 B at row clamp(row, 0, nrows - 1), column c: branch-free, for dk = 64 operands with 16-B aligned rows.
+// A prefetch through ld8's zero-fill branches makes the compiler wait for the load at the branch join (an
+// s_waitcnt vmcnt(0) right behind the prefetch, which also waits for every older store): with one wave per
+// SIMD that exposed a full memory round trip per tile.  Clamped rows hold finite data of the same operand,
+// and every consumer masks them (keys >= len, queries >= T, relative rows no valid (i, j) pair reaches).
+__device__ __forceinline__ uint4 ld8c(const bf16* base, long ld, int row, int nrows, int c) {
+  row = min(max(row, 0), nrows - 1);
+  return *reinterpret_cast<const uint4*>(base + (long)row * ld + c);
+}
+
 // stage a [64 rows][64 cols] bf16 tile (row r0.., column offset col of qkv) into LDS; 2 x 16 B per thread
+// (VEC: ld8c, rows past T clamped)
+template <bool VEC = false>
 __device__ __forceinline__ void tile_load(const AttnM& p, int b, int r0, int col, uint4 (&reg)[2], int tid) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int v = tid + 256 * i;
-    reg[i] = ld8(p.qkv + (long)b * p.T * p.D3 + col, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+    if constexpr (VEC) reg[i] = ld8c(p.qkv + (long)b * p.T * p.D3 + col, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8);
+    else reg[i] = ld8(p.qkv + (long)b * p.T * p.D3 + col, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
   }
 }
 __device__ __forceinline__ void tile_store(bf16* t, const uint4 (&reg)[2], int tid) {
