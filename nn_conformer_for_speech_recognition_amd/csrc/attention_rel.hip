@@ -588,33 +588,43 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
       }
       const float* tL = sLD[cur][0] + 32 * t;
       const float* tD = sLD[cur][1] + 32 * t;
-      f32x16 pd;
-      const uint32_t wkm = (drop && p.km) ? km_word(p, b, h, 2 * qt + t, kj) >> (16 * hh) : 0u;
+      // the block's lse / D values up front (broadcast LDS reads, one wait), dropout keep-scales per register in
+      // one uniform branch, then a branch-free softmax: (written per register with `kvalid ? ... : -inf` inside
+      // the mode branches, the compiler emitted an exec-masked branch + LDS read + wait per register)
+      float tl[16], td[16], mk[16];
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        // dropout of (query of register r / r+1, key kj): lanes kj, kj^1 share one 32-bit hash per query
-        // (index (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2); the even lane hashes register r's query,
-        // the odd lane register r+1's, and a DPP swap hands each lane its partner's
-        float m0 = 1.f, m1 = 1.f;
-        if (drop && p.km) {
-          m0 = mbit(wkm, r, dkeep);
-          m1 = mbit(wkm, r + 1, dkeep);
-        } else if (drop) {
+      for (int r = 0; r < 16; ++r) {
+        tl[r] = tL[acc_row(r, hh)];
+        td[r] = tD[acc_row(r, hh)];
+      }
+      if (drop && p.km) {
+        const uint32_t wkm = km_word(p, b, h, 2 * qt + t, kj) >> (16 * hh);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mk[r] = mbit(wkm, r, dkeep);
+      } else if (drop) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          // dropout of (query of register r / r+1, key kj): lanes kj, kj^1 share one 32-bit hash per query
+          // (index (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2); the even lane hashes register r's query,
+          // the odd lane register r+1's, and a DPP swap hands each lane its partner's
           const uint32_t hm = cfm_mix32(
               (hbase + __builtin_amdgcn_readfirstlane((qt * TILE + 32 * t + (r & 3) + 8 * (r >> 2)) * (int)T2)) ^ dkey);
           const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
           const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
-          m0 = ((h0 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
-          m1 = ((h1 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
+          mk[r] = ((h0 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
+          mk[r + 1] = ((h1 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
         }
+      } else {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int qa = acc_row(r + e, hh);
-          const float ma = e ? m1 : m0;
-          const float pa = fast_exp2(kvalid ? sa[r + e] * c - tL[qa] : -INFINITY);   // lse = +inf for q >= T
-          pd[r + e] = pa * ma;
-          sa[r + e] = pa * (ga[r + e] * ma - tD[qa]);
-        }
+        for (int r = 0; r < 16; ++r) mk[r] = 1.f;
+      }
+      f32x16 pd;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e2 = fast_exp2(__builtin_fmaf(sa[r], c, -tl[r]));   // lse = +inf for q >= T: 0
+        const float pa = kvalid ? e2 : 0.f;
+        pd[r] = pa * mk[r];
+        sa[r] = pa * (ga[r] * mk[r] - td[r]);
       }
       // scale * dS -> dsbuf[i][j] (query-major): the 32 x 32 block goes through the wave's stage (free after
       // the skew reads) as bf16 [query][40] and out as 16-B row chunks, 2 stores per lane instead of 16
