@@ -194,64 +194,6 @@ __device__ __forceinline__ void head_stage(const AttnM& p, const bf16* base0, co
   }
 }
 
-// One key tile of the forward's online softmax for a wave (queries on the lanes, keys k0 + acc_row(r, hh)
-// [+ 32] in s0 / s1, raw unscaled scores): masking only on the utterance's last tile (`tail`, uniform), the
-// running max kept in scaled log2 units (c = scale * log2 e > 0, so max(c s) = c max(s)), p = 2^(c s - m) as
-// one FMA + v_exp; rescales o0/o1 and l; attention dropout applied to p (the returned P is dropped/scaled,
-// l stays the undropped sum, as nn.MultiheadAttention: dropout after the softmax).
-__device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16& s1, f32x16& o0, f32x16& o1,
-                                             float& m, float& l, float c, int kbase, int len, bool tail, int b,
-                                             int h, int qi, int hh, uint32_t dthr, float dkeep, uint32_t dkey,
-                                             uint32_t w) {
-  if (tail && kbase + TILE > len) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int k0 = kbase + acc_row(r, hh);
-      s0[r] = (k0 < len) ? s0[r] : -INFINITY;
-      s1[r] = (k0 + 32 < len) ? s1[r] : -INFINITY;
-    }
-  }
-  float mloc = fmaxf(s0[0], s1[0]);
-#pragma unroll
-  for (int r = 1; r < 16; ++r) mloc = fmaxf(mloc, fmaxf(s0[r], s1[r]));
-  mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-  const float mn = fmaxf(m, mloc * c);
-  const float alpha = fast_exp2(m - mn);
-  float ls = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    s0[r] = fast_exp2(__builtin_fmaf(s0[r], c, -mn));
-    s1[r] = fast_exp2(__builtin_fmaf(s1[r], c, -mn));
-    ls += s0[r] + s1[r];
-  }
-  ls += __shfl_xor(ls, 32, 64);
-  l = l * alpha + ls;
-  m = mn;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    o0[r] *= alpha;
-    o1[r] *= alpha;
-  }
-  if (p.drop_p > 0.f && p.qm) {     // precomputed keep bits (cfm_attn_dropmask), w loaded a tile ahead
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] *= mbit(w, r, dkeep);
-      s1[r] *= mbit(w, 16 + r, dkeep);
-    }
-  } else if (p.drop_p > 0.f) {
-    const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kbase) >> 1);   // even: 32-bit pair indices
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
-      const int k0 = acc_row(r, hh);
-      float m0, m1, m2, m3;
-      dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
-      dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
-      s0[r] *= m0; s0[r + 1] *= m1;
-      s1[r] *= m2; s1[r + 1] *= m3;
-    }
-  }
-}
-
 // forward: grid (B*H), block 64 * ceil(T/32); dynamic LDS head_lds_bytes(T)
 __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(AttnM p, bf16* __restrict__ o,
                                                                             float* __restrict__ lse) {

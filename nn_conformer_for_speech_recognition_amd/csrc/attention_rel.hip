@@ -209,51 +209,9 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
     }
     f32x16 s0, s1;
     scores_qlanes(sK, band_rows_q(sring, kt, wv), qu, qv, st, s0, s1, lane);
-    float mloc = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int k0 = kt * TILE + acc_row(r, hh);
-      s0[r] = (k0 < len) ? s0[r] * c : -INFINITY;
-      s1[r] = (k0 + 32 < len) ? s1[r] * c : -INFINITY;
-      mloc = fmaxf(mloc, fmaxf(s0[r], s1[r]));
-    }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float mn = fmaxf(m, mloc);
-    const float alpha = fast_exp2(m - mn);
-    float ls = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = fast_exp2(s0[r] - mn);
-      s1[r] = fast_exp2(s1[r] - mn);
-      ls += s0[r] + s1[r];
-    }
-    ls += __shfl_xor(ls, 32, 64);
-    l = l * alpha + ls;
-    m = mn;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      o0[r] *= alpha;
-      o1[r] *= alpha;
-    }
-    if (p.drop_p > 0.f && p.qm) {      // precomputed keep bits (cfm_attn_dropmask)
-      const uint32_t w = wcur;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s0[r] *= mbit(w, r, dkeep);
-        s1[r] *= mbit(w, 16 + r, dkeep);
-      }
-    } else if (p.drop_p > 0.f) {
-      const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int k0 = acc_row(r, hh);
-        float m0, m1, m2, m3;
-        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
-        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
-        s0[r] *= m0; s0[r + 1] *= m1;
-        s1[r] *= m2; s1[r + 1] *= m3;
-      }
-    }
+    // the non-rel kernels' online-softmax step (attn_common.h): masking only on the last key tile, the running max
+    // over raw scores (c > 0), exp2 as one FMA + v_exp, then the same dropout hash / keep bits as before
+    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey, wcur);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -301,7 +259,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
   load_q_uv(p, rp, b, h, qi, qu, qv, lane);
   load_bfrags(p, dout + (long)b * p.T * p.HD + h * p.dk, p.HD, qi, p.T, gf, lane);
   const bool qvalid = qi < p.T;
-  const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : 0.f;
+  const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : INFINITY;   // +inf: P = 0 past T
   const float Dq = qvalid ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
   const float c = p.scale * LOG2E;
   float* st = sst + wv * 32 * SS;
@@ -365,13 +323,18 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
         d1[r] *= m2; d1[r + 1] *= m3;
       }
     }
+    // P = 2^(c s - lse log2 e) as one FMA + v_exp; key masking only on the utterance's last tile (uniform)
+    const bool tail = kt == nkt - 1 && kt * TILE + TILE > len;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int k0 = kt * TILE + acc_row(r, hh);
-      const float p0 = fast_exp2(k0 < len && qvalid ? s0[r] * c - L2 : -INFINITY);
-      const float p1 = fast_exp2(k0 + 32 < len && qvalid ? s1[r] * c - L2 : -INFINITY);
-      s0[r] = p0 * (d0[r] - Dq);
-      s1[r] = p1 * (d1[r] - Dq);
+      float a0 = __builtin_fmaf(s0[r], c, -L2), a1 = __builtin_fmaf(s1[r], c, -L2);
+      if (tail) {
+        const int k0 = kt * TILE + acc_row(r, hh);
+        a0 = k0 < len ? a0 : -INFINITY;
+        a1 = k0 + 32 < len ? a1 : -INFINITY;
+      }
+      s0[r] = fast_exp2(a0) * (d0[r] - Dq);
+      s1[r] = fast_exp2(a1) * (d1[r] - Dq);
     }
     // K-term: dQ^T[d][q] += sum_key K[key][d] dS^T[key][q]
 #pragma unroll
