@@ -636,11 +636,12 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
 // partials are summed by one deterministic column reduction); 4 waves = (d half, r half).
 // part[b][r][h*dk+d] = sum_i dsbuf[b,h,i, i+r-(T-1)] * (q_i + v)[d]   (keys j < len[b] only)
 // The next 64-query tile is loaded into registers while the current one runs through the MFMAs.
+template <bool VEC>
 __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp, const bf16* __restrict__ dsbuf,
                                                                 int ldS, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) bf16 sA[2][TILE * KS];    // (q+v)[ii][d]
   __shared__ __attribute__((aligned(16))) bf16 sB[2][TILE * KS];    // dS_diag[ii][rr]
-  __shared__ float sO[TILE * 65];
+  float* const sO = reinterpret_cast<float*>(&sA[0][0]);   // [TILE][65] after the loop (fits sA: 18 KiB)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int R0 = blockIdx.x * TILE, h = blockIdx.y, b = blockIdx.z;
   const int dh = wv & 1, rh = wv >> 1;
@@ -656,28 +657,60 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp
   float pv8[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) pv8[e] = c8 + e < p.dk ? rp.pv[h * p.dk + c8 + e] : 0.f;
-  uint4 ra[2], rb[2];
-  auto load = [&](int I0) {
+  const int nch = ldS >> 3;        // 16-B chunks per dS row
+  auto load = [&](int I0, uint4 (&ra)[2], uint4 (&rb)[2]) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int row = (tid + 256 * k) >> 3, i = I0 + row;
-      const bf16x8 q = __builtin_bit_cast(bf16x8, ld8(qbase, p.D3, i, T, c8, p.dk, p.vec));
-      bf16x8 qv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) qv[e] = (bf16)(i < T && c8 + e < p.dk ? (float)q[e] + pv8[e] : 0.f);
-      ra[k] = __builtin_bit_cast(uint4, qv);
       const int j0 = i + R0 + c8 - (T - 1);
-      const unsigned short* srow = reinterpret_cast<const unsigned short*>(dsb + (long)min(i, T - 1) * ldS);
-      unsigned short t8[8];
+      if constexpr (VEC) {
+        // q + v: one clamped 16-B load (rows >= T zeroed below)
+        const bf16x8 q = __builtin_bit_cast(bf16x8, ld8c(qbase, p.D3, i, T, c8));
+        bf16x8 qv;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int j = j0 + e;
-        t8[e] = (i < T && j >= 0 && j < len && R0 + c8 + e < nrel) ? srow[j] : (unsigned short)0;
+        for (int e = 0; e < 8; ++e) qv[e] = (bf16)(i < T ? (float)q[e] + pv8[e] : 0.f);
+        ra[k] = __builtin_bit_cast(uint4, qv);
+        // dS[i][j0 .. j0+7] (j0 unaligned): the two aligned 16-B chunks around it (chunk indices clamped to the
+        // row: a clamped chunk only ever supplies columns outside [0, len), which are zeroed), then a per-lane
+        // funnel shift by j0 & 7 elements and the validity mask -- branch-free, no per-element 2-B loads
+        const bf16* srow = dsb + (long)min(i, T - 1) * ldS;
+        const int cA = j0 >> 3;      // floor (j0 may be negative)
+        const uint4 A = *reinterpret_cast<const uint4*>(srow + 8 * min(max(cA, 0), nch - 1));
+        const uint4 Bc = *reinterpret_cast<const uint4*>(srow + 8 * min(max(cA + 1, 0), nch - 1));
+        const uint32_t w[8] = {A.x, A.y, A.z, A.w, Bc.x, Bc.y, Bc.z, Bc.w};
+        const int o = j0 & 7, oh = o >> 1;
+        uint32_t out[4];
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          // words oh + q4 and oh + q4 + 1 (oh in 0..3): select by the bits of oh
+          const uint32_t a01 = (oh & 1) ? w[q4 + 1] : w[q4], a23 = (oh & 1) ? w[q4 + 3] : w[q4 + 2];
+          const uint32_t b01 = (oh & 1) ? w[q4 + 2] : w[q4 + 1], b23 = (oh & 1) ? w[q4 + 4] : w[q4 + 3];
+          const uint32_t lo = (oh & 2) ? a23 : a01, hi = (oh & 2) ? b23 : b01;
+          const uint32_t v = (o & 1) ? __builtin_amdgcn_alignbit(hi, lo, 16) : lo;
+          const int ja = j0 + 2 * q4;
+          const bool va = i < T && ja >= 0 && ja < len && R0 + c8 + 2 * q4 < nrel;
+          const bool vb = i < T && ja + 1 >= 0 && ja + 1 < len && R0 + c8 + 2 * q4 + 1 < nrel;
+          out[q4] = v & ((va ? 0xFFFFu : 0u) | (vb ? 0xFFFF0000u : 0u));
+        }
+        rb[k] = make_uint4(out[0], out[1], out[2], out[3]);
+      } else {
+        const bf16x8 q = __builtin_bit_cast(bf16x8, ld8(qbase, p.D3, i, T, c8, p.dk, p.vec));
+        bf16x8 qv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qv[e] = (bf16)(i < T && c8 + e < p.dk ? (float)q[e] + pv8[e] : 0.f);
+        ra[k] = __builtin_bit_cast(uint4, qv);
+        const unsigned short* srow = reinterpret_cast<const unsigned short*>(dsb + (long)min(i, T - 1) * ldS);
+        unsigned short t8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int j = j0 + e;
+          t8[e] = (i < T && j >= 0 && j < len && R0 + c8 + e < nrel) ? srow[j] : (unsigned short)0;
+        }
+        rb[k] = make_uint4(t8[0] | (t8[1] << 16), t8[2] | (t8[3] << 16), t8[4] | (t8[5] << 16), t8[6] | (t8[7] << 16));
       }
-      rb[k] = make_uint4(t8[0] | (t8[1] << 16), t8[2] | (t8[3] << 16), t8[4] | (t8[5] << 16), t8[6] | (t8[7] << 16));
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const uint4 (&ra)[2], const uint4 (&rb)[2]) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int row = (tid + 256 * k) >> 3;
@@ -688,20 +721,28 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp
   f32x16 acc = (f32x16){0};
   const int it0 = ilo & ~(TILE - 1);
   const int nit = (len > 0 && ihi >= ilo) ? (ihi - it0) / TILE + 1 : 0;
+  // two register stages ahead of the LDS double buffer: tile it+2 is loaded while tile it runs through the MFMAs
+  // and tile it+1 goes to LDS (four MFMAs per wave per tile cannot cover a load issued one tile ahead)
+  uint4 ra0[2], rb0[2], ra1[2], rb1[2];
   if (nit > 0) {
-    load(it0);
-    store(0);
+    load(it0, ra0, rb0);
+    if (nit > 1) load(it0 + TILE, ra1, rb1);
+    store(0, ra0, rb0);
     __syncthreads();
   }
-  for (int it = 0; it < nit; ++it) {
+  auto step = [&](int it, uint4 (&af)[2], uint4 (&bfree)[2], const uint4 (&an)[2], const uint4 (&bn)[2]) {
     const int cur = it & 1;
-    if (it + 1 < nit) load(it0 + (it + 1) * TILE);
+    if (it + 2 < nit) load(it0 + (it + 2) * TILE, af, bfree);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sA[cur], 16 * s, 32 * dh, lane),
                                                     trfrag_perm(sB[cur], 16 * s, 32 * rh, lane), acc, 0, 0, 0);
-    if (it + 1 < nit) store(cur ^ 1);
+    if (it + 1 < nit) store(cur ^ 1, an, bn);
     __syncthreads();
+  };
+  for (int it = 0; it < nit; it += 2) {
+    step(it, ra0, rb0, ra1, rb1);                          // ra0 (tile it, stored) refills with tile it+2
+    if (it + 1 < nit) step(it + 1, ra1, rb1, ra0, rb0);    // ra1 (tile it+1, stored) refills with tile it+3
   }
   // acc: rows d (32 dh + acc_row), lanes rr (32 rh + lane&31) -> sO[rr][d] -> this utterance's partial rows
   const int hh = lane >> 5;
@@ -788,8 +829,12 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
   }
   const size_t ds_bytes = ((size_t)p.B * p.H * p.T * ldS * sizeof(bf16) + 255) & ~(size_t)255;
   float* dpos_part = reinterpret_cast<float*>(reinterpret_cast<char*>(dsbuf) + ds_bytes);
-  hipLaunchKernelGGL(attn_rel_bwd_dpos_kernel, dim3(cdiv(2 * p.T - 1, TILE), p.H, p.B), dim3(256), 0, s, p, rp,
-                     (const bf16*)dsbuf, ldS, dpos_part);
+  if (rel_vec(p, rp))
+    hipLaunchKernelGGL(attn_rel_bwd_dpos_kernel<true>, dim3(cdiv(2 * p.T - 1, TILE), p.H, p.B), dim3(256), 0, s, p, rp,
+                       (const bf16*)dsbuf, ldS, dpos_part);
+  else
+    hipLaunchKernelGGL(attn_rel_bwd_dpos_kernel<false>, dim3(cdiv(2 * p.T - 1, TILE), p.H, p.B), dim3(256), 0, s, p,
+                       rp, (const bf16*)dsbuf, ldS, dpos_part);
   colreduce(dpos_part, p.B, (long)(2 * p.T - 1) * p.HD, dpos, 0, s);
   const int nrows = p.B * 4 * cdiv(p.T, 128);
   colreduce(part, nrows, (long)p.HD, dpu, 0, s, 2L * p.HD);
