@@ -111,25 +111,42 @@ struct BandRows {
 __device__ __forceinline__ void scores_qlanes(const bf16* sK, const BandRows& br, const bf16x8 (&qu)[4],
                                               const bf16x8 (&qv)[4], float* st, f32x16& s0, f32x16& s1, int lane) {
   const int hh = lane >> 5, ii = lane & 31;
+  float* col = st + ii * SS;
+  // X[r'][i] -> stage[i][r'] (16-B stores of 4 consecutive accumulator rows), one 32-row band block at a time:
+  // only one X accumulator is live (the three at once pushed the dQ kernel past 256 VGPRs into AGPR copies)
+  auto put = [&](const f32x16& x, int base) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int r0 = 8 * g + 4 * hh;
+      *reinterpret_cast<float4*>(col + base + r0) = make_float4(x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]);
+    }
+  };
   s0 = (f32x16){0};
   s1 = (f32x16){0};
-  f32x16 x0 = (f32x16){0}, x1 = (f32x16){0}, x2 = (f32x16){0};
+  {
+    f32x16 x0 = (f32x16){0};
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qu[s], s0, 0, 0, 0);
-    s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
-    x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(br.blk[0], 0, 16 * s, lane), qv[s], x0, 0, 0, 0);
-    x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(br.blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
-    x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(br.blk[2], 0, 16 * s, lane), qv[s], x2, 0, 0, 0);
+    for (int s = 0; s < 4; ++s) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qu[s], s0, 0, 0, 0);
+      x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(br.blk[0], 0, 16 * s, lane), qv[s], x0, 0, 0, 0);
+    }
+    put(x0, 0);
   }
-  // X[r'][i] -> stage[i][r'] (16-B stores of 4 consecutive accumulator rows)
-  float* col = st + ii * SS;
+  {
+    f32x16 x1 = (f32x16){0};
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int r0 = 8 * g + 4 * hh;
-    *reinterpret_cast<float4*>(col + r0) = make_float4(x0[4 * g], x0[4 * g + 1], x0[4 * g + 2], x0[4 * g + 3]);
-    *reinterpret_cast<float4*>(col + 32 + r0) = make_float4(x1[4 * g], x1[4 * g + 1], x1[4 * g + 2], x1[4 * g + 3]);
-    *reinterpret_cast<float4*>(col + 64 + r0) = make_float4(x2[4 * g], x2[4 * g + 1], x2[4 * g + 2], x2[4 * g + 3]);
+    for (int s = 0; s < 4; ++s) {
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
+      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(br.blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
+    }
+    put(x1, 32);
+  }
+  {
+    f32x16 x2 = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(br.blk[2], 0, 16 * s, lane), qv[s], x2, 0, 0, 0);
+    put(x2, 64);
   }
   __builtin_amdgcn_wave_barrier();
   // bd[j][i] = X[j - i + 31][i]

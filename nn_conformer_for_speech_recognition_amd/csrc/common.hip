@@ -319,6 +319,27 @@ __global__ __launch_bounds__(1024) void colreduce2_kernel(const float* __restric
     out[n] = t;
   }
 }
+// few partial rows over many columns (the rel-pos dpos per-utterance partials: 8 rows x 1.5 M columns): the
+// 16-wave-per-64-columns kernel above left half its waves idle and launched 24 K blocks; here each thread sums
+// float4 columns over the parts in the same order (0 + p0 + p1 + ...: bit-identical to colreduce_kernel for
+// nparts <= 16, whose waves hold at most one part each)
+__global__ __launch_bounds__(256) void colreduce_few_kernel(const float* __restrict__ part, int nparts, long N,
+                                                            long ldp, float* __restrict__ out, int acc) {
+  const long n4 = N / 4;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = 0; p < nparts; ++p) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (long)p * ldp + 4 * i);
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    float4* o = reinterpret_cast<float4*>(out + 4 * i);
+    if (acc) {
+      const float4 u = *o;
+      t = make_float4(u.x + t.x, u.y + t.y, u.z + t.z, u.w + t.w);
+    }
+    *o = t;
+  }
+}
 }  // namespace
 
 namespace cfm {
@@ -328,6 +349,14 @@ void colreduce_pair(const float* partA, const float* partB, int nparts, long N, 
                      outA, outB);
 }
 void colreduce(const float* part, int nparts, long N, float* out, int accumulate, hipStream_t s, long ldp) {
+  const long lp = ldp > 0 ? ldp : N;
+  if (nparts <= 16 && N % 4 == 0 && lp % 4 == 0 && (uintptr_t)part % 16 == 0 && (uintptr_t)out % 16 == 0 &&
+      N >= 65536) {
+    const long blocks = (N / 4 + 255) / 256;
+    hipLaunchKernelGGL(colreduce_few_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, s, part,
+                       nparts, N, lp, out, accumulate);
+    return;
+  }
   hipLaunchKernelGGL(colreduce_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, part, nparts, N,
                      ldp > 0 ? ldp : N, out, accumulate);
 }
