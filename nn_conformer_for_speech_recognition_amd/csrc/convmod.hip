@@ -127,6 +127,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_fwd_kernel(const void* __restr
 
 // Vectorised forward (bf16 a, C % 4 == 0, compiled K): staging loads and the y stores move 4 channels per lane
 // (8- / 16-byte accesses) through LDS; the taps run lane = channel as above.  Same partial-sum layout.
+// (Packed-fp32 taps as in the backward measured slower here: 17.2 -> 20.0 us, 94 -> 195 VGPRs, occupancy 5 -> 2.)
 template <int KT>
 __global__ __launch_bounds__(256) void glu_dwconv_fwd_vec_kernel(const bf16* __restrict__ a,
                                                                  const float* __restrict__ w,
@@ -610,18 +611,38 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_vec_kernel(const float* __
     wd[j] = sdy[(tb + j) * CT + lane];
     wg[j] = sg[(tb + j) * CT + lane];
   }
+  // packed fp32 FMAs (v_pk_fma_f32, two per lane per instruction): dg over frame pairs (f, f+1), dw over tap
+  // pairs (k, k+1) -- every output keeps the scalar loop's accumulation order (dg[f] over k, dw[k] over f),
+  // so the results are bit-identical
+  typedef float f2 __attribute__((ext_vector_type(2)));
   float dw[KT + 1], dg[FB];
 #pragma unroll
   for (int k = 0; k <= KT; ++k) dw[k] = 0.f;
 #pragma unroll
+  for (int f = 0; f < FB; f += 2) {
+    f2 s = {0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const f2 x = {wd[f - k + 2 * PAD], wd[f + 1 - k + 2 * PAD]};
+      const f2 w = {wr[k], wr[k]};
+      s = __builtin_elementwise_fma(w, x, s);
+    }
+    dg[f] = s.x;
+    dg[f + 1] = s.y;
+  }
+#pragma unroll
   for (int f = 0; f < FB; ++f) {
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < KT; ++k) s += wr[k] * wd[f - k + 2 * PAD];
-    dg[f] = s;
     const float dyt = wd[f + PAD];
+    const f2 d2 = {dyt, dyt};
 #pragma unroll
-    for (int k = 0; k < KT; ++k) dw[k] += dyt * wg[f + k];
+    for (int k = 0; k + 1 < KT; k += 2) {
+      f2 a = {dw[k], dw[k + 1]};
+      const f2 x = {wg[f + k], wg[f + k + 1]};
+      a = __builtin_elementwise_fma(d2, x, a);
+      dw[k] = a.x;
+      dw[k + 1] = a.y;
+    }
+    if constexpr (KT & 1) dw[KT - 1] += dyt * wg[f + KT - 1];
     dw[KT] += dyt;
   }
   __syncthreads();
