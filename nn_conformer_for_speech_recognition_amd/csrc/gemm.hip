@@ -173,7 +173,6 @@ constexpr int BK16 = 64;
 constexpr int KM_STRIDE = BK16 + 8;        // K-major tile [128][72]: 144-B rows, conflict-free b128
 constexpr int MN_STRIDE = 128 + 32;        // MN-major tile [64][160]: 320-B rows, conflict-free tr16
 constexpr int TILE16 = (128 * KM_STRIDE > BK16 * MN_STRIDE) ? 128 * KM_STRIDE : BK16 * MN_STRIDE;  // 20 KiB
-constexpr int NV16 = 128 * BK16 / 8 / NT;  // 16-B vectors per thread per operand tile (4)
 constexpr int KV16 = BK16 / 8;             // vectors per K-major row (8)
 
 // XCD-aware tile order: blocks b and b+8 share an XCD under round-robin dispatch, so hand each
@@ -210,8 +209,6 @@ __device__ __forceinline__ void xcd_tile3(int& tm, int& tn, int& zz) {
 
 // fp32 LDS geometry: both operands stored [BK][128+4] (k-rows)
 constexpr int BK32 = 16;
-constexpr int F_STRIDE = 128 + 4;
-constexpr int TILE32 = BK32 * F_STRIDE;
 
 // Read one 32x32x16 operand fragment (8 bf16, natural k order) from a staged tile.
 // MNS: row stride of the MN-major image (rows + 32 elements: 64 mod 256 bytes -> conflict-free tr16)
@@ -255,6 +252,16 @@ __device__ __forceinline__ void epilogue_store(const GemmP& p, int z, int zs, in
   v *= p.out_scale;
   if (p.res) v += ld_dyn(p.res, p.dtr, (long)z * p.sc + (long)m * p.ldr + n);
   st_dyn(p.C, p.dtc, cidx, v);
+}
+
+// split-K partial of one element: the whole epilogue a split-K launch may carry (cfm_gemm requires a plain fp32
+// epilogue for split_k > 1): alpha, the bias on the first slice, atomic accumulation -- a small body, so the
+// 64-element loops over an accumulator tile unroll fully (epilogue_store's general body did not)
+__device__ __forceinline__ void splitk_atomic_store(const GemmP& p, int z, int zs, int m, int n, float acc) {
+  if (m >= p.M || n >= p.N) return;
+  float v = acc * p.alpha;
+  if (p.bias && zs % p.split_k == 0) v += p.bias[n];
+  atomicAdd(reinterpret_cast<float*>(p.C) + (long)z * p.sc + out_row(p, m) * p.ldc + n, v);
 }
 
 constexpr int EP_STRIDE = 128 + 4;   // f32 staging row stride: rows r and r+4 land 16 banks apart
@@ -456,7 +463,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmP& p, f32x16 (&acc)[2][2
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           const int n = n0 + wn * 64 + j * 32 + (lane & 31);
-          epilogue_store(p, z, zs, m, n, acc[i][j][r]);
+          splitk_atomic_store(p, z, zs, m, n, acc[i][j][r]);
         }
     return;
   }
@@ -519,7 +526,7 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * BAND + i * 32 + accr<M16>(r, lane);
           const int n = n0 + wn * FN * 32 + j * 32 + accc<M16>(r, lane);
-          epilogue_store(p, z, zs, m, n, acc[i][j][r]);
+          splitk_atomic_store(p, z, zs, m, n, acc[i][j][r]);
         }
     return;
   }
@@ -646,12 +653,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pipe_rsrc(const PipeOp& o, int
 // conservative `s_waitcnt vmcnt(0)` in front of the next LDS read it cannot prove disjoint (it did so in the
 // grouped weight-gradient loop, where every K step then waited for the DMA it had just issued).  Every
 // consumer waits with its own counted vmcnt + barrier, so no compiler-inserted wait is needed.
+// (m0 is declared clobbered -- the asm does overwrite it -- which clang reports as a reserved register once per
+// instantiation; the warning is silenced here only)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, unsigned voff) {
   const unsigned l = __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_base);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                :: "s"(l), "v"(voff), "s"(r) : "memory", "m0");
 }
+#pragma clang diagnostic pop
 
 // K-major [R][BKt] image: BKt*2-B rows, RPB rows per 256-B bank row, CPR 16-B chunks per row;
 // chunk c of row r sits in slot c ^ ((r / RPB) % CPR): 16 consecutive rows read at one k hit 16
