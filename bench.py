@@ -205,10 +205,22 @@ class KernelProbe:
         return (tot / self.khz / n) if n else float("nan"), n
 
 
-def cpu_baseline(cfg, threads, steps=2):
+def cpu_model():
+    """The host CPU's model name (reported next to the CPU baseline)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg, threads, steps=3):
     """The CPU oracle (torch fp32 restatement of the same composition) on a bounded sample:
     1 utterance of the config's length through front-end + encoder + CTC, fwd+bwd, 1 warm-up then
-    `steps` timed."""
+    the best of `steps` timed steps."""
     from oracle import conformer as oc
     from oracle import frontend as of
     name, L, d, H, ffn, K, _, secs, pos = cfg
@@ -236,16 +248,19 @@ def cpu_baseline(cfg, threads, steps=2):
         loss.backward()
 
     step()
-    t0 = time.perf_counter()
+    ts = []
     for _ in range(steps):
+        t0 = time.perf_counter()
         step()
-    dt = (time.perf_counter() - t0) / steps
+        ts.append(time.perf_counter() - t0)
+    dt = min(ts)
     return {"value": round(T_in / dt, 1), "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "cpu": cpu_model(),
             "sample": f"{name} fp32 oracle (torch CPU), 1 x {secs} s utterance ({T_in} frames), front-end + "
-                      f"{L} layers ({pos} pos) + CTC, fwd+bwd, mean of {steps} steps after 1 warm-up"}
+                      f"{L} layers ({pos} pos) + CTC, fwd+bwd, best of {steps} steps after 1 warm-up"}
 
 
-def cpu_baseline_s10(threads, steps=2):
+def cpu_baseline_s10(threads, steps=3):
     """BASELINE.json configs[0]: Conformer-S (16 L, d 144, 4 heads, ffn 576, K 31) forward on 4 x 10 s
     80-bin mel clips, the CPU plumbing path -- the fp32 oracle (front-end + frame projection + encoder),
     eval mode, no autograd."""
@@ -268,13 +283,16 @@ def cpu_baseline_s10(threads, steps=2):
         def fwd():
             return conf(of.frame_projection(of.convsub_forward(x, w1, b1, w2, b2), wf, bf), lens)
         fwd()
-        t0 = time.perf_counter()
+        ts = []
         for _ in range(steps):
+            t0 = time.perf_counter()
             fwd()
-        dt = (time.perf_counter() - t0) / steps
+            ts.append(time.perf_counter() - t0)
+        dt = min(ts)
     return {"value": round(B * T_in / dt, 1), "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "cpu": cpu_model(),
             "sample": f"configs[0]: Conformer-S fp32 oracle forward (eval), 4 x 10 s clips ({T_in} frames), "
-                      f"front-end + frame projection + 16 layers, mean of {steps} after 1 warm-up"}
+                      f"front-end + frame projection + 16 layers, best of {steps} after 1 warm-up"}
 
 
 class Harness:
