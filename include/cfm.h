@@ -171,6 +171,22 @@ int cfm_gemm(const cfm_gemm_desc* d, void* stream);
    cfm_gemm_desc.alpha_*_dev); amax_ws: cfm_quant_fp8_ws_bytes() of scratch.  x fp32 or bf16, 16-B aligned. */
 size_t cfm_quant_fp8_ws_bytes(void);
 int cfm_quant_fp8(const void* x, int dtype_x, long n, void* y, float* inv_scale, unsigned* amax_ws, void* stream);
+/* Batched cfm_quant_fp8 over a device table of tensors (the per-step fp8 copies of a model's forward GEMM
+   weights, configs[4]): TWO launches for the whole list instead of two per tensor; per tensor the same
+   current scaling, scale and e4m3 bytes as cfm_quant_fp8 (the max is order-independent: bit-identical).
+   Replaces the per-weight quantisation loop of the fp8 path (no reference counterpart: the reference has
+   no fp8).  tasks: device array; blk0 = prefix sum of cfm_quant_fp8_batch_blocks(n) over the tasks;
+   amax_ws: nblocks floats of scratch. */
+typedef struct {
+  const void* x;      /* fp32 or bf16 (dtype_x of the call), 16-B aligned */
+  void* y;            /* e4m3 bytes, 8-B aligned */
+  float* inv_scale;   /* dequantisation factor 2^-k (device scalar) */
+  long n;
+  long blk0;
+} cfm_q8_task;
+long cfm_quant_fp8_batch_blocks(long n);
+int cfm_quant_fp8_batch(const cfm_q8_task* tasks, int ntasks, long nblocks, int dtype_x, float* amax_ws,
+                        void* stream);
 /* y = float(x) * inv_scale (inv_scale NULL: 1) -- the dequantised view, for tests. */
 int cfm_dequant_fp8(const void* x, long n, const float* inv_scale, float* y, void* stream);
 /* Grouped weight gradients: every dW_i (N_i x K_i, fp32) = dY_i^T X_i over the same M tokens (dY_i (M x N_i),

@@ -71,6 +71,8 @@ _SIGS = {
     "cfm_gemm_set_mode": (c_int, [c_int]),
     "cfm_quant_fp8": (c_int, [c_void_p, c_int, c_long, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cfm_quant_fp8_ws_bytes": (c_size_t, []),
+    "cfm_quant_fp8_batch_blocks": (c_long, [c_long]),
+    "cfm_quant_fp8_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_void_p]),
     "cfm_dequant_fp8": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     "cfm_wgrad_group_task_bytes": (c_size_t, []),
     "cfm_wgrad_group_tiles": (c_long, [c_int, c_int]),

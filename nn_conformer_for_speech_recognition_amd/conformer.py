@@ -532,6 +532,7 @@ class Conformer(nn.Module):
         self._pe_cache = {}
         self._step = 0
         self._shadow = None
+        self._q8 = None         # (key, ops.Quant8Batch) of the fp8 forward weights
         # data-parallel hooks (dist.GradAllReducer.attach): per-layer {weight index: (dW, db) bucket views},
         # the layers whose backward flushes the grouped launch, and the callback run after each flush
         self.grad_dest = None
@@ -565,11 +566,17 @@ class Conformer(nn.Module):
         self._shadow[1].refresh()
         if not self.fp8:
             return self._shadow[2]
-        # per-step fp8 copies (+ dequantisation scalars) of the forward GEMM weights, from the fp32 masters
+        # per-step fp8 copies (+ dequantisation scalars) of the forward GEMM weights, from the fp32 masters: ONE
+        # batched quantisation (two launches for all layers; was two launches per weight)
+        if getattr(self, "_q8", None) is None or self._q8[0] != key:
+            srcs8 = [layer.params()[i].detach().view(layer.params()[i].shape[0], -1)
+                     for layer in self.conformer_layers for i in _FP8_W]
+            self._q8 = (key, ops.Quant8Batch(srcs8))
+        outs = self._q8[1].refresh()
+        nw = len(_FP8_W)
         out = []
-        for layer, (plain, trans) in zip(self.conformer_layers, self._shadow[2]):
-            ps = layer.params()
-            q8 = {i: ops.quant_fp8(ps[i].detach().view(ps[i].shape[0], -1)) for i in _FP8_W}
+        for j, (plain, trans) in enumerate(self._shadow[2]):
+            q8 = dict(zip(_FP8_W, outs[j * nw:(j + 1) * nw]))
             out.append((plain, trans, q8))
         return out
 

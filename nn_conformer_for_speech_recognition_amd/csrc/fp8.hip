@@ -81,6 +81,75 @@ __global__ __launch_bounds__(256) void dequant_fp8_kernel(const uint8_t* __restr
     y[i] = __builtin_amdgcn_cvt_f32_fp8((int)x[i], 0) * s;
 }
 
+// ---------------------------------------------------------------- batched (one table, two launches)
+// task of a block: the last task whose blk0 <= block (wave-uniform binary search over the small table)
+__device__ __forceinline__ int q8_task_of(const cfm_q8_task* t, int n, long blk) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t[mid].blk0 <= blk) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+__host__ __device__ inline long q8_blocks(long n) {
+  const long b = (n / 8 + 255) / 256;
+  return b > 64 ? 64 : (b < 1 ? 1 : b);
+}
+
+// pass 1: block j of task i writes the partial |x| max of its grid-stride share to part[blk0_i + j]
+__global__ __launch_bounds__(256) void amax_batch_kernel(const cfm_q8_task* __restrict__ t, int nt, int dt,
+                                                         float* __restrict__ part) {
+  __shared__ float red[4];
+  const long blk = blockIdx.x;
+  const cfm_q8_task q = t[q8_task_of(t, nt, blk)];
+  const long j = blk - q.blk0, nb = q8_blocks(q.n);
+  float m = 0.f;
+  const long n8 = q.n / 8;
+  for (long i = j * 256 + threadIdx.x; i < n8; i += nb * 256) {
+    float v[8];
+    ld8_dyn(q.x, dt, i * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+  }
+  for (long i = n8 * 8 + j * 256 + threadIdx.x; i < q.n; i += nb * 256) m = fmaxf(m, fabsf(ld_dyn(q.x, dt, i)));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blk] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// pass 2: every block of task i reduces the task's partials, then casts its share (quant_fp8_kernel's math)
+__global__ __launch_bounds__(256) void quant_batch_kernel(const cfm_q8_task* __restrict__ t, int nt, int dt,
+                                                          const float* __restrict__ part) {
+  __shared__ float red[4];
+  const long blk = blockIdx.x;
+  const cfm_q8_task q = t[q8_task_of(t, nt, blk)];
+  const long j = blk - q.blk0, nb = q8_blocks(q.n);
+  float m = 0.f;
+  for (long i = threadIdx.x; i < nb; i += 256) m = fmaxf(m, part[q.blk0 + i]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  const float sc = fp8_scale(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  if (j == 0 && threadIdx.x == 0) q.inv_scale[0] = 1.f / sc;
+  uint8_t* y = reinterpret_cast<uint8_t*>(q.y);
+  const long n8 = q.n / 8;
+  for (long i = j * 256 + threadIdx.x; i < n8; i += nb * 256) {
+    float v[8];
+    ld8_dyn(q.x, dt, i * 8, v);
+    int lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * sc, v[1] * sc, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * sc, v[3] * sc, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * sc, v[5] * sc, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * sc, v[7] * sc, hi, true);
+    *reinterpret_cast<uint2*>(y + i * 8) = make_uint2((unsigned)lo, (unsigned)hi);
+  }
+  for (long i = n8 * 8 + j * 256 + threadIdx.x; i < q.n; i += nb * 256) {
+    const int w = __builtin_amdgcn_cvt_pk_fp8_f32(ld_dyn(q.x, dt, i) * sc, 0.f, 0, false);
+    y[i] = (uint8_t)(w & 0xFF);
+  }
+}
+
 int grid_for(long n) {
   long b = (n / 8 + 255) / 256;
   return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
@@ -100,6 +169,19 @@ CFM_EXPORT int cfm_quant_fp8(const void* x, int dtx, long n, void* y, float* inv
   hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, dtx, n, (const float*)amax_ws,
                      (uint8_t*)y, inv_scale);
   return cfm::check_launch("cfm_quant_fp8");
+}
+
+CFM_EXPORT long cfm_quant_fp8_batch_blocks(long n) { return q8_blocks(n); }
+
+CFM_EXPORT int cfm_quant_fp8_batch(const cfm_q8_task* tasks, int ntasks, long nblocks, int dtx, float* amax_ws,
+                                   void* stream) {
+  CFM_REQUIRE(tasks && amax_ws && ntasks > 0 && nblocks > 0, CFM_ERR_ARG, "null table / empty batch");
+  CFM_REQUIRE(dtx == CFM_F32 || dtx == CFM_BF16, CFM_ERR_DTYPE, "x must be fp32 or bf16");
+  hipStream_t s = cfm::as_stream(stream);
+  hipLaunchKernelGGL(amax_batch_kernel, dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks, dtx, amax_ws);
+  hipLaunchKernelGGL(quant_batch_kernel, dim3((unsigned)nblocks), dim3(256), 0, s, tasks, ntasks, dtx,
+                     (const float*)amax_ws);
+  return cfm::check_launch("cfm_quant_fp8_batch");
 }
 
 CFM_EXPORT int cfm_dequant_fp8(const void* x, long n, const float* inv_scale, float* y, void* stream) {

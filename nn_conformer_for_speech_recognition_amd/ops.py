@@ -399,6 +399,42 @@ class CastTBatch:
         L.call("cfm_cast_transpose_batch", L.ptr(self.table), self.n, self.nblocks, self.dtx, self.dty, L.stream())
 
 
+class Quant8Batch:
+    """Per-step e4m3 copies of a fixed list of tensors in TWO launches (cfm_quant_fp8_batch): the same current
+    scaling, scales and bytes as quant_fp8 per tensor.  outs[i] = (y float8_e4m3fn of srcs[i]'s shape,
+    inv_scale (1,) fp32), persistent across refresh() calls (graph-capturable: the table is built once)."""
+
+    def __init__(self, srcs):
+        import numpy as np
+        if not srcs:
+            raise L.CfmError("Quant8Batch: empty list")
+        dts = {L.dt(t) for t in srcs}
+        if len(dts) != 1 or dts & {L.F32, L.BF16} != dts:
+            raise L.CfmError("Quant8Batch: one fp32 or bf16 source dtype per batch")
+        self.dtx = dts.pop()
+        dev = srcs[0].device
+        self.outs = []
+        rec = np.zeros((len(srcs), 5), dtype=np.int64)
+        blk = 0
+        for i, x in enumerate(srcs):
+            if not x.is_contiguous() or L.ptr(x) % 16:
+                raise L.CfmError("Quant8Batch: contiguous 16-B aligned sources required")
+            y = torch.empty(x.shape, device=dev, dtype=torch.float8_e4m3fn)
+            sc = torch.empty(1, device=dev, dtype=torch.float32)
+            self.outs.append((y, sc))
+            rec[i] = (L.ptr(x), L.ptr(y), L.ptr(sc), x.numel(), blk)
+            blk += L.load().cfm_quant_fp8_batch_blocks(x.numel())
+        self.nblocks = blk
+        self.table = torch.from_numpy(rec.view(np.uint8).reshape(-1).copy()).to(dev)
+        self.part = torch.empty(blk, device=dev, dtype=torch.float32)
+        self._keep = list(srcs)
+
+    def refresh(self):
+        L.call("cfm_quant_fp8_batch", L.ptr(self.table), len(self.outs), self.nblocks, self.dtx, L.ptr(self.part),
+               L.stream())
+        return self.outs
+
+
 def cast_into(x, y):
     L.call("cfm_cast", L.ptr(x), L.dt(x), L.ptr(y), L.dt(y), x.numel(), L.stream())
     return y

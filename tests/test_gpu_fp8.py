@@ -110,3 +110,19 @@ def test_conformer_fp8_forward_vs_fp32_oracle(T, lens):
         if n.endswith("conv_module.sequential.2.bias"):
             continue
         assert _rel(prm.grad, rp[n].grad) < 1e-1 * (3 if "pos_bias" in n else 1), n
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_quant_fp8_batch_matches_per_tensor(dt):
+    """cfm_quant_fp8_batch (ops.Quant8Batch: the per-step fp8 weight copies, two launches for the list) gives the
+    same bytes and scales as cfm_quant_fp8 tensor by tensor (bit-exact; sizes with tails and one-block tensors)."""
+    g = torch.Generator().manual_seed(11)
+    shapes = [(2048, 512), (512, 2048), (1536, 512), (7, 13), (1, 8), (3000, 1)]
+    srcs = [(torch.randn(*s, generator=g) * (10.0 ** (i - 2))).to(DEV, dt).contiguous() for i, s in enumerate(shapes)]
+    qb = ops.Quant8Batch(srcs)
+    for _ in range(2):                       # refresh twice: persistent outputs overwritten in place
+        outs = qb.refresh()
+    for x, (y, sc) in zip(srcs, outs):
+        y_ref, sc_ref = ops.quant_fp8(x)
+        assert torch.equal(sc, sc_ref), (x.shape, sc.item(), sc_ref.item())
+        assert torch.equal(y.view(torch.uint8), y_ref.view(torch.uint8)), x.shape
