@@ -1646,6 +1646,15 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
   if constexpr (AK) {
     // auto: outputs <= 512 columns (the encoder's d-wide outputs) take the 192-row tiles: 63 x 4 = 252
     // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
+    // 96 x 128 tiles, 4 waves of 96 x 32, BK 32, two workgroups per CU (cfm_gemm_set_mode bit 18, A/B): 125 x 4 =
+    // 500 tiles of the encoder's d-wide outputs fill the 512 slots in one round, and one workgroup's epilogue can
+    // run under the other's main loop (the 192-row variant below holds one 8-wave workgroup per CU)
+    if (v == 0 && (g_gemm_mode & 262144) && p.N <= 512 && p.split_k == 1 && (long)p.M * batch >= 4096) {
+      const dim3 g96(cdiv(p.N, BN), cdiv(p.M, 96), batch * p.split_k);
+      hipLaunchKernelGGL((gemm_pipe_kernel<96, 32, 3, 2, AK, BKM, 4, 4, false, false, false, BN, M16>), g96,
+                         dim3(256), 0, s, p, oa, ob, GatherA{});
+      return;
+    }
     if (v == 5 || (v == 0 && p.N <= 512 && p.split_k == 1 && (long)p.M * batch >= 4096)) {
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
       // 4-deep ring (4 x 40 KiB = the whole 160 KiB LDS): FFN-up data gradient 34.2 -> 32.5 us same-box;
