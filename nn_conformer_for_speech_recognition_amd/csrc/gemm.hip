@@ -1646,9 +1646,11 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
   if constexpr (AK) {
     // auto: outputs <= 512 columns (the encoder's d-wide outputs) take the 192-row tiles: 63 x 4 = 252
     // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
-    // 96 x 128 tiles, 4 waves of 96 x 32, BK 32, two workgroups per CU (cfm_gemm_set_mode bit 18, A/B): 125 x 4 =
-    // 500 tiles of the encoder's d-wide outputs fill the 512 slots in one round, and one workgroup's epilogue can
-    // run under the other's main loop (the 192-row variant below holds one 8-wave workgroup per CU)
+    // 96 x 128 tiles, 4 waves of 96 x 32, BK 32, two workgroups per CU (cfm_gemm_set_mode bit 18, opt-in): 125 x 4 =
+    // 500 tiles of the encoder's d-wide outputs in one round of the 512 slots.  Bit-identical to the 192-row tiles
+    // but SLOWER (profiles/r03/gemm_v96_ab.txt: FFN-down forward 41.0 -> 54.3 us, FFN-up data gradient 33.4 ->
+    // 47.1 us; L15 step 21.0 -> 22.0 ms same box): half the FLOP per staged byte, and the two workgroups of a CU
+    // reach their epilogues together
     if (v == 0 && (g_gemm_mode & 262144) && p.N <= 512 && p.split_k == 1 && (long)p.M * batch >= 4096) {
       const dim3 g96(cdiv(p.N, BN), cdiv(p.M, 96), batch * p.split_k);
       hipLaunchKernelGGL((gemm_pipe_kernel<96, 32, 3, 2, AK, BKM, 4, 4, false, false, false, BN, M16>), g96,
