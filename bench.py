@@ -71,6 +71,21 @@ def algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, F2, C1=512, C2=128, r
     return fwd / T_in, fwdbwd / T_in
 
 
+def executed_flops_per_frame(L, d, H, ffn, K, T_in, T2, rel=False, B=1, Kp=1792, T2p=None):
+    """The FLOPs the step EXECUTES per mel frame (fwd+bwd), for step_algorithmic_tflops / step_mfma_frac: the
+    encoder as in algorithmic_flops_per_frame, but the front-end as the folded GEMMs that replace conv1 + conv2 +
+    projection: the forward GEMM 2*T2*Kp*d and the weight-gradient GEMM 2*T2p*Kp*d per utterance
+    (Kp = 11 frames x 80 mels x hi+lo, padded; no input gradient); the fold's ~1 GFLOP/step of fp32 weight
+    contractions is not counted.  The CTC head is excluded (reported separately)."""
+    per = 4 * d * ffn + 7 * d * d + K * d + 2 * T2 * d
+    if rel:
+        per += T2 * d + (2 * T2 - 1) * d * d / (B * T2)
+    enc = L * T2 * per
+    T2p = T2 + 2 if T2p is None else T2p
+    front = 2 * T2 * Kp * d + 2 * T2p * Kp * d
+    return (3 * 2 * enc + front) / T_in
+
+
 class EncoderCTC(torch.nn.Module):
     """Front-end + Conformer encoder + CTC head (the hot path of SURVEY.md §8a, 'frame' mode)."""
 
@@ -173,7 +188,7 @@ class KernelProbe:
     and one-lane kernels on the same stream reset the slot before and accumulate it after the
     launch.  Works eagerly and inside a captured HIP graph (every replay accumulates)."""
 
-    MAX_SLOTS = 512
+    MAX_SLOTS = 1024
 
     def __init__(self, match, device):
         self.match = match
@@ -181,12 +196,16 @@ class KernelProbe:
         self.slots = torch.zeros(self.MAX_SLOTS, 4, dtype=torch.int64, device=device)
         self.used = 0
         self.khz = _lib.load().cfm_wallclock_khz()
+        self.slot_flops = [0.0] * self.MAX_SLOTS    # 2*M*N*K*batch of the launch each slot times (GEMMs)
 
     def __call__(self, kind, shape, desc, launch):
         if not (self.active and self.match(kind, shape, desc)) or self.khz <= 0:
             return launch()
         slot = self.used % self.MAX_SLOTS
         self.used += 1
+        if kind == "gemm":
+            M, N, K = shape
+            self.slot_flops[slot] = 2.0 * M * N * K * max(1, int(desc.batch))
         ptr = _lib.ptr(self.slots[slot])
         _lib.call("cfm_probe_slot", ptr, 0, _lib.stream())
         desc.probe = ptr
@@ -203,6 +222,90 @@ class KernelProbe:
         tot = self.slots[:, 2].double().sum().item()
         n = int(self.slots[:, 3].sum().item())
         return (tot / self.khz / n) if n else float("nan"), n
+
+    def mean_flops(self):
+        """Launch-weighted mean FLOPs per timed launch (a family of GEMM shapes)."""
+        cnt = self.slots[:, 3].double().cpu()
+        n = cnt.sum().item()
+        return (sum(f * c for f, c in zip(self.slot_flops, cnt.tolist())) / n) if n else float("nan")
+
+
+def dgemm_bytes(probe, M, d):
+    """Mean algorithmic bytes per launch of the d-wide GEMM family: A (M x K) + B (d x K) bf16 read, C (M x d)
+    written (fp32 + an fp32 residual read for the residual-stream forwards, bf16 for data gradients).  Approximated
+    per launch from its FLOPs (K = flops / 2Md) with the bf16-output form; the fp32 forwards (3 of 10 per layer)
+    move 12 more bytes per output element."""
+    cnt = probe.slots[:, 3].double().cpu().tolist()
+    tot = n = 0.0
+    for f, c in zip(probe.slot_flops, cnt):
+        if c and f:
+            Kx = f / (2.0 * M * d)
+            tot += c * (2.0 * (M * Kx + d * Kx) + 2.0 * M * d)
+            n += c
+    return tot / n if n else float("nan")
+
+
+def time_ctc_head(h, reps=20):
+    """The fused CTC head (Linear d->V + log_softmax + CTC loss, fwd + bwd, ctc.hip) alone at the step's shape,
+    as one captured HIP graph replayed `reps` times (HIP events): its share of the timed step, which SURVEY.md
+    §8d reports separately from the encoder metric.  Runs after the timed region on copies of the head's
+    weights (the model's gradients are untouched)."""
+    m = h.model
+    M = h.B * h.T2
+    g = torch.Generator(device="cpu").manual_seed(7)
+    y = (torch.randn(M, h.d, generator=g) * 0.5).to(h.dev).requires_grad_()
+    w = m.ctc_fc.weight.detach().clone().requires_grad_()
+    b = m.ctc_fc.bias.detach().clone().requires_grad_()
+
+    def run():
+        loss, _ = ctc_head_loss(y, w, b, h.tgt_i32, h.lens_i32, h.tlen_i32, h.B, h.T2, blank=0, reduction="mean",
+                                zero_infinity=True, compute_dtype=m.cd)
+        loss.backward()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            run()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    y.grad = w.grad = b.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        run()
+    graph.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        graph.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def physical_cores():
+    """(physical cores of the host, CPUs this process may run on): unique (physical id, core id) pairs of
+    /proc/cpuinfo, and the scheduler affinity mask."""
+    cores, phys, core = set(), None, None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":", 1)[1].strip()
+                elif not line.strip() and core is not None:
+                    cores.add((phys, core))
+                    phys = core = None
+        if core is not None:
+            cores.add((phys, core))
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    return len(cores) or (os.cpu_count() or 1), aff
 
 
 def cpu_model():
@@ -411,6 +514,7 @@ class Harness:
         else:
             with torch.cuda.graph(self.graph):
                 self.static_loss = self.fwd_bwd()
+            self.reducer.mark_graph()
         for p in probes:
             p.active = False
         grads_timed = [p.grad for p in self.params]
@@ -482,7 +586,9 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-optimizer", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline threads (default: the host's physical cores, SURVEY.md §8d; a 16-thread "
+                         "figure -- one GPU's CPU share on the pool -- is reported beside it)")
     ap.add_argument("--gemm-mode", type=int, default=int(os.environ["CFM_GEMM_MODE"]) if "CFM_GEMM_MODE" in os.environ
                     else None, help="cfm_gemm_set_mode value (A/B tuning; env CFM_GEMM_MODE)")
     ap.add_argument("--attn-mode", type=int, default=int(os.environ.get("CFM_ATTN_MODE", "0")),
@@ -551,17 +657,24 @@ def main():
                         and not dsc.act_grad and dsc.a_kmajor and dsc.b_kmajor, dev)
     # second probed family: the grouped weight-gradient launch (one per step)
     wprobe = KernelProbe(lambda kind, shape, dsc: kind == "wgroup", dev)
-    ops.PROBE = lambda kind, shape, dsc, launch: probe(kind, shape, dsc, lambda: wprobe(kind, shape, dsc, launch))
-    h.setup(args.warmup, probes=(probe, wprobe))
+    # the dominant kernel family (round-3 kernel trace): every bf16 GEMM with a d-wide output over the step's
+    # tokens -- FFN-down / out-projection / pointwise-conv-2 forward, every d-wide data gradient (FFN-up, QKV,
+    # out-projection, pointwise convs) and the folded front-end GEMM (batch x T2 rows)
+    dprobe = KernelProbe(lambda kind, shape, dsc: kind == "gemm" and shape[1] == d and shape[0] * dsc.batch == M_ffn
+                         and dsc.dtype_ab == _lib.BF16 and dsc.split_k <= 1 and dsc.a_kmajor and dsc.b_kmajor, dev)
+    ops.PROBE = lambda kind, shape, dsc, launch: probe(kind, shape, dsc, lambda: wprobe(
+        kind, shape, dsc, lambda: dprobe(kind, shape, dsc, launch)))
+    h.setup(args.warmup, probes=(probe, wprobe, dprobe))
     probe.reset()
     wprobe.reset()
+    dprobe.reset()
     bad_before = h.nonfinite_steps()
 
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     if h.graph is None:
-        probe.active = wprobe.active = True
+        probe.active = wprobe.active = dprobe.active = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = h.step()
@@ -569,7 +682,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
-    probe.active = wprobe.active = False
+    probe.active = wprobe.active = dprobe.active = False
     elapsed = t1 - t0
     if world > 1:
         tt = torch.tensor([elapsed], device=dev)
@@ -607,11 +720,17 @@ def main():
     # y and the saved pre-activation (M x ffn each, bf16) written
     gemm_bytes = 2.0 * (M_ffn * d + ffn * d) + 4.0 * ffn + 2.0 * 2.0 * M_ffn * ffn
     wg_ms, wg_n = wprobe.mean_ms()
+    dg_ms, dg_n = dprobe.mean_ms()
+    dg_flops = dprobe.mean_flops()
     wg_shapes = [(d, ffn), (ffn, d)] * 2 + [(3 * d, d), (d, d), (2 * d, d), (d, d)]   # (N, K) per layer
     wg_flops = 2.0 * M_ffn * L * sum(n * k for n, k in wg_shapes)
     wg_bytes = L * sum(2.0 * M_ffn * (n + k) + 4.0 * n * k + 4.0 * n for n, k in wg_shapes)
     _, fpf = algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, model.F2, rel=pos_enc == "rel", B=B)
-    step_tflops = fpf * B * T_in / (ms_step * 1e-3) / 1e12
+    fg = ops.ffold_geometry(B, 80, T_in, 512, 128, d, 7, 2, 3, 2, torch.bfloat16, True)
+    xpf = executed_flops_per_frame(L, d, H, ffn, K, T_in, T2, rel=pos_enc == "rel", B=B, Kp=fg.Kp, T2p=fg.T2p)
+    step_tflops = xpf * B * T_in / (ms_step * 1e-3) / 1e12
+    ref_tflops = fpf * B * T_in / (ms_step * 1e-3) / 1e12
+    ctc_ms = time_ctc_head(h) if rank == 0 else float("nan")
 
     def roofline_entry(kernel, flops, nbytes, ms, n_launch, pmc_file):
         """bound from the kernel's arithmetic intensity against the machine balance (peak FLOP/s over peak
@@ -629,7 +748,7 @@ def main():
              "intensity_flop_per_byte": round(intensity, 1), "machine_balance_flop_per_byte": round(balance, 1),
              "avg_launch_ms": round(ms, 4), "launches_timed": n_launch, "timing": timing,
              "flops_per_launch": flops, "algorithmic_bytes": nbytes}
-        for rnd in ("r03", "r02"):
+        for rnd in ("r04", "r03", "r02"):
             path = os.path.join(REPO, "profiles", rnd, pmc_file)
             if not os.path.exists(path):
                 continue
@@ -658,14 +777,29 @@ def main():
                                                       else "hip-graph (fwd+bwd)"),
                    "grad_reduce_dtype": "bf16" if h.reducer.grad_dtype == torch.bfloat16 else "fp32"},
         "per_gpu_value": round(value / world, 1),
+        # FLOPs the step executes (encoder + the folded front-end GEMMs; CTC head excluded), and the reference
+        # composition's count (conv1 + conv2 + projection as the reference computes them) beside it
         "step_algorithmic_tflops": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
+        "step_flops_basis": "executed: encoder (SURVEY.md 8d per-layer MACs) + folded front-end GEMMs; CTC head "
+                            "excluded",
+        "step_ref_composition_tflops": round(ref_tflops, 1),
+        "ctc_head": {"ms": round(ctc_ms, 4), "share_of_step": round(ctc_ms / ms_step, 4),
+                     "flops": 3 * 2.0 * B * T2 * d * h.V,
+                     "timing": "fused Linear + log_softmax + CTC fwd+bwd alone at the step's shape, one HIP graph "
+                               "replayed 20x after the timed region (HIP events); it runs inside the timed step"},
         "loss": loss_val,
         "steps_checked": h.steps_run, "nonfinite_steps": nonfinite, "nonfinite_before_timing": bad_before,
         "params_finite": params_ok, "valid": valid,
-        "roofline": roofline_entry(f"gemm_pipe FFN up-projection M={M_ffn} N={ffn} K={d} (+bias+SiLU+dropout, "
-                                   f"y and pre-activation stored)", gemm_flops, gemm_bytes, gemm_ms, n_launch,
-                                   "gemm_ffn_up_pmc.json"),
+        # the dominant kernel family: d-wide-output GEMMs (mean FLOP / mean launch; bytes: A + B read, C written
+        # in its dtype -- bf16 data gradients, fp32 residual-stream forwards read + written -- averaged likewise)
+        "roofline": roofline_entry(f"gemm_pipe d-wide outputs (N={d}, M={M_ffn} tokens): FFN-down / out-proj / pw2 "
+                                   f"forward + every d-wide data gradient + the front-end fold, {dg_n // max(1, args.steps)}"
+                                   f" launches per step", dg_flops, dgemm_bytes(dprobe, M_ffn, d), dg_ms, dg_n,
+                                   "gemm_dwide_pmc.json"),
+        "roofline_ffn_up": roofline_entry(f"gemm_pipe FFN up-projection M={M_ffn} N={ffn} K={d} (+bias+SiLU+dropout, "
+                                          f"y and pre-activation stored)", gemm_flops, gemm_bytes, gemm_ms, n_launch,
+                                          "gemm_ffn_up_pmc.json"),
         "roofline_wgrad": roofline_entry(f"grouped weight gradients (cfm_wgrad_group): {L} layers x 8 GEMMs, "
                                          f"M={M_ffn} tokens", wg_flops, wg_bytes, wg_ms, wg_n,
                                          "wgrad_group_pmc.json"),
@@ -673,8 +807,13 @@ def main():
     if args.poison:
         result["poison"] = True
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_threads)
-        result["cpu_baseline_configs0"] = cpu_baseline_s10(args.cpu_threads)
+        phys, aff = physical_cores()
+        nt = args.cpu_threads or phys
+        result["cpu_baseline"] = cpu_baseline(cfg, nt)
+        result["cpu_baseline"]["host_physical_cores"] = phys
+        result["cpu_baseline"]["affinity_cpus"] = aff
+        result["cpu_baseline_16t"] = cpu_baseline(cfg, 16)
+        result["cpu_baseline_configs0"] = cpu_baseline_s10(nt)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

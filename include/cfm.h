@@ -124,7 +124,8 @@ int cfm_logmel_fwd(const float* wave, long ld_wave, const int32_t* lens, int B, 
  * (asrnn.py:208 / frame projection) and the projection block (asrnn.py:73-89).
  *   A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]
  *   B(n,k) = B[n*ldb + k] if b_kmajor else B[k*ldb + n]
- * (A / B rows may overlap, ld below the row length: read-only windowed views, cfm_ffold_*.)
+ * (A / B rows may overlap, ld below the row length, only with allow_overlap: read-only windowed views,
+ *  cfm_ffold_*.)
  * Epilogue, in order: v = alpha*acc + bias[n];  v *= act'(pre[m,n]) if act_grad;
  *   if act == SILU { pre[m,n] = v (if pre != NULL); v = silu(v) };  v *= dropout(seed, idx);
  *   v *= out_scale;  v += residual[m,n];  C = v  (or atomically C += v when split_k > 1).
@@ -164,6 +165,10 @@ typedef struct cfm_gemm_desc {
      written by cfm_quant_fp8); NULL: 1 */
   const float* alpha_a_dev;
   const float* alpha_b_dev;
+  /* nonzero: A / B rows may overlap (lda / ldb below the row length: the folded front-end's read-only windowed
+     view of the packed mels, cfm_ffold_*).  0: lda >= (a_kmajor ? K : M) and ldb >= (b_kmajor ? K : N) are
+     enforced (CFM_ERR_SHAPE), so a wrongly transposed view fails instead of reading overlapping rows. */
+  int allow_overlap;
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 /* Per-tensor fp8 (e4m3fn) quantisation for the fp8 GEMM path (configs[4]; no reference counterpart -- the

@@ -43,6 +43,7 @@ class GemmDesc(ctypes.Structure):
         ("a_colsum", c_void_p),
         ("rowdot_with", c_void_p), ("rowdot_out", c_void_p), ("rowdot_T", c_int),
         ("alpha_a_dev", c_void_p), ("alpha_b_dev", c_void_p),
+        ("allow_overlap", c_int),
     ]
 
 
@@ -224,12 +225,20 @@ def load():
     return lib
 
 
+# True while a device dropout step counter is bound (cfm_rng_bind with a non-NULL pointer): the compiled
+# encoder route (Conformer._forward_tokens_ops) needs it for fresh masks per step
+RNG_BOUND = False
+
+
 def call(name, *args):
+    global RNG_BOUND
     lib = load()
     rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.cfm_get_last_error().decode(errors="replace")
         raise CfmError(f"{name} failed ({rc}): {msg}")
+    if name == "cfm_rng_bind":
+        RNG_BOUND = bool(args and args[0])
     return rc
 
 

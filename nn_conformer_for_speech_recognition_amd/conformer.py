@@ -622,7 +622,13 @@ class Conformer(nn.Module):
         (fullgraph=True).  Same kernels as the fused layer node; dropout seeds are fixed per call site unless
         `seed` is given (a device step counter bound with cfm_rng_bind salts them per step, as in HIP-graph
         replay), so no Python-side step counter is mutated inside the traced region."""
-        from . import library
+        from . import library, _lib
+        if seed is None and self.training and not _lib.RNG_BOUND and any(
+                float(ly.dropout) > 0 for ly in self.conformer_layers):
+            # fixed per-call-site seeds would apply the SAME dropout masks every compiled step
+            raise RuntimeError("compiled Conformer training with dropout > 0 needs fresh masks per step: pass "
+                               "seed=<per-step int> to forward_tokens or bind a device step counter "
+                               "(cfm_rng_bind) whose value advances every step")
         base = 12345 if seed is None else seed
         for i, layer in enumerate(self.conformer_layers):
             x = library.layer_forward(layer, x, lens_i32, B, T, self.compute_dtype, base + 100 * i)

@@ -1844,8 +1844,10 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
                              !d->residual && d->drop_p <= 0.f),
               CFM_ERR_ARG, "split_k needs a plain fp32 epilogue");
   // A and B are read-only: rows may overlap (ld below the row length -- the folded front-end's windowed view
-  // of the packed mels, frontfold.hip); C rows may not
+  // of the packed mels, frontfold.hip) when the caller says so (allow_overlap); C rows may not
   CFM_REQUIRE(d->lda >= 1 && d->ldb >= 1, CFM_ERR_SHAPE, "lda / ldb");
+  CFM_REQUIRE(d->allow_overlap || (d->lda >= (d->a_kmajor ? d->K : d->M) && d->ldb >= (d->b_kmajor ? d->K : d->N)),
+              CFM_ERR_SHAPE, "lda / ldb below the row length (overlapping rows need allow_overlap)");
   CFM_REQUIRE(d->ldc >= d->N, CFM_ERR_SHAPE, "ldc");
   if (d->M == 0 || d->N == 0) return CFM_OK;
 

@@ -94,6 +94,11 @@ class GradAllReducer:
         self.routed = set()       # Conformer layers whose grouped gradients all landed in the buckets
         self._no_sync = False
         self.conformer = None
+        # HIP-graph steps: (captured gradient tensor, bucket view) of grouped gradients that were NOT routed into
+        # their bucket at capture -- every replay rewrites the captured tensor, so allreduce() copies it in again
+        # (a one-time copy + re-pointed .grad would reduce the first replay's values forever: ADVICE r3)
+        self.graph_mode = False
+        self._replay_src = {}
         owned = set()
         if model is not None:
             from .conformer import Conformer
@@ -247,10 +252,22 @@ class GradAllReducer:
         gradient living elsewhere is copied in first.  copy=False (chunk reduced during backward, only from
         fully routed layers): the bucket already holds the reduced gradient, so .grad is just re-pointed."""
         for p, v in self._chunk_views(chunk):
+            if copy:
+                src = self._replay_src.get(v.data_ptr())
+                if src is not None:                 # graph replay rewrote the captured (un-routed) gradient
+                    v.copy_(src.reshape(v.shape))
             if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
                 if copy:
                     v.copy_(p.grad.reshape(v.shape))
+                    if self.graph_mode:
+                        self._replay_src[v.data_ptr()] = p.grad
                 p.grad = v.view(p.shape)
+
+    def mark_graph(self):
+        """The step's backward is now a captured HIP graph (replayed, not re-run): gradients the capture left
+        outside their bucket views are copied in on every allreduce(), not only the first."""
+        self.graph_mode = True
+        self._replay_src = {}
 
     def allreduce(self):
         if self._world() == 1:
@@ -356,6 +373,16 @@ class SegmentedStepGraph:
             red.segmenter = self
             try:
                 out = fn()
+            except BaseException:
+                # end the in-flight capture so the stream leaves capture mode and the original error surfaces
+                # (not a confusing capture error from the next HIP call); the partial graphs are discarded
+                try:
+                    self._g.capture_end()
+                except Exception:
+                    pass
+                self._g = None
+                self.graphs = []
+                raise
             finally:
                 red.segmenter = None
             self._g.capture_end()
@@ -363,6 +390,7 @@ class SegmentedStepGraph:
             self._g = None
         torch.cuda.current_stream().wait_stream(s)
         red.launched = set()
+        red.mark_graph()
         return out
 
     def replay(self):

@@ -72,7 +72,7 @@ class _FrameFoldFn(torch.autograd.Function):
         wfull, bfull, ws = ops.ffold_compose(w1, b1, w2, b2, wp, bp, g, cd)
         h = torch.empty(B * g.T2, D, device=x.device, dtype=torch.float32)
         ops.gemm(xt, wfull, h, g.T2, D, g.Kp, lda=g.lda, stride_a=g.Tslot * g.Cx, batch=B, stride_c=g.T2 * D,
-                 bias=bfull, drop_p=drop_p, seed=seed)
+                 bias=bfull, drop_p=drop_p, seed=seed, allow_overlap=True)
         ctx.save_for_backward(xt, ws, w1, b1, w2, wp)
         ctx.g = g
         ctx.cfg = (cd, drop_p, seed)
@@ -95,11 +95,11 @@ class _FrameFoldFn(torch.autograd.Function):
             S = torch.empty(D, device=dh.device, dtype=torch.float32)
             wsk = ops.workspace(4 * (split * D * g.Kp + split * D), dh.device)
             ops.gemm(gpad.view(K, D), xt, H, D, g.Kp, K, a_kmajor=False, lda=D, b_kmajor=False, ldb=g.lda,
-                     split_k=split, workspace=wsk, a_colsum=S)
+                     split_k=split, workspace=wsk, a_colsum=S, allow_overlap=True)
         else:
             wsk = ops.workspace(4 * split * D * g.Kp, dh.device)
             ops.gemm(gpad.view(K, D), xt, H, D, g.Kp, K, a_kmajor=False, lda=D, b_kmajor=False, ldb=g.lda,
-                     split_k=split, workspace=wsk)
+                     split_k=split, workspace=wsk, allow_overlap=True)
             S = ops.colsum(gpad.view(K, D))
         dw1, db1, dw2, db2, dwp = ops.ffold_bwd_weights(H, S, w1, b1, w2, wp, ws, g)
         return None, dw1, db1, dw2, db2, dwp, S, None, None, None, None, None, None

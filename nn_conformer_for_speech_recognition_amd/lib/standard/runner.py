@@ -116,6 +116,7 @@ class Runner:
                 eloss.append(cur)
                 if want_wer:
                     emetric.append(self._metric(train_set, logits.detach(), target))
+            self._check_device_errors()
             self.history["loss"].append(mean([100 if isnan(x) else x for x in eloss]))
             self.history["metric"].append(mean(emetric) if emetric else float("nan"))
             if "validation" in train_set.idxes:
@@ -142,6 +143,7 @@ class Runner:
                 loss = self.loss(logits.transpose(0, 1), target, output_lens, target_lens)
                 eloss.append(loss.item())
                 emetric.append(self._metric(test_set, logits, target))
+        self._check_device_errors()
         eloss = mean([100 if isnan(x) else x for x in eloss])
         return eloss, mean(emetric)
 
@@ -162,6 +164,7 @@ class Runner:
                 # ASRNN.predict + Vocab.decode in one device pass: argmax, <pad>/<blank> removed, no collapse
                 _, toks, cnt = greedy_decode(logits, None, blank=voc.blank_idx, pad=voc.pad_idx, collapse=False)
                 mine[i] = voc.decode(toks, cnt)
+        self._check_device_errors()
         if world > 1:
             parts = [None] * world
             torch.distributed.all_gather_object(parts, mine)
@@ -171,6 +174,14 @@ class Runner:
         for i in range(n):
             targets += mine[i]
         return targets
+
+    def _check_device_errors(self):
+        """End-of-pass synchronising check of the BiLSTM recurrences' wait-limit flags: each forward only polls
+        the flags of EARLIER passes (no host sync per launch), so a failure in the last pass of an epoch / test /
+        label pass would otherwise go unreported."""
+        from ...lstm import LSTM
+        if any(isinstance(m, LSTM) for m in self.model.modules()):
+            LSTM.check_errors()
 
     def _write_history(self):
         d = getattr(self.hp, "plots_dir", None)

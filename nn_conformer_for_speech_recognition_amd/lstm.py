@@ -166,6 +166,10 @@ class LSTM(nn.Module):
         return [""] + (["_reverse"] if self.bidirectional else [])
 
     def forward(self, input, hx=None):
+        """Wait-limit failures of the recurrence kernels are reported WITHOUT a host sync: this call raises for a
+        failure of an earlier pass whose flag copy has completed (typically one forward late), so the failing
+        pass's outputs are already consumed.  Call LSTM.check_errors() at the end of a pass (Runner does, after
+        every epoch / test / label pass) for a synchronising check of everything launched so far."""
         if hx is not None:
             raise NotImplementedError("LSTM: an initial state hx is not supported (the reference passes none)")
         if input.dim() != 2:

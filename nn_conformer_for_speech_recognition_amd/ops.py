@@ -21,7 +21,7 @@ def _gemm_desc(**kw):
 def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, alpha=1.0,
          bias=None, act=ACT_NONE, act_grad=False, pre=None, drop_p=0.0, seed=0, offset=0, out_scale=1.0,
          residual=None, ldr=None, split_k=1, batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None,
-         a_colsum=None, rowdot=None, alpha_a=None, alpha_b=None):
+         a_colsum=None, rowdot=None, alpha_a=None, alpha_b=None, allow_overlap=False):
     """C = epilogue(alpha * A·Bᵀ) — see cfm_gemm_desc in include/cfm.h.  fp8 (e4m3fn) A and B: alpha_a /
     alpha_b are their device dequantisation scalars (quant_fp8)."""
     if A.dtype != B.dtype:
@@ -38,7 +38,8 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         ldr=ldr if ldr is not None else N, dtype_r=L.dt(residual) if residual is not None else F32,
         split_k=int(split_k), workspace=L.ptr(workspace), a_colsum=L.ptr(a_colsum),
         rowdot_with=L.ptr(rowdot[0]) if rowdot else None, rowdot_out=L.ptr(rowdot[1]) if rowdot else None,
-        rowdot_T=int(rowdot[2]) if rowdot else 0, alpha_a_dev=L.ptr(alpha_a), alpha_b_dev=L.ptr(alpha_b))
+        rowdot_T=int(rowdot[2]) if rowdot else 0, alpha_a_dev=L.ptr(alpha_a), alpha_b_dev=L.ptr(alpha_b),
+        allow_overlap=int(bool(allow_overlap)))
     if PROBE is not None:
         PROBE("gemm", (M, N, K), d, lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
     else:

@@ -83,9 +83,24 @@ def test_encoder_compiles_fullgraph_on_meta(conv_first):
         x = torch.randn(B * T, d, requires_grad=True)
         lens = torch.full((B,), T, dtype=torch.int32)
     torch._dynamo.reset()
-    y = torch.compile(model.forward_tokens, fullgraph=True, backend=backend)(x, lens, B, T)
+    y = torch.compile(model.forward_tokens, fullgraph=True, backend=backend)(x, lens, B, T, 123)
     y.sum().backward()
     assert y.shape == (B * T, d)
     assert x.grad is not None and all(p.grad is not None for p in model.parameters())
     for op in ("linear", "linear_silu", "layer_norm", "attention", "conv_glu_dwconv_bn_silu"):
         assert f"cfm.{op}.default" in seen and f"cfm.{op}_bwd.default" in seen, op
+
+
+def test_compiled_route_refuses_repeated_dropout_masks():
+    """The torch.ops route with dropout > 0, no per-step seed and no bound device step counter would apply the
+    same masks every step: it raises instead; eval mode, p = 0 or an explicit seed are fine."""
+    B, T, d = 2, 9, 64
+    with torch.device(M):
+        model = Conformer(d, 4, 128, 1, 31, dropout=0.1)
+        x = torch.randn(B * T, d)
+        lens = torch.full((B,), T, dtype=torch.int32)
+    with pytest.raises(RuntimeError, match="fresh masks"):
+        model._forward_tokens_ops(x, lens, B, T, None)
+    assert model._forward_tokens_ops(x, lens, B, T, 5).shape == (B * T, d)
+    model.eval()
+    assert model._forward_tokens_ops(x, lens, B, T, None).shape == (B * T, d)
