@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU session on the box: steps chained so that a crash / timeout / abort ends the session (test failures do
+# not).  usage: bash benchmarks/gpu_session.sh OUTDIR STEP...
+#   steps: fulldepth | gputests | dgemm | bench | benchL60 | pmc_dgemm | ktrace | <any shell command in quotes>
+R=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$(realpath -m "$1"); shift
+mkdir -p "$OUT"
+cd "$R"
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
+run() {   # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$lim" bash -c "$*" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(date +%T))"
+  tail -n 3 "$OUT/$name.log"
+  if [ $rc -ge 124 ]; then echo "ABORT: $name rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    fulldepth) run fulldepth 900 "$PYT -s tests/test_gpu_fulldepth.py" ;;
+    gputests) run gputests 900 "$PYT -q -m gpu tests --ignore=tests/test_gpu_fulldepth.py" ;;
+    dgemm) run dgemm 300 "python -u benchmarks/dgemm_family.py" ;;
+    bench) run bench 600 "python -u bench.py --gpus 1 --steps 20 --warmup 5" ;;
+    benchL60) run benchL60 600 "python -u bench.py --config L60 --steps 10 --warmup 3 --no-cpu-baseline" ;;
+    pmc_dgemm) run pmc_dgemm 900 "bash benchmarks/pmc_dgemm.sh $OUT 5" ;;
+    ktrace) run ktrace 600 "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline && python3 $R/profiles/summarize.py \$(find $OUT/ktrace -name '*kernel_stats.csv' | head -1) auto 45 > $OUT/kernel_summary.txt" ;;
+    *) run custom 900 "$s" ;;
+  esac
+done
+echo "=== session done"
