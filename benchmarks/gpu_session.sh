@@ -25,7 +25,7 @@ for s in "$@"; do
     bench) run bench 600 "python -u bench.py --gpus 1 --steps 20 --warmup 5" ;;
     benchL60) run benchL60 600 "python -u bench.py --config L60 --steps 10 --warmup 3 --no-cpu-baseline" ;;
     pmc_dgemm) run pmc_dgemm 900 "bash benchmarks/pmc_dgemm.sh $OUT 5" ;;
-    ktrace) run ktrace 600 "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline && python3 $R/profiles/summarize.py \$(find $OUT/ktrace -name '*kernel_stats.csv' | head -1) auto 45 > $OUT/kernel_summary.txt" ;;
+    ktrace) run ktrace 600 "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline && python3 $R/profiles/summarize.py \$(find $OUT/ktrace -name '*kernel_stats.csv' | head -1) auto 45 > $OUT/kernel_summary.txt" ;;
     *) run custom 900 "$s" ;;
   esac
 done

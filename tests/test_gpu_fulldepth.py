@@ -9,11 +9,17 @@ Reference: n_conformers (/root/reference/lib/hparams.py:42) consumed by the Conf
 (/root/reference/lib/standard/asrnn.py:29); its forward (:214); the CTC training step
 (/root/reference/lib/standard/runner.py:143-146); the NST label pass (runner.py:253-281).
 
-Tolerances (relative L2 over the whole tensor; measured values on MI355X in DESIGN.md §1 and printed by each test
-as a `FULLDEPTH {json}` line):
-  fp32 parity mode: 1e-3 on outputs, losses and every gradient (the north-star "logits match to 1e-3 rel")
-  bf16: set from the 17-layer measurements (about 3x the measured error), per quantity below
-  fp8 (forward GEMMs e4m3, backward bf16): likewise."""
+Tolerances (relative L2 over the whole tensor; every test prints its measured errors as a `FULLDEPTH {json}` line;
+the round-4 MI355X values are quoted here and in DESIGN.md §1):
+  fp32 parity mode: 1e-3 on outputs, losses and every gradient (the north-star "logits match to 1e-3 rel").
+    measured: 17 layers y 1.3e-6, dx 2.1e-6, worst weight gradient 3.4e-6; + front-end + CTC head: loss 2e-7,
+    log-probs 3e-7, worst gradient 1.1e-4 (the folded front-end's weight gradients, 6e-5).
+  bf16: about 2-3x the measured 16/17-layer error.  measured: y 0.59-0.65 %, dx 0.88-0.99 %, worst weight gradient
+    1.3-1.6 %; + front-end + CTC: loss 7.7e-5, log-probs 0.13 %, worst gradient 3.1 % (layer-0 pointwise conv 1).
+  NST (bf16, eval, 17 layers): 100 % of the 325 valid frames agree with the oracle's argmax (all have a top-2
+    margin > 0.25 nats).
+  fp8 (forward GEMMs e4m3, backward bf16, rel-pos, T 373): measured y 4.5 %, dx 3.7 %, worst gradient 9.1 %
+    (layer-16 linear_pos)."""
 import json
 
 import pytest
@@ -28,7 +34,9 @@ from oracle import conformer as oc  # noqa: E402
 from oracle import frontend as of  # noqa: E402
 
 # (output, input gradient, worst parameter gradient) relative L2
-TOL = {torch.float32: (1e-3, 1e-3, 1e-3), torch.bfloat16: (5e-2, 1e-1, 1e-1)}
+TOL = {torch.float32: (1e-3, 1e-3, 1e-3), torch.bfloat16: (2e-2, 3e-2, 4e-2)}
+# bench.py's step (front-end + encoder + CTC head): (loss, log-probs, worst parameter gradient)
+TOL_CTC = {torch.float32: (1e-3, 1e-3, 1e-3), torch.bfloat16: (1e-3, 5e-3, 7e-2)}
 
 
 def rel_err(a, b):
@@ -158,9 +166,9 @@ def test_encoder_ctc_step_vs_oracle(cd):
     front = {k: eg[k] for k in eg if not k.startswith("conformers.")}
     _report(f"encoder+ctc L17 {str(cd)[6:]} T_in{T_in}", loss=el, loss_value=float(loss_r), logprobs=elog,
             worst_grad=eg[worst], worst_param=worst, median_grad=sorted(eg.values())[len(eg) // 2], **front)
-    ty, tx, tg = TOL[cd]
-    assert el < ty, el
-    assert elog < ty, elog
+    tl_, tlog, tg = TOL_CTC[cd]
+    assert el < tl_, el
+    assert elog < tlog, elog
     assert eg[worst] < tg, (worst, eg[worst])
 
 
@@ -235,5 +243,5 @@ def test_fp8_L17_vs_oracle():
     worst = max(eg, key=eg.get)
     _report("encoder L17 fp8 rel T373", y=ey, dx=ex, worst_grad=eg[worst], worst_param=worst,
             median_grad=sorted(eg.values())[len(eg) // 2])
-    assert ey < 1e-1 and ex < 2e-1, (ey, ex)
+    assert ey < 1e-1 and ex < 1e-1, (ey, ex)
     assert eg[worst] < 2e-1, (worst, eg[worst])
