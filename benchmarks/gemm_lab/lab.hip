@@ -178,6 +178,322 @@ __global__ __launch_bounds__(WM * WN * 64) void kk_kernel(P p) {
     }
 }
 
+// Pipelined variant: the fragments of the next half-step (KSPLIT 1) or next K step (KSPLIT 2) are read while the
+// current MFMAs run; one barrier per K step, placed where the next stage must become visible; the freed slot (stage
+// kt - 1) is refilled right after it (NST - 1 stages issued ahead).
+//   KSPLIT 1: WM x WN waves each own (BM/WM) x (BN/WN) and process both 32-deep halves of every stage.
+//   KSPLIT 2: the waves form two groups of WM x WN; group g processes half g of every stage (wave tile twice as big
+//             for the same wave count: fewer LDS reads per MFMA); the groups' partial sums are added through LDS.
+// MODE bits: 1 load-only, 2 compute-only, 8 no stores, 32 s_setprio(1) around the MFMAs, 64 DMA interleaved.
+template <int BM, int BN, int WM, int WN, int KSPLIT, int NST, int MODE>
+__global__ __launch_bounds__(WM * WN * KSPLIT * 64) void kk2_kernel(P p) {
+  constexpr int BK = 64, NW = WM * WN * KSPLIT;
+  constexpr int ABY = BM * BK * 2, BBY = BN * BK * 2, STAGE = ABY + BBY;
+  constexpr int AP = ABY / 1024, BPc = BBY / 1024, PIECES = AP + BPc;
+  static_assert(PIECES % NW == 0, "even DMA split");
+  constexpr int PW = PIECES / NW;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  static_assert(NST >= 3, "ring");
+  static_assert(KSPLIT == 1 || BM * (BN + 4) * 4 <= NST * STAGE, "reduction staging fits the ring");
+  __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid / (WM * WN), wl = wid % (WM * WN);
+  const int wm = wl / WN, wn = wl % WN;
+  const int ntn = p.N / BN;
+  const int id = xcd_id(blockIdx.x, gridDim.x);
+  const int tm = id / ntn, tn = id % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const __amdgpu_buffer_rsrc_t ra = mk_rsrc(p.A, p.abytes), rb = mk_rsrc(p.B, p.bbytes);
+  unsigned off[PW];
+  int ldsoff[PW];
+  bool isA[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int q = wid + NW * i;
+    const bool a = q < AP;
+    const int qq = a ? q : q - AP;
+    const int r = qq * 8 + (lane >> 3), c = slot64(r, lane & 7);
+    const int lim = a ? p.M : p.N;
+    const int row = (a ? m0 : n0) + r < lim ? (a ? m0 : n0) + r : lim - 1;
+    off[i] = (unsigned)(((long)row * p.K + 8 * c) * 2);
+    ldsoff[i] = (a ? 0 : ABY) + qq * 1024;
+    isA[i] = a;
+  }
+  const int nk = p.K / BK;
+  auto issue_piece = [&](int kt, int i) {
+    dma16(isA[i] ? ra : rb, lds + (kt % NST) * STAGE + ldsoff[i], off[i] + kt * (BK * 2));
+  };
+  auto issue = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i) issue_piece(kt, i);
+  };
+  auto frag = [&](const char* img, int row0, int kk) {
+    const int r = row0 + (lane & 15), c = (kk >> 3) + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + r * 128 + 16 * slot64(r, c));
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][FM], bfr[2][FN];
+  auto read = [&](int buf, int kt, int sub) {
+    const char* sa = lds + (kt % NST) * STAGE;
+    const char* sb = sa + ABY;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[buf][j] = frag(sb, wn * FN * 16 + 16 * j, 32 * sub);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[buf][i] = frag(sa, wm * FM * 16 + 16 * i, 32 * sub);
+  };
+  auto mma = [&](int buf, bool dma, int kt_dma) {
+    if constexpr (MODE & 32) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
+      if constexpr (MODE & 64) {
+#pragma unroll
+        for (int q = 0; q < PW; ++q)
+          if (i == (q * FM) / PW && dma) issue_piece(kt_dma, q);
+      }
+    }
+    if constexpr (MODE & 32) __builtin_amdgcn_s_setprio(0);
+  };
+  // wait until stage s is complete given the stages issued so far (up to `last`)
+  auto wait_stage = [&](int s, int last) {
+    const int younger = min(NST - 2, last - s);
+    if (younger >= 3) vm_wait<3 * PW>();
+    else if (younger == 2) vm_wait<2 * PW>();
+    else if (younger == 1) vm_wait<PW>();
+    else vm_wait<0>();
+  };
+  constexpr bool LOADS = !(MODE & 2), MATH = !(MODE & 1);
+  int last = -1;
+  if constexpr (LOADS) {
+    for (int s = 0; s < NST - 1 && s < nk; ++s) issue(s);
+    last = min(NST - 2, nk - 1);
+    wait_stage(0, last);
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if constexpr (MATH) read(0, 0, KSPLIT == 1 ? 0 : grp);
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    const int kn = kt + NST - 1;                 // the stage that refills slot (kt - 1) after this step's barrier
+    const bool pf = LOADS && kn < nk;
+    if constexpr (KSPLIT == 1) {
+      if constexpr (MATH) {
+        read(1, kt, 1);
+        mma(0, false, 0);
+      }
+      if (more) {
+        if constexpr (LOADS) wait_stage(kt + 1, last);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (!(MODE & 64) || !MATH) {
+          if (pf) issue(kn);
+        }
+        if (pf) last = kn;
+        if constexpr (MATH) read(0, kt + 1, 0);
+      }
+      if constexpr (MATH) mma(1, (MODE & 64) && pf, kn);
+    } else {
+      // two K steps per iteration so the fragment buffers are compile-time indexed (a run-time index sends them
+      // to scratch)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = kt + u;
+        if (k < nk) {
+          const bool mr = k + 1 < nk;
+          const int kn2 = k + NST - 1;
+          const bool pf2 = LOADS && kn2 < nk;
+          if (mr) {
+            if constexpr (LOADS) wait_stage(k + 1, last);
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (!(MODE & 64) || !MATH) {
+              if (pf2) issue(kn2);
+            }
+            if (pf2) last = kn2;
+            if constexpr (MATH) read(1 - u, k + 1, grp);
+          }
+          if constexpr (MATH) mma(u, (MODE & 64) && pf2, kn2);
+        }
+      }
+      ++kt;
+    }
+  }
+  if constexpr (KSPLIT == 2) {
+    // group 1 stages its partial sums in LDS (the ring is free once every wave passed this barrier)
+    __syncthreads();
+    float* st = reinterpret_cast<float*>(lds);
+    constexpr int EPS = BN + 4;
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            st[(wm * FM * 16 + 16 * i + 4 * (lane >> 4) + e) * EPS + wn * FN * 16 + 16 * j + (lane & 15)] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (grp == 1) return;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc[i][j][e] += st[(wm * FM * 16 + 16 * i + 4 * (lane >> 4) + e) * EPS + wn * FN * 16 + 16 * j + (lane & 15)];
+  }
+  if constexpr (MODE & 8) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) t += acc[i][j][0] + acc[i][j][3];
+    if (t == -1234.5f) p.C[tid] = (bf16)t;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * FN * 16 + 16 * j + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * FM * 16 + 16 * i + 4 * (lane >> 4) + e;
+        if (m < p.M) p.C[(long)m * p.N + n] = (bf16)acc[i][j][e];
+      }
+    }
+}
+
+// Warp-specialised loading: NC = WM x WN compute waves (the KSPLIT-1 pipelined loop, no VMEM at all) + NL loader waves
+// that only issue the LDS-DMA, wait for it and join the one barrier per K step.
+template <int BM, int BN, int WM, int WN, int NL, int NST, int MODE>
+__global__ __launch_bounds__((WM * WN + NL) * 64) void kk3_kernel(P p) {
+  constexpr int BK = 64, NC = WM * WN;
+  constexpr int ABY = BM * BK * 2, BBY = BN * BK * 2, STAGE = ABY + BBY;
+  constexpr int AP = ABY / 1024, BPc = BBY / 1024, PIECES = AP + BPc;
+  static_assert(PIECES % NL == 0, "even DMA split");
+  constexpr int PW = PIECES / NL;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntn = p.N / BN;
+  const int id = xcd_id(blockIdx.x, gridDim.x);
+  const int tm = id / ntn, tn = id % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = p.K / BK;
+  if (wid >= NC) {
+    const int lw = wid - NC;
+    const __amdgpu_buffer_rsrc_t ra = mk_rsrc(p.A, p.abytes), rb = mk_rsrc(p.B, p.bbytes);
+    unsigned off[PW];
+    int ldsoff[PW];
+    bool isA[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int q = lw + NL * i;
+      const bool a = q < AP;
+      const int qq = a ? q : q - AP;
+      const int r = qq * 8 + (lane >> 3), c = slot64(r, lane & 7);
+      const int lim = a ? p.M : p.N;
+      const int row = (a ? m0 : n0) + r < lim ? (a ? m0 : n0) + r : lim - 1;
+      off[i] = (unsigned)(((long)row * p.K + 8 * c) * 2);
+      ldsoff[i] = (a ? 0 : ABY) + qq * 1024;
+      isA[i] = a;
+    }
+    auto issue = [&](int kt) {
+#pragma unroll
+      for (int i = 0; i < PW; ++i)
+        dma16(isA[i] ? ra : rb, lds + (kt % NST) * STAGE + ldsoff[i], off[i] + kt * (BK * 2));
+    };
+    auto wait_stage = [&](int s, int last) {
+      const int younger = min(NST - 2, last - s);
+      if (younger >= 3) vm_wait<3 * PW>();
+      else if (younger == 2) vm_wait<2 * PW>();
+      else if (younger == 1) vm_wait<PW>();
+      else vm_wait<0>();
+    };
+    for (int s = 0; s < NST - 1 && s < nk; ++s) issue(s);
+    int last = min(NST - 2, nk - 1);
+    wait_stage(0, last);
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt + 1 < nk; ++kt) {
+      wait_stage(kt + 1, last);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int kn = kt + NST - 1;
+      if (kn < nk) {
+        issue(kn);
+        last = kn;
+      }
+    }
+    return;
+  }
+  const int wm = wid / WN, wn = wid % WN;
+  auto frag = [&](const char* img, int row0, int kk) {
+    const int r = row0 + (lane & 15), c = (kk >> 3) + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + r * 128 + 16 * slot64(r, c));
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][FM], bfr[2][FN];
+  auto read = [&](int buf, int kt, int sub) {
+    const char* sa = lds + (kt % NST) * STAGE;
+    const char* sb = sa + ABY;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[buf][j] = frag(sb, wn * FN * 16 + 16 * j, 32 * sub);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[buf][i] = frag(sa, wm * FM * 16 + 16 * i, 32 * sub);
+  };
+  auto mma = [&](int buf) {
+    if constexpr (MODE & 32) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
+    if constexpr (MODE & 32) __builtin_amdgcn_s_setprio(0);
+  };
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read(0, 0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    read(1, kt, 1);
+    mma(0);
+    if (kt + 1 < nk) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      read(0, kt + 1, 0);
+    }
+    mma(1);
+  }
+  if constexpr (MODE & 8) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) t += acc[i][j][0] + acc[i][j][3];
+    if (t == -1234.5f) p.C[tid] = (bf16)t;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * FN * 16 + 16 * j + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * FM * 16 + 16 * i + 4 * (lane >> 4) + e;
+        if (m < p.M) p.C[(long)m * p.N + n] = (bf16)acc[i][j][e];
+      }
+    }
+}
+
 __global__ void ref_kernel(const bf16* A, const bf16* B, float* C, int M, int N, int K) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)M * N) return;
@@ -233,8 +549,79 @@ void run(const char* name, P p) {
          2.0 * p.M * p.N * p.K / us / 1e6, 2.0 * p.M * p.N * p.K / us / 1e6 / 2500, maxerr);
 }
 
+template <int BM, int BN, int WM, int WN, int KS, int NST, int MODE>
+void run2(const char* name, P p) {
+  auto kfn = kk2_kernel<BM, BN, WM, WN, KS, NST, MODE>;
+  const int tiles = ((p.M + BM - 1) / BM) * (p.N / BN);
+  dim3 g(tiles), b(WM * WN * KS * 64);
+  hipLaunchKernelGGL(kfn, g, b, 0, 0, p);
+  CK(hipDeviceSynchronize());
+  double maxerr = -1;
+  if (!(MODE & 11)) {
+    std::vector<bf16> c((size_t)p.M * p.N);
+    CK(hipMemcpy(c.data(), p.C, c.size() * 2, hipMemcpyDeviceToHost));
+    double num = 0, den = 0;
+    for (size_t i = 0; i < c.size(); ++i) {
+      const double d = (double)(float)c[i] - g_ref[i];
+      num += d * d; den += (double)g_ref[i] * g_ref[i];
+    }
+    maxerr = sqrt(num / den);
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  std::vector<float> ts;
+  for (int r = 0; r < 7; ++r) {
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(kfn, g, b, 0, 0, p);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    ts.push_back(ms * 1000.f / 20);
+  }
+  std::sort(ts.begin(), ts.end());
+  const double us = ts[3];
+  printf("%-44s tiles %4d  %8.2f us  %6.0f TF/s  %.3f of peak  relL2 %.2e\n", name, tiles, us,
+         2.0 * p.M * p.N * p.K / us / 1e6, 2.0 * p.M * p.N * p.K / us / 1e6 / 2500, maxerr);
+}
+
+template <int BM, int BN, int WM, int WN, int NL, int NST, int MODE>
+void run3(const char* name, P p) {
+  auto kfn = kk3_kernel<BM, BN, WM, WN, NL, NST, MODE>;
+  const int tiles = ((p.M + BM - 1) / BM) * (p.N / BN);
+  dim3 g(tiles), b((WM * WN + NL) * 64);
+  hipLaunchKernelGGL(kfn, g, b, 0, 0, p);
+  CK(hipDeviceSynchronize());
+  double maxerr = -1;
+  if (!(MODE & 11)) {
+    std::vector<bf16> c((size_t)p.M * p.N);
+    CK(hipMemcpy(c.data(), p.C, c.size() * 2, hipMemcpyDeviceToHost));
+    double num = 0, den = 0;
+    for (size_t i = 0; i < c.size(); ++i) {
+      const double d = (double)(float)c[i] - g_ref[i];
+      num += d * d; den += (double)g_ref[i] * g_ref[i];
+    }
+    maxerr = sqrt(num / den);
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  std::vector<float> ts;
+  for (int r = 0; r < 7; ++r) {
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(kfn, g, b, 0, 0, p);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    ts.push_back(ms * 1000.f / 20);
+  }
+  std::sort(ts.begin(), ts.end());
+  const double us = ts[3];
+  printf("%-44s tiles %4d  %8.2f us  %6.0f TF/s  %.3f of peak  relL2 %.2e\n", name, tiles, us,
+         2.0 * p.M * p.N * p.K / us / 1e6, 2.0 * p.M * p.N * p.K / us / 1e6 / 2500, maxerr);
+}
+
 int main(int argc, char** argv) {
   if (argc > 1) K = atoi(argv[1]);
+  if (argc > 2) N = atoi(argv[2]);
   bf16 *A, *B, *C;
   float* R;
   CK(hipMalloc(&A, (size_t)M * K * 2));
@@ -249,25 +636,15 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(g_ref.data(), R, g_ref.size() * 4, hipMemcpyDeviceToHost));
   P p{A, B, C, M, N, K, (unsigned)((size_t)M * K * 2), (unsigned)((size_t)N * K * 2)};
   printf("M %d N %d K %d\n", M, N, K);
-  // the shipped structure: 192 x 128, 8 waves of 96 x 32, 4-deep ring, 3 stages in flight
-  run<192, 128, 2, 4, 4, 3, 0>("192x128 8w(96x32) ring4 pref3", p);
-  run<192, 128, 2, 4, 4, 3, 8>("  .. no stores", p);
-  run<192, 128, 2, 4, 4, 3, 1>("  .. load only", p);
-  run<192, 128, 2, 4, 4, 3, 2>("  .. compute only", p);
-  run<192, 128, 2, 4, 4, 3, 4>("  .. DMA interleaved", p);
-  run<192, 128, 2, 4, 4, 2, 0>("192x128 8w ring4 pref2", p);
-  run<192, 128, 2, 4, 4, 2, 4>("  .. DMA interleaved", p);
-  run<192, 128, 2, 4, 4, 2, 1>("  .. load only", p);
-  // 4 waves of 96 x 64 (one per SIMD)
-  run<192, 128, 2, 2, 4, 3, 0>("192x128 4w(96x64) ring4 pref3", p);
-  run<192, 128, 2, 2, 4, 3, 4>("  .. DMA interleaved", p);
-  run<192, 128, 2, 2, 4, 3, 2>("  .. compute only", p);
-  run<192, 128, 2, 2, 4, 3, 1>("  .. load only", p);
-  // bigger tiles (fewer than 256 workgroups at N = 512): load density vs fill
-  run<256, 256, 2, 4, 2, 1, 0>("256x256 8w(128x64) ring2 pref1", p);
-  run<256, 256, 2, 4, 2, 1, 1>("  .. load only", p);
-  run<256, 256, 2, 4, 2, 1, 2>("  .. compute only", p);
-  run<128, 128, 2, 2, 4, 3, 0>("128x128 4w(64x64) ring4 pref3", p);
-  run<128, 128, 2, 2, 4, 3, 1>("  .. load only", p);
+  run<192, 128, 2, 4, 4, 3, 0>("old 192x128 8w(96x32) ring4", p);
+  run3<192, 128, 2, 4, 4, 4, 0>("ws 8c(96x32)+4L ring4", p);
+  run3<192, 128, 2, 4, 4, 4, 8>("  .. no stores", p);
+  run3<192, 128, 2, 2, 4, 4, 0>("ws 4c(96x64)+4L ring4", p);
+  run3<192, 128, 2, 2, 4, 4, 8>("  .. no stores", p);
+  run3<256, 128, 4, 2, 4, 3, 0>("ws 256x128 8c(64x64)+4L ring3", p);
+  run3<256, 128, 4, 2, 4, 3, 8>("  .. no stores", p);
+  run3<256, 128, 2, 2, 4, 3, 8>("ws 256x128 4c(128x64)+4L ring3 no stores", p);
+  run3<128, 128, 2, 2, 4, 4, 0>("ws 128x128 4c(64x64)+4L ring4", p);
+  run3<128, 128, 2, 2, 4, 4, 8>("  .. no stores", p);
   return 0;
 }

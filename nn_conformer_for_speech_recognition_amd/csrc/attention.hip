@@ -262,87 +262,6 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
   if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
 }
 
-// Forward, whole head staged by LDS-DMA (dk = 64, 16-B aligned rows): every wave first issues the 4 pieces
-// of its own 32 query rows, then its share of the K/V pieces in key-tile order (tile kt = K pieces 8kt..8kt+7
-// then V pieces 8kt..8kt+7; piece P of that sequence goes to wave P mod nw).  Nothing passes through VGPRs,
-// so the whole head (up to 144 KiB with Q) is in flight at once and tile kt's MFMAs start as soon as its
-// pieces have landed: per tile one counted vmcnt (this wave's pieces of tiles <= kt) + one s_barrier.
-// Same arithmetic, order and dropout as attn_fwd_head_kernel (bit-identical outputs).
-__global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_dma_kernel(AttnM p, bf16* __restrict__ o,
-                                                                                float* __restrict__ lse) {
-  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
-  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
-  const float dkeep = drop_keep_scale(dthr);
-  extern __shared__ __attribute__((aligned(1024))) char hsb[];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
-  const int nw = blockDim.x >> 6;
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
-  const int len = p.len[b];
-  const int nkt = (len + TILE - 1) / TILE, Tq = nw * 32;
-  char* sQ = hsb;                          // [Tq][128 B]
-  char* sK = sQ + Tq * 128;                // [nkt * 64][128 B]
-  char* sV = sK + nkt * TILE * 128;
-  const bf16* base = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
-  const long ext = ((long)p.T * p.D3 - h * p.dk) * 2;
-  const __amdgpu_buffer_rsrc_t rq = head_rsrc(base, ext), rk = head_rsrc(base + p.HD, ext - 2L * p.HD),
-                               rv = head_rsrc(base + 2 * p.HD, ext - 4L * p.HD);
-  const int q0 = wv * 32;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) head_dma_piece(rq, sQ, 4 * wv + i, p.D3, p.T, lane);   // own query rows first
-  const int npc = 16 * nkt;                // K/V pieces in tile order
-  int issued = 0;
-  for (int P = wv; P < npc; P += nw, ++issued) {
-    const int kt = P >> 4, i = P & 15;
-    if (i < 8) head_dma_piece(rk, sK, 8 * kt + i, p.D3, p.T, lane);
-    else head_dma_piece(rv, sV, 8 * kt + i - 8, p.D3, p.T, lane);
-  }
-  wait_vm_n(issued);                       // own Q rows landed (wave-private: no barrier)
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = hfrag(sQ, q0, 16 * s, lane);
-  f32x16 o0 = (f32x16){0}, o1 = (f32x16){0};
-  float m = -INFINITY, l = 0.f;
-  const float c = p.scale * LOG2E;
-  const int qi = q0 + (lane & 31);
-  const bool pm = p.drop_p > 0.f && p.qm;
-  uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const uint32_t wcur = wnext;
-    if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
-    const int last = 16 * kt + 15;         // this wave's pieces of tiles <= kt: P = wv + j nw <= last
-    const int done = last >= wv ? min(issued, (last - wv) / nw + 1) : 0;
-    wait_vm_n(issued - done);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const char* tK = sK + kt * TILE * 128;
-    const char* tV = sV + kt * TILE * 128;
-    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hfrag(tK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
-      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hfrag(tK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
-    }
-    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey, wcur);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
-        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(htrfrag(tV, 32 * t + 16 * s, 0, lane), pf, o0, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(htrfrag(tV, 32 * t + 16 * s, 32, lane), pf, o1, 0, 0, 0);
-      }
-    }
-  }
-  wait_vm_n(0);
-  __syncthreads();     // every wave is done with the images: they become the epilogue staging
-  float* stage = reinterpret_cast<float*>(hsb) + wv * 32 * 65;
-  const float inv = 1.f / l;
-  if (q0 < p.T)
-    store_transposed(stage, o0, o1, inv, o + (long)b * p.T * p.HD + h * p.dk, p.HD, q0, min(32, p.T - q0), p.dk,
-                     lane);
-  if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
-}
-
 // dQ: grid (B*H), block 64 * ceil(T/32); K and V staged whole
 __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(AttnM p, const bf16* __restrict__ dout,
                                                                                const float* __restrict__ lse,
@@ -965,13 +884,6 @@ __global__ __launch_bounds__(256) void attn_dropmask_kernel(AttnM p, uint32_t* _
   qm[((long)(bh * g.nkt + kt) * g.Tq) * 2 + f] = w;
 }
 
-// Q rows of every wave + K and V of the padded length; the epilogue staging aliases them
-size_t head_dma_lds_bytes(int T) {
-  const size_t img = ((size_t)cdiv(T, 32) * 32 + 2 * (size_t)cdiv(T, TILE) * TILE) * 128;
-  const size_t stage = (size_t)cdiv(T, 32) * 32 * 65 * sizeof(float);
-  return img > stage ? img : stage;
-}
-
 }  // namespace
 
 CFM_EXPORT size_t cfm_attn_dropmask_bytes(int B, int T, int H) {
@@ -1026,13 +938,6 @@ static int attn_fwd_impl(const void* qkv, void* o, float* lse, const int32_t* le
           ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 6,
           cfm::g_rng_salt};
   if (use_head(T)) set_mask(p, mask);     // the whole-head kernels read the bits; the tiled ones hash
-  if (use_head(T) && p.vec && dk == DKP && (g_attn_mode & 32)) {
-    // LDS-DMA staging (cfm_attn_set_mode bit 5; measured no faster than register staging at T = 373:
-    // profiles/r03/attn_fwd_dma_ab.txt)
-    hipLaunchKernelGGL(attn_fwd_head_dma_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), head_dma_lds_bytes(T), s, p,
-                       (bf16*)o, lse);
-    return cfm::check_launch("cfm_attn_fwd");
-  }
   if (use_head(T)) {
     // LDS sized for the full padded length (lengths are device data; len <= T)
     hipLaunchKernelGGL(attn_fwd_head_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), head_lds_bytes(T), s, p, (bf16*)o,

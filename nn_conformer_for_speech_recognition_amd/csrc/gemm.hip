@@ -509,10 +509,12 @@ template <bool M16> __device__ __forceinline__ int accc(int r, int lane) {
   return M16 ? 16 * ((r >> 2) & 1) + (lane & 15) : (lane & 31);
 }
 
-template <int FM, int FN, int WM, int WN, int NTt, int BNt = BN, bool M16 = false>
+template <int FM, int FN, int WM, int WN, int NTt, int BNt = BN, bool M16 = false, int ROWS = 128>
 __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM][FN], float* st, int z, int zs,
                                                 int m0, int n0, int wm, int wn, int lane, int tid) {
-  constexpr int BAND = FM * 32, CHB = (128 / BAND) >= 1 && WM % (128 / BAND) == 0 ? 128 / BAND : 1;
+  // ROWS: the staging rows `st` holds (ROWS x (BNt + 4) floats)
+  constexpr int BAND = FM * 32, CHB = (ROWS / BAND) >= 1 && WM % (ROWS / BAND) == 0 ? ROWS / BAND : 1;
+  static_assert(BAND <= ROWS, "one wave band fits the staging");
   constexpr int RC = CHB * BAND;
   constexpr int EPS = BNt + 4;         // staging row stride (floats): = 4 mod 32 for both widths
   constexpr int CPW = BNt / 8;         // 8-column chunks per row
@@ -530,7 +532,8 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
         }
     return;
   }
-#pragma unroll
+  // (one pass per band chunk; not unrolled -- the epilogue body is large and nothing in it is indexed by hf)
+#pragma nounroll
   for (int hf = 0; hf < WM / CHB; ++hf) {
     if (wm / CHB == hf) {
 #pragma unroll
@@ -936,7 +939,8 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     if constexpr (!AK) {
       if (acs) {
 #pragma unroll
-        for (int k = acs_r; k < BKt; k += RG) {
+        for (int kq = 0; kq < BKt / RG; ++kq) {
+          const int k = acs_r + kq * RG;
           const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + k * (BMt * 2) + 16 * (acs_c ^ (4 * (k & 3))));
 #pragma unroll
           for (int e = 0; e < 8; ++e) csum[e] += (float)v[e];
@@ -987,395 +991,168 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   probe_end(p.probe);
 }
 
-extern int g_gemm_mode;
-// ---------------------------------------------------------------- persistent, register-deferred epilogue
-// For the encoder's wide-output, short-reduction GEMMs (K = 512; N = 1024-2048: FFN up-projection with its
-// bias + SiLU + dropout + pre-activation epilogue, QKV and pointwise-conv-1 forward), whose store traffic
-// (up to 98 MB per launch) left the MFMAs idle through every tile's epilogue.  One workgroup per CU walks
-// a contiguous, XCD-local range of 256 x 128 tiles and the K steps of ALL its tiles form one continuous
-// LDS-DMA stage stream (3-deep ring, BK 64: the next tile's first stages load during the current tile's
-// last steps).  The product is computed TRANSPOSED (16x16x32 MFMA with the weight rows as the A operand),
-// so each lane holds 4 consecutive output columns of one row: a finished tile's accumulators are copied to
-// a second register set and its epilogue -- bias from LDS, SiLU, dropout, bf16 packing, 8-byte range-
-// checked buffer stores -- runs two 16x16 blocks per K step INSIDE the next tile's main loop.  Every K step
-// issues the same number of vector-memory ops (dummy out-of-range DMA / stores where there is nothing to
-// move), so each wait is one compile-time `vmcnt`.  No LDS staging, no barrier for the epilogue.
-constexpr int PS_BM = 256, PS_BN = 128, PS_BK = 64, PS_NK = 8, PS_NST = 3;
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-
-template <bool PRE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-void gemm_pers_kernel(GemmP p, PipeOp oa, PipeOp ob, int ntm, int ntn, int tper) {
-  constexpr int BMt = PS_BM, BNt = PS_BN, BKt = PS_BK, NK = PS_NK, NST = PS_NST, NWV = 8;
+// ---------------------------------------------------------------- warp-specialised K-major GEMM
+// For the encoder's d-wide outputs (one BMt x 128 tile per CU, K up to 2048): NL loader waves only issue the
+// LDS-DMA of the ring's stages, wait for it (their vmcnt counts nothing else) and join the one barrier per K step;
+// the WM x WN compute waves never touch vector memory in the main loop, so no stage wait ever stalls an MFMA wave
+// and no DMA issue sits between its MFMAs.  The compute waves read the next half-step's fragments (16x16x32 MFMA,
+// conflict-free ds_read_b128 from the source-swizzled image) while the current half-step's MFMAs run; the barrier
+// sits where the next stage must become visible, and the slot of stage kt - 1 is refilled right after it (NST - 1
+// stages issued ahead).  Gemm lab (benchmarks/gemm_lab, M 11,936 N 512 K 2048, naive stores): 33.9 -> 27.0 us.
+// Epilogue: the whole f32 tile staged in the ring's LDS, then every wave (loaders included) finishes 8-column
+// chunks through epilogue_store8 (+ rowdot), as tile_epilogue_g does.
+template <int BMt, int WM, int WN, int NL, int NST>
+__global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, PipeOp oa, PipeOp ob) {
+  constexpr int BKt = 64, BNt = BN, NC = WM * WN, NTt = (NC + NL) * 64;
   constexpr int ABYTES = BMt * BKt * 2, BBYTES = BNt * BKt * 2, STAGE = ABYTES + BBYTES;
-  constexpr int AP = ABYTES / 1024 / NWV, BP = BBYTES / 1024 / NWV;     // DMA pieces per wave per stage (4, 2)
-  constexpr int P = AP + BP;
-  constexpr int SB = PRE ? 2 : 1;       // stores per epilogue block
-  constexpr int S = 2 * SB;             // stores per K step (two 16x16 blocks)
-  static_assert(AP * NWV * 1024 == ABYTES && BP * NWV * 1024 == BBYTES, "whole DMA pieces per wave");
-  constexpr int RING = NST * STAGE;
-  __shared__ __attribute__((aligned(1024))) char lds[RING + 2048 * 4];
-  float* sbias = reinterpret_cast<float*>(lds + RING);
+  constexpr int AP = ABYTES / 1024, BP = BBYTES / 1024, PW = (AP + BP) / NL;
+  static_assert(PW * NL == AP + BP && AP * 1024 == ABYTES && BP * 1024 == BBYTES, "whole DMA pieces per loader");
+  constexpr int FM = BMt / WM / 16, FN = BNt / WN / 16;
+  static_assert(FM * WM * 16 == BMt && FN * WN * 16 == BNt, "wave tiling");
+  constexpr int EPS = BNt + 4, CPW = BNt / 8;
+  constexpr int RING = NST * STAGE, EPI = BMt * EPS * 4;
+  static_assert(NST >= 3 && NST <= 5, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char lds[RING > EPI ? RING : EPI];
   probe_begin(p.probe);
   gemm_drop_prep(p);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;            // 4 x 2 waves of 64 (m) x 64 (n)
-  const int ntiles = ntm * ntn, GW = gridDim.x, Lb = blockIdx.x;
-  const int pos = (GW % 8 == 0) ? (Lb & 7) * (GW / 8) + (Lb >> 3) : Lb;   // XCD-contiguous tile ranges
-  const int t_begin = min(pos * tper, ntiles), t_end = min(t_begin + tper, ntiles);
-  const int ntl = t_end - t_begin;
-  // bias of every output column in LDS for the whole launch (N <= 2048)
-  for (int c = tid; c < p.N; c += 512) sbias[c] = p.bias ? p.bias[c] : 0.f;
-  __syncthreads();
-  if (ntl <= 0) return;
-  const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, 0), rb = pipe_rsrc(ob, 0);
-  const int crec = __builtin_amdgcn_readfirstlane((int)((long)p.M * p.ldc * 2));
-  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, crec, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(PRE ? p.pre : p.C, (short)0, crec, 0x00020000);
-
-  // per-lane DMA source offsets of a tile's stage 0 (later stages add kt * 128 B)
-  auto tile_offs = [&](int t, unsigned (&oA)[AP], unsigned (&oB)[BP]) {
-    const int tm = t / ntn, tn = t % ntn;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int tm, tn, zz;
+  xcd_tile3(tm, tn, zz);
+  const int m0 = tm * BMt, n0 = tn * BNt;
+  const int z = zz;                       // split_k == 1: the batch index
+  const int nk = p.K / BKt;
+  f32x4 acc[FM][FN];
 #pragma unroll
-    for (int i = 0; i < AP; ++i) oA[i] = pipe_src<true, BMt, BKt>(oa, (i * NWV + wid) * 64 + lane, tm * BMt, 0);
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int i = 0; i < BP; ++i) oB[i] = pipe_src<true, BNt, BKt>(ob, (i * NWV + wid) * 64 + lane, tn * BNt, 0);
-  };
-  auto issue = [&](int slot, const unsigned (&oA)[AP], const unsigned (&oB)[BP], int kt, bool real) {
-    char* sa = lds + slot * STAGE;
-    char* sb = sa + ABYTES;
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (wid >= NC) {
+    // ---- loader waves
+    const int lw = wid - NC;
+    const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, z), rb = pipe_rsrc(ob, z);
+    unsigned off[PW];
+    int ldo[PW];
+    bool isa[PW];
 #pragma unroll
-    for (int i = 0; i < AP; ++i) dma16(ra, sa + (i * NWV + wid) * 1024, real ? oA[i] + kt * (BKt * 2) : 0xFFFFFF00u);
-#pragma unroll
-    for (int i = 0; i < BP; ++i) dma16(rb, sb + (i * NWV + wid) * 1024, real ? oB[i] + kt * (BKt * 2) : 0xFFFFFF00u);
-  };
-
-  // epilogue of block b (0..15: jn = b >> 2 over n, im = b & 3 over m) of a finished tile held in `a`
-  // (transposed 16x16 layout: register q <-> column n0w + 16 jn + 4 (lane >> 4) + q, row m0w + 16 im + (lane & 15))
-  auto epi_block = [&](const f32x4& a, int m0w, int n0w, int jn, int im, bool real) {
-    const int n = n0w + 16 * jn + 4 * (lane >> 4), m = m0w + 16 * im + (lane & 15);
-    float v[4] = {a[0], a[1], a[2], a[3]};
-    const float4 bs = *reinterpret_cast<const float4*>(sbias + n);
-    v[0] = v[0] * p.alpha + bs.x; v[1] = v[1] * p.alpha + bs.y; v[2] = v[2] * p.alpha + bs.z; v[3] = v[3] * p.alpha + bs.w;
-    const unsigned off = (real && !(p.dbg & 16)) ? (unsigned)(((long)m * p.ldc + n) * 2) : 0xFFFFFFF0u;
-    if constexpr (PRE) {
-      bf16x4 pv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) pv[e] = (bf16)v[e];
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, pv), rp, off, 0, 0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = silu_f(v[e]);
+    for (int i = 0; i < PW; ++i) {
+      const int q = lw + NL * i;
+      isa[i] = q < AP;
+      const int qq = isa[i] ? q : q - AP;
+      off[i] = isa[i] ? pipe_src<true, BMt, BKt>(oa, qq * 64 + lane, m0, 0)
+                      : pipe_src<true, BNt, BKt>(ob, qq * 64 + lane, n0, 0);
+      ldo[i] = (isa[i] ? 0 : ABYTES) + qq * 1024;
     }
-    if (p.drop_p > 0.f) {   // the epilogue_store8 keying: pair (n, n+1) of row m shares one 32-bit hash
-      const uint32_t j0 = (uint32_t)((p.doff + (uint64_t)((long)m * p.N + n)) >> 1);
-      const uint32_t h0 = cfm_mix32(j0 ^ p.dkey0), h1 = cfm_mix32((j0 + 1) ^ p.dkey0);
-      v[0] *= (h0 & 0xFFFFu) >= p.dthr ? p.dkeep : 0.f;
-      v[1] *= (h0 >> 16) >= p.dthr ? p.dkeep : 0.f;
-      v[2] *= (h1 & 0xFFFFu) >= p.dthr ? p.dkeep : 0.f;
-      v[3] *= (h1 >> 16) >= p.dthr ? p.dkeep : 0.f;
-    }
-    bf16x4 cv;
+    auto issue = [&](int kt) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) cv[e] = (bf16)(v[e] * p.out_scale);
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, cv), rc, off, 0, 0);
-  };
-
-  f32x4 acc[4][4], prv[4][4];   // [jn][im]
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = prv[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  int pm0w = 0, pn0w = 0;
-  bool pend = false;
-  unsigned cA[AP], cB[BP], nA[AP], nB[BP];
-  tile_offs(t_begin, cA, cB);
-  if (ntl > 1) tile_offs(t_begin + 1, nA, nB);
-  else {
-#pragma unroll
-    for (int i = 0; i < AP; ++i) nA[i] = cA[i];
-#pragma unroll
-    for (int i = 0; i < BP; ++i) nB[i] = cB[i];
-  }
-  // prologue: stages 0, 1 of the first tile, each followed by S dropped stores (uniform vmcnt accounting)
-  const u32x2_t zero2 = {0u, 0u};
-  issue(0, cA, cB, 0, true);
-  asm volatile("" ::: "memory");
-#pragma unroll
-  for (int s2 = 0; s2 < S; ++s2) __builtin_amdgcn_raw_buffer_store_b64(zero2, rc, 0xFFFFFFF0u, 0, 0);
-  asm volatile("" ::: "memory");
-  issue(1, cA, cB, 1, true);
-  asm volatile("" ::: "memory");
-#pragma unroll
-  for (int s2 = 0; s2 < S; ++s2) __builtin_amdgcn_raw_buffer_store_b64(zero2, rc, 0xFFFFFFF0u, 0, 0);
-  asm volatile("" ::: "memory");
-
-  int g = 0;    // global stage index of this workgroup (slot = g % NST)
-  for (int lt = 0; lt < ntl; ++lt) {
-    const int t = t_begin + lt;
-    const int m0w = (t / ntn) * BMt + wm * 64, n0w = (t % ntn) * BNt + wn * 64;
-    const bool has_next = lt + 1 < ntl;
-#pragma unroll
-    for (int kt = 0; kt < NK; ++kt, ++g) {
-      // stage g landed once only stores(g-2), DMA(g+1), stores(g-1) are younger than it
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * S + P) : "memory");
+      for (int i = 0; i < PW; ++i)
+        dma16(isa[i] ? ra : rb, lds + (kt % NST) * STAGE + ldo[i], off[i] + kt * (BKt * 2));
+    };
+    // stage s has landed once only the stages issued after it (up to `last`) are outstanding
+    auto wait_stage = [&](int s, int last) {
+      const int younger = min(NST - 2, last - s);
+      if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PW) : "memory");
+      else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    for (int s = 0; s < NST - 1 && s < nk; ++s) issue(s);
+    int last = min(NST - 2, nk - 1);
+    wait_stage(0, last);
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt + 1 < nk; ++kt) {
+      wait_stage(kt + 1, last);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      // DMA of stage g+2: this tile's kt+2, or the next tile's first stages (dropped past the last tile)
-      if (kt + 2 < NK) issue((g + 2) % NST, cA, cB, kt + 2, true);
-      else issue((g + 2) % NST, nA, nB, kt + 2 - NK, has_next);
-      asm volatile("" ::: "memory");   // (issue order = the vmcnt accounting: DMA(g+2) before this step's stores)
-      // two 16x16 epilogue blocks of the previous tile (dropped stores when there is none)
-      epi_block(prv[(2 * kt) >> 2][(2 * kt) & 3], pm0w, pn0w, (2 * kt) >> 2, (2 * kt) & 3, pend);
-      epi_block(prv[(2 * kt + 1) >> 2][(2 * kt + 1) & 3], pm0w, pn0w, (2 * kt + 1) >> 2, (2 * kt + 1) & 3, pend);
-      asm volatile("" ::: "memory");
-      const char* sa = lds + (g % NST) * STAGE;
+      const int kn = kt + NST - 1;          // refills the slot of stage kt - 1 (every wave is past its reads)
+      if (kn < nk) {
+        issue(kn);
+        last = kn;
+      }
+    }
+  } else {
+    // ---- compute waves
+    const int wm = wid / WN, wn = wid % WN;
+    bf16x8 af[2][FM], bfr[2][FN];
+    auto read = [&](bf16x8 (&fa)[FM], bf16x8 (&fb)[FN], int kt, int sub) {
+      const char* sa = lds + (kt % NST) * STAGE;
       const char* sb = sa + ABYTES;
 #pragma unroll
-      for (int q = 0; q < BKt / 32; ++q) {
-        bf16x8 fa[4], fb[4];
+      for (int j = 0; j < FN; ++j) fb[j] = pipe_frag16k<BKt>(sb, wn * FN * 16 + 16 * j, 32 * sub, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = pipe_frag16k<BKt>(sb, wn * 64 + 16 * j, 32 * q, lane);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = pipe_frag16k<BKt>(sa, wm * 64 + 16 * i, 32 * q, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
-      }
-    }
-    // this tile becomes the pending one; the next tile's offsets move up
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        prv[j][i] = acc[j][i];
-        acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      }
-    pm0w = m0w;
-    pn0w = n0w;
-    pend = true;
-#pragma unroll
-    for (int i = 0; i < AP; ++i) cA[i] = nA[i];
-#pragma unroll
-    for (int i = 0; i < BP; ++i) cB[i] = nB[i];
-    if (lt + 2 < ntl) tile_offs(t_begin + lt + 2, nA, nB);
-  }
-  // the last tile's epilogue
-#pragma unroll
-  for (int b = 0; b < 16; ++b) epi_block(prv[b >> 2][b & 3], pm0w, pn0w, b >> 2, b & 3, true);
-  probe_end(p.probe);
-}
-
-// the persistent kernel serves K-major bf16 GEMMs with K == 512, N a multiple of 128 (<= 2048), bf16 output and
-// an epilogue of bias / alpha / (SiLU + pre) / dropout / out_scale only.  Opt-in (cfm_gemm_set_mode bit 15):
-// same-box A/B, FFN up-projection 63.7 -> 56.7 us but QKV 37.8 -> 39.9 us and the L15 step 24.0 -> 24.3 ms
-// (the epilogue's stores and the stage waits share one in-order vmcnt, so a K step that waits for its stage
-// also waits for the previous tile's stores)
-bool pers_ok(const cfm_gemm_desc& d, const GemmP& p) {
-  return (g_gemm_mode & 32768) && d.a_kmajor && d.b_kmajor && d.batch == 1 && p.split_k == 1 && d.K == 512 &&
-         p.N % PS_BN == 0 && p.N <= 2048 && p.N >= 1024 && !p.res && !p.act_grad && !p.cmap && !p.rd_out &&
-         !p.acs_slab && !p.slab && p.dtc == CFM_BF16 && p.ldc % 4 == 0 && (p.act == 0 || (p.act == CFM_ACT_SILU &&
-         p.pre && p.dtpre == CFM_BF16)) && (long)p.M * p.ldc * 2 < (1L << 31) - 64 && !p.dbg &&
-         p.alpha_a == nullptr && p.alpha_b == nullptr && ((uintptr_t)p.C % 8) == 0 &&
-         (p.pre == nullptr || ((uintptr_t)p.pre % 8) == 0) && d.lda == 512 && d.ldb == 512;
-}
-
-// ---------------------------------------------------------------- persistent, interleaved epilogue
-// For K-major bf16 GEMMs whose epilogue loads nothing but the bias (forward projections incl. the FFN
-// up-projection's bias + SiLU + dropout + pre-activation store, and the plain data-gradient GEMMs): one
-// workgroup per CU loops over 192 x 128 tiles (XCD-contiguous tile ranges), and the epilogue of tile i
-// -- staged in its own LDS buffer as f32 -- is stored one 8-column unit per thread per K step INSIDE
-// tile i+1's main loop, so its VALU work and HBM writes overlap the MFMAs instead of following them.
-// The stores are range-checked buffer stores (rows past M are dropped by the hardware, not skipped),
-// so every unit issues exactly E vector-memory ops and the ring's counted vmcnt waits stay exact.
-// Status: bit-identical to the pipeline kernels (test_gemm_interleaved_epilogue_matches_pipeline) but
-// SLOWER on the encoder's shapes (profiles/r02/gemm_ie_ab.txt: its BK-32 single-workgroup main loop loses
-// more than the overlap gains; only the N = 1024 / 1536 SiLU cases won) -- off by default (mode bit 11).
-constexpr int IE_BM = 192, IE_BK = 32, IE_NST = 3, IE_NWV = 8, IE_WN = 4;
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-
-template <int N>
-__device__ __forceinline__ void vm_wait_le() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-
-// wait until at most (stages * PER + stores * E) vector-memory ops are outstanding
-template <int PER, int E>
-__device__ __forceinline__ void ie_wait(int stages, int stores) {
-  const int sel = stages * 3 + stores;   // stages in {0, 1}, stores in {0, 1, 2}
-  switch (sel) {
-    case 0: vm_wait_le<0>(); break;
-    case 1: vm_wait_le<E>(); break;
-    case 2: vm_wait_le<2 * E>(); break;
-    case 3: vm_wait_le<PER>(); break;
-    case 4: vm_wait_le<PER + E>(); break;
-    default: vm_wait_le<PER + 2 * E>(); break;
-  }
-}
-
-template <bool PRE>
-__global__ __launch_bounds__(IE_NWV * 64) void gemm_pipe_ie_kernel(GemmP p, PipeOp oa, PipeOp ob, int ntm, int ntn) {
-  constexpr int BMt = IE_BM, BKt = IE_BK, NST = IE_NST, NWV = IE_NWV, WN = IE_WN;
-  constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BN / WN / 32;
-  constexpr int NTt = NWV * 64, UPT = BMt * 16 / NTt;   // 8-column units per thread per tile (6)
-  constexpr int ABYTES = BMt * BKt * 2, BBYTES = BN * BKt * 2, STAGE = ABYTES + BBYTES;
-  constexpr int AW = ABYTES / 1024, BW = BBYTES / 1024;  // wave-instructions of DMA per stage (12, 8)
-  static_assert(BW == NWV && AW > NWV && AW <= 2 * NWV, "A: every wave one piece, waves < AW-NWV a second");
-  constexpr int E = PRE ? 2 : 1;
-  constexpr int RING = NST * STAGE, STG = BMt * EP_STRIDE * 4;
-  static_assert(UPT * NTt == BMt * 16 && RING + STG + 512 <= 163840, "ie geometry");
-  __shared__ __attribute__((aligned(1024))) char lds[RING + STG + 512];
-  float* st = reinterpret_cast<float*>(lds + RING);
-  float* sbias = reinterpret_cast<float*>(lds + RING + STG);
-  probe_begin(p.probe);
-  gemm_drop_prep(p);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const int ntiles = ntm * ntn, GW = gridDim.x, Lb = blockIdx.x;
-  const int pos = (GW % 8 == 0) ? (Lb & 7) * (GW / 8) + (Lb >> 3) : Lb;   // XCD-contiguous tile ranges
-  const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, 0), rb = pipe_rsrc(ob, 0);
-  // bf16 C (and pre): rows past M fall outside num_records and their stores are dropped
-  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-      p.C, (short)0, __builtin_amdgcn_readfirstlane((int)((long)p.M * p.ldc * 2)), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-      PRE ? p.pre : p.C, (short)0, __builtin_amdgcn_readfirstlane((int)((long)p.M * p.ldc * 2)), 0x00020000);
-  const int nk = (p.K + BKt - 1) / BKt;
-  int pm0 = -1, pn0 = 0;   // pending staged tile (its epilogue runs inside the next main loop)
-
-  // unit j of this thread of the pending tile: 8 consecutive columns of one row -> E buffer stores
-  const bool two = wid < AW - NWV;         // this wave issues a second A piece per stage (wave-uniform)
-  auto unit = [&](int j) {
-    const int u = j * NTt + tid, row = u >> 4, c8 = (u & 15) * 8;
-    const float4 lo = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8);
-    const float4 hi = *reinterpret_cast<const float4*>(st + row * EP_STRIDE + c8 + 4);
-    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    const int m = pm0 + row, n = pn0 + c8;
-    if (p.alpha != 1.f) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
-    }
-    if (p.bias) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += sbias[c8 + e];
-    }
-    const unsigned off = (unsigned)(((long)m * p.ldc + n) * 2);
-    if constexpr (PRE) {
-      bf16x8 pv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) pv[e] = (bf16)v[e];
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, pv), rp,
-                                             (unsigned)(((long)m * p.ldc + n) * 2), 0, 0);
-    }
-    if (p.act == CFM_ACT_SILU) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
-    }
-    if (p.drop_p > 0.f) {
-      const uint64_t base = p.doff + (uint64_t)((long)m * p.N + n);
-      const uint32_t j0 = (uint32_t)(base >> 1);
-      uint32_t h[5];
-#pragma unroll
-      for (int q = 0; q < 5; ++q) h[q] = cfm_mix32((j0 + q) ^ p.dkey0);
-      const int odd = (int)(base & 1);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int q = (odd + e) >> 1;
-        const uint32_t b = ((odd + e) & 1) ? (h[q] >> 16) : (h[q] & 0xFFFFu);
-        v[e] *= b >= p.dthr ? p.dkeep : 0.f;
-      }
-    }
-    if (p.out_scale != 1.f) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
-    }
-    bf16x8 cv;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) cv[e] = (bf16)v[e];
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, cv), rc, off, 0, 0);
-  };
-
-  for (int tile = pos; tile < ntiles; tile += GW) {
-    const int tm = tile / ntn, tn = tile % ntn;
-    const int m0 = tm * BMt, n0 = tn * BN;
-    const unsigned offa0 = pipe_src<true, BMt, BKt>(oa, wid * 64 + lane, m0, 0);
-    const unsigned offa1 = pipe_src<true, BMt, BKt>(oa, ((NWV + wid) * 64 + lane) % (AW * 64), m0, 0);
-    const unsigned offb0 = pipe_src<true, BN, BKt>(ob, wid * 64 + lane, n0, 0);
-    auto issue = [&](int kt) {
-      char* sa = lds + (kt % NST) * STAGE;
-      char* sb = sa + ABYTES;
-      dma16(ra, sa + wid * 1024, offa0 + kt * (BKt * 2));
-      if (two) dma16(ra, sa + (NWV + wid) * 1024, offa1 + kt * (BKt * 2));
-      dma16(rb, sb + wid * 1024, offb0 + kt * (BKt * 2));
+      for (int i = 0; i < FM; ++i) fa[i] = pipe_frag16k<BKt>(sa, wm * FM * 16 + 16 * i, 32 * sub, lane);
     };
-    f32x16 acc[FM][FN];
+    auto mma = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN]) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    };
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read(af[0], bfr[0], 0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      read(af[1], bfr[1], kt, 1);
+      mma(af[0], bfr[0]);
+      if (kt + 1 < nk) {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        read(af[0], bfr[0], kt + 1, 0);
+      }
+      mma(af[1], bfr[1]);
+    }
+  }
+  if (p.dbg & 1) {   // timing experiment: keep the accumulators live, store nothing
+    float t = 0.f;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x16){0};
-    vm_wait_le<0>();   // nothing of the previous tile outstanding: the counted waits below are exact
-#pragma unroll
-    for (int s2 = 0; s2 < NST - 1; ++s2)
-      if (s2 < nk) issue(s2);
-    const bool pend = pm0 >= 0;
-    // unit j of the pending tile runs at K step j (front-loaded: spreading the units over the whole loop
-    // measured slower); short K: the rest after the loop
-    auto unit_at = [&](int k) -> int { return (pend && k >= 0 && k < nk && k < UPT) ? k : -1; };
-    for (int kt = 0; kt < nk; ++kt) {
-      // outstanding after stage kt's DMA: stage kt+1 (issued at kt-1) and the units of kt-1, kt-2
-      const int ys = min(NST - 2, nk - 1 - kt);
-      const int yu = (unit_at(kt - 1) >= 0 ? 1 : 0) + (unit_at(kt - 2) >= 0 ? 1 : 0);
-      if (two) ie_wait<3, E>(ys, yu);
-      else ie_wait<2, E>(ys, yu);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (kt + NST - 1 < nk) issue(kt + NST - 1);
-      const char* sa = lds + (kt % NST) * STAGE;
-      const char* sb = sa + ABYTES;
-      constexpr int KST = BKt / 16;
-      bf16x8 af[KST][FM], bfr[KST][FN];
-#pragma unroll
-      for (int q = 0; q < KST; ++q) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[q][j] = pipe_frag<true, BN, BKt>(sb, wn * FN * 32 + j * 32, 16 * q, lane);
-#pragma unroll
-        for (int i = 0; i < FM; ++i) af[q][i] = pipe_frag<true, BMt, BKt>(sa, wm * FM * 32 + i * 32, 16 * q, lane);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int q = 0; q < KST; ++q)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[q][i], bfr[q][j], acc[i][j], 0, 0, 0);
-      const int uj = unit_at(kt);
-      if (uj >= 0) unit(uj);             // the previous tile's epilogue, spread over the K steps
-    }
-    if (pend)
-      for (int j = nk; j < UPT; ++j) unit(j);   // short K: the rest after the loop
-    __syncthreads();   // ring and staging free (every wave past its last reads)
+      for (int j = 0; j < FN; ++j) t += acc[i][j][0] + acc[i][j][3];
+    if (t == -1234.5f) reinterpret_cast<float*>(p.C)[tid] = t;
+    return;
+  }
+  __syncthreads();   // every DMA landed (the loaders' last wait was vmcnt(0)), every fragment read consumed
+  float* st = reinterpret_cast<float*>(lds);
+  if (wid < NC) {
+    const int wm = wid / WN, wn = wid % WN;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = wm * FM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const int col = wn * FN * 32 + j * 32 + (lane & 31);
-          st[row * EP_STRIDE + col] = acc[i][j][r];
-        }
-    if (p.bias && tid < BN) sbias[tid] = p.bias[n0 + tid];
-    pm0 = m0;
-    pn0 = n0;
-    __syncthreads();   // staging + bias visible before the next tile's units read them
+        for (int e = 0; e < 4; ++e)
+          st[(wm * FM * 16 + 16 * i + 4 * (lane >> 4) + e) * EPS + wn * FN * 16 + 16 * j + (lane & 15)] = acc[i][j][e];
   }
-  if (pm0 >= 0) {
-    __syncthreads();
+  __syncthreads();
+  static_assert((BMt * CPW) % NTt == 0 && NTt % CPW == 0, "whole rows per pass");
+#pragma unroll 2
+  for (int it = 0; it < BMt * CPW / NTt; ++it) {
+    const int row = it * (NTt / CPW) + tid / CPW, c8 = (tid % CPW) * 8;
+    const float4 lo = *reinterpret_cast<const float4*>(st + row * EPS + c8);
+    const float4 hi = *reinterpret_cast<const float4*>(st + row * EPS + c8 + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const int m = m0 + row;
+    epilogue_store8(p, z, zz, m, n0 + c8, v);
+    if (p.rd_out) {   // (vectorised bf16 epilogue: v now holds the stored values) 8-lane group = 64 columns
+      float t = 0.f;
+      if (m < p.M && n0 + c8 < p.N) {
+        const uint4 u = *reinterpret_cast<const uint4*>(p.rd_with + (long)m * p.ldc + n0 + c8);
+        const bf16x8 w = __builtin_bit_cast(bf16x8, u);
 #pragma unroll
-    for (int j = 0; j < UPT; ++j) unit(j);
+        for (int e = 0; e < 8; ++e) t += (float)(bf16)v[e] * (float)w[e];
+      }
+      t += __shfl_xor(t, 1, 64);
+      t += __shfl_xor(t, 2, 64);
+      t += __shfl_xor(t, 4, 64);
+      if ((tid & 7) == 0 && m < p.M && n0 + c8 < p.N) {
+        const int b = m / p.rd_T, tt = m - b * p.rd_T, g = (n0 + c8) >> 6;
+        p.rd_out[((long)b * (p.N >> 6) + g) * p.rd_T + tt] = t;
+      }
+    }
   }
   probe_end(p.probe);
 }
 
+extern int g_gemm_mode;
 // ---------------------------------------------------------------- grouped weight gradients
 // All weight-gradient GEMMs dW_i = dY_iᵀ X_i (+ bias gradient sum_rows dY_i) of a backward pass in ONE
 // launch: every task reduces over the same token dimension, so each 256x128 output tile is one
@@ -1395,7 +1172,7 @@ __device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& 
   const WgTask* tab = reinterpret_cast<const WgTask*>(ga.group_tab);
   const int nwg = gridDim.x, L = blockIdx.x;
   int id = L;
-  if (nwg > 8 && ga.Jn == 0) {   // Jn != 0: plain dispatch order (A/B)
+  if (nwg > 8) {
     const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
     id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
   }
@@ -1507,17 +1284,11 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmP p, OA oa, OB ob) {
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
-
-#pragma unroll
-  for (int i = 0; i < FR; ++i)
-#pragma unroll
-    for (int j = 0; j < FR; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (TBM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int n = n0 + wn * (TBM / 2) + j * 32 + (lane & 31);
-        epilogue_store(p, z, blockIdx.z, m, n, acc[i][j][r]);
-      }
+  // (the K loop ends on a barrier: the staging may reuse the operand LDS) one wave band (TBM / 2 rows) of the
+  // f32 tile at a time through LDS, then 8-column chunks through epilogue_store8 (was a per-element epilogue the
+  // compiler could not unroll, leaving the accumulators run-time indexed)
+  static_assert((TBM / 2) * (TBM + 4) <= 4 * TT, "one band of the tile fits the staging");
+  tile_epilogue_g<FR, FR, 2, 2, NT, TBM, false, TBM / 2>(p, acc, lds, z, blockIdx.z, m0, n0, wm, wn, lane, tid);
 }
 
 GemmP plain_params(int M, int N, int K, void* C, long ldc, int dtc) {
@@ -1634,39 +1405,36 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 //   V256: 256x128 tile, BK 64, 3-stage ring (144 KiB: one workgroup of 8 waves per CU)
 //   V256S: 256x128 tile, BK 32, 3-stage ring (72 KiB: two workgroups per CU, one's epilogue
 //          overlapping the other's main loop)
-//   V128: 128x128 tile, BK 64, 3-stage ring (96 KiB, 4 waves)
-//   V128S: 128x128 tile, BK 32, 3-stage ring (68 KiB incl. the aliased epilogue staging: two
-//          workgroups of 4 waves per CU) -- narrow outputs (N = 512) fill the chip
+//   V192: 192x128 tile for d-wide outputs (warp-specialised for K-major x K-major operands)
+//   V192S8: 192x128 tile, 8 waves, BK 32, two workgroups per CU
+// (measured slower and removed in round 4, A/B records in DESIGN.md §8: 128-row tiles, 96-row tiles, a persistent
+//  register-deferred epilogue, an interleaved-epilogue persistent kernel, a tail-balanced row split, 32x32x16
+//  main loops for K-major operands, a 3-deep 192-row ring)
 template <bool AK, bool BKM, bool M16 = false>
-void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s, int force = 0) {
-  // 0 auto, 1 V256, 2 V256S, 3 V128, 4 V128S, 5 V192, 6 V192S, 7 V192S8
-  const int sel = force ? force : (g_gemm_mode >> 4) & 7;
-  const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k), g128(cdiv(p.N, BN), cdiv(p.M, 128), batch * p.split_k);
+void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
+  // 0 auto, 1 V256, 2 V256S, 5 V192, 7 V192S8
+  const int sel = (g_gemm_mode >> 4) & 7;
+  const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k);
   int v = sel;
   if constexpr (AK) {
     // auto: outputs <= 512 columns (the encoder's d-wide outputs) take the 192-row tiles: 63 x 4 = 252
     // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
-    // 96 x 128 tiles, 4 waves of 96 x 32, BK 32, two workgroups per CU (cfm_gemm_set_mode bit 18, opt-in): 125 x 4 =
-    // 500 tiles of the encoder's d-wide outputs in one round of the 512 slots.  Bit-identical to the 192-row tiles
-    // but SLOWER (profiles/r03/gemm_v96_ab.txt: FFN-down forward 41.0 -> 54.3 us, FFN-up data gradient 33.4 ->
-    // 47.1 us; L15 step 21.0 -> 22.0 ms same box): half the FLOP per staged byte, and the two workgroups of a CU
-    // reach their epilogues together
-    if (v == 0 && (g_gemm_mode & 262144) && p.N <= 512 && p.split_k == 1 && (long)p.M * batch >= 4096) {
-      const dim3 g96(cdiv(p.N, BN), cdiv(p.M, 96), batch * p.split_k);
-      hipLaunchKernelGGL((gemm_pipe_kernel<96, 32, 3, 2, AK, BKM, 4, 4, false, false, false, BN, M16>), g96,
-                         dim3(256), 0, s, p, oa, ob, GatherA{});
-      return;
-    }
     if (v == 5 || (v == 0 && p.N <= 512 && p.split_k == 1 && (long)p.M * batch >= 4096)) {
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
-      // 4-deep ring (4 x 40 KiB = the whole 160 KiB LDS): FFN-up data gradient 34.2 -> 32.5 us same-box;
-      // cfm_gemm_set_mode bit 14 keeps the 3-deep ring (A/B)
-      if (!(g_gemm_mode & 16384))
-        hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 4, 1, AK, BKM, 8, 4, false, false, false, BN, M16>), g192,
-                           dim3(512), 0, s, p, oa, ob, GatherA{});
-      else
-        hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, AK, BKM, 8, 4, false, false, false, BN, M16>), g192,
-                           dim3(512), 0, s, p, oa, ob, GatherA{});
+      if constexpr (BKM) {
+        // warp-specialised loading (cfm_gemm_set_mode bit 19 keeps the shared-DMA kernel below for A/B; bit 20
+        // selects 4 compute waves of 96 x 64 instead of 8 of 96 x 32)
+        if (!(g_gemm_mode & 524288) && p.split_k == 1) {
+          if (g_gemm_mode & 1048576)
+            hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 2, 4, 4>), g192, dim3(512), 0, s, p, oa, ob);
+          else
+            hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 4, 4, 4>), g192, dim3(768), 0, s, p, oa, ob);
+          return;
+        }
+      }
+      // 4-deep ring (4 x 40 KiB = the whole 160 KiB LDS): FFN-up data gradient 34.2 -> 32.5 us same-box
+      hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 4, 1, AK, BKM, 8, 4, false, false, false, BN, M16>), g192,
+                         dim3(512), 0, s, p, oa, ob, GatherA{});
       return;
     }
     // auto: 1024- / 1536-wide outputs of short reductions (QKV, pointwise-conv-1 forward) take 192-row tiles
@@ -1682,13 +1450,8 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
                          0, s, p, oa, ob, GatherA{});
       return;
     }
-    if (v == 6) {   // 192 x 128 tiles, 4 waves of 96x64, BK 32: two workgroups per CU
-      const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
-      hipLaunchKernelGGL((gemm_pipe_kernel<192, 32, 3, 2, AK, BKM, 4, 2>), g192, dim3(256), 0, s, p, oa, ob, GatherA{});
-      return;
-    }
   }
-  if (v >= 5) v = 0;
+  if (v != 1 && v != 2) v = 0;
   if (!v) {
     // auto: short reductions (K <= 512: the epilogue is a large share of the tile's time) run two
     // 256-row workgroups per CU so one's epilogue hides under the other's MFMAs; long ones keep BK 64
@@ -1697,20 +1460,9 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
   if (v == 1)
     hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, AK, BKM, 8, 2, false, false, false, BN, M16>), g256, dim3(512), 0,
                        s, p, oa, ob, GatherA{});
-  else if (v == 2)
+  else
     hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, AK, BKM, 8, 2, false, false, false, BN, M16>), g256, dim3(512), 0,
                        s, p, oa, ob, GatherA{});
-  else if (v == 4) hipLaunchKernelGGL((gemm_pipe_kernel<128, 32, 3, 2, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob, GatherA{});
-  else hipLaunchKernelGGL((gemm_pipe_kernel<128, 64, 3, 1, AK, BKM>), g128, dim3(256), 0, s, p, oa, ob, GatherA{});
-}
-
-// the persistent interleaved-epilogue kernel takes K-major bf16 GEMMs whose epilogue needs no global
-// loads besides the bias (cfm_gemm_set_mode bit 11 enables it; bits 8-9 select grouped-wgrad A/B variants)
-bool ie_ok(const cfm_gemm_desc& d, const GemmP& p) {
-  return (g_gemm_mode & 2048) && d.a_kmajor && d.b_kmajor && d.batch == 1 && p.split_k == 1 && !p.res &&
-         !p.act_grad && !p.cmap && !p.rd_out && !p.acs_slab && !p.slab && p.vec_c && p.N % BN == 0 &&
-         p.dtc == CFM_BF16 && (p.act == 0 || p.act == CFM_ACT_SILU) && (!p.pre || p.dtpre == CFM_BF16) &&
-         (long)p.M * p.ldc * 2 < (1L << 31) && !p.dbg && p.alpha_a == nullptr && p.alpha_b == nullptr;
 }
 
 int num_cus() {
@@ -1731,71 +1483,9 @@ int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   const PipeOp oa{(const bf16*)d.A, d.lda, d.stride_a, d.M, (unsigned)(ea * 2)};
   const PipeOp ob{(const bf16*)d.B, d.ldb, d.stride_b, d.N, (unsigned)(eb * 2)};
   const bool ak = d.a_kmajor != 0, bkm = d.b_kmajor != 0;
-  if (pers_ok(d, p)) {
-    const int ntm = cdiv(p.M, PS_BM), ntn = p.N / PS_BN, ntiles = ntm * ntn;
-    const int grid = min(ntiles, num_cus());
-    const int tper = cdiv(ntiles, grid);
-    if (g_gemm_mode & 65536) p.dbg |= 16;   // timing experiment: every epilogue store dropped (range check)
-    if (p.act == CFM_ACT_SILU)
-      hipLaunchKernelGGL((gemm_pers_kernel<true>), dim3(grid), dim3(512), 0, s, p, oa, ob, ntm, ntn, tper);
-    else
-      hipLaunchKernelGGL((gemm_pers_kernel<false>), dim3(grid), dim3(512), 0, s, p, oa, ob, ntm, ntn, tper);
-    return CFM_OK;
-  }
-  if (ie_ok(d, p)) {
-    const int ntm = cdiv(p.M, IE_BM), ntn = p.N / BN;
-    const int grid = min(ntm * ntn, num_cus());
-    if (p.pre)
-      hipLaunchKernelGGL((gemm_pipe_ie_kernel<true>), dim3(grid), dim3(IE_NWV * 64), 0, s, p, oa, ob, ntm, ntn);
-    else
-      hipLaunchKernelGGL((gemm_pipe_ie_kernel<false>), dim3(grid), dim3(IE_NWV * 64), 0, s, p, oa, ob, ntm, ntn);
-    return CFM_OK;
-  }
-  // Tail-balanced row split for wide, short-reduction K-major GEMMs that would run on 256 x 128 tiles two per CU
-  // (FFN up-projection forward, FFN down-projection data gradient: M 11,936, N 2048, K 512 -> 752 tiles on 512
-  // slots, the second round 47 % full): the first full rounds on 256-row tiles, the remaining rows on 128-row
-  // tiles in ONE round (half-height tiles: the tail costs half a round).  Epilogue indices stay global (C / pre /
-  // residual row offsets, dropout index offset).  Opt-in (cfm_gemm_set_mode bit 17): measured SLOWER at L15 (step
-  // 21.61 -> 22.01 ms, profiles/r03/gemm_tail_split_ab.txt) -- one 512-tile round takes 46 us vs 68 us for all 752
-  // tiles, i.e. the kernel's time follows its tile count (store-bound epilogues), not its rounds.
-  if (ak && bkm && d.batch == 1 && p.split_k == 1 && !p.cmap && !p.rd_out && !p.acs_slab && (g_gemm_mode & 131072) &&
-      ((g_gemm_mode >> 4) & 7) == 0 && p.N > 1536 && p.k_per_split <= 512) {
-    const long slots = 2L * num_cus();
-    const int ntn = cdiv(p.N, BN);
-    const long tiles = (long)cdiv(p.M, 256) * ntn;
-    const long per_round = slots / ntn;                 // 256-row panels per full round
-    const int rows_big = (int)((tiles / slots) * per_round * 256);
-    const int rest = p.M - rows_big;
-    if (tiles > slots && rows_big > 0 && rest > 0 && (long)cdiv(rest, 128) * ntn <= slots) {
-      GemmP p1 = p, p2 = p;
-      p1.M = rows_big;
-      p2.M = rest;
-      const int ec = p.dtc == CFM_BF16 ? 2 : 4;
-      p2.C = (char*)p.C + (long)rows_big * p.ldc * ec;
-      if (p.pre) p2.pre = (char*)p.pre + (long)rows_big * p.ldc * (p.dtpre == CFM_BF16 ? 2 : 4);
-      if (p.res) p2.res = (const char*)p.res + (long)rows_big * p.ldr * (p.dtr == CFM_BF16 ? 2 : 4);
-      p2.doff = p.doff + (uint64_t)rows_big * (uint64_t)p.N;
-      PipeOp oa1 = oa, oa2 = oa;
-      oa1.lim = rows_big;
-      oa2.base = oa.base + (long)rows_big * oa.ld;
-      oa2.lim = rest;
-      oa2.bytes = (unsigned)(pipe_extent(1, rest, p.K, oa.ld) * 2);
-      p1.vec_c = vec_epilogue_ok(p1);
-      p2.vec_c = vec_epilogue_ok(p2);
-      if (!(g_gemm_mode & 8192)) {
-        launch_pipe_t<true, true, true>(p1, oa1, ob, 1, s, 2);
-        launch_pipe_t<true, true, true>(p2, oa2, ob, 1, s, 4);
-      } else {
-        launch_pipe_t<true, true>(p1, oa1, ob, 1, s, 2);
-        launch_pipe_t<true, true>(p2, oa2, ob, 1, s, 4);
-      }
-      return CFM_OK;
-    }
-  }
   // the K-major x K-major GEMMs (forward and data-gradient) run 16x16x32 MFMA main loops (L15 step 25.0 -> 24.7 ms
-  // same-box A/B); cfm_gemm_set_mode bit 13 selects the 32x32x16 form
-  if (ak && bkm && !(g_gemm_mode & 8192)) launch_pipe_t<true, true, true>(p, oa, ob, d.batch, s);
-  else if (ak && bkm) launch_pipe_t<true, true>(p, oa, ob, d.batch, s);
+  // same-box A/B)
+  if (ak && bkm) launch_pipe_t<true, true, true>(p, oa, ob, d.batch, s);
   else if (ak) launch_pipe_t<true, false>(p, oa, ob, d.batch, s);
   else if (bkm) launch_pipe_t<false, true>(p, oa, ob, d.batch, s);
   else launch_pipe_t<false, false>(p, oa, ob, d.batch, s);
@@ -1918,13 +1608,12 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
 }
 
 CFM_EXPORT size_t cfm_wgrad_group_task_bytes(void) { return sizeof(WgTask); }
-// grouped weight-gradient launch (cfm_gemm_set_mode bits 8-9): 0 = 256 x 256 tiles, BK 32, 4-deep ring (half
-// the dY panel re-reads of 256 x 128; 17 layers 5.46 -> 4.89 ms, L15 step -0.8 ms same-box), 1 = 256 x 128 BK 32
-// two per CU, 2 = variant 0 in plain dispatch order, 3 = 256 x 128 BK 64 (round-2 default until then; a
-// 256 x 256 BK 64 double-buffered form spilled and ran 2.4x slower)
-int wg_variant() { return (g_gemm_mode >> 8) & 3; }
-int wg_bn() { return (wg_variant() == 1 || wg_variant() == 3) ? BN : 256; }
-CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, wg_bn()); }
+// grouped weight-gradient launch: 256 x 256 output tiles, BK 32, 4-deep ring (half the dY panel re-reads of
+// 256 x 128; 17 layers 5.46 -> 4.89 ms, L15 step -0.8 ms same-box; 256 x 128 BK 32 two per CU, 256 x 128 BK 64 and
+// plain dispatch order measured slower and were removed in round 4; a 256 x 256 BK 64 double-buffered form spilled
+// and ran 2.4x slower)
+constexpr int WG_BN = 256;
+CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, WG_BN); }
 
 // fill task i of a HOST table: dW (N x K, fp32) = dYᵀ X over M tokens, dY (M x N) / X (M x K) bf16
 // row-major; db (N, fp32, may be NULL) = sum_rows dY; tile0 = first workgroup id of the task
@@ -1943,7 +1632,7 @@ CFM_EXPORT int cfm_wgrad_group_fill(void* host_tab, int i, const void* dy, const
   t.oa = PipeOp{(const bf16*)dy, N, 0, N, (unsigned)((long)M * N * 2)};
   t.ob = PipeOp{(const bf16*)x, K, 0, K, (unsigned)((long)M * K * 2)};
   t.tile0 = tile0;
-  t.tiles_n = cdiv(K, wg_bn());
+  t.tiles_n = cdiv(K, WG_BN);
   reinterpret_cast<WgTask*>(host_tab)[i] = t;
   return CFM_OK;
 }
@@ -1956,17 +1645,8 @@ CFM_EXPORT int cfm_wgrad_group_probed(const void* dev_tab, int ntasks, long tota
   GatherA ga{};
   ga.group_tab = dev_tab;
   ga.group_n = ntasks;
-  const int gv = wg_variant();   // (tables filled with the same variant's wg_bn())
-  ga.Jn = gv == 2;
-  if (gv == 0 || gv == 2)   // 256 x 256 tiles (8 waves of 64 x 128), BK 32, 4-deep ring
-    hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 4, 1, false, false, 8, 2, false, true, false, 256>),
-                       dim3((unsigned)total_tiles), dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
-  else if (gv == 1)
-    hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, false, false, 8, 2, false, true>), dim3((unsigned)total_tiles),
-                       dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
-  else
-    hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, false, false, 8, 2, false, true>), dim3((unsigned)total_tiles),
-                       dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
+  hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 4, 1, false, false, 8, 2, false, true, false, WG_BN>),
+                     dim3((unsigned)total_tiles), dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
   return cfm::check_launch("cfm_wgrad_group");
 }
 

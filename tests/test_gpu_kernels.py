@@ -46,9 +46,9 @@ def gemm_mode():
     _lib.call("cfm_gemm_set_mode", 3)
 
 
-# register-staged / LDS-DMA 256x128 BK64 / BK32 / 128x128 / 192x128 BK64, BK32 4 waves, BK32 8 waves (AK only);
-# K-major x K-major run 16x16x32 MFMA main loops by default, + 8192 the 32x32x16 form; + 16384: 4-deep ring (192 rows)
-@pytest.mark.parametrize("mode", [1, 18, 34, 50, 82, 98, 114, 8192 | 18, 8192 | 34, 8192 | 82, 8192 | 114, 16384 | 82])
+# register-staged / LDS-DMA auto / 256x128 BK64 / BK32 / 192x128 (K-major x K-major: warp-specialised, 8 compute
+# waves; + 1048576: 4 compute waves; + 524288: the shared-DMA 192-row pipeline) / 192x128 BK32 8 waves (AK only)
+@pytest.mark.parametrize("mode", [1, 2, 18, 34, 82, 82 | 1048576, 82 | 524288, 114])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(1000, 512, 512), (264, 136, 192), (520, 264, 1000), (8, 8, 64)])
 def test_gemm_kernel_variants(gemm_mode, mode, ak, bk, M, N, K):
@@ -375,87 +375,67 @@ def test_wgrad_group_matches_per_gemm():
         assert _rel(db, rb) < 1e-5
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 512, 512), (11936 // 8, 2048, 512), (200, 256, 64), (385, 384, 2048)])
-@pytest.mark.parametrize("epi", ["bias", "silu_pre_drop", "plain_scaled"])
-def test_gemm_interleaved_epilogue_matches_pipeline(gemm_mode, M, N, K, epi):
-    """The persistent interleaved-epilogue kernel (cfm_gemm_set_mode bit 11) against the default LDS-DMA
-    pipeline on the same inputs: identical K loops and epilogue arithmetic -> bit-identical outputs
-    (ragged M, short K with the epilogue finished after the loop, several tiles per workgroup)."""
-    g = torch.Generator().manual_seed(M + N + K)
-    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
-    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
-    b = torch.randn(N, generator=g).to(DEV)
-    outs = []
-    for mode in (3, 3 | 2048):
-        gemm_mode(mode)
-        y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        if epi == "bias":
-            ops.linear(x, w, b, out=y)
-        elif epi == "silu_pre_drop":
-            ops.linear(x, w, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=5, out=y)
-        else:
-            ops.gemm(x, w, y, M, N, K, a_kmajor=True, b_kmajor=True, alpha=0.5)
-        torch.cuda.synchronize()
-        outs.append((y.clone(), pre.clone()))
-    assert torch.equal(outs[0][0], outs[1][0])
-    if epi == "silu_pre_drop":
-        assert torch.equal(outs[0][1], outs[1][1])
-
-
-def test_wgrad_group_wide_tiles_match_per_gemm(gemm_mode):
-    """The 256 x 256-tile grouped weight-gradient launch (default) against the 256 x 128 one
-    (cfm_gemm_set_mode bits 8-9 = 3) on the encoder's shapes, incl. the fused bias gradient and ragged N / K."""
+def test_wgrad_group_wide_tiles_vs_reference():
+    """The 256 x 256-tile grouped weight-gradient launch on the encoder's shapes, incl. the fused bias gradient and
+    ragged N / K, against fp32 references."""
     g = torch.Generator().manual_seed(11)
     M = 1000
     shapes = [(2048, 512), (512, 2048), (1536, 512), (512, 512), (136, 264)]
     ops_ = [(torch.randn(M, N, generator=g).to(DEV, torch.bfloat16), torch.randn(M, K, generator=g).to(DEV, torch.bfloat16))
             for N, K in shapes]
-    outs = []
-    for mode in (3, 3 | 768):
-        gemm_mode(mode)
-        grp = ops.WgradGroup()
-        res = [grp.add(d, x) for d, x in ops_]
-        grp.flush()
-        torch.cuda.synchronize()
-        outs.append([(dw.clone(), db.clone()) for dw, db in res])
-    for (a, ab), (b, bb), (d, x) in zip(outs[0], outs[1], ops_):
+    grp = ops.WgradGroup()
+    res = [grp.add(d, x) for d, x in ops_]
+    grp.flush()
+    torch.cuda.synchronize()
+    for (a, ab), (d, x) in zip(res, ops_):
         ref = d.float().T @ x.float()
-        assert _rel(b, ref) < 1e-5 and _rel(a, ref) < 1e-5
-        assert _rel(bb, d.float().sum(0)) < 1e-5
+        assert _rel(a, ref) < 1e-5
+        assert _rel(ab, d.float().sum(0)) < 1e-5
 
 
-@pytest.mark.parametrize("M,N", [(11936, 2048), (1000, 1536), (300, 1024), (11936, 1024)])
-@pytest.mark.parametrize("epi", ["bias", "silu_pre_drop", "scaled"])
-def test_gemm_persistent_deferred_epilogue_matches_pipeline(gemm_mode, M, N, epi):
-    """The persistent register-deferred-epilogue kernel (K = 512, N 1024-2048, bf16 out; opt-in with
-    cfm_gemm_set_mode bit 15) against the tiled LDS-DMA pipeline (the default) on the same inputs:
-    fp32 pre-activations within accumulation-order noise, bf16 outputs within one rounding step, and the
-    dropout masks identical (same element keying)."""
-    K = 512
-    g = torch.Generator().manual_seed(M + N)
+@pytest.mark.parametrize("ws", [3, 3 | 1048576])
+@pytest.mark.parametrize("M,K", [(11936, 2048), (11936, 512), (1000, 1536), (385, 1024), (192, 64)])
+@pytest.mark.parametrize("epi", ["bf16", "residual_drop", "rowdot", "batched"])
+def test_gemm_warp_specialised_matches_shared_dma(gemm_mode, ws, M, K, epi):
+    """The warp-specialised d-wide kernel (default for K-major x K-major GEMMs with <= 512 output columns; 8 or 4
+    compute waves) against the shared-DMA 192-row pipeline (cfm_gemm_set_mode bit 19): the same 16x16x32 MFMAs in
+    the same k order and the same epilogue -> bit-identical outputs (ragged M, every epilogue the encoder uses:
+    bf16 data gradients, fp32 residual-stream forwards with dropout + 0.5 scale, the rowdot of attention's D,
+    batched overlapping-row operands as the front-end fold uses)."""
+    N = 512
+    g = torch.Generator().manual_seed(M + K)
     x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
     w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
     b = torch.randn(N, generator=g).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV)
+    with_ = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    T = M // 8 if M % 8 == 0 else M
     outs = []
-    for mode in (3 | 32768, 3):
+    for mode in (ws, 3 | 524288):
         gemm_mode(mode)
-        y = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
-        pre = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
-        if epi == "bias":
-            ops.linear(x, w, b, out=y)
-        elif epi == "silu_pre_drop":
-            ops.linear(x, w, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=5, out=y)
+        if epi == "bf16":
+            y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(x, w, y, M, N, K)
+            outs.append((y.clone(),))
+        elif epi == "residual_drop":
+            y = torch.empty(M, N, device=DEV, dtype=torch.float32)
+            ops.linear(x, w, b, out=y, drop_p=0.1, seed=7, out_scale=0.5, residual=res)
+            outs.append((y.clone(),))
+        elif epi == "rowdot":
+            y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            D = torch.empty(M * N // 64, device=DEV, dtype=torch.float32)
+            ops.gemm(x, w, y, M, N, K, rowdot=(with_, D, T))
+            outs.append((y.clone(), D.clone()))
         else:
-            ops.gemm(x, w, y, M, N, K, a_kmajor=True, b_kmajor=True, alpha=0.5, bias=b, out_scale=2.0)
-        torch.cuda.synchronize()
-        outs.append((y.float().clone(), pre.float().clone()))
-    (y0, p0), (y1, p1) = outs
-    assert torch.isfinite(y0).all() and (y0 != 7.0).float().mean() > 0.99       # every element written
-    assert _rel(y0, y1) < 4e-3
-    if epi == "silu_pre_drop":
-        assert _rel(p0, p1) < 4e-3
-        assert torch.equal(y0 == 0, y1 == 0)          # identical dropout masks
+            # 4 batches of overlapping A rows (lda < K) as the folded front-end's windowed view
+            Bb, Mb, lda = 4, M // 4, max(64, K // 2)
+            y = torch.empty(Bb * Mb, N, device=DEV, dtype=torch.float32)
+            ops.gemm(x, w, y, Mb, N, K, lda=lda, stride_a=Mb * lda, batch=Bb, stride_c=Mb * N, bias=b,
+                     allow_overlap=True)
+            outs.append((y.clone(),))
+    torch.cuda.synchronize()
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
 
 
 @pytest.mark.parametrize("training", [True, False])
@@ -516,34 +496,3 @@ def test_bn_folded_dwconv_bwd(training, sync, B, T, C, K, dt):
     assert _rel(da.float(), da2.float()) < 1e-5
     assert _rel(dw, dw2) < 1e-5 and (db - db2).norm() < 1e-5 * dw.norm()
     assert torch.equal(dg, dg2) and torch.equal(dbt, dbt2)
-
-
-@pytest.mark.parametrize("M", [11936, 9000])
-def test_gemm_tail_split_matches_single_launch(gemm_mode, M):
-    """The tail-balanced row split of wide short-K K-major GEMMs (256-row tiles for whole rounds, 128-row tiles
-    for the rest; opt-in cfm_gemm_set_mode bit 17) against one launch: FFN up-projection forward (bias +
-    SiLU + pre-activation + dropout) and FFN down-projection data gradient (silu'(pre) + dropout) epilogues.
-    Same dropout masks (global element index), values within the two MFMA shapes' fp32 summation order."""
-    N, K = 2048, 512
-    g = torch.Generator().manual_seed(M)
-    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
-    w = (0.05 * torch.randn(N, K, generator=g)).to(DEV, torch.bfloat16)
-    b = (0.1 * torch.randn(N, generator=g)).to(DEV)
-    dz = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
-    w2t = (0.05 * torch.randn(N, K, generator=g)).to(DEV, torch.bfloat16)
-    outs = []
-    for mode in (3 | 131072, 3):
-        gemm_mode(mode)
-        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        y = ops.linear(x, w, b, out_dtype=torch.bfloat16, act=1, pre=pre, drop_p=0.1, seed=5)
-        gd = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        ops.gemm(dz, w2t, gd, M, N, K, act_grad=True, pre=pre, drop_p=0.1, seed=6)
-        torch.cuda.synchronize()
-        outs.append((y.float(), pre.float(), gd.float()))
-    (y1, p1, g1), (y0, p0, g0) = outs
-    assert _rel(p1, p0) < 2e-3
-    assert _rel(y1, y0) < 2e-3
-    assert _rel(g1, g0) < 2e-3
-    drop1, drop0 = (y1 == 0) & (p1 != 0), (y0 == 0) & (p0 != 0)
-    assert (drop1 != drop0).float().mean().item() < 1e-4
-    assert 0.08 < drop0.float().mean().item() < 0.12
