@@ -1152,6 +1152,169 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
   probe_end(p.probe);
 }
 
+// XCD-contiguous position of workgroup L among G (blocks b, b + 8 share an XCD; bijective for any G)
+__device__ __forceinline__ int xcd_id_any(int L, int G) {
+  if (G <= 8) return L;
+  const int xcd = L & 7, q = G >> 3, r = G & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+}
+
+// ---------------------------------------------------------------- persistent warp-specialised K-major GEMM
+// For the wide outputs of short reductions (FFN-up forward / FFN-down data gradient N 2048, QKV N 1536, pointwise-
+// conv-1 N 1024; K 512): one workgroup per CU walks tiles t = pos, pos + grid, ... (row-major tile order, XCD-
+// contiguous positions: the WGs of one XCD hold neighbouring tiles of the same A rows).  The 4 loader waves stream
+// the stages of ALL its tiles through one 3-deep ring (global stage index g = tile * nk + kt), so the next tile's
+// first stages land while the current tile's epilogue runs; the 8 compute waves run the ws kernel's pipelined
+// K loop.  The epilogue stages the f32 tile in 64-row chunks in an LDS area of its own (the ring stays live) and
+// the compute waves finish 8-column chunks through epilogue_store8 (the loaders issue no stores, so their vmcnt
+// counts only their DMA).  All waves pass the same barrier sequence: one per stage (where stage g + 1 becomes
+// visible) + two per epilogue chunk.
+template <int BMt, int WM, int WN, int NL, int NST>
+__global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_wsp_kernel(GemmP p, PipeOp oa, PipeOp ob, int ntm, int ntn) {
+  constexpr int BKt = 64, BNt = BN, NC = WM * WN;
+  constexpr int ABYTES = BMt * BKt * 2, BBYTES = BNt * BKt * 2, STAGE = ABYTES + BBYTES;
+  constexpr int AP = ABYTES / 1024, BP = BBYTES / 1024, PW = (AP + BP) / NL;
+  static_assert(PW * NL == AP + BP && AP * 1024 == ABYTES && BP * 1024 == BBYTES, "whole DMA pieces per loader");
+  constexpr int FM = BMt / WM / 16, FN = BNt / WN / 16;
+  static_assert(FM * WM * 16 == BMt && FN * WN * 16 == BNt, "wave tiling");
+  constexpr int EPS = BNt + 4, CPW = BNt / 8, CR = 64;                 // staging: CR-row chunks of the f32 tile
+  static_assert(BMt % CR == 0 && (CR * CPW) % 64 == 0, "chunking");
+  constexpr int RING = NST * STAGE, STG = CR * EPS * 4;
+  static_assert(NST == 3, "the slot refilled after stage g+1's barrier is g-1's: NST - 1 = 2 stages ahead");
+  __shared__ __attribute__((aligned(1024))) char lds[RING + STG];
+  probe_begin(p.probe);
+  gemm_drop_prep(p);
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntiles = ntm * ntn, G = gridDim.x;
+  const int pos = xcd_id_any(blockIdx.x, G);
+  const int my_tiles = pos < ntiles ? (ntiles - 1 - pos) / G + 1 : 0;
+  const int nk = p.K / BKt;
+  const int gtot = my_tiles * nk;                 // this workgroup's stages
+  float* st = reinterpret_cast<float*>(lds + RING);
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const bool loader = wid >= NC;
+  // ---- loader state: piece i of a stage is 1-KiB piece q = lw + NL i of the [A | B] stage image
+  const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, 0), rb = pipe_rsrc(ob, 0);
+  auto stage_src = [&](int i, int g) {             // source byte offset of loader piece i of global stage g
+    const int t = pos + (g / nk) * G, kt = g % nk;
+    const int tm = t / ntn, tn = t % ntn;
+    const int q = (wid - NC) + NL * i;
+    return (q < AP ? pipe_src<true, BMt, BKt>(oa, q * 64 + lane, tm * BMt, 0)
+                   : pipe_src<true, BNt, BKt>(ob, (q - AP) * 64 + lane, tn * BNt, 0)) + (unsigned)(kt * BKt * 2);
+  };
+  auto issue = [&](int g) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int q = (wid - NC) + NL * i;
+      dma16(q < AP ? ra : rb, lds + (g % NST) * STAGE + q * 1024, stage_src(i, g));
+    }
+  };
+  auto wait_stage = [&](int s, int last) {       // stage s landed: only stages issued after it outstanding
+    if (last - s >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // ---- compute state
+  const int wm = wid / WN, wn = wid % WN;
+  bf16x8 af[2][FM], bfr[2][FN];
+  auto read = [&](bf16x8 (&fa)[FM], bf16x8 (&fb)[FN], int g, int sub) {
+    const char* sa = lds + (g % NST) * STAGE;
+    const char* sb = sa + ABYTES;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j] = pipe_frag16k<BKt>(sb, wn * FN * 16 + 16 * j, 32 * sub, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = pipe_frag16k<BKt>(sa, wm * FM * 16 + 16 * i, 32 * sub, lane);
+  };
+  auto mma = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  };
+  int last = -1;
+  if (loader && gtot > 0) {
+    for (int s = 0; s < NST - 1 && s < gtot; ++s) issue(s);
+    last = min(NST - 2, gtot - 1);
+    wait_stage(0, last);
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (!loader && gtot > 0) read(af[0], bfr[0], 0, 0);
+  for (int lt = 0; lt < my_tiles; ++lt) {
+    const int t = pos + lt * G;
+    const int m0 = (t / ntn) * BMt, n0 = (t % ntn) * BNt;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int g = lt * nk + kt;
+      const bool more = g + 1 < gtot;
+      if (!loader) {
+        read(af[1], bfr[1], g, 1);
+        mma(af[0], bfr[0]);
+      }
+      if (more) {
+        if (loader) wait_stage(g + 1, last);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (loader) {
+          const int gn = g + NST - 1;            // refills the slot of stage g - 1
+          if (gn < gtot) {
+            issue(gn);
+            last = gn;
+          }
+        } else {
+          read(af[0], bfr[0], g + 1, 0);
+        }
+      }
+      if (!loader) mma(af[1], bfr[1]);
+    }
+    // ---- epilogue of tile t: CR-row chunks through the staging area, every wave finishes 8-column chunks
+#pragma nounroll
+    for (int c = 0; c < BMt / CR; ++c) {
+      if (!loader) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int r16 = wm * FM * 16 + 16 * i;          // first row of accumulator block i (wave-uniform)
+          if (r16 >= c * CR && r16 < (c + 1) * CR) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                st[(r16 - c * CR + 4 * (lane >> 4) + e) * EPS + wn * FN * 16 + 16 * j + (lane & 15)] = acc[i][j][e];
+          }
+        }
+      }
+      // raw barriers: the loaders' prefetch DMA of the next tile stays in flight (a __syncthreads would drain it)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (!loader) {     // (the loaders issue no stores: their vmcnt counts their DMA only)
+        static_assert((CR * CPW) % (NC * 64) == 0, "whole items per compute thread");
+#pragma unroll
+        for (int it = 0; it < CR * CPW / (NC * 64); ++it) {
+          const int item = it * NC * 64 + tid;
+          const int row = item / CPW, c8 = (item % CPW) * 8;
+          const float4 lo = *reinterpret_cast<const float4*>(st + row * EPS + c8);
+          const float4 hi = *reinterpret_cast<const float4*>(st + row * EPS + c8 + 4);
+          float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+          epilogue_store8(p, 0, 0, m0 + c * CR + row, n0 + c8, v);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (!loader) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  probe_end(p.probe);
+}
+
 extern int g_gemm_mode;
 // ---------------------------------------------------------------- grouped weight gradients
 // All weight-gradient GEMMs dW_i = dY_iᵀ X_i (+ bias gradient sum_rows dY_i) of a backward pass in ONE
@@ -1410,12 +1573,25 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 // (measured slower and removed in round 4, A/B records in DESIGN.md §8: 128-row tiles, 96-row tiles, a persistent
 //  register-deferred epilogue, an interleaved-epilogue persistent kernel, a tail-balanced row split, 32x32x16
 //  main loops for K-major operands, a 3-deep 192-row ring)
+int num_cus();
+
 template <bool AK, bool BKM, bool M16 = false>
 void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
   // 0 auto, 1 V256, 2 V256S, 5 V192, 7 V192S8
   const int sel = (g_gemm_mode >> 4) & 7;
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k);
   int v = sel;
+  if constexpr (AK && BKM) {
+    // wide outputs (N > 512; cfm_gemm_set_mode bit 22 also the d-wide ones) on the persistent warp-specialised kernel:
+    // 192 x 128 tiles, one workgroup per CU, the next tile's stages prefetched under the epilogue (bit 21: off, A/B)
+    const bool wide = p.N > 512 || (g_gemm_mode & 4194304);
+    if (v == 0 && wide && p.split_k == 1 && batch == 1 && !(g_gemm_mode & 2097152)) {
+      const int ntm = cdiv(p.M, 192), ntn = cdiv(p.N, BN);
+      const int grid = min(ntm * ntn, num_cus());
+      hipLaunchKernelGGL((gemm_wsp_kernel<192, 2, 4, 4, 3>), dim3(grid), dim3(768), 0, s, p, oa, ob, ntm, ntn);
+      return;
+    }
+  }
   if constexpr (AK) {
     // auto: outputs <= 512 columns (the encoder's d-wide outputs) take the 192-row tiles: 63 x 4 = 252
     // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
