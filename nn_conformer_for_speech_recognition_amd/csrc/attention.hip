@@ -222,20 +222,25 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
   float m = -INFINITY, l = 0.f;
   const float c = p.scale * LOG2E;
   const int qi = q0 + (lane & 31);
+  // Software-pipelined over key tiles: the S = K Q^T MFMAs of tile kt + 1 are issued before tile kt's softmax
+  // VALU, so they run on the matrix pipe while the wave works through the exponentials and the dropout hashes
+  // (the loop is unrolled by two so the two score buffers keep static register names).  The dropout keep scale
+  // is applied once to the output (o * keep / l), not to every P entry (no mask path: mask words are only read
+  // when cfm_attn_dropmask is in use, which takes the plain order below).
   const bool pm = p.drop_p > 0.f && p.qm;
-  uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
-  for (int kt = 0; kt < nkt; ++kt) {
+  const bool late = p.drop_p > 0.f && !pm;
+  auto qk = [&](int kt, f32x16& s0, f32x16& s1) {
     const bf16* sK = sKall + kt * TILE * KS;
-    const bf16* sV = sVall + kt * TILE * KS;
-    const uint32_t wcur = wnext;
-    if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
-    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
+    s0 = (f32x16){0};
+    s1 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qf[s], s0, 0, 0, 0);
       s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qf[s], s1, 0, 0, 0);
     }
-    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey, wcur);
+  };
+  auto pv = [&](int kt, const f32x16& s0, const f32x16& s1) {
+    const bf16* sV = sVall + kt * TILE * KS;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -245,10 +250,39 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
         o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 32, lane), pf, o1, 0, 0, 0);
       }
     }
+  };
+  if (pm) {
+    uint32_t wnext = qm_word(p, b, h, 0, qi, hh);
+    for (int kt = 0; kt < nkt; ++kt) {
+      const uint32_t wcur = wnext;
+      if (kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
+      f32x16 s0, s1;
+      qk(kt, s0, s1);
+      softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey, wcur);
+      pv(kt, s0, s1);
+    }
+  } else {
+    f32x16 sa0, sa1, sb0, sb1;
+    qk(0, sa0, sa1);
+    for (int kt = 0; kt < nkt; kt += 2) {
+      const bool n1 = kt + 1 < nkt;
+      if (n1) qk(kt + 1, sb0, sb1);
+      __builtin_amdgcn_sched_barrier(0);
+      softmax_tile<true>(p, sa0, sa1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep,
+                         dkey, 0u);
+      pv(kt, sa0, sa1);
+      if (n1) {
+        if (kt + 2 < nkt) qk(kt + 2, sa0, sa1);
+        __builtin_amdgcn_sched_barrier(0);
+        softmax_tile<true>(p, sb0, sb1, o0, o1, m, l, c, (kt + 1) * TILE, len, kt + 1 == nkt - 1, b, h, qi, hh, dthr,
+                           dkeep, dkey, 0u);
+        pv(kt + 1, sb0, sb1);
+      }
+    }
   }
   __syncthreads();     // every wave is done with K/V: the images become the epilogue staging
   float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
-  const float inv = 1.f / l;
+  const float inv = (late ? dkeep : 1.f) / l;
   if (p.dbg & 4) {   // timing experiment: no epilogue stores
     float t = 0.f;
 #pragma unroll

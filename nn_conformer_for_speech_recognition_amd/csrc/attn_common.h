@@ -203,6 +203,9 @@ __device__ void store_transposed(float* stage, const f32x16& a0, const f32x16& a
 // running max kept in scaled log2 units (c = scale * log2 e > 0, so max(c s) = c max(s)), p = 2^(c s - m) as
 // one FMA + v_exp; rescales o0/o1 and l; attention dropout applied to p (the returned P is dropped/scaled,
 // l stays the undropped sum, as nn.MultiheadAttention: dropout after the softmax).
+// LATE: the dropout keep scale 1 / (1 - p) is NOT applied to P here (dropped entries are zeroed by one select per
+// score); the caller multiplies it into the output once per element instead (o * keep / l).
+template <bool LATE = false>
 __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16& s1, f32x16& o0, f32x16& o1,
                                              float& m, float& l, float c, int kbase, int len, bool tail, int b,
                                              int h, int qi, int hh, uint32_t dthr, float dkeep, uint32_t dkey,
@@ -247,11 +250,19 @@ __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16&
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
       const int k0 = acc_row(r, hh);
-      float m0, m1, m2, m3;
-      dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
-      dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
-      s0[r] *= m0; s0[r + 1] *= m1;
-      s1[r] *= m2; s1[r + 1] *= m3;
+      if constexpr (LATE) {
+        const uint32_t h0 = cfm_mix32((rowj + (k0 >> 1)) ^ dkey), h1 = cfm_mix32((rowj + (k0 >> 1) + 16) ^ dkey);
+        s0[r] = (h0 & 0xFFFFu) >= dthr ? s0[r] : 0.f;
+        s0[r + 1] = (h0 >> 16) >= dthr ? s0[r + 1] : 0.f;
+        s1[r] = (h1 & 0xFFFFu) >= dthr ? s1[r] : 0.f;
+        s1[r + 1] = (h1 >> 16) >= dthr ? s1[r + 1] : 0.f;
+      } else {
+        float m0, m1, m2, m3;
+        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
+        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
+        s0[r] *= m0; s0[r + 1] *= m1;
+        s1[r] *= m2; s1[r + 1] *= m3;
+      }
     }
   }
 }

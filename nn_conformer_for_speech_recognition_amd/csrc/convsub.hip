@@ -106,8 +106,8 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const TI* __restrict__
     for (int r = 0; r < KK; ++r)
 #pragma unroll
       for (int q = 0; q < KK; ++q) win[r][q] = patch[r][q];
-#pragma unroll
-    for (int tt = 0; tt < TW; ++tt) {
+#pragma nounroll
+    for (int tt = 0; tt < TW; ++tt) {   // (not unrolled: win[][] is statically indexed inside the body)
       if (tt >= nt) break;
       if (tt > 0) {
 #pragma unroll

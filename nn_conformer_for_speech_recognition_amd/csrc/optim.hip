@@ -68,8 +68,7 @@ __global__ __launch_bounds__(EB) void ada_colpart(const AdaP* __restrict__ t, in
   // the wave's RB/4 rows: their sums stay in registers (lane j keeps row j's) and the row EMAs are updated
   // once after the loop -- a read-modify-write per row inside it serialised every row on a memory round trip
   float rsum = 0.f;
-#pragma unroll 2
-  for (int j = 0; j < RB / 4; ++j) {
+  for (int j = 0; j < RB / 4; ++j) {   // (the early exit keeps this loop rolled)
     const int r = r0 + wv + 4 * j;
     if (r >= r1) break;
     const float* g = q.g + ((long)b * q.R + r) * q.C;
