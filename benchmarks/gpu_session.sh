@@ -21,7 +21,11 @@ for s in "$@"; do
   case $s in
     fulldepth) run fulldepth 900 "$PYT -s tests/test_gpu_fulldepth.py" ;;
     gputests) run gputests 900 "$PYT -q -m gpu tests --ignore=tests/test_gpu_fulldepth.py" ;;
-    dgemm) run dgemm 300 "python -u benchmarks/dgemm_family.py" ;;
+    dgemm) run dgemm 300 "python -u benchmarks/dgemm_family.py && python -u benchmarks/dgemm_family.py --mode 1048579 && python -u benchmarks/dgemm_family.py --mode 524291 && python -u benchmarks/dgemm_family.py --mode 4194307" ;;
+    wide) run wide 300 "python -u benchmarks/wide_gemm.py --modes 3,2097155" ;;
+    wgrad) run wgrad 300 "python -u benchmarks/wgrad_modes.py --modes 3,8388611" ;;
+    attn) run attn 300 "python -u benchmarks/attn_probe.py" ;;
+    ktests) run ktests 900 "$PYT -q tests/test_gpu_kernels.py tests/test_gpu_attention.py tests/test_gpu_conformer.py tests/test_gpu_fulldepth.py tests/test_gpu_frontfold.py tests/test_gpu_graph.py" ;;
     bench) run bench 600 "python -u bench.py --gpus 1 --steps 20 --warmup 5" ;;
     benchL60) run benchL60 600 "python -u bench.py --config L60 --steps 10 --warmup 3 --no-cpu-baseline" ;;
     pmc_dgemm) run pmc_dgemm 900 "bash benchmarks/pmc_dgemm.sh $OUT 5" ;;

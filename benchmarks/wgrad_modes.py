@@ -1,0 +1,63 @@
+"""The grouped weight-gradient launch of one L15 backward (17 layers x 8 GEMMs, M = 11,936 tokens) under several
+cfm_gemm_set_mode values (interleaved rounds, HIP events).
+    python benchmarks/wgrad_modes.py [--modes 3,8388611] [--layers 17]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nn_conformer_for_speech_recognition_amd import _lib, ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--modes", default="3,8388611")
+    ap.add_argument("--layers", type=int, default=17)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    modes = [int(m) for m in a.modes.split(",")]
+    M, d, F = 32 * 373, 512, 2048
+    g = torch.Generator(device="cuda").manual_seed(0)
+
+    def rn(*s):
+        return torch.randn(*s, device="cuda", generator=g).to(torch.bfloat16)
+    # per layer (dY, X): FFN down / up x2, QKV, out-proj, pointwise conv 1 / 2 (N, K) = dW shape
+    shapes = [(d, F), (F, d)] * 2 + [(3 * d, d), (d, d), (2 * d, d), (d, d)]
+    acts = {n: rn(M, n) for n in {d, F, 2 * d, 3 * d}}
+    pairs = [(acts[n], acts[k]) for _ in range(a.layers) for n, k in shapes]
+    fl = sum(2.0 * M * dy.shape[1] * x.shape[1] for dy, x in pairs)
+    res = {m: [] for m in modes}
+    grps = {}
+    for _ in range(a.reps):
+        for m in modes:
+            _lib.call("cfm_gemm_set_mode", m)
+            grp = grps.setdefault(m, ops.WgradGroup())
+
+            def run():
+                for dy, x in pairs:
+                    grp.add(dy, x)
+                grp.flush()
+            for _ in range(2):
+                run()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(5):
+                run()
+            e.record()
+            torch.cuda.synchronize()
+            res[m].append(s.elapsed_time(e) / 5)
+    _lib.call("cfm_gemm_set_mode", 3)
+    out = {}
+    for m in modes:
+        t = sorted(res[m])[len(res[m]) // 2]
+        out[m] = round(t, 3)
+        print(f"mode {m:9d}: {t:7.3f} ms  {fl / t / 1e9:6.0f} TF/s  {fl / t / 1e9 / 2500:.3f} of peak")
+    print("WGRAD " + json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

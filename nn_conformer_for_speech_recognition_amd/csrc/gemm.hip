@@ -1783,13 +1783,181 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   return cfm::check_launch("cfm_gemm");
 }
 
+// ---------------------------------------------------------------- warp-specialised grouped weight gradients
+// The grouped weight-gradient launch (dW = dY^T X over the tokens, MN-major operands read through
+// ds_read_b64_tr_b16) with the ws kernel's roles: 4 loader waves issue every stage's LDS-DMA and, while the
+// compute waves run, fold the staged dY tile into the bias-gradient column sums (they idle otherwise); 8 compute
+// waves of 64 x 64 (32x32x16 MFMA) read the next 16-deep step's fragments while the current MFMAs run.  256 x 128
+// tiles (a 64 x 128 wave tile would not fit the 12-wave register budget), BK 32, 4-deep ring.  cfm_gemm_set_mode
+// bit 23 (A/B against the 256 x 256 shared-DMA kernel).
+constexpr int WSG_BN = 128;
+template <int NST>
+__global__ __launch_bounds__(12 * 64) void gemm_wsg_kernel(GemmP p0, GatherA ga) {
+  constexpr int BMt = 256, BNt = WSG_BN, BKt = 32, WM = 4, WN = 2, NC = WM * WN, NL = 4;
+  constexpr int ABYTES = BMt * BKt * 2, BBYTES = BNt * BKt * 2, STAGE = ABYTES + BBYTES;
+  constexpr int AP = ABYTES / 1024, BP = BBYTES / 1024, PW = (AP + BP) / NL;
+  static_assert(PW * NL == AP + BP, "whole DMA pieces per loader");
+  constexpr int FM = BMt / WM / 32, FN = BNt / WN / 32;
+  constexpr int EPS = BNt + 4, CPW = BNt / 8, CR = 128;             // epilogue: 128-row chunks
+  constexpr int RING = NST * STAGE, EPI = CR * EPS * 4;
+  constexpr int ACH = BMt / 8, RG = NL * 64 / ACH;                    // column sums: 8-column chunk x row group
+  constexpr int RED = EPI;                                            // their partials: after the staging
+  static_assert(RED + RG * BMt * 4 <= (RING > EPI ? RING : EPI), "column-sum partials fit");
+  __shared__ __attribute__((aligned(1024))) char lds[RING > EPI ? RING : EPI];
+  GemmP p = p0;
+  PipeOp oa, ob;
+  int tm, tn;
+  group_task(ga, p, oa, ob, tm, tn);
+  p.probe = p0.probe;
+  probe_begin(p.probe);
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = tm * BMt, n0 = tn * BNt;
+  const int nk = (p.K + BKt - 1) / BKt;
+  const bool loader = wid >= NC;
+  const bool acs = p.acs_slab != nullptr && tn == 0;
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x16){0};
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int acs_c = (tid - NC * 64) % ACH, acs_r = (tid - NC * 64) / ACH;
+  if (loader) {
+    const int lw = wid - NC;
+    const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, 0), rb = pipe_rsrc(ob, 0);
+    unsigned off[PW];
+    int ldo[PW];
+    bool isa[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int q = lw + NL * i;
+      isa[i] = q < AP;
+      const int qq = isa[i] ? q : q - AP;
+      off[i] = isa[i] ? pipe_src<false, BMt, BKt>(oa, qq * 64 + lane, m0, 0)
+                      : pipe_src<false, BNt, BKt>(ob, qq * 64 + lane, n0, 0);
+      ldo[i] = (isa[i] ? 0 : ABYTES) + qq * 1024;
+    }
+    const unsigned stepa = (unsigned)(BKt * oa.ld * 2), stepb = (unsigned)(BKt * ob.ld * 2);
+    auto issue = [&](int kt) {
+#pragma unroll
+      for (int i = 0; i < PW; ++i)
+        dma16(isa[i] ? ra : rb, lds + (kt % NST) * STAGE + ldo[i], off[i] + kt * (isa[i] ? stepa : stepb));
+    };
+    auto wait_stage = [&](int s, int last) {
+      const int younger = min(NST - 2, last - s);
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto colsum = [&](int kt) {       // the staged dY tile's column sums (chunk c of k-row k at slot c ^ 4(k & 3))
+      const char* sa = lds + (kt % NST) * STAGE;
+#pragma unroll
+      for (int kq = 0; kq < BKt / RG; ++kq) {
+        const int k = acs_r + kq * RG;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + k * (BMt * 2) + 16 * (acs_c ^ (4 * (k & 3))));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += (float)v[e];
+      }
+    };
+    for (int s = 0; s < NST - 1 && s < nk; ++s) issue(s);
+    int last = min(NST - 2, nk - 1);
+    wait_stage(0, last);
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt + 1 < nk; ++kt) {
+      wait_stage(kt + 1, last);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int kn = kt + NST - 1;
+      if (kn < nk) {
+        issue(kn);
+        last = kn;
+      }
+      if (acs) colsum(kt);          // stage kt stays resident until the barrier after stage kt + NST - 2
+    }
+    if (acs) colsum(nk - 1);
+  } else {
+    const int wm = wid / WN, wn = wid % WN;
+    bf16x8 af[2][FM], bfr[2][FN];
+    auto read = [&](bf16x8 (&fa)[FM], bf16x8 (&fb)[FN], int kt, int sub) {
+      const char* sa = lds + (kt % NST) * STAGE;
+      const char* sb = sa + ABYTES;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = pipe_frag<false, BNt, BKt>(sb, wn * FN * 32 + 32 * j, 16 * sub, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = pipe_frag<false, BMt, BKt>(sa, wm * FM * 32 + 32 * i, 16 * sub, lane);
+    };
+    auto mma = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN]) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    };
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read(af[0], bfr[0], 0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      read(af[1], bfr[1], kt, 1);
+      mma(af[0], bfr[0]);
+      if (kt + 1 < nk) {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        read(af[0], bfr[0], kt + 1, 0);
+      }
+      mma(af[1], bfr[1]);
+    }
+  }
+  __syncthreads();   // every DMA landed (the loaders' last wait was vmcnt(0)), every fragment read consumed
+  float* st = reinterpret_cast<float*>(lds);
+  float* red = reinterpret_cast<float*>(lds + RED);
+  const int wm = wid / WN, wn = wid % WN;
+#pragma nounroll
+  for (int c = 0; c < BMt / CR; ++c) {
+    if (!loader && (wm * FM * 32) / CR == c) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            st[(wm * FM * 32 - c * CR + 32 * i + accr<false>(r, lane)) * EPS + wn * FN * 32 + 32 * j + accc<false>(r, lane)] =
+                acc[i][j][r];
+    }
+    if (c == 0 && loader && acs) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[acs_r * BMt + acs_c * 8 + e] = csum[e];
+    }
+    __syncthreads();
+    if (!loader) {
+#pragma unroll
+      for (int it = 0; it < CR * CPW / (NC * 64); ++it) {
+        const int item = it * NC * 64 + tid;
+        const int row = item / CPW, c8 = (item % CPW) * 8;
+        const float4 lo = *reinterpret_cast<const float4*>(st + row * EPS + c8);
+        const float4 hi = *reinterpret_cast<const float4*>(st + row * EPS + c8 + 4);
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        epilogue_store8(p, 0, 0, m0 + c * CR + row, n0 + c8, v);
+      }
+    } else if (c == 0 && acs) {
+      const int t = tid - NC * 64;
+      if (t < BMt && m0 + t < p.M) {
+        float s = 0.f;
+        for (int g = 0; g < RG; ++g) s += red[g * BMt + t];
+        p.acs_slab[m0 + t] = s;
+      }
+    }
+    __syncthreads();
+  }
+  probe_end(p.probe);
+}
+
 CFM_EXPORT size_t cfm_wgrad_group_task_bytes(void) { return sizeof(WgTask); }
 // grouped weight-gradient launch: 256 x 256 output tiles, BK 32, 4-deep ring (half the dY panel re-reads of
 // 256 x 128; 17 layers 5.46 -> 4.89 ms, L15 step -0.8 ms same-box; 256 x 128 BK 32 two per CU, 256 x 128 BK 64 and
 // plain dispatch order measured slower and were removed in round 4; a 256 x 256 BK 64 double-buffered form spilled
 // and ran 2.4x slower)
 constexpr int WG_BN = 256;
-CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, WG_BN); }
+int wg_bn() { return (g_gemm_mode & 8388608) ? WSG_BN : WG_BN; }
+CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, wg_bn()); }
 
 // fill task i of a HOST table: dW (N x K, fp32) = dYᵀ X over M tokens, dY (M x N) / X (M x K) bf16
 // row-major; db (N, fp32, may be NULL) = sum_rows dY; tile0 = first workgroup id of the task
@@ -1808,7 +1976,7 @@ CFM_EXPORT int cfm_wgrad_group_fill(void* host_tab, int i, const void* dy, const
   t.oa = PipeOp{(const bf16*)dy, N, 0, N, (unsigned)((long)M * N * 2)};
   t.ob = PipeOp{(const bf16*)x, K, 0, K, (unsigned)((long)M * K * 2)};
   t.tile0 = tile0;
-  t.tiles_n = cdiv(K, WG_BN);
+  t.tiles_n = cdiv(K, wg_bn());
   reinterpret_cast<WgTask*>(host_tab)[i] = t;
   return CFM_OK;
 }
@@ -1821,8 +1989,11 @@ CFM_EXPORT int cfm_wgrad_group_probed(const void* dev_tab, int ntasks, long tota
   GatherA ga{};
   ga.group_tab = dev_tab;
   ga.group_n = ntasks;
-  hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 4, 1, false, false, 8, 2, false, true, false, WG_BN>),
-                     dim3((unsigned)total_tiles), dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
+  if (g_gemm_mode & 8388608)   // (tables filled under the same mode: 256 x WSG_BN tiles)
+    hipLaunchKernelGGL((gemm_wsg_kernel<4>), dim3((unsigned)total_tiles), dim3(768), 0, cfm::as_stream(stream), gp, ga);
+  else
+    hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 4, 1, false, false, 8, 2, false, true, false, WG_BN>),
+                       dim3((unsigned)total_tiles), dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
   return cfm::check_launch("cfm_wgrad_group");
 }
 

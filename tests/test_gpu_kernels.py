@@ -375,11 +375,14 @@ def test_wgrad_group_matches_per_gemm():
         assert _rel(db, rb) < 1e-5
 
 
-def test_wgrad_group_wide_tiles_vs_reference():
-    """The 256 x 256-tile grouped weight-gradient launch on the encoder's shapes, incl. the fused bias gradient and
-    ragged N / K, against fp32 references."""
-    g = torch.Generator().manual_seed(11)
-    M = 1000
+@pytest.mark.parametrize("mode", [3, 3 | 8388608])
+@pytest.mark.parametrize("M", [1000, 11936, 37])
+def test_wgrad_group_wide_tiles_vs_reference(gemm_mode, mode, M):
+    """The grouped weight-gradient launch (256 x 256 shared-DMA tiles, or with cfm_gemm_set_mode bit 23 the
+    warp-specialised 256 x 128 kernel) on the encoder's shapes, incl. the fused bias gradient, ragged N / K and a
+    token count that is not a multiple of the 32-deep step, against fp32 references."""
+    gemm_mode(mode)
+    g = torch.Generator().manual_seed(11 + M)
     shapes = [(2048, 512), (512, 2048), (1536, 512), (512, 512), (136, 264)]
     ops_ = [(torch.randn(M, N, generator=g).to(DEV, torch.bfloat16), torch.randn(M, K, generator=g).to(DEV, torch.bfloat16))
             for N, K in shapes]
@@ -391,6 +394,27 @@ def test_wgrad_group_wide_tiles_vs_reference():
         ref = d.float().T @ x.float()
         assert _rel(a, ref) < 1e-5
         assert _rel(ab, d.float().sum(0)) < 1e-5
+
+
+def test_wgrad_group_warp_specialised_bitwise(gemm_mode):
+    """Both grouped kernels accumulate every dW element over the same 16-deep token steps in the same order on the
+    same 32x32x16 MFMA: bit-identical weight gradients (the bias column sums differ only in summation order)."""
+    g = torch.Generator().manual_seed(5)
+    M = 11936
+    shapes = [(2048, 512), (512, 2048), (1536, 512), (512, 512)]
+    ops_ = [(torch.randn(M, N, generator=g).to(DEV, torch.bfloat16), torch.randn(M, K, generator=g).to(DEV, torch.bfloat16))
+            for N, K in shapes]
+    outs = []
+    for mode in (3, 3 | 8388608):
+        gemm_mode(mode)
+        grp = ops.WgradGroup()
+        res = [grp.add(d, x) for d, x in ops_]
+        grp.flush()
+        torch.cuda.synchronize()
+        outs.append([(a.clone(), b.clone()) for a, b in res])
+    for (a0, b0), (a1, b1) in zip(*outs):
+        assert torch.equal(a0, a1)
+        assert _rel(b1, b0) < 1e-6
 
 
 @pytest.mark.parametrize("ws", [3, 3 | 1048576])
