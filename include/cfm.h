@@ -347,23 +347,6 @@ int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* dout, const 
                         const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                         void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H,
                         int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream);
-/* Attention dropout keep bits, computed once per forward instead of per element in the forward and dQ
- * kernels: the same counter-based hash as the per-element path (so the masks are identical), stored
- * query-major (one 32-bit word per lane per 64-key tile; the dK/dV kernels keep hashing in-kernel).
- * mask: cfm_attn_dropmask_bytes(B, T, H) bytes; nothing is written when
- * drop_p == 0.  The _m entry points take it (NULL = hash per element, as cfm_attn_fwd / cfm_attn_bwd);
- * kernels without a mask path hash, with the same result.  Replaces the attention-weight nn.Dropout of
- * nn.MultiheadAttention (torchaudio ConformerLayer self_attn, dropout = hparams.dropout). */
-size_t cfm_attn_dropmask_bytes(int B, int T, int H);
-int cfm_attn_dropmask(void* mask, int B, int T, int H, float drop_p, uint64_t seed, void* stream);
-int cfm_attn_fwd_m(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
-                   const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
-                   float drop_p, uint64_t seed, const void* mask, void* stream);
-int cfm_attn_bwd_m(const void* qkv, const void* o, const void* dout, const float* lse,
-                   const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
-                   void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
-                   int dtype, float drop_p, uint64_t seed, float* ws, int d_ready, const void* mask,
-                   void* stream);
 
 /* ---------------------------------------------------------------- ConvSubSampling
  * lib/convsubsampling.py:16-45: Conv2d(1->C1, 7x7, s2) -> Conv2d(C1->C2, 3x3, s2), no padding.

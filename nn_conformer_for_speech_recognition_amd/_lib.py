@@ -140,11 +140,6 @@ _SIGS = {
     "cfm_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                              c_int, c_int, c_int, c_float, c_u64, c_void_p]),
     "cfm_attn_bwd_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
-    "cfm_attn_dropmask_bytes": (c_size_t, [c_int, c_int, c_int]),
-    "cfm_attn_dropmask": (c_int, [c_void_p, c_int, c_int, c_int, c_float, c_u64, c_void_p]),
-    "cfm_attn_fwd_m": (c_int, [c_void_p] * 7 + [c_int] * 5 + [c_float, c_u64, c_void_p, c_void_p]),
-    "cfm_attn_bwd_m": (c_int, [c_void_p] * 12 + [c_int] * 5 + [c_float, c_u64, c_void_p, c_int, c_void_p,
-                                                                  c_void_p]),
     "cfm_attn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
                              c_u64, c_void_p, c_void_p]),

@@ -261,20 +261,16 @@ def _mha_fwd(x, P, R, cfg, seed, lens):
         pos = ops.linear(_w(cfg.pe, cd), wpos)          # (2T-1, d) projected table (no bias)
         pu = R[1].reshape(-1).float().contiguous()
         pv = R[2].reshape(-1).float().contiguous()
-    # attention-dropout keep bits once per step (cfm_attn_dropmask; opt-in CFM_ENABLE=dropmask: measured no faster
-    # than the in-kernel hashes at L15 / L60, profiles/r03/dropmask_ab.txt)
-    mask = (ops.attn_dropmask(B, T, H, cfg.p, seed, qkv.device)
-            if cfg.p > 0 and cd == torch.bfloat16 and "dropmask" in ops.ENABLED else None)
-    o, lse = ops.attn_fwd(qkv, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed, mask=mask)
+    o, lse = ops.attn_fwd(qkv, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
     y = _fp8_linear(o, cfg, 10, bias=P[11], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, residual=x)
     if y is None:
         y = ops.linear(o, wout, P[11], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, residual=x)
     _chk("mha_fwd", xn, mu, rs, qkv, pos, o, lse, y)
-    return y, (xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv, mask)
+    return y, (xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv)
 
 
 def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=None):
-    xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv, mask = sv
+    xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv = sv
     cd = cfg.cd
     B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
     g4 = _g2(g, g2, "mha", cfg, seed)
@@ -288,7 +284,7 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
         Dh = None
         do = ops.linear_dgrad(g4, wout, wt=wt)
     dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed,
-                                        D=Dh, mask=mask)
+                                        D=Dh)
     if cfg.rel:
         rgrads[0] = ops.linear_wgrad(_w(dpos, cd), _w(cfg.pe, cd))
         rgrads[1] = dpu.view(H, d // H)

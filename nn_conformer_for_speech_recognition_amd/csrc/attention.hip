@@ -25,11 +25,10 @@ size_t attn_simt_ws_bytes(int B, int T, int H);
 size_t attn_rel_ws_bytes(int B, int T, int H, int dk);
 extern int g_rel_mode;   // attention_rel.hip: cfm_attn_set_mode's bits for the rel-pos kernels
 int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len, const void* pos, const float* pu,
-                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s,
-                        const void* mask);
+                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s);
 int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, const int32_t* len, const void* pos,
                         const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
-                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s, const void* mask);
+                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s);
 int attn_simt_bwd_launch(const void*, const void*, const void*, const float*, const int32_t*, const void*,
                          const float*, const float*, void*, float*, float*, float*, int, int, int, int, int, float,
                          uint64_t, float*, hipStream_t);
@@ -225,10 +224,8 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
   // Software-pipelined over key tiles: the S = K Q^T MFMAs of tile kt + 1 are issued before tile kt's softmax
   // VALU, so they run on the matrix pipe while the wave works through the exponentials and the dropout hashes
   // (the loop is unrolled by two so the two score buffers keep static register names).  The dropout keep scale
-  // is applied once to the output (o * keep / l), not to every P entry (no mask path: mask words are only read
-  // when cfm_attn_dropmask is in use, which takes the plain order below).
-  const bool pm = p.drop_p > 0.f && p.qm;
-  const bool late = p.drop_p > 0.f && !pm;
+  // is applied once to the output (o * keep / l), not to every P entry.
+  const bool late = p.drop_p > 0.f;
   auto qk = [&](int kt, f32x16& s0, f32x16& s1) {
     const bf16* sK = sKall + kt * TILE * KS;
     s0 = (f32x16){0};
@@ -251,33 +248,20 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
       }
     }
   };
-  if (pm) {
-    uint32_t wnext = qm_word(p, b, h, 0, qi, hh);
-    for (int kt = 0; kt < nkt; ++kt) {
-      const uint32_t wcur = wnext;
-      if (kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
-      f32x16 s0, s1;
-      qk(kt, s0, s1);
-      softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey, wcur);
-      pv(kt, s0, s1);
-    }
-  } else {
-    f32x16 sa0, sa1, sb0, sb1;
-    qk(0, sa0, sa1);
-    for (int kt = 0; kt < nkt; kt += 2) {
-      const bool n1 = kt + 1 < nkt;
-      if (n1) qk(kt + 1, sb0, sb1);
+  f32x16 sa0, sa1, sb0, sb1;
+  qk(0, sa0, sa1);
+  for (int kt = 0; kt < nkt; kt += 2) {
+    const bool n1 = kt + 1 < nkt;
+    if (n1) qk(kt + 1, sb0, sb1);
+    __builtin_amdgcn_sched_barrier(0);
+    softmax_tile<true>(p, sa0, sa1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
+    pv(kt, sa0, sa1);
+    if (n1) {
+      if (kt + 2 < nkt) qk(kt + 2, sa0, sa1);
       __builtin_amdgcn_sched_barrier(0);
-      softmax_tile<true>(p, sa0, sa1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep,
-                         dkey, 0u);
-      pv(kt, sa0, sa1);
-      if (n1) {
-        if (kt + 2 < nkt) qk(kt + 2, sa0, sa1);
-        __builtin_amdgcn_sched_barrier(0);
-        softmax_tile<true>(p, sb0, sb1, o0, o1, m, l, c, (kt + 1) * TILE, len, kt + 1 == nkt - 1, b, h, qi, hh, dthr,
-                           dkeep, dkey, 0u);
-        pv(kt + 1, sb0, sb1);
-      }
+      softmax_tile<true>(p, sb0, sb1, o0, o1, m, l, c, (kt + 1) * TILE, len, kt + 1 == nkt - 1, b, h, qi, hh, dthr,
+                         dkeep, dkey);
+      pv(kt + 1, sb0, sb1);
     }
   }
   __syncthreads();     // every wave is done with K/V: the images become the epilogue staging
@@ -330,14 +314,8 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
   const int nks = (len + 31) / 32;
   const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
   const uint32_t hq = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)qi) * T2 + (uint32_t)(2 * hh);
-  const bool pm = p.drop_p > 0.f && p.qm;
-  uint32_t wcur = 0u, wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int ks = 0; ks < nks; ++ks) {
     const int k0 = ks * 32;
-    if (pm && (ks & 1) == 0) {       // a new 64-key tile: its word was loaded a tile ahead
-      wcur = wnext;
-      if (2 * ((ks >> 1) + 1) < nks) wnext = qm_word(p, b, h, (ks >> 1) + 1, qi, hh);
-    }
     f32x16 s0 = (f32x16){0}, d0 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -346,11 +324,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
       if (s == 1) __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (pm) {
-      const uint32_t w = wcur >> (16 * (ks & 1));
-#pragma unroll
-      for (int r = 0; r < 16; ++r) d0[r] *= mbit(w, r, dkeep);
-    } else if (p.drop_p > 0.f) {
+    if (p.drop_p > 0.f) {
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
         const uint32_t hsh = cfm_mix32(
@@ -382,94 +356,6 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
   if (q0 < p.T)
     store_transposed(stage, a0, a1, p.scale, dqkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, q0, min(32, p.T - q0),
                      p.dk, lane);
-}
-
-// dK, dV: grid (B*H), 4 waves (one per SIMD: the kernel keeps ~400 registers live); the head's whole
-// Q and dO (and lse, D) are staged once; wave w handles key blocks w, w+4, ... over all query tiles
-constexpr int DKDV_WAVES = 4;
-__global__ __launch_bounds__(64 * DKDV_WAVES) void attn_bwd_dkdv_head_kernel(AttnM p, const bf16* __restrict__ dout,
-                                                                             const float* __restrict__ lse,
-                                                                             const float* __restrict__ Dg,
-                                                                             bf16* __restrict__ dqkv) {
-  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
-  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
-  const float dkeep = drop_keep_scale(dthr);
-  extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
-  const int len = p.len[b];
-  const int nqt = (p.T + TILE - 1) / TILE, Tq = nqt * TILE;
-  bf16* sQall = hsm;
-  bf16* sGall = hsm + (long)Tq * KS;
-  float* sL = reinterpret_cast<float*>(sGall + (long)Tq * KS);      // [Tq] lse * log2(e) (+inf past T)
-  float* sD = sL + Tq;                                              // [Tq] D
-  float* stage = sD + Tq + wv * 32 * 65;
-  const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
-  head_stage(p, qbase, dout + (long)b * p.T * p.HD + h * p.dk, p.D3, p.HD, Tq, sQall, sGall, tid, blockDim.x);
-  for (int i = tid; i < Tq; i += blockDim.x) {
-    sL[i] = i < p.T ? lse[((long)b * p.H + h) * p.T + i] * LOG2E : INFINITY;
-    sD[i] = i < p.T ? Dg[((long)b * p.H + h) * p.T + i] : 0.f;
-  }
-  __syncthreads();
-  const float c = p.scale * LOG2E;
-  const int nkb = (p.T + 31) / 32;
-  bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
-  for (int kb = wv; kb < nkb; kb += DKDV_WAVES) {
-    const int k0w = kb * 32;
-    const int kj = k0w + (lane & 31);
-    const bool kvalid = kj < len;
-    bf16x8 kf[4], vf[4];
-    load_bfrags(p, qbase + p.HD, p.D3, kj, p.T, kf, lane);
-    load_bfrags(p, qbase + 2 * p.HD, p.D3, kj, p.T, vf, lane);
-    f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
-    const int nq = k0w < len ? nqt : 0;      // key blocks past len: zero gradients
-    for (int qt = 0; qt < nq; ++qt) {
-      const bf16* sQ = sQall + qt * TILE * KS;
-      const bf16* sG = sGall + qt * TILE * KS;
-      const float* tL = sL + qt * TILE;
-      const float* tD = sD + qt * TILE;
-      f32x16 s0 = (f32x16){0}, s1 = (f32x16){0}, g0 = (f32x16){0}, g1 = (f32x16){0};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQ, 0, 16 * s, lane), kf[s], s0, 0, 0, 0);
-        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQ, 32, 16 * s, lane), kf[s], s1, 0, 0, 0);
-        g0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sG, 0, 16 * s, lane), vf[s], g0, 0, 0, 0);
-        g1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sG, 32, 16 * s, lane), vf[s], g1, 0, 0, 0);
-      }
-      f32x16 pd0, pd1;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qa = acc_row(r, hh), qb = 32 + qa;
-        const int qia = qt * TILE + qa, qib = qt * TILE + qb;
-        const float pa = kvalid ? fast_exp2(s0[r] * c - tL[qa]) : 0.f;   // lse = +inf for q >= T
-        const float pb = kvalid ? fast_exp2(s1[r] * c - tL[qb]) : 0.f;
-        float ma = 1.f, mb = 1.f;
-        if (p.drop_p > 0.f) {
-          ma = dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qia, kj));
-          mb = dropout_keyed(dthr, dkeep, dkey, didx(p, b, h, qib, kj));
-        }
-        pd0[r] = pa * ma;
-        pd1[r] = pb * mb;
-        s0[r] = pa * (g0[r] * ma - tD[qa]);
-        s1[r] = pb * (g1[r] * mb - tD[qb]);
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16x8 pf = acc2frag(t == 0 ? pd0 : pd1, s);
-          const bf16x8 sf = acc2frag(t == 0 ? s0 : s1, s);
-          dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s, 0, lane), pf, dv0, 0, 0, 0);
-          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s, 32, lane), pf, dv1, 0, 0, 0);
-          dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQ, 32 * t + 16 * s, 0, lane), sf, dk0, 0, 0, 0);
-          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQ, 32 * t + 16 * s, 32, lane), sf, dk1, 0, 0, 0);
-        }
-      }
-    }
-    const int nvalid = min(32, p.T - k0w);
-    store_transposed(stage, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
-    store_transposed(stage, dv0, dv1, 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
-  }
 }
 
 // write a wave's 64(d) x 32(key) f32 accumulator pair transposed into bf16 rows, straight from the
@@ -561,17 +447,13 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
         sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, q0, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       bf16x8 pf[2];
-      const bool pre = drop && p.km != nullptr;     // precomputed keep bits: this lane's 16 bits of the step
-      unsigned bits = pre ? (km_word(p, b, h, qt, kj) >> (16 * hh)) & 0xFFFFu : 0u;
+      unsigned bits = 0u;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {          // registers 4g .. 4g+3 = queries q0 + 8g + 4hh + 0..3
         const float4 Lg = *reinterpret_cast<const float4*>(sL + q0 + 8 * g + 4 * hh);
         const float Lr[4] = {Lg.x, Lg.y, Lg.z, Lg.w};
         float mk[4] = {1.f, 1.f, 1.f, 1.f};
-        if (pre) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) mk[e] = mbit(bits, 4 * g + e, dkeep);
-        } else if (drop) {
+        if (drop) {
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
             // (the wave-uniform offset through readfirstlane: otherwise the per-register bases are
@@ -650,11 +532,6 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
 size_t dkdv_wave_lds_bytes(int T) {
   const size_t nq = (size_t)cdiv(T, 32), rows = nq * 32;
   return 2 * rows * KS * sizeof(bf16) + 2 * rows * sizeof(float) + nq * nq * 64 * sizeof(unsigned short);
-}
-
-size_t dkdv_head_lds_bytes(int T) {
-  const size_t rows = (size_t)cdiv(T, TILE) * TILE;
-  return 2 * rows * KS * sizeof(bf16) + 2 * rows * sizeof(float) + (size_t)DKDV_WAVES * 32 * 65 * sizeof(float);
 }
 
 // ------------------------------------------------------------------------------------ D = rowsum(dO*O)
@@ -882,8 +759,7 @@ bool use_mfma(int dtype, const void* pos, int dk) {
   return dtype == CFM_BF16 && dk <= DKP && (pos == nullptr || (g_attn_mode & 16) == 0);
 }
 
-// whole-head kernels: T <= HEAD_TMAX; cfm_attn_set_mode bit 0 forces the tiled kernels, bit 3 selects
-// the four-wave dK/dV kernel instead of the wave-per-key-block one (A/B)
+// whole-head kernels: T <= HEAD_TMAX; cfm_attn_set_mode bit 0 forces the tiled kernels (A/B, parity)
 bool use_head(int T) { return T <= HEAD_TMAX && (g_attn_mode & 1) == 0; }
 size_t head_lds_bytes(int T) {
   const size_t rows = (size_t)cdiv(T, TILE) * TILE;
@@ -892,71 +768,11 @@ size_t head_lds_bytes(int T) {
   return img > stage ? img : stage;
 }
 
-// ------------------------------------------------------------------------------------ dropout keep bits
-// The query-major keep bits (AttnM::qm) from the same counter-based hash as the per-element path (didx pairs,
-// cfm_mix32 with the step-salted key, 16 bits per element).  grid (ceil(2 Tq / 256), nkt, B*H): one thread per
-// word, 16 pair hashes, 32-bit index math.  (The dK/dV kernels keep hashing in-kernel: their DPP-shared hash
-// costs less than a second, key-major layout would.)
-__global__ __launch_bounds__(256) void attn_dropmask_kernel(AttnM p, uint32_t* __restrict__ qm, MaskGeo g) {
-  const uint64_t seed = salted_seed(p.seed, p.salt);
-  const uint32_t key = drop_key(seed, 0), thr = drop_thr(p.drop_p);
-  const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
-  const int f = blockIdx.x * 256 + threadIdx.x;
-  if (f >= 2 * g.Tq) return;
-  const int q = f >> 1, hh = f & 1, kt = blockIdx.y;
-  const uint32_t bh = blockIdx.z;
-  const uint32_t rowj = (bh * (uint32_t)p.T + (uint32_t)q) * T2 + (uint32_t)(32 * kt);
-  uint32_t w = 0;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      const uint32_t hs = cfm_mix32((rowj + (uint32_t)((32 * t + acc_row(r, hh)) >> 1)) ^ key);
-      w |= ((hs & 0xFFFFu) >= thr ? 1u : 0u) << (16 * t + r);
-      w |= ((hs >> 16) >= thr ? 1u : 0u) << (16 * t + r + 1);
-    }
-  qm[((long)(bh * g.nkt + kt) * g.Tq) * 2 + f] = w;
-}
-
 }  // namespace
-
-CFM_EXPORT size_t cfm_attn_dropmask_bytes(int B, int T, int H) {
-  const MaskGeo g = mask_geo(B, T, H);
-  return (size_t)(g.qwords + g.kwords) * sizeof(uint32_t);
-}
-
-CFM_EXPORT int cfm_attn_dropmask(void* mask, int B, int T, int H, float drop_p, uint64_t seed, void* stream) {
-  CFM_REQUIRE(mask, CFM_ERR_ARG, "null pointer");
-  CFM_REQUIRE(B > 0 && T > 0 && H > 0, CFM_ERR_SHAPE, "bad shape");
-  CFM_REQUIRE((double)B * H * T * (T + 1) < 8589934592.0, CFM_ERR_SHAPE, "attention dropout index space (2^33)");
-  if (drop_p <= 0.f) return CFM_OK;
-  const MaskGeo g = mask_geo(B, T, H);
-  AttnM p{};
-  p.B = B; p.T = T; p.H = H; p.drop_p = drop_p; p.seed = seed; p.salt = cfm::g_rng_salt;
-  hipLaunchKernelGGL(attn_dropmask_kernel, dim3((unsigned)cdiv(2 * g.Tq, 256), g.nkt, B * H), dim3(256), 0,
-                     cfm::as_stream(stream), p, (uint32_t*)mask, g);
-  return cfm::check_launch("cfm_attn_dropmask");
-}
-
-static int attn_fwd_impl(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
-                         const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
-                         float drop_p, uint64_t seed, void* stream, const void* mask);
 
 CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
                             const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
                             float drop_p, uint64_t seed, void* stream) {
-  return attn_fwd_impl(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, stream, nullptr);
-}
-
-CFM_EXPORT int cfm_attn_fwd_m(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
-                              const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
-                              float drop_p, uint64_t seed, const void* mask, void* stream) {
-  return attn_fwd_impl(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, stream, mask);
-}
-
-static int attn_fwd_impl(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
-                         const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,
-                         float drop_p, uint64_t seed, void* stream, const void* mask) {
   CFM_REQUIRE(qkv && o && lse && lengths, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0 && dk <= 1024, CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(!pos || (pos_u && pos_v), CFM_ERR_ARG, "rel-pos needs pos_u and pos_v");
@@ -967,11 +783,10 @@ static int attn_fwd_impl(const void* qkv, void* o, float* lse, const int32_t* le
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, dtype, drop_p, seed, s);
   if (pos)
-    return cfm::attn_rel_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, drop_p, seed, s, mask);
+    return cfm::attn_rel_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, drop_p, seed, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 6,
           cfm::g_rng_salt};
-  if (use_head(T)) set_mask(p, mask);     // the whole-head kernels read the bits; the tiled ones hash
   if (use_head(T)) {
     // LDS sized for the full padded length (lengths are device data; len <= T)
     hipLaunchKernelGGL(attn_fwd_head_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), head_lds_bytes(T), s, p, (bf16*)o,
@@ -991,8 +806,7 @@ CFM_EXPORT size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel, in
 static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const float* lse,
                          const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                          void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
-                         int dtype, float drop_p, uint64_t seed, float* ws, void* stream, bool d_ready,
-                         const void* mask = nullptr) {
+                         int dtype, float drop_p, uint64_t seed, float* ws, void* stream, bool d_ready) {
   CFM_REQUIRE(qkv && o && dout && lse && lengths && dqkv && ws, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0, CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(!pos || (pos_u && pos_v && dpos && dpos_u && dpos_v), CFM_ERR_ARG, "rel-pos grads need buffers");
@@ -1013,13 +827,9 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
                        (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
   if (pos)
     return cfm::attn_rel_bwd_launch(qkv, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H,
-                                    dk, drop_p, seed, ws, s, mask);
-  if (use_head(T) && (g_attn_mode & 8) == 0) set_mask(p, mask);   // whole-head dQ + wave dK/dV read the bits
-  if (use_head(T) && (g_attn_mode & 8) == 0)
+                                    dk, drop_p, seed, ws, s);
+  if (use_head(T))
     hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), dkdv_wave_lds_bytes(T), s, p,
-                       (const bf16*)dout, lse, ws, (bf16*)dqkv);
-  else if (use_head(T))
-    hipLaunchKernelGGL(attn_bwd_dkdv_head_kernel, dim3(B * H), dim3(64 * DKDV_WAVES), dkdv_head_lds_bytes(T), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);
   else
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse,
@@ -1047,15 +857,6 @@ CFM_EXPORT int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* d
                                    int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
   return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H, dk, dtype,
                        drop_p, seed, ws, stream, true);
-}
-
-CFM_EXPORT int cfm_attn_bwd_m(const void* qkv, const void* o, const void* dout, const float* lse,
-                              const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
-                              void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
-                              int dtype, float drop_p, uint64_t seed, float* ws, int d_ready, const void* mask,
-                              void* stream) {
-  return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H, dk, dtype,
-                       drop_p, seed, ws, stream, d_ready != 0, mask);
 }
 
 CFM_EXPORT int cfm_attn_set_mode(int mode) {

@@ -211,13 +211,9 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
     __syncthreads();
   }
   wait_prologue_loads();
-  const bool pm = p.drop_p > 0.f && p.qm;
-  uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int kt = 0; kt < nkt; ++kt) {
     const bf16* sK = skv + (kt & 1) * 2 * TILE * KS;
     const bf16* sV = sK + TILE * KS;
-    const uint32_t wcur = wnext;
-    if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
     if (kt + 1 < nkt) {
       tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
       tile_load<VEC>(p, b, (kt + 1) * TILE, vcol, rv, tid);
@@ -227,8 +223,8 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
     f32x16 s0, s1;
     scores_qlanes(sK, band_rows_q(sring, kt, wv), qu, qv, st, s0, s1, lane);
     // the non-rel kernels' online-softmax step (attn_common.h): masking only on the last key tile, the running max
-    // over raw scores (c > 0), exp2 as one FMA + v_exp, then the same dropout hash / keep bits as before
-    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey, wcur);
+    // over raw scores (c > 0), exp2 as one FMA + v_exp, then the same dropout hash as before
+    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -299,13 +295,9 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
     __syncthreads();
   }
   wait_prologue_loads();
-  const bool pm = p.drop_p > 0.f && p.qm;
-  uint32_t wnext = pm ? qm_word(p, b, h, 0, qi, hh) : 0u;
   for (int kt = 0; kt < nkt; ++kt) {
     const bf16* sK = skv + (kt & 1) * 2 * TILE * KS;
     const bf16* sV = sK + TILE * KS;
-    const uint32_t wcur = wnext;
-    if (pm && kt + 1 < nkt) wnext = qm_word(p, b, h, kt + 1, qi, hh);
     if (kt + 1 < nkt) {
       tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
       tile_load<VEC>(p, b, (kt + 1) * TILE, vcol, rv, tid);
@@ -321,14 +313,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
       d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 0, 16 * s, lane), gf[s], d0, 0, 0, 0);
       d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32, 16 * s, lane), gf[s], d1, 0, 0, 0);
     }
-    if (p.drop_p > 0.f && p.qm) {
-      const uint32_t w = wcur;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        d0[r] *= mbit(w, r, dkeep);
-        d1[r] *= mbit(w, 16 + r, dkeep);
-      }
-    } else if (p.drop_p > 0.f) {
+    if (p.drop_p > 0.f) {
       const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
@@ -577,11 +562,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
         tl[r] = tL[acc_row(r, hh)];
         td[r] = tD[acc_row(r, hh)];
       }
-      if (drop && p.km) {
-        const uint32_t wkm = km_word(p, b, h, 2 * qt + t, kj) >> (16 * hh);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mk[r] = mbit(wkm, r, dkeep);
-      } else if (drop) {
+      if (drop) {
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
           // dropout of (query of register r / r+1, key kj): lanes kj, kj^1 share one 32-bit hash per query
@@ -800,18 +781,16 @@ int g_rel_mode = 0;
 static bool rel_vec(const AttnM& p, const RelP& rp) { return p.vec && rp.pvec && p.dk == 64 && !(g_rel_mode & 64); }
 
 static AttnM make_attnm(const void* qkv, const void* dout, const int32_t* len, int B, int T, int H, int dk,
-                        float drop_p, uint64_t seed, const void* mask) {
+                        float drop_p, uint64_t seed) {
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, len, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), 0,
           g_rng_salt};
-  set_mask(p, mask);
   return p;
 }
 
 int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len, const void* pos, const float* pu,
-                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s,
-                        const void* mask) {
-  const AttnM p = make_attnm(qkv, qkv, len, B, T, H, dk, drop_p, seed, mask);
+                        const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s) {
+  const AttnM p = make_attnm(qkv, qkv, len, B, T, H, dk, drop_p, seed);
   const RelP rp = make_relp(pos, pu, pv, p.dk);
   if (rel_vec(p, rp))
     hipLaunchKernelGGL(attn_rel_fwd_kernel<true>, dim3(cdiv(p.T, 128), p.H, p.B), dim3(256), 0, s, p, rp, (bf16*)o, lse);
@@ -823,9 +802,8 @@ int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len
 // D (rowsum dO*O per head) must already be in ws[0 .. B*H*T)
 int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, const int32_t* len, const void* pos,
                         const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
-                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s,
-                        const void* mask) {
-  const AttnM p = make_attnm(qkv, dout, len, B, T, H, dk, drop_p, seed, mask);
+                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s) {
+  const AttnM p = make_attnm(qkv, dout, len, B, T, H, dk, drop_p, seed);
   const RelP rp = make_relp(pos, pu, pv, p.dk);
   const size_t d_bytes = ((size_t)p.B * p.H * p.T * sizeof(float) + 255) & ~(size_t)255;
   float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + d_bytes);

@@ -21,43 +21,7 @@ struct AttnM {
   bool vec;    // 16-B vector loads legal
   int dbg;     // timing experiments (cfm_attn_set_mode bits 1-2)
   const uint64_t* salt;   // bound dropout step counter or nullptr
-  // precomputed attention-dropout keep bits (cfm_attn_dropmask; nullptr: hash per element pair)
-  const uint32_t* qm;     // query-major: word (bh, kt, q, hh), bit 16 t + r = keep(q, 64 kt + 32 t + acc_row(r, hh))
-  const uint32_t* km;     // key-major:   word (bh, qs, k),     bit 16 hh + r = keep(32 qs + acc_row(r, hh), k)
-  int m_nkt, m_Tq, m_nqs, m_Tk;
 };
-
-// mask geometry of a (B, T, H) attention: 64-key tiles, 32-query steps, rows padded to 128
-struct MaskGeo {
-  int nkt, Tq, nqs, Tk;
-  long qwords, kwords;
-};
-inline MaskGeo mask_geo(int B, int T, int H) {
-  MaskGeo g;
-  g.nkt = (T + 63) / 64;
-  g.Tq = (T + 127) / 128 * 128;
-  g.nqs = 2 * g.nkt;
-  g.Tk = g.Tq;
-  g.qwords = (long)B * H * g.nkt * g.Tq * 2;
-  g.kwords = 0;   // (key-major words: not materialised; the dK/dV kernels hash in-kernel)
-  return g;
-}
-__device__ __forceinline__ uint32_t qm_word(const AttnM& p, int b, int h, int kt, int q, int hh) {
-  return p.qm[(((long)(b * p.H + h) * p.m_nkt + kt) * p.m_Tq + q) * 2 + hh];
-}
-__device__ __forceinline__ uint32_t km_word(const AttnM& p, int b, int h, int qs, int k) {
-  return p.km[((long)(b * p.H + h) * p.m_nqs + qs) * p.m_Tk + k];
-}
-// point p at the keep-bit mask (layout of cfm_attn_dropmask) when dropout is on and a mask is given
-inline void set_mask(AttnM& p, const void* mask) {
-  if (!mask || p.drop_p <= 0.f) return;
-  const MaskGeo g = mask_geo(p.B, p.T, p.H);
-  p.qm = (const uint32_t*)mask;
-  p.km = nullptr;
-  p.m_nkt = g.nkt; p.m_Tq = g.Tq; p.m_nqs = g.nqs; p.m_Tk = g.Tk;
-}
-// keep scale of bit `bit` of w
-__device__ __forceinline__ float mbit(uint32_t w, int bit, float keep) { return (w >> bit) & 1u ? keep : 0.f; }
 
 // attention-dropout element index: rows of an EVEN stride (T rounded up to even), so the keys 2m and
 // 2m+1 of one (query, key-pair) share one 32-bit hash (low / high 16 bits): kernels holding both keys of
@@ -208,8 +172,7 @@ __device__ void store_transposed(float* stage, const f32x16& a0, const f32x16& a
 template <bool LATE = false>
 __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16& s1, f32x16& o0, f32x16& o1,
                                              float& m, float& l, float c, int kbase, int len, bool tail, int b,
-                                             int h, int qi, int hh, uint32_t dthr, float dkeep, uint32_t dkey,
-                                             uint32_t w) {
+                                             int h, int qi, int hh, uint32_t dthr, float dkeep, uint32_t dkey) {
   if (tail && kbase + TILE > len) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -239,13 +202,7 @@ __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16&
     o0[r] *= alpha;
     o1[r] *= alpha;
   }
-  if (p.drop_p > 0.f && p.qm) {     // precomputed keep bits (cfm_attn_dropmask), w loaded a tile ahead
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] *= mbit(w, r, dkeep);
-      s1[r] *= mbit(w, 16 + r, dkeep);
-    }
-  } else if (p.drop_p > 0.f) {
+  if (p.drop_p > 0.f) {
     const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kbase) >> 1);   // even: 32-bit pair indices
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash

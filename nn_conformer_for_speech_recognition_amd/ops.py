@@ -649,25 +649,18 @@ def _dwconv_wgrad(ws, B, T, C, K, da, dw, db, side):
 
 
 # ----------------------------------------------------------------------------- attention
-def attn_dropmask(B, T, H, drop_p, seed, device):
-    """Attention-dropout keep bits of one step (cfm_attn_dropmask): pass to attn_fwd / attn_bwd as `mask`."""
-    m = torch.empty((L.size_call("cfm_attn_dropmask_bytes", B, T, H) + 3) // 4, device=device, dtype=torch.int32)
-    L.call("cfm_attn_dropmask", L.ptr(m), B, T, H, float(drop_p), int(seed) & (2**64 - 1), L.stream())
-    return m
-
-
-def attn_fwd(qkv, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, drop_p=0.0, seed=0, mask=None):
+def attn_fwd(qkv, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, drop_p=0.0, seed=0):
     o = torch.empty(B * T, H * dk, device=qkv.device, dtype=qkv.dtype)
     lse = torch.empty(B * H * T, device=qkv.device, dtype=torch.float32)
-    L.call("cfm_attn_fwd_m", L.ptr(qkv), L.ptr(o), L.ptr(lse), L.ptr(lengths_i32), L.ptr(pos), L.ptr(pos_u),
-           L.ptr(pos_v), B, T, H, dk, L.dt(qkv), float(drop_p), int(seed) & (2**64 - 1), L.ptr(mask), L.stream())
+    L.call("cfm_attn_fwd", L.ptr(qkv), L.ptr(o), L.ptr(lse), L.ptr(lengths_i32), L.ptr(pos), L.ptr(pos_u),
+           L.ptr(pos_v), B, T, H, dk, L.dt(qkv), float(drop_p), int(seed) & (2**64 - 1), L.stream())
     return o, lse
 
 
 def attn_bwd(qkv, o, dout, lse, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, drop_p=0.0, seed=0,
-             D=None, mask=None):
+             D=None):
     """D: optional (B*H*T,) fp32 rowsum(dO * O) per head, precomputed by the GEMM that produced dout
-    (linear_dgrad(rowdot=...)); bf16 MFMA path only.  mask: the forward's attn_dropmask (or None: hash)."""
+    (linear_dgrad(rowdot=...)); bf16 MFMA path only."""
     rel = pos is not None
     if D is not None:
         ws = D
@@ -677,9 +670,9 @@ def attn_bwd(qkv, o, dout, lse, lengths_i32, B, T, H, dk, pos=None, pos_u=None, 
     dpos = torch.empty(pos.shape, device=qkv.device, dtype=torch.float32) if rel else None
     dpu = torch.empty(H * dk, device=qkv.device, dtype=torch.float32) if rel else None
     dpv = torch.empty(H * dk, device=qkv.device, dtype=torch.float32) if rel else None
-    L.call("cfm_attn_bwd_m", L.ptr(qkv), L.ptr(o), L.ptr(dout), L.ptr(lse), L.ptr(lengths_i32), L.ptr(pos),
-           L.ptr(pos_u), L.ptr(pos_v), L.ptr(dqkv), L.ptr(dpos), L.ptr(dpu), L.ptr(dpv), B, T, H, dk, L.dt(qkv),
-           float(drop_p), int(seed) & (2**64 - 1), L.ptr(ws), int(D is not None), L.ptr(mask), L.stream())
+    L.call("cfm_attn_bwd_with_d" if D is not None else "cfm_attn_bwd", L.ptr(qkv), L.ptr(o), L.ptr(dout), L.ptr(lse),
+           L.ptr(lengths_i32), L.ptr(pos), L.ptr(pos_u), L.ptr(pos_v), L.ptr(dqkv), L.ptr(dpos), L.ptr(dpu), L.ptr(dpv),
+           B, T, H, dk, L.dt(qkv), float(drop_p), int(seed) & (2**64 - 1), L.ptr(ws), L.stream())
     return dqkv, dpos, dpu, dpv
 
 

@@ -1,8 +1,8 @@
 """MFMA attention kernels (cfm_attn_fwd / cfm_attn_bwd, bf16) against a torch fp32 reference of
 nn.MultiheadAttention's core: softmax(q k^T / sqrt(dk) + key_padding_mask) v, ragged lengths.
-Every kernel family is checked: whole-head with the wave-per-key-block dK/dV (default), tiled (mode 1),
-four-wave whole-head dK/dV (mode 8); and the three must agree with each other under dropout (same
-counter-based masks; the dQ, dK and dV slices compared separately)."""
+Both kernel families are checked: whole-head with the wave-per-key-block dK/dV (default) and tiled (mode 1);
+the two must agree with each other under dropout (same counter-based masks; the dQ, dK and dV slices compared
+separately), and the masks themselves are read back exactly and checked against a numpy restatement of the hash."""
 import numpy as np
 import pytest
 import torch
@@ -35,7 +35,7 @@ def _ref(qkv, lens, B, T, H, dk, do):
     return o.detach(), x.grad.view(B * T, 3 * H * dk)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 8, 32])
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("B,T,H", [(3, 373, 2), (2, 64, 4), (2, 97, 1)])
 def test_attention_vs_torch(attn_mode, mode, B, T, H):
     attn_mode(mode)
@@ -58,7 +58,7 @@ def test_attention_kernels_agree_under_dropout(attn_mode):
     lens = torch.tensor([T, 300], dtype=torch.int32, device=DEV)
     do = torch.randn(B * T, H * dk, generator=g).to(DEV, torch.bfloat16)
     outs = []
-    for mode in (0, 1, 8):
+    for mode in (0, 1):
         attn_mode(mode)
         o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=0.1, seed=9)
         dqkv, _, _, _ = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=0.1, seed=9)
@@ -167,7 +167,7 @@ def test_rel_attention_mfma_matches_simt_under_dropout(attn_mode):
         assert _rel(a, b) < 3e-2
 
 
-# ------------------------------------------------------------------------------------ precomputed dropout bits
+# ------------------------------------------------------------------------------------ dropout masks, read back
 def _mix32(x):
     x = x.astype(np.uint64) & 0xFFFFFFFF
     x ^= x >> 16
@@ -178,83 +178,44 @@ def _mix32(x):
     return x
 
 
-def _acc_row(r, hh):
-    return (r & 3) + 8 * (r >> 2) + 4 * hh
-
-
-def _mask_words(B, T, H, p, seed):
-    """numpy restatement of cfm_attn_dropmask (attention.hip attn_dropmask_kernel): query-major words (and, for the
-    layout cross-check, key-major ones) from the per-element-pair hash the attention kernels use (cfm_common.h
-    cfm_mix32 / drop_key)."""
+def _keep(B, T, H, p, seed):
+    """numpy restatement of the attention-dropout keep mask (cfm_common.h cfm_mix32 / drop_key, attn_common.h
+    didx): element (b, h, i, j) keeps iff the 16-bit half (j & 1) of mix32(((bh T + i) T2 + j/2) ^ key) >= thr,
+    T2 = (T rounded up to even) / 2.  Returns (B, H, T, T) bool."""
     key = int(_mix32(np.array([(seed & 0xFFFFFFFF) ^ int(_mix32(np.array([((seed >> 32) + 0x9E3779B9) & 0xFFFFFFFF]))[0])]))[0])
     thr = int(np.float32(p) * np.float32(65536.0) + np.float32(0.5))
     T2 = (T + (T & 1)) >> 1
-    nkt, Tq = (T + 63) // 64, (T + 127) // 128 * 128
-    nqs, Tk = 2 * nkt, Tq
-    bh = np.arange(B * H, dtype=np.uint64)[:, None, None, None]
-    kt = np.arange(nkt, dtype=np.uint64)[None, :, None, None]
-    q = np.arange(Tq, dtype=np.uint64)[None, None, :, None]
-    hh = np.arange(2)[None, None, None, :]
-    qm = np.zeros((B * H, nkt, Tq, 2), dtype=np.uint64)
-    for t in range(2):
-        for r in range(0, 16, 2):
-            k = 64 * kt + 32 * t + _acc_row(r, hh).astype(np.uint64)
-            hs = _mix32((((bh * T + q) * T2 + k // 2) & 0xFFFFFFFF) ^ key)
-            qm |= ((hs & 0xFFFF) >= thr).astype(np.uint64) << (16 * t + r)
-            qm |= ((hs >> 16) >= thr).astype(np.uint64) << (16 * t + r + 1)
     bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
-    qs = np.arange(nqs, dtype=np.uint64)[None, :, None]
-    kp = np.arange(Tk // 2, dtype=np.uint64)[None, None, :]
-    w0 = np.zeros((B * H, nqs, Tk // 2), dtype=np.uint64)
-    w1 = np.zeros_like(w0)
-    for h2 in range(2):
-        for r in range(16):
-            qq = 32 * qs + _acc_row(r, h2)
-            hs = _mix32((((bh * T + qq) * T2 + kp) & 0xFFFFFFFF) ^ key)
-            w0 |= ((hs & 0xFFFF) >= thr).astype(np.uint64) << (16 * h2 + r)
-            w1 |= ((hs >> 16) >= thr).astype(np.uint64) << (16 * h2 + r)
-    km = np.stack([w0, w1], -1).reshape(B * H, nqs, Tk)
-    return qm.reshape(-1).astype(np.uint32), km.reshape(-1).astype(np.uint32)
+    i = np.arange(T, dtype=np.uint64)[None, :, None]
+    j = np.arange(T, dtype=np.uint64)[None, None, :]
+    hs = _mix32((((bh * T + i) * T2 + j // 2) & 0xFFFFFFFF) ^ key)
+    half = np.where(j % 2 == 0, hs & 0xFFFF, hs >> 16)
+    return (half >= thr).reshape(B, H, T, T)
 
 
-@pytest.mark.parametrize("B,T,H,seed", [(2, 373, 2, 9), (1, 97, 3, (1 << 40) + 5), (2, 64, 1, 77)])
-def test_dropmask_bits_match_hash(B, T, H, seed):
-    m = ops.attn_dropmask(B, T, H, 0.1, seed, DEV)
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("T,seed", [(64, 9), (63, (1 << 40) + 5), (37, 77)])
+def test_dropout_masks_read_back(attn_mode, mode, T, seed):
+    """q = k = 0 makes P uniform (1 / T); V = identity rows makes o[i, j] = keep(i, j) / ((1 - p) T), and dO =
+    identity rows makes dV[j, i] = the same (P^T dO): both masks -- the forward's query-major one and the dK/dV
+    kernel's key-major one -- come back exactly and must equal the numpy restatement of the hash."""
+    attn_mode(mode)
+    B, H, dk, p = 2, 2, 64, 0.1
+    qkv = torch.zeros(B, T, 3, H, dk)
+    eye = torch.eye(T, dk)
+    qkv[:, :, 2] = eye[None, :, None, :]
+    qkv = qkv.reshape(B * T, 3 * H * dk).to(DEV, torch.bfloat16)
+    lens = torch.full((B,), T, dtype=torch.int32, device=DEV)
+    o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=p, seed=seed)
+    do = eye[None, :, None, :].expand(B, T, H, dk).reshape(B * T, H * dk).to(DEV, torch.bfloat16).contiguous()
+    dqkv, _, _, _ = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=p, seed=seed)
     torch.cuda.synchronize()
-    got = m.cpu().numpy().view(np.uint32)
-    qm, _ = _mask_words(B, T, H, 0.1, seed)
-    assert got.size == qm.size           # query-major words only (the dK/dV kernels hash in-kernel)
-    np.testing.assert_array_equal(got, qm)
-    keep = np.unpackbits(got.view(np.uint8)).mean()
-    assert 0.88 < keep < 0.92
-
-
-@pytest.mark.parametrize("rel", [False, True])
-@pytest.mark.parametrize("T", [373, 97])
-def test_dropmask_path_matches_hash_path(rel, T):
-    """Forward + every gradient with the precomputed bits == the per-element hash path (same masks; only the
-    bf16 rounding order differs), ragged lengths, relative positions on and off."""
-    B, H, dk = 2, 2, 64
-    g = torch.Generator().manual_seed(T + 3 * rel)
-    qkv = torch.randn(B * T, 3 * H * dk, generator=g).to(DEV, torch.bfloat16)
-    lens = torch.tensor([T, T - 31], dtype=torch.int32, device=DEV)
-    do = torch.randn(B * T, H * dk, generator=g).to(DEV, torch.bfloat16)
-    pos = pu = pv = None
-    if rel:
-        pos = (0.5 * torch.randn(2 * T - 1, H * dk, generator=g)).to(DEV, torch.bfloat16)
-        pu = (0.3 * torch.randn(H * dk, generator=g)).to(DEV)
-        pv = (0.3 * torch.randn(H * dk, generator=g)).to(DEV)
-    outs = []
-    for use_mask in (False, True):
-        mask = ops.attn_dropmask(B, T, H, 0.1, 21, DEV) if use_mask else None
-        o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, pos, pu, pv, drop_p=0.1, seed=21, mask=mask)
-        dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, pos, pu, pv, drop_p=0.1, seed=21,
-                                            mask=mask)
-        outs.append((o.float(), dqkv.float(), dpos, dpu))
-    HD = H * dk
-    assert _rel(outs[1][0], outs[0][0]) < 3e-3
-    for sl in range(3):
-        assert _rel(outs[1][1][:, sl * HD:(sl + 1) * HD], outs[0][1][:, sl * HD:(sl + 1) * HD]) < 5e-3, sl
-    if rel:
-        assert _rel(outs[1][2], outs[0][2]) < 5e-3
-        assert _rel(outs[1][3], outs[0][3]) < 5e-3
+    ref = _keep(B, T, H, p, seed)                                                   # (B, H, i, j)
+    got_f = (o.float().view(B, T, H, dk)[..., :T] > 0).permute(0, 2, 1, 3).cpu().numpy()
+    np.testing.assert_array_equal(got_f, ref)
+    dv = dqkv.float().view(B, T, 3, H, dk)[:, :, 2, :, :T]                          # (B, j, H, i)
+    got_b = (dv > 0).permute(0, 2, 3, 1).cpu().numpy()
+    np.testing.assert_array_equal(got_b, ref)
+    val = o.float().view(B, T, H, dk)[..., :T][torch.from_numpy(ref).permute(0, 2, 1, 3).to(DEV)]
+    assert torch.allclose(val, torch.full_like(val, 1.0 / ((1 - p) * T)), rtol=1e-2)
+    assert 0.85 < ref.mean() < 0.95
