@@ -249,6 +249,15 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
     }
   };
   f32x16 sa0, sa1, sb0, sb1;
+  if (p.dbg & 8) {   // A/B: the unpipelined order
+    for (int kt = 0; kt < nkt; ++kt) {
+      qk(kt, sa0, sa1);
+      __builtin_amdgcn_sched_barrier(0);
+      softmax_tile<true>(p, sa0, sa1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
+      pv(kt, sa0, sa1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
   qk(0, sa0, sa1);
   for (int kt = 0; kt < nkt; kt += 2) {
     const bool n1 = kt + 1 < nkt;
@@ -263,6 +272,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
                          dkeep, dkey);
       pv(kt + 1, sb0, sb1);
     }
+  }
   }
   __syncthreads();     // every wave is done with K/V: the images become the epilogue staging
   float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
@@ -314,23 +324,28 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
   const int nks = (len + 31) / 32;
   const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
   const uint32_t hq = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)qi) * T2 + (uint32_t)(2 * hh);
-  for (int ks = 0; ks < nks; ++ks) {
+  const float keep = p.drop_p > 0.f ? dkeep : 1.f;
+  // Software-pipelined as the forward: the S^T / dP^T MFMAs of key step ks + 1 are issued before step ks's
+  // VALU (exponentials, dropout hashes), unrolled by two so both score buffers keep static register names.
+  auto sd = [&](int ks, f32x16& s0, f32x16& d0) {
     const int k0 = ks * 32;
-    f32x16 s0 = (f32x16){0}, d0 = (f32x16){0};
+    s0 = (f32x16){0};
+    d0 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sKall, k0, 16 * s, lane), qf[s], s0, 0, 0, 0);
       d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sVall, k0, 16 * s, lane), gf[s], d0, 0, 0, 0);
-      if (s == 1) __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto ds = [&](int ks, f32x16& s0, f32x16& d0) {   // s0 <- dS^T = P (dP keep - D), then dQ^T += K^T dS^T
+    const int k0 = ks * 32;
     if (p.drop_p > 0.f) {
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
         const uint32_t hsh = cfm_mix32(
             (hq + __builtin_amdgcn_readfirstlane((k0 + (r & 3) + 8 * (r >> 2)) >> 1)) ^ dkey);
-        d0[r] *= (hsh & 0xFFFFu) >= dthr ? dkeep : 0.f;
-        d0[r + 1] *= (hsh >> 16) >= dthr ? dkeep : 0.f;
+        d0[r] = (hsh & 0xFFFFu) >= dthr ? d0[r] : 0.f;
+        d0[r + 1] = (hsh >> 16) >= dthr ? d0[r + 1] : 0.f;
       }
     }
     if (k0 + 32 > len) {     // the last (partial) key step only: masked keys
@@ -340,16 +355,36 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float p0 = fast_exp2(__builtin_fmaf(s0[r], c, -L2));
-      s0[r] = p0 * (d0[r] - Dq);
+      s0[r] = p0 * __builtin_fmaf(d0[r], keep, -Dq);
     }
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bf16x8 pf = acc2frag(s0, s);
       a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sKall, k0 + 16 * s, 0, lane), pf, a0, 0, 0, 0);
       a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sKall, k0 + 16 * s, 32, lane), pf, a1, 0, 0, 0);
     }
+  };
+  f32x16 sa, da, sb, db;
+  if (p.dbg & 8) {   // A/B: the unpipelined order
+    for (int ks = 0; ks < nks; ++ks) {
+      sd(ks, sa, da);
+      __builtin_amdgcn_sched_barrier(0);
+      ds(ks, sa, da);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+  if (nks > 0) sd(0, sa, da);
+  for (int ks = 0; ks < nks; ks += 2) {
+    const bool n1 = ks + 1 < nks;
+    if (n1) sd(ks + 1, sb, db);
     __builtin_amdgcn_sched_barrier(0);
+    ds(ks, sa, da);
+    if (n1) {
+      if (ks + 2 < nks) sd(ks + 2, sa, da);
+      __builtin_amdgcn_sched_barrier(0);
+      ds(ks + 1, sb, db);
+    }
+  }
   }
   __syncthreads();
   float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
@@ -436,16 +471,21 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
   const int nvalid = min(32, p.T - k0w);
   const bool v8 = p.vec && ((uintptr_t)dqkv & 7) == 0;
 
+  // Both passes are software-pipelined as the forward: the next query step's score MFMAs are issued before the
+  // current step's VALU (exponentials, dropout hashes), unrolled by two for static register names; cfm_attn_set_mode
+  // bit 3 runs the unpipelined order (A/B).
+  const bool pipe = !(p.dbg & 8);
   // ---- pass 1: P, dV^T += dO^T P
   {
     f32x16 dv0 = (f32x16){0}, dv1 = (f32x16){0};
-    for (int qt = 0; qt < nqs; ++qt) {
-      const int q0 = qt * 32;
-      f32x16 sa = (f32x16){0};
+    auto sc = [&](int qt, f32x16& sa) {
+      sa = (f32x16){0};
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4)
-        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, q0, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, qt * 32, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
+    };
+    auto pdv = [&](int qt, const f32x16& sa) {
+      const int q0 = qt * 32;
       bf16x8 pf[2];
       unsigned bits = 0u;
 #pragma unroll
@@ -474,7 +514,6 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
           const float pa = fast_exp2(__builtin_fmaf(sa[r], c, -Lr[e]));   // lse = +inf for q >= T
           pf[r >> 3][r & 7] = (bf16)(pa * mk[e]);
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
       if (drop) myM[qt * 64] = (unsigned short)bits;
       if (!kvalid) pf[0] = pf[1] = (bf16x8){0};     // keys past len: P = 0 (one select per packed register)
@@ -483,7 +522,28 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
         dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 0, lane), pf[s2], dv0, 0, 0, 0);
         dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 32, lane), pf[s2], dv1, 0, 0, 0);
       }
-      __builtin_amdgcn_sched_barrier(0);
+    };
+    f32x16 sa, sb;
+    if (!pipe) {
+      for (int qt = 0; qt < nqs; ++qt) {
+        sc(qt, sa);
+        __builtin_amdgcn_sched_barrier(0);
+        pdv(qt, sa);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      if (nqs > 0) sc(0, sa);
+      for (int qt = 0; qt < nqs; qt += 2) {
+        const bool n1 = qt + 1 < nqs;
+        if (n1) sc(qt + 1, sb);
+        __builtin_amdgcn_sched_barrier(0);
+        pdv(qt, sa);
+        if (n1) {
+          if (qt + 2 < nqs) sc(qt + 2, sa);
+          __builtin_amdgcn_sched_barrier(0);
+          pdv(qt + 1, sb);
+        }
+      }
     }
     store_acc_rows(dv0, dv1, 1.f, obase + 2 * p.HD, p.D3, k0w, nvalid, p.dk, v8, lane);
   }
@@ -491,16 +551,17 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
   {
     const float keep = drop ? dkeep : 1.f;
     f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0};
-    for (int qt = 0; qt < nqs; ++qt) {
-      const int q0 = qt * 32;
-      f32x16 sa = (f32x16){0}, ga = (f32x16){0};
+    auto sg = [&](int qt, f32x16& sa, f32x16& ga) {
+      sa = (f32x16){0};
+      ga = (f32x16){0};
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
-        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, q0, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
-        ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sGall, q0, 16 * s4, lane), vf[s4], ga, 0, 0, 0);
-        if (s4 == 1) __builtin_amdgcn_sched_barrier(0);   // at most 4 operand fragments in flight
+        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sQall, qt * 32, 16 * s4, lane), kf[s4], sa, 0, 0, 0);
+        ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sGall, qt * 32, 16 * s4, lane), vf[s4], ga, 0, 0, 0);
       }
-      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto dsk = [&](int qt, const f32x16& sa, const f32x16& ga) {
+      const int q0 = qt * 32;
       const unsigned bits = drop ? (unsigned)myM[qt * 64] : 0xFFFFu;
       bf16x8 sf[2];
 #pragma unroll
@@ -512,10 +573,9 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e;
           const float pa = fast_exp2(__builtin_fmaf(sa[r], c, -Lr[e]));
-          const float m = (bits >> r) & 1u ? keep : 0.f;
-          sf[r >> 3][r & 7] = (bf16)(pa * (ga[r] * m - Dr[e]));
+          const float gk = (bits >> r) & 1u ? ga[r] : 0.f;
+          sf[r >> 3][r & 7] = (bf16)(pa * __builtin_fmaf(gk, keep, -Dr[e]));
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
       if (!kvalid) sf[0] = sf[1] = (bf16x8){0};
 #pragma unroll
@@ -523,7 +583,28 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
         dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 0, lane), sf[s2], dk0, 0, 0, 0);
         dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 32, lane), sf[s2], dk1, 0, 0, 0);
       }
-      __builtin_amdgcn_sched_barrier(0);
+    };
+    f32x16 sa, ga, sb, gb;
+    if (!pipe) {
+      for (int qt = 0; qt < nqs; ++qt) {
+        sg(qt, sa, ga);
+        __builtin_amdgcn_sched_barrier(0);
+        dsk(qt, sa, ga);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      if (nqs > 0) sg(0, sa, ga);
+      for (int qt = 0; qt < nqs; qt += 2) {
+        const bool n1 = qt + 1 < nqs;
+        if (n1) sg(qt + 1, sb, gb);
+        __builtin_amdgcn_sched_barrier(0);
+        dsk(qt, sa, ga);
+        if (n1) {
+          if (qt + 2 < nqs) sg(qt + 2, sa, ga);
+          __builtin_amdgcn_sched_barrier(0);
+          dsk(qt + 1, sb, gb);
+        }
+      }
     }
     store_acc_rows(dk0, dk1, p.scale, obase + p.HD, p.D3, k0w, nvalid, p.dk, v8, lane);
   }
@@ -785,7 +866,7 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   if (pos)
     return cfm::attn_rel_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, drop_p, seed, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
-          ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 6,
+          ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 14,
           cfm::g_rng_salt};
   if (use_head(T)) {
     // LDS sized for the full padded length (lengths are device data; len <= T)
@@ -818,7 +899,7 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
                                      T, H, dk, dtype, drop_p, seed, ws, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0),
-          g_attn_mode & 6, cfm::g_rng_salt};
+          g_attn_mode & 14, cfm::g_rng_salt};
   const long nrow = (long)B * H * T;
   (void)nrow;
   CFM_REQUIRE(H * dk <= 1024, CFM_ERR_UNSUPPORTED, "H*dk must be <= 1024");
