@@ -248,6 +248,136 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
   if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
 }
 
+// ------------------------------------------------------------------------------------ forward, two waves per SIMD
+// The same tile walk as attn_rel_fwd_kernel in <= 80 KiB of LDS and <= 256 registers, so two workgroups share a
+// CU (two waves per SIMD: one wave's softmax VALU issues beside the other's MFMAs, and the VALU issue cost per
+// instruction halves -- one wave alone on a SIMD pays 4 cycles per v_fma, two pay 2 each).  LDS: one K/V tile
+// (18 KiB, the next tile prefetched into registers and stored between two barriers), a ring of 3 band chunks
+// (27 KiB: tile kt reads chunks kt..kt+2, chunk kt+3 replaces kt), and a 64-row circular skew stage per wave
+// (34 KiB): X0 -> rows 0..31, X1 -> 32..63, the s0 block (band rows 0..62) is read, then X2 -> rows 64..94 at
+// row & 63 over the consumed X0, and the s1 block reads rows 32..94.  The dropout keep scale is applied once to
+// the output (o * keep / l).
+constexpr int SC = 68;      // circular stage column stride (floats): 68 = 4 mod 32
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp, bf16* __restrict__ o,
+                                                               float* __restrict__ lse) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  __shared__ __attribute__((aligned(16))) bf16 skv[2 * TILE * KS];        // [K, V][64][72]        18 KiB
+  __shared__ __attribute__((aligned(16))) bf16 sring[3 * TILE * KS];      // band ring of 3 chunks 27 KiB
+  __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SC];          // circular skew stages  34 KiB
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, ii = lane & 31;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int Q0 = blockIdx.x * 128, q0 = Q0 + wv * 32;
+  const int qi = q0 + ii;
+  const int len = p.len[b];
+  const int rbase = p.T - 1 - Q0 - 127;          // relative row of band row 0 at key tile 0
+  bf16x8 qu[4], qv[4];
+  load_q_uv(p, rp, b, h, qi, qu, qv, lane);
+  float* col = sst + wv * 32 * SC + ii * SC;
+  f32x16 o0 = (f32x16){0}, o1 = (f32x16){0};
+  float m = -INFINITY, l = 0.f;
+  const float c = p.scale * LOG2E;
+  const int nkt = (len + TILE - 1) / TILE;
+  uint4 rk[2], rv[2], rq[2];
+  const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
+  if (nkt > 0) {
+    tile_load<VEC>(p, b, 0, kcol, rk, tid);
+    tile_load<VEC>(p, b, 0, vcol, rv, tid);
+    tile_store(skv, rk, tid);
+    tile_store(skv + TILE * KS, rv, tid);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
+      ring_chunk_store(sring + ch * TILE * KS, rq, tid);
+    }
+    __syncthreads();
+  }
+  wait_prologue_loads();
+  // X[r'][i] -> stage rows (base + r') & 63 of column i (16-B stores of 4 consecutive accumulator rows)
+  auto put = [&](const f32x16& x, int base) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int r0 = (base + 8 * g + 4 * hh) & 63;
+      *reinterpret_cast<float4*>(col + r0) = make_float4(x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]);
+    }
+  };
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* sK = skv;
+    const bf16* sV = skv + TILE * KS;
+    if (kt + 1 < nkt) {
+      tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
+      tile_load<VEC>(p, b, (kt + 1) * TILE, vcol, rv, tid);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
+    }
+    const bf16* blk[3];
+#pragma unroll
+    for (int mm = 0; mm < 3; ++mm) {
+      const int off = 32 * (3 - wv) + 32 * mm;
+      blk[mm] = sring + ((kt + (off >> 6)) % 3) * TILE * KS + (off & 63) * KS;
+    }
+    // S^T = K (q+u)^T + skew(P_band (q+v)^T), unscaled (queries on the lanes, keys on the accumulator rows)
+    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
+    {
+      f32x16 x0 = (f32x16){0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qu[s], s0, 0, 0, 0);
+        x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[0], 0, 16 * s, lane), qv[s], x0, 0, 0, 0);
+      }
+      put(x0, 0);
+    }
+    {
+      f32x16 x1 = (f32x16){0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
+        x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
+      }
+      put(x1, 32);
+    }
+    f32x16 x2 = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qv[s], x2, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s0[r] += col[acc_row(r, hh) - ii + 31];          // band rows 0..62
+    __builtin_amdgcn_wave_barrier();
+    put(x2, 64);                                                                   // over the consumed X0 rows
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s1[r] += col[(acc_row(r, hh) + 63 - ii) & 63];    // band rows 32..94
+    __builtin_amdgcn_wave_barrier();
+    softmax_tile<true>(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 0, lane), pf, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 32, lane), pf, o1, 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nkt) {
+      __syncthreads();           // every wave is done with K/V (kt) and with band chunk kt
+      tile_store(skv, rk, tid);
+      tile_store(skv + TILE * KS, rv, tid);
+      ring_chunk_store(sring + (kt % 3) * TILE * KS, rq, tid);
+      __syncthreads();
+    }
+  }
+  __syncthreads();               // the stage region of store_transposed (32 x 65 floats) spans wave boundaries
+  float* st = sst + wv * 32 * SC;
+  const float inv = (p.drop_p > 0.f ? dkeep : 1.f) / l;
+  if (q0 < p.T)
+    store_transposed(st, o0, o1, inv, o + (long)b * p.T * p.HD + h * p.dk, p.HD, q0, min(32, p.T - q0), p.dk, lane);
+  if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
+}
+
 // ------------------------------------------------------------------------------------ dQ (+ du, dv partials)
 // grid (ceil(T/128), H, B).  part: (B * 4*gridDim.x, 2*H*dk) fp32 -- row (b, 32-query block): per-column
 // sums over the block's queries of scale * sum_j dS k_j (u half) and scale * sum_j dS p_r (v half).
@@ -792,10 +922,14 @@ int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len
                         const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s) {
   const AttnM p = make_attnm(qkv, qkv, len, B, T, H, dk, drop_p, seed);
   const RelP rp = make_relp(pos, pu, pv, p.dk);
-  if (rel_vec(p, rp))
-    hipLaunchKernelGGL(attn_rel_fwd_kernel<true>, dim3(cdiv(p.T, 128), p.H, p.B), dim3(256), 0, s, p, rp, (bf16*)o, lse);
-  else
-    hipLaunchKernelGGL(attn_rel_fwd_kernel<false>, dim3(cdiv(p.T, 128), p.H, p.B), dim3(256), 0, s, p, rp, (bf16*)o, lse);
+  const dim3 grid(cdiv(p.T, 128), p.H, p.B);
+  if (g_rel_mode & 32) {   // A/B: the one-wave-per-SIMD forward
+    if (rel_vec(p, rp)) hipLaunchKernelGGL(attn_rel_fwd_kernel<true>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
+    else hipLaunchKernelGGL(attn_rel_fwd_kernel<false>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
+  } else {
+    if (rel_vec(p, rp)) hipLaunchKernelGGL(attn_rel_fwd2_kernel<true>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
+    else hipLaunchKernelGGL(attn_rel_fwd2_kernel<false>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
+  }
   return check_launch("cfm_attn_fwd(rel)");
 }
 
