@@ -253,11 +253,11 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
 // CU (two waves per SIMD: one wave's softmax VALU issues beside the other's MFMAs, and the VALU issue cost per
 // instruction halves -- one wave alone on a SIMD pays 4 cycles per v_fma, two pay 2 each).  LDS: one K/V tile
 // (18 KiB, the next tile prefetched into registers and stored between two barriers), a ring of 3 band chunks
-// (27 KiB: tile kt reads chunks kt..kt+2, chunk kt+3 replaces kt), and a 64-row circular skew stage per wave
-// (34 KiB): X0 -> rows 0..31, X1 -> 32..63, the s0 block (band rows 0..62) is read, then X2 -> rows 64..94 at
-// row & 63 over the consumed X0, and the s1 block reads rows 32..94.  The dropout keep scale is applied once to
-// the output (o * keep / l).
-constexpr int SC = 68;      // circular stage column stride (floats): 68 = 4 mod 32
+// (27 KiB: tile kt reads chunks kt..kt+2, chunk kt+3 replaces kt), and a 64-row skew stage per wave (34 KiB):
+// X0 -> rows 0..31 and X1 -> 32..63 for the s0 block (band rows 0..62), then X1 -> 0..31 and X2 -> 32..63 for the
+// s1 block (band rows 32..94): both blocks read the same per-lane addresses (one base + immediate offsets).  The
+// dropout keep scale is applied once to the output (o * keep / l).
+constexpr int SC = 68;      // 64-row skew stage column stride (floats): 68 = 4 mod 32
 template <bool VEC>
 __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp, bf16* __restrict__ o,
                                                                float* __restrict__ lse) {
@@ -297,12 +297,12 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
   }
   wait_prologue_loads();
   // X[r'][i] -> stage rows (base + r') & 63 of column i (16-B stores of 4 consecutive accumulator rows)
+  float* colh = col + 4 * hh;                 // the lane's 4-row groups: rows 8g + 4hh .. +3
+  const float* sk = col + 31 - ii + 4 * hh;   // bd of accumulator row acc_row(r, hh): sk[(r & 3) + 8 (r >> 2)]
   auto put = [&](const f32x16& x, int base) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int r0 = (base + 8 * g + 4 * hh) & 63;
-      *reinterpret_cast<float4*>(col + r0) = make_float4(x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]);
-    }
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<float4*>(colh + base + 8 * g) = make_float4(x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]);
   };
   for (int kt = 0; kt < nkt; ++kt) {
     const bf16* sK = skv;
@@ -330,27 +330,26 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
       }
       put(x0, 0);
     }
-    {
-      f32x16 x1 = (f32x16){0};
+    f32x16 x1 = (f32x16){0};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
-        x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
-      }
-      put(x1, 32);
+    for (int s = 0; s < 4; ++s) {
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
+      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
     }
+    put(x1, 32);
     f32x16 x2 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qv[s], x2, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s0[r] += col[acc_row(r, hh) - ii + 31];          // band rows 0..62
+    for (int r = 0; r < 16; ++r) s0[r] += sk[(r & 3) + 8 * (r >> 2)];              // band rows 0..62
     __builtin_amdgcn_wave_barrier();
-    put(x2, 64);                                                                   // over the consumed X0 rows
+    put(x1, 0);                                                                    // band rows 32..94 -> 0..62
+    put(x2, 32);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s1[r] += col[(acc_row(r, hh) + 63 - ii) & 63];    // band rows 32..94
+    for (int r = 0; r < 16; ++r) s1[r] += sk[(r & 3) + 8 * (r >> 2)];
     __builtin_amdgcn_wave_barrier();
     softmax_tile<true>(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
 #pragma unroll
@@ -510,6 +509,197 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, 
     __syncthreads();
   }
   // per-wave column sums (queries) of both terms -> du / dv partial rows (zeros for blocks past T)
+  const float su = wave_rowsum(st, a0, a1, lane) * p.scale;
+  const float sv = wave_rowsum(st, e0, e1, lane) * p.scale;
+  const long prow = (long)b * (4 * gridDim.x) + blockIdx.x * 4 + wv;
+  if (lane < p.dk) {
+    part[prow * 2 * p.HD + h * p.dk + lane] = su;
+    part[prow * 2 * p.HD + p.HD + h * p.dk + lane] = sv;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    a0[r] += e0[r];
+    a1[r] += e1[r];
+  }
+  if (q0 < p.T)
+    store_transposed(st, a0, a1, p.scale, dqkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, q0, min(32, p.T - q0),
+                     p.dk, lane);
+}
+
+// ------------------------------------------------------------------------------------ dQ, two waves per SIMD
+// attn_rel_bwd_dq_kernel's work in <= 80 KiB of LDS and <= 256 registers (two workgroups per CU): one K/V tile
+// (the next one loaded between two barriers: a register prefetch across the tile spilled, the partner workgroup
+// covers the load), a ring of 3 band chunks, and per wave one 64-row f32 skew
+// stage (as attn_rel_fwd2_kernel) whose bytes also hold the bf16 band-coordinate image of dS^T
+// ([query][96 + 8 pad] bf16, 6.5 KiB of the wave's 8.5): the scatter writes bf16 directly (the MFMA operand type)
+// and the band-term MFMA reads 16-B fragments of it.
+constexpr int SB = 104;     // band image column stride (bf16 elements): 208 B
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP rp, const bf16* __restrict__ dout,
+                                                                  const float* __restrict__ lse,
+                                                                  const float* __restrict__ Dg,
+                                                                  bf16* __restrict__ dqkv, float* __restrict__ part) {
+  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  __shared__ __attribute__((aligned(16))) bf16 skv[2 * TILE * KS];
+  __shared__ __attribute__((aligned(16))) bf16 sring[3 * TILE * KS];
+  __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SC];
+  static_assert(32 * SB * 2 <= 32 * SC * 4, "band image fits the wave's stage");
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, ii = lane & 31;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int Q0 = blockIdx.x * 128, q0 = Q0 + wv * 32;
+  const int qi = q0 + ii;
+  const int len = p.len[b];
+  const int rbase = p.T - 1 - Q0 - 127;
+  bf16x8 qu[4], qv[4], gf[4];
+  load_q_uv(p, rp, b, h, qi, qu, qv, lane);
+  load_bfrags(p, dout + (long)b * p.T * p.HD + h * p.dk, p.HD, qi, p.T, gf, lane);
+  const bool qvalid = qi < p.T;
+  const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : INFINITY;   // +inf: P = 0 past T
+  const float Dq = qvalid ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
+  const float c = p.scale * LOG2E;
+  float* st = sst + wv * 32 * SC;
+  float* col = st + ii * SC;
+  bf16* bimg = reinterpret_cast<bf16*>(st);            // [query][SB] band image of dS^T
+  bf16* bcol = bimg + ii * SB;
+  bf16* bsk = bcol + 31 - ii + 4 * hh;         // band row of (key acc_row(r, hh), query ii): bsk[(r & 3) + 8 (r >> 2)]
+  f32x16 a0 = (f32x16){0}, a1 = (f32x16){0}, e0 = (f32x16){0}, e1 = (f32x16){0};   // K-term, band term
+  const int nkt = (len + TILE - 1) / TILE;
+  uint4 rk[2], rv[2], rq[2];
+  const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
+  if (nkt > 0) {
+    tile_load<VEC>(p, b, 0, kcol, rk, tid);
+    tile_load<VEC>(p, b, 0, vcol, rv, tid);
+    tile_store(skv, rk, tid);
+    tile_store(skv + TILE * KS, rv, tid);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
+      ring_chunk_store(sring + ch * TILE * KS, rq, tid);
+    }
+    __syncthreads();
+  }
+  wait_prologue_loads();
+  float* colh = col + 4 * hh;                 // the lane's 4-row groups: rows 8g + 4hh .. +3
+  const float* sk = col + 31 - ii + 4 * hh;   // bd of accumulator row acc_row(r, hh): sk[(r & 3) + 8 (r >> 2)]
+  auto put = [&](const f32x16& x, int base) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<float4*>(colh + base + 8 * g) = make_float4(x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]);
+  };
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bf16* sK = skv;
+    const bf16* sV = skv + TILE * KS;
+    const bf16* blk[3];
+#pragma unroll
+    for (int mm = 0; mm < 3; ++mm) {
+      const int off = 32 * (3 - wv) + 32 * mm;
+      blk[mm] = sring + ((kt + (off >> 6)) % 3) * TILE * KS + (off & 63) * KS;
+    }
+    f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
+    {
+      f32x16 x0 = (f32x16){0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qu[s], s0, 0, 0, 0);
+        x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[0], 0, 16 * s, lane), qv[s], x0, 0, 0, 0);
+      }
+      put(x0, 0);
+    }
+    f32x16 x1 = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
+      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
+    }
+    put(x1, 32);
+    {
+      f32x16 x2 = (f32x16){0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qv[s], x2, 0, 0, 0);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s0[r] += sk[(r & 3) + 8 * (r >> 2)];
+      __builtin_amdgcn_wave_barrier();
+      put(x1, 0);
+      put(x2, 32);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s1[r] += sk[(r & 3) + 8 * (r >> 2)];
+      __builtin_amdgcn_wave_barrier();
+    }
+    // per 32-key half t: dP^T = V dO^T, dropout, dS^T = P (dP keep - D) in place of the scores, then the K-term
+    // dQ^T[d][q] += sum_key K[key][d] dS^T[key][q] (one dP half live at a time)
+    const float keep = p.drop_p > 0.f ? dkeep : 1.f;
+    const bool tail = kt == nkt - 1 && kt * TILE + TILE > len;
+    const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
+    auto half = [&](f32x16& sx, int t) {
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 dd = (f32x16){0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        dd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32 * t, 16 * s, lane), gf[s], dd, 0, 0, 0);
+      if (p.drop_p > 0.f) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const uint32_t hs = cfm_mix32((rowj + ((acc_row(r, hh) + 32 * t) >> 1)) ^ dkey);
+          dd[r] = (hs & 0xFFFFu) >= dthr ? dd[r] : 0.f;
+          dd[r + 1] = (hs >> 16) >= dthr ? dd[r + 1] : 0.f;
+        }
+      }
+      // P = 2^(c s - lse log2 e); key masking only on the utterance's last tile (uniform)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float x = __builtin_fmaf(sx[r], c, -L2);
+        if (tail) x = kt * TILE + 32 * t + acc_row(r, hh) < len ? x : -INFINITY;
+        sx[r] = fast_exp2(x) * __builtin_fmaf(dd[r], keep, -Dq);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc2frag(sx, s);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 0, lane), pf, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 32, lane), pf, a1, 0, 0, 0);
+      }
+    };
+    half(s0, 0);
+    half(s1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    // band term: dS^T in band coordinates, bf16 image [i][j - i + 31] (zero elsewhere), then
+    // dQ^T[d][q] += sum_r' P_band[r'][d] dS_band^T[r'][q]
+#pragma unroll
+    for (int g = 0; g < 6; ++g) *reinterpret_cast<uint4*>(bcol + 48 * hh + 8 * g) = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      bsk[(r & 3) + 8 * (r >> 2)] = (bf16)s0[r];
+      bsk[(r & 3) + 8 * (r >> 2) + 32] = (bf16)s1[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(bcol + 16 * s + 8 * hh);
+      const bf16* bk = blk[s >> 1];
+      e0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(bk, 16 * (s & 1), 0, lane), bfr, e0, 0, 0, 0);
+      e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(bk, 16 * (s & 1), 32, lane), bfr, e1, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (kt + 1 < nkt) {
+      __syncthreads();
+      tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
+      tile_load<VEC>(p, b, (kt + 1) * TILE, vcol, rv, tid);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
+      tile_store(skv, rk, tid);
+      tile_store(skv + TILE * KS, rv, tid);
+      ring_chunk_store(sring + (kt % 3) * TILE * KS, rq, tid);
+      __syncthreads();
+    }
+  }
+  __syncthreads();      // wave_rowsum / store_transposed stage 32 x 65 floats: past the wave's 32 x 68 region? no --
+                        // 32 * 65 <= 32 * 68, but keep every wave's band-image reads done before the reuse
   const float su = wave_rowsum(st, a0, a1, lane) * p.scale;
   const float sv = wave_rowsum(st, e0, e1, lane) * p.scale;
   const long prow = (long)b * (4 * gridDim.x) + blockIdx.x * 4 + wv;
@@ -948,13 +1138,21 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
   if (rel_vec(p, rp)) {
     hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                        (bf16*)dqkv, dsbuf, ldS);
-    hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                       (bf16*)dqkv, part);
+    if (g_rel_mode & 32)
+      hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, part);
+    else
+      hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, part);
   } else {
     hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                        (bf16*)dqkv, dsbuf, ldS);
-    hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                       (bf16*)dqkv, part);
+    if (g_rel_mode & 32)
+      hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, part);
+    else
+      hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, part);
   }
   const size_t ds_bytes = ((size_t)p.B * p.H * p.T * ldS * sizeof(bf16) + 255) & ~(size_t)255;
   float* dpos_part = reinterpret_cast<float*>(reinterpret_cast<char*>(dsbuf) + ds_bytes);
