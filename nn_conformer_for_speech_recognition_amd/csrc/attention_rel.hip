@@ -248,6 +248,40 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
   if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
 }
 
+// ------------------------------------------------------------------------------------ band bias column
+// (q + v) . p_r = (q + u) . p_r + c_r with c_r = (v - u) . p_r: the two-waves kernels form the band product from
+// the (q + u) operand they already hold and add c_r (fp32, per relative row) -- no (q + v) operand in registers or
+// LDS.  c of a ring chunk is computed from the chunk's staged rows: the 8 threads that store one row's 8 16-B
+// pieces each dot 8 columns with (v - u) and sum over the 8 lanes (three xor shuffles).
+__device__ __forceinline__ void load_dvu8(const AttnM& p, const RelP& rp, int h, int tid, float (&dvu)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int d = (tid & 7) * 8 + e;
+    dvu[e] = d < p.dk ? rp.pv[h * p.dk + d] - rp.pu[h * p.dk + d] : 0.f;
+  }
+}
+__device__ __forceinline__ void ring_c_store(float* cslot, const uint4 (&reg)[2], const float (&dvu)[8], int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const bf16x8 v = __builtin_bit_cast(bf16x8, reg[i]);
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t = __builtin_fmaf((float)v[e], dvu[e], t);
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    t += __shfl_xor(t, 4, 64);
+    if ((tid & 7) == 0) cslot[(tid + 256 * i) >> 3] = t;
+  }
+}
+// x (band rows 8g + 4hh + e of a 32-row block on the accumulator rows) += c of those rows
+__device__ __forceinline__ void add_band_c(f32x16& x, const float* cb, int hh) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 cv = *reinterpret_cast<const float4*>(cb + 8 * g + 4 * hh);
+    x[4 * g] += cv.x; x[4 * g + 1] += cv.y; x[4 * g + 2] += cv.z; x[4 * g + 3] += cv.w;
+  }
+}
+
 // ------------------------------------------------------------------------------------ forward, two waves per SIMD
 // The same tile walk as attn_rel_fwd_kernel in <= 80 KiB of LDS and <= 256 registers, so two workgroups share a
 // CU (two waves per SIMD: one wave's softmax VALU issues beside the other's MFMAs, and the VALU issue cost per
@@ -265,7 +299,8 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
   const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
   const float dkeep = drop_keep_scale(dthr);
   __shared__ __attribute__((aligned(16))) bf16 skv[2 * TILE * KS];        // [K, V][64][72]        18 KiB
-  __shared__ __attribute__((aligned(16))) bf16 sring[3 * TILE * KS];      // band ring of 3 chunks 27 KiB
+  __shared__ __attribute__((aligned(16))) bf16 sring[3 * TILE * KS];
+  __shared__ __attribute__((aligned(16))) float scr[3 * TILE];              // c of the ring's rows      // band ring of 3 chunks 27 KiB
   __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SC];          // circular skew stages  34 KiB
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, ii = lane & 31;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -273,8 +308,13 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
   const int qi = q0 + ii;
   const int len = p.len[b];
   const int rbase = p.T - 1 - Q0 - 127;          // relative row of band row 0 at key tile 0
-  bf16x8 qu[4], qv[4];
-  load_q_uv(p, rp, b, h, qi, qu, qv, lane);
+  bf16x8 qu[4];
+  {
+    bf16x8 qv_unused[4];
+    load_q_uv(p, rp, b, h, qi, qu, qv_unused, lane);
+  }
+  float dvu[8];
+  load_dvu8(p, rp, h, tid, dvu);
   float* col = sst + wv * 32 * SC + ii * SC;
   f32x16 o0 = (f32x16){0}, o1 = (f32x16){0};
   float m = -INFINITY, l = 0.f;
@@ -292,6 +332,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
 #pragma unroll
       for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
       ring_chunk_store(sring + ch * TILE * KS, rq, tid);
+      ring_c_store(scr + ch * TILE, rq, dvu, tid);
     }
     __syncthreads();
   }
@@ -314,10 +355,12 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
       for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
     }
     const bf16* blk[3];
+    const float* cbk[3];
 #pragma unroll
     for (int mm = 0; mm < 3; ++mm) {
       const int off = 32 * (3 - wv) + 32 * mm;
       blk[mm] = sring + ((kt + (off >> 6)) % 3) * TILE * KS + (off & 63) * KS;
+      cbk[mm] = scr + ((kt + (off >> 6)) % 3) * TILE + (off & 63);
     }
     // S^T = K (q+u)^T + skew(P_band (q+v)^T), unscaled (queries on the lanes, keys on the accumulator rows)
     f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
@@ -326,21 +369,24 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qu[s], s0, 0, 0, 0);
-        x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[0], 0, 16 * s, lane), qv[s], x0, 0, 0, 0);
+        x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[0], 0, 16 * s, lane), qu[s], x0, 0, 0, 0);
       }
+      add_band_c(x0, cbk[0], hh);
       put(x0, 0);
     }
     f32x16 x1 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
-      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
+      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qu[s], x1, 0, 0, 0);
     }
+    add_band_c(x1, cbk[1], hh);
     put(x1, 32);
     f32x16 x2 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s)
-      x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qv[s], x2, 0, 0, 0);
+      x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qu[s], x2, 0, 0, 0);
+    add_band_c(x2, cbk[2], hh);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < 16; ++r) s0[r] += sk[(r & 3) + 8 * (r >> 2)];              // band rows 0..62
@@ -366,6 +412,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
       tile_store(skv, rk, tid);
       tile_store(skv + TILE * KS, rv, tid);
       ring_chunk_store(sring + (kt % 3) * TILE * KS, rq, tid);
+      ring_c_store(scr + (kt % 3) * TILE, rq, dvu, tid);
       __syncthreads();
     }
   }
@@ -544,6 +591,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
   const float dkeep = drop_keep_scale(dthr);
   __shared__ __attribute__((aligned(16))) bf16 skv[2 * TILE * KS];
   __shared__ __attribute__((aligned(16))) bf16 sring[3 * TILE * KS];
+  __shared__ __attribute__((aligned(16))) float scr[3 * TILE];              // c of the ring's rows
   __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SC];
   static_assert(32 * SB * 2 <= 32 * SC * 4, "band image fits the wave's stage");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, ii = lane & 31;
@@ -552,8 +600,13 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
   const int qi = q0 + ii;
   const int len = p.len[b];
   const int rbase = p.T - 1 - Q0 - 127;
-  bf16x8 qu[4], qv[4], gf[4];
-  load_q_uv(p, rp, b, h, qi, qu, qv, lane);
+  bf16x8 qu[4], gf[4];
+  {
+    bf16x8 qv_unused[4];
+    load_q_uv(p, rp, b, h, qi, qu, qv_unused, lane);
+  }
+  float dvu[8];
+  load_dvu8(p, rp, h, tid, dvu);
   load_bfrags(p, dout + (long)b * p.T * p.HD + h * p.dk, p.HD, qi, p.T, gf, lane);
   const bool qvalid = qi < p.T;
   const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : INFINITY;   // +inf: P = 0 past T
@@ -578,6 +631,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
 #pragma unroll
       for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
       ring_chunk_store(sring + ch * TILE * KS, rq, tid);
+      ring_c_store(scr + ch * TILE, rq, dvu, tid);
     }
     __syncthreads();
   }
@@ -593,10 +647,12 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
     const bf16* sK = skv;
     const bf16* sV = skv + TILE * KS;
     const bf16* blk[3];
+    const float* cbk[3];
 #pragma unroll
     for (int mm = 0; mm < 3; ++mm) {
       const int off = 32 * (3 - wv) + 32 * mm;
       blk[mm] = sring + ((kt + (off >> 6)) % 3) * TILE * KS + (off & 63) * KS;
+      cbk[mm] = scr + ((kt + (off >> 6)) % 3) * TILE + (off & 63);
     }
     f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
     {
@@ -604,22 +660,25 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qu[s], s0, 0, 0, 0);
-        x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[0], 0, 16 * s, lane), qv[s], x0, 0, 0, 0);
+        x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[0], 0, 16 * s, lane), qu[s], x0, 0, 0, 0);
       }
+      add_band_c(x0, cbk[0], hh);
       put(x0, 0);
     }
     f32x16 x1 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
-      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
+      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qu[s], x1, 0, 0, 0);
     }
+    add_band_c(x1, cbk[1], hh);
     put(x1, 32);
     {
       f32x16 x2 = (f32x16){0};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qv[s], x2, 0, 0, 0);
+        x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qu[s], x2, 0, 0, 0);
+    add_band_c(x2, cbk[2], hh);
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int r = 0; r < 16; ++r) s0[r] += sk[(r & 3) + 8 * (r >> 2)];
@@ -695,6 +754,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
       tile_store(skv, rk, tid);
       tile_store(skv + TILE * KS, rv, tid);
       ring_chunk_store(sring + (kt % 3) * TILE * KS, rq, tid);
+      ring_c_store(scr + (kt % 3) * TILE, rq, dvu, tid);
       __syncthreads();
     }
   }
