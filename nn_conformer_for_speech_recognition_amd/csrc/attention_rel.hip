@@ -251,7 +251,8 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
 // ------------------------------------------------------------------------------------ band bias column
 // (q + v) . p_r = (q + u) . p_r + c_r with c_r = (v - u) . p_r: the two-waves kernels form the band product from
 // the (q + u) operand they already hold and add c_r (fp32, per relative row) -- no (q + v) operand in registers or
-// LDS.  c of a ring chunk is computed from the chunk's staged rows: the 8 threads that store one row's 8 16-B
+// LDS (dQ: 16 registers, dK/dV: a 9-KiB Q + v image; the forward has the registers and keeps (q + v), as the
+// c_r path costs ~80 VALU per tile).  c of a ring chunk is computed from the chunk's staged rows: the 8 threads that store one row's 8 16-B
 // pieces each dot 8 columns with (v - u) and sum over the 8 lanes (three xor shuffles).
 __device__ __forceinline__ void load_dvu8(const AttnM& p, const RelP& rp, int h, int tid, float (&dvu)[8]) {
 #pragma unroll
@@ -299,8 +300,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
   const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
   const float dkeep = drop_keep_scale(dthr);
   __shared__ __attribute__((aligned(16))) bf16 skv[2 * TILE * KS];        // [K, V][64][72]        18 KiB
-  __shared__ __attribute__((aligned(16))) bf16 sring[3 * TILE * KS];
-  __shared__ __attribute__((aligned(16))) float scr[3 * TILE];              // c of the ring's rows      // band ring of 3 chunks 27 KiB
+  __shared__ __attribute__((aligned(16))) bf16 sring[3 * TILE * KS];      // band ring of 3 chunks 27 KiB
   __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SC];          // circular skew stages  34 KiB
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, ii = lane & 31;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -308,13 +308,8 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
   const int qi = q0 + ii;
   const int len = p.len[b];
   const int rbase = p.T - 1 - Q0 - 127;          // relative row of band row 0 at key tile 0
-  bf16x8 qu[4];
-  {
-    bf16x8 qv_unused[4];
-    load_q_uv(p, rp, b, h, qi, qu, qv_unused, lane);
-  }
-  float dvu[8];
-  load_dvu8(p, rp, h, tid, dvu);
+  bf16x8 qu[4], qv[4];
+  load_q_uv(p, rp, b, h, qi, qu, qv, lane);
   float* col = sst + wv * 32 * SC + ii * SC;
   f32x16 o0 = (f32x16){0}, o1 = (f32x16){0};
   float m = -INFINITY, l = 0.f;
@@ -332,7 +327,6 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
 #pragma unroll
       for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
       ring_chunk_store(sring + ch * TILE * KS, rq, tid);
-      ring_c_store(scr + ch * TILE, rq, dvu, tid);
     }
     __syncthreads();
   }
@@ -355,12 +349,10 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
       for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
     }
     const bf16* blk[3];
-    const float* cbk[3];
 #pragma unroll
     for (int mm = 0; mm < 3; ++mm) {
       const int off = 32 * (3 - wv) + 32 * mm;
       blk[mm] = sring + ((kt + (off >> 6)) % 3) * TILE * KS + (off & 63) * KS;
-      cbk[mm] = scr + ((kt + (off >> 6)) % 3) * TILE + (off & 63);
     }
     // S^T = K (q+u)^T + skew(P_band (q+v)^T), unscaled (queries on the lanes, keys on the accumulator rows)
     f32x16 s0 = (f32x16){0}, s1 = (f32x16){0};
@@ -369,24 +361,21 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 0, 16 * s, lane), qu[s], s0, 0, 0, 0);
-        x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[0], 0, 16 * s, lane), qu[s], x0, 0, 0, 0);
+        x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[0], 0, 16 * s, lane), qv[s], x0, 0, 0, 0);
       }
-      add_band_c(x0, cbk[0], hh);
       put(x0, 0);
     }
     f32x16 x1 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sK, 32, 16 * s, lane), qu[s], s1, 0, 0, 0);
-      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qu[s], x1, 0, 0, 0);
+      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[1], 0, 16 * s, lane), qv[s], x1, 0, 0, 0);
     }
-    add_band_c(x1, cbk[1], hh);
     put(x1, 32);
     f32x16 x2 = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s)
-      x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qu[s], x2, 0, 0, 0);
-    add_band_c(x2, cbk[2], hh);
+      x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qv[s], x2, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < 16; ++r) s0[r] += sk[(r & 3) + 8 * (r >> 2)];              // band rows 0..62
@@ -412,7 +401,6 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
       tile_store(skv, rk, tid);
       tile_store(skv + TILE * KS, rv, tid);
       ring_chunk_store(sring + (kt % 3) * TILE * KS, rq, tid);
-      ring_c_store(scr + (kt % 3) * TILE, rq, dvu, tid);
       __syncthreads();
     }
   }
@@ -758,8 +746,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
       __syncthreads();
     }
   }
-  __syncthreads();      // wave_rowsum / store_transposed stage 32 x 65 floats: past the wave's 32 x 68 region? no --
-                        // 32 * 65 <= 32 * 68, but keep every wave's band-image reads done before the reuse
+  __builtin_amdgcn_wave_barrier();   // the band-image reads are done before wave_rowsum reuses the stage
   const float su = wave_rowsum(st, a0, a1, lane) * p.scale;
   const float sv = wave_rowsum(st, e0, e1, lane) * p.scale;
   const long prow = (long)b * (4 * gridDim.x) + blockIdx.x * 4 + wv;
@@ -1009,6 +996,220 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
   }
 }
 
+// ------------------------------------------------------------------------------------ dK, dV, two waves per SIMD
+// attn_rel_bwd_dkdv_kernel's work in <= 80 KiB of LDS and <= 256 registers: one query tile staged as Q + u and dO
+// (no Q + v image: the band product uses Q + u and adds c_r, as the other two-waves kernels), lse / D of the tile,
+// a ring of 3 band chunks with their c, and per wave a 64-row f32 skew stage of column stride 66 (the budget's
+// last KiB; 68 would not fit).  The next query tile is loaded between two barriers.
+constexpr int SD = 66;      // dK/dV skew stage column stride (floats)
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, RelP rp, const bf16* __restrict__ dout,
+                                                                    const float* __restrict__ lse,
+                                                                    const float* __restrict__ Dg,
+                                                                    bf16* __restrict__ dqkv, bf16* __restrict__ dsbuf,
+                                                                    int ldS) {
+  const bool drop = p.drop_p > 0.f;
+  if (drop) p.seed = salted_seed(p.seed, p.salt);
+  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
+  const float dkeep = drop_keep_scale(dthr);
+  __shared__ __attribute__((aligned(16))) bf16 sq[2 * TILE * KS];         // [Qu, dO][64][72]        18 KiB
+  __shared__ __attribute__((aligned(16))) bf16 sring[3 * TILE * KS];      // band ring                27 KiB
+  __shared__ __attribute__((aligned(16))) float scr[3 * TILE];             // c of the ring's rows
+  __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SD];          // skew stages              33 KiB
+  __shared__ __attribute__((aligned(16))) float sLD[2][TILE];              // lse * log2 e, D
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, jj = lane & 31;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int J0 = blockIdx.x * 128;
+  const int k0w = J0 + wv * 32;
+  const int kj = k0w + jj;
+  const int len = p.len[b];
+  const bool kvalid = kj < len;
+  const int odd = lane & 1, sh = 16 * odd;
+  const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
+  const uint32_t hbase = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)(4 * hh + odd)) * T2 + (uint32_t)(kj >> 1);
+  bf16x8 kf[4], vf[4];
+  load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + p.HD + h * p.dk, p.D3, kj, p.T, kf, lane);
+  load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + 2 * p.HD + h * p.dk, p.D3, kj, p.T, vf, lane);
+  const float c = p.scale * LOG2E;
+  f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
+  const bool block_live = J0 < len;
+  const int nqt = block_live ? (p.T + TILE - 1) / TILE : 0;
+  const int cb = p.T - 64 + J0;                  // relative row of band row 0 at query tile 0
+  float* st = sst + wv * 32 * SD;
+  const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
+  const bf16* gbase = dout + (long)b * p.T * p.HD + h * p.dk;
+  float pu8[8], dvu[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int d = (tid & 7) * 8 + e;
+    pu8[e] = d < p.dk ? rp.pu[h * p.dk + d] : 0.f;
+  }
+  load_dvu8(p, rp, h, tid, dvu);
+  // query tile qt -> LDS (Q + u, dO, lse * log2 e, D); VEC: clamped branch-free rows
+  auto qtile = [&](int qt) {
+    const int r0 = qt * TILE;
+    uint4 rq[2], rg[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int v = tid + 256 * i;
+      if constexpr (VEC) {
+        rq[i] = ld8c(qbase, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8);
+        rg[i] = ld8c(gbase, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8);
+      } else {
+        rq[i] = ld8(qbase, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+        rg[i] = ld8(gbase, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
+      }
+    }
+    float rl = 0.f, rd = 0.f;
+    const int qi = r0 + (tid & 63);
+    if (tid < TILE) {
+      const long li = ((long)b * p.H + h) * p.T + min(qi, p.T - 1);
+      rl = lse[li];
+      rd = Dg[li];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int v = tid + 256 * i;
+      const int row = v >> 3, c8 = (v & 7) * 8;
+      const bf16x8 q = __builtin_bit_cast(bf16x8, rq[i]);
+      bf16x8 qu;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qu[e] = (bf16)((float)q[e] + pu8[e]);
+      *reinterpret_cast<bf16x8*>(sq + row * KS + c8) = qu;
+      *reinterpret_cast<uint4*>(sq + TILE * KS + row * KS + c8) = rg[i];
+    }
+    if (tid < TILE) {
+      sLD[0][tid] = qi < p.T ? rl * LOG2E : INFINITY;   // lse = +inf for q >= T: P = 0
+      sLD[1][tid] = qi < p.T ? rd : 0.f;
+    }
+  };
+  auto rchunk = [&](int ch, int slot) {
+    uint4 rr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load<VEC>(p, rp, h, cb - 64 * (ch - 2), tid + 256 * i);
+    ring_chunk_store(sring + slot * TILE * KS, rr, tid);
+    ring_c_store(scr + slot * TILE, rr, dvu, tid);
+  };
+  if (nqt > 0) {
+    qtile(0);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) rchunk(ch, ch);
+    __syncthreads();
+  }
+  bf16* dsb = dsbuf + ((long)b * p.H + h) * p.T * (long)ldS;
+  const bf16* sQu = sq;
+  const bf16* sG = sq + TILE * KS;
+  const float* skw = st + jj + 31 + 4 * hh * (SD - 1);   // bd of (query acc_row(r, hh), key jj): skw[((r & 3) + 8 (r >> 2)) (SD - 1)]
+  float* colw = st + jj * SD + 4 * hh;                   // the lane's column (query jj), rows 8g + 4hh .. +3
+  for (int qt = 0; qt < nqt; ++qt) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      // S[q][key], dP[q][key] of queries 32t..32t+31 of the tile (accumulator rows) x the wave's 32 keys
+      f32x16 sa = (f32x16){0}, ga = (f32x16){0};
+      const int o = 32 * (1 + wv - t);           // band offset of the wave's 64 rows in the tile window
+      const int sl0 = (qt + 2 - (o >> 6)) % 3, sl1 = (qt + 2 - ((o + 32) >> 6)) % 3;
+      const bf16* blk0 = sring + sl0 * TILE * KS + (o & 63) * KS;
+      const bf16* blk1 = sring + sl1 * TILE * KS + ((o + 32) & 63) * KS;
+      {
+        f32x16 x0 = (f32x16){0}, x1 = (f32x16){0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 qf = rowfrag(sQu, 32 * t, 16 * s, lane);     // A of S, B of the band product
+          sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf, kf[s], sa, 0, 0, 0);
+          x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk0, 0, 16 * s, lane), qf, x0, 0, 0, 0);
+          x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk1, 0, 16 * s, lane), qf, x1, 0, 0, 0);
+        }
+        add_band_c(x0, scr + sl0 * TILE + (o & 63), hh);
+        add_band_c(x1, scr + sl1 * TILE + ((o + 32) & 63), hh);
+        // X[r'][i] (lanes = queries) -> stage[i][r']; bd[i][j] = X[j - i + 31][i]
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          *reinterpret_cast<float4*>(colw + 8 * g) = make_float4(x0[4 * g], x0[4 * g + 1], x0[4 * g + 2], x0[4 * g + 3]);
+          *reinterpret_cast<float4*>(colw + 32 + 8 * g) =
+              make_float4(x1[4 * g], x1[4 * g + 1], x1[4 * g + 2], x1[4 * g + 3]);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sG, 32 * t, 16 * s, lane), vf[s], ga, 0, 0, 0);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sa[r] += skw[((r & 3) + 8 * (r >> 2)) * (SD - 1)];
+      __builtin_amdgcn_wave_barrier();
+      const float* tL = sLD[0] + 32 * t + 4 * hh;
+      const float* tD = sLD[1] + 32 * t + 4 * hh;
+      f32x16 pd;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 Lg = *reinterpret_cast<const float4*>(tL + 8 * g);
+        const float4 Dq = *reinterpret_cast<const float4*>(tD + 8 * g);
+        const float Lr[4] = {Lg.x, Lg.y, Lg.z, Lg.w}, Dr[4] = {Dq.x, Dq.y, Dq.z, Dq.w};
+        bool kp[4] = {true, true, true, true};
+        if (drop) {
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            // dropout of (query of register r / r+1, key kj): lanes kj, kj^1 share one 32-bit hash per query
+            // (index (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2); the even lane hashes register r's query,
+            // the odd lane register r+1's, and a DPP swap hands each lane its partner's
+            const uint32_t hm = cfm_mix32(
+                (hbase + __builtin_amdgcn_readfirstlane((qt * TILE + 32 * t + 8 * g + e) * (int)T2)) ^ dkey);
+            const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
+            const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
+            kp[e] = ((h0 >> sh) & 0xFFFFu) >= dthr;
+            kp[e + 1] = ((h1 >> sh) & 0xFFFFu) >= dthr;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          const float e2 = fast_exp2(__builtin_fmaf(sa[r], c, -Lr[e]));   // lse = +inf for q >= T: 0
+          const float pa = kvalid ? e2 : 0.f;
+          const float pk = kp[e] ? pa : 0.f;
+          pd[r] = pk;                                                     // keep scale applied to dV once
+          sa[r] = pa * __builtin_fmaf(kp[e] ? ga[r] : 0.f, drop ? dkeep : 1.f, -Dr[e]);
+        }
+      }
+      // scale * dS -> dsbuf[i][j] (query-major) through the wave's stage as bf16 [query][40], 16-B row chunks
+      {
+        bf16* sd = reinterpret_cast<bf16*>(st);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sd[acc_row(r, hh) * 40 + jj] = (bf16)(sa[r] * p.scale);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int idx = 64 * it + lane, qr = idx >> 2, kc = k0w + 8 * (idx & 3);
+          const int qia = qt * TILE + 32 * t + qr;
+          const uint4 v = *reinterpret_cast<const uint4*>(sd + qr * 40 + 8 * (idx & 3));
+          if (qia < p.T && kc < ldS) *reinterpret_cast<uint4*>(dsb + (long)qia * ldS + kc) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = acc2frag(pd, s2);
+        const bf16x8 sf = acc2frag(sa, s2);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 0, lane), pf, dv0, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 32, lane), pf, dv1, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 0, lane), sf, dk0, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 32, lane), sf, dk1, 0, 0, 0);
+      }
+    }
+    if (qt + 1 < nqt) {
+      __syncthreads();          // every wave is done with query tile qt and with band chunk qt
+      qtile(qt + 1);
+      rchunk(qt + 3, qt % 3);
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  const int nvalid = min(32, p.T - k0w);
+  if (nvalid > 0) {
+    bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
+    store_transposed(st, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
+    store_transposed(st, dv0, dv1, drop ? dkeep : 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
+  }
+}
+
 // ------------------------------------------------------------------------------------ dpos
 // grid (ceil((2T-1)/64), H, B): 64 relative rows R0.. of head h for utterance b -> part[b] (the per-utterance
 // partials are summed by one deterministic column reduction); 4 waves = (d half, r half).
@@ -1196,8 +1397,12 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
   const int ldS = rel_ldS(p.T);
   const dim3 grid(cdiv(p.T, 128), p.H, p.B);
   if (rel_vec(p, rp)) {
-    hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                       (bf16*)dqkv, dsbuf, ldS);
+    if (g_rel_mode & 32)
+      hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, dsbuf, ldS);
+    else
+      hipLaunchKernelGGL(attn_rel_bwd_dkdv2_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, dsbuf, ldS);
     if (g_rel_mode & 32)
       hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                          (bf16*)dqkv, part);
@@ -1205,8 +1410,12 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
       hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                          (bf16*)dqkv, part);
   } else {
-    hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                       (bf16*)dqkv, dsbuf, ldS);
+    if (g_rel_mode & 32)
+      hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, dsbuf, ldS);
+    else
+      hipLaunchKernelGGL(attn_rel_bwd_dkdv2_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, dsbuf, ldS);
     if (g_rel_mode & 32)
       hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                          (bf16*)dqkv, part);
