@@ -68,31 +68,59 @@ __global__ __launch_bounds__(EB) void ada_colpart(const AdaP* __restrict__ t, in
   // the wave's RB/4 rows: their sums stay in registers (lane j keeps row j's) and the row EMAs are updated
   // once after the loop -- a read-modify-write per row inside it serialised every row on a memory round trip
   float rsum = 0.f;
-  for (int j = 0; j < RB / 4; ++j) {   // (the early exit keeps this loop rolled)
-    const int r = r0 + wv + 4 * j;
-    if (r >= r1) break;
-    const float* g = q.g + ((long)b * q.R + r) * q.C;
-    float s = 0.f;
+  if (q.C % 4 == 0 && ((uintptr_t)q.g & 15) == 0) {
+    // float4 columns: lane owns columns 4 lane + 256 k4 .. +3 (k4 < nk4); cacc[4 k4 + e] = column 4 lane + 256 k4 + e
+    const int nk4 = (q.C + 255) / 256;
+    for (int j = 0; j < RB / 4; ++j) {
+      const int r = r0 + wv + 4 * j;
+      if (r >= r1) break;
+      const float* g = q.g + ((long)b * q.R + r) * q.C;
+      float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const int c = lane + 64 * k;
-      if (k < nk && c < q.C) {
-        const float v = g[c];
-        const float e = v * v + eps1;
-        s += e;
-        cacc[k] += e;
+      for (int k4 = 0; k4 < KMAX / 4; ++k4) {
+        const int c = 4 * lane + 256 * k4;
+        if (k4 < nk4 && c < q.C) {
+          const float4 v = *reinterpret_cast<const float4*>(g + c);
+          const float e0 = v.x * v.x + eps1, e1 = v.y * v.y + eps1, e2 = v.z * v.z + eps1, e3 = v.w * v.w + eps1;
+          s += (e0 + e1) + (e2 + e3);
+          cacc[4 * k4] += e0; cacc[4 * k4 + 1] += e1; cacc[4 * k4 + 2] += e2; cacc[4 * k4 + 3] += e3;
+        }
       }
+      s = wave_sum(s);
+      rsum = lane == j ? s : rsum;
     }
-    s = wave_sum(s);
-    rsum = lane == j ? s : rsum;
+#pragma unroll
+    for (int k4 = 0; k4 < KMAX / 4; ++k4)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (k4 < nk4 && 4 * lane + 256 * k4 + e < q.C) red[wv][4 * lane + 256 * k4 + e] = cacc[4 * k4 + e];
+  } else {
+    for (int j = 0; j < RB / 4; ++j) {   // (the early exit keeps this loop rolled)
+      const int r = r0 + wv + 4 * j;
+      if (r >= r1) break;
+      const float* g = q.g + ((long)b * q.R + r) * q.C;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        const int c = lane + 64 * k;
+        if (k < nk && c < q.C) {
+          const float v = g[c];
+          const float e = v * v + eps1;
+          s += e;
+          cacc[k] += e;
+        }
+      }
+      s = wave_sum(s);
+      rsum = lane == j ? s : rsum;
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < nk) red[wv][lane + 64 * k] = cacc[k];
   }
   {
     const int r = r0 + wv + 4 * lane;
     if (lane < RB / 4 && r < r1) row_update(q, (long)b * q.R + r, rsum, b2t);
   }
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k)
-    if (k < nk) red[wv][lane + 64 * k] = cacc[k];
   __syncthreads();
   float* dst = part + q.part_off + ((long)b * nrb + rb) * q.C;
   for (int c = threadIdx.x; c < q.C; c += EB) dst[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
