@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void attn_simt_fwd(AttnP p, void* __restrict__
     l = l * alpha + wave_sum(e);
     acc *= alpha;
     m = mn;
-    sp[wv][lane] = (j < len) ? e * dropout_scale(p.drop_p, p.seed, drop_idx(p, b, h, i, j)) : 0.f;
+    sp[wv][lane] = (j < len) ? e * attn_dropout_scale(p.drop_p, p.seed, drop_idx(p, b, h, i, j)) : 0.f;
     __builtin_amdgcn_wave_barrier();
     if (lane < p.dk) {
       const int jn = min(64, len - j0);
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void attn_simt_bwd_dq(AttnP p, const void* __r
       float dp = 0.f;
       const long vrow = ((long)b * p.T + j) * p.D3 + 2 * HD + h * p.dk;
       for (int d = 0; d < p.dk; ++d) dp += sdo[wv][d] * ld_dyn(p.qkv, p.dt, vrow + d);
-      dp *= dropout_scale(p.drop_p, p.seed, drop_idx(p, b, h, i, j));
+      dp *= attn_dropout_scale(p.drop_p, p.seed, drop_idx(p, b, h, i, j));
       ds = pr * (dp - Di) * p.scale;
     }
     if (j < p.T) dsrow[j] = ds;
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void attn_simt_bwd_dkdv(AttnP p, const void* _
           if (p.pos) s += (q + p.pv[h * p.dk + d]) * pos_at(p, p.T - 1 - i + j, h, d);
         }
         s *= p.scale;
-        pd = __expf(s - lse[((long)b * p.H + h) * p.T + i]) * dropout_scale(p.drop_p, p.seed, drop_idx(p, b, h, i, j));
+        pd = __expf(s - lse[((long)b * p.H + h) * p.T + i]) * attn_dropout_scale(p.drop_p, p.seed, drop_idx(p, b, h, i, j));
       }
       sw[wv][0][lane] = pd;
       sw[wv][1][lane] = ds;
