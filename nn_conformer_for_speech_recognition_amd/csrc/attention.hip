@@ -343,7 +343,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
         const uint32_t hsh = attn_mix(
-            (hq + __builtin_amdgcn_readfirstlane((k0 + (r & 3) + 8 * (r >> 2)) >> 1)) ^ dkey);
+            hq + dkey + __builtin_amdgcn_readfirstlane((k0 + (r & 3) + 8 * (r >> 2)) >> 1));
         d0[r] = (hsh & 0xFFFFu) >= dthr ? d0[r] : 0.f;
         d0[r + 1] = (hsh >> 16) >= dthr ? d0[r + 1] : 0.f;
       }
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
           for (int e = 0; e < 4; e += 2) {
             // (the wave-uniform offset through readfirstlane: otherwise the per-register bases are
             // hoisted out of the loop as VGPRs)
-            const uint32_t hm = attn_mix((hbase + __builtin_amdgcn_readfirstlane((q0 + 8 * g + e) * (int)T2)) ^ dkey);
+            const uint32_t hm = attn_mix(hbase + dkey + __builtin_amdgcn_readfirstlane((q0 + 8 * g + e) * (int)T2));
             const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);  // lane ^ 1
             const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
             const bool k0 = ((h0 >> sh) & 0xFFFFu) >= dthr, k1 = ((h1 >> sh) & 0xFFFFu) >= dthr;

@@ -692,7 +692,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
       if (p.drop_p > 0.f) {
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const uint32_t hs = attn_mix((rowj + ((acc_row(r, hh) + 32 * t) >> 1)) ^ dkey);
+          const uint32_t hs = attn_mix(rowj + ((acc_row(r, hh) + 32 * t) >> 1) + dkey);
           dd[r] = (hs & 0xFFFFu) >= dthr ? dd[r] : 0.f;
           dd[r + 1] = (hs >> 16) >= dthr ? dd[r + 1] : 0.f;
         }
@@ -936,7 +936,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
           // (index (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2); the even lane hashes register r's query,
           // the odd lane register r+1's, and a DPP swap hands each lane its partner's
           const uint32_t hm = attn_mix(
-              (hbase + __builtin_amdgcn_readfirstlane((qt * TILE + 32 * t + (r & 3) + 8 * (r >> 2)) * (int)T2)) ^ dkey);
+              hbase + dkey + __builtin_amdgcn_readfirstlane((qt * TILE + 32 * t + (r & 3) + 8 * (r >> 2)) * (int)T2));
           const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
           const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
           mk[r] = ((h0 >> sh) & 0xFFFFu) >= dthr ? dkeep : 0.f;
@@ -1152,7 +1152,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
             // (index (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2); the even lane hashes register r's query,
             // the odd lane register r+1's, and a DPP swap hands each lane its partner's
             const uint32_t hm = attn_mix(
-                (hbase + __builtin_amdgcn_readfirstlane((qt * TILE + 32 * t + 8 * g + e) * (int)T2)) ^ dkey);
+                hbase + dkey + __builtin_amdgcn_readfirstlane((qt * TILE + 32 * t + 8 * g + e) * (int)T2));
             const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
             const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
             kp[e] = ((h0 >> sh) & 0xFFFFu) >= dthr;

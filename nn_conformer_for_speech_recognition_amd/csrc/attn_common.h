@@ -32,7 +32,7 @@ __device__ __forceinline__ uint64_t didx(const AttnM& p, int b, int h, int i, in
 // keep-scales of elements idx (even) and idx + 1: one mix for both (== dropout_keyed of each)
 __device__ __forceinline__ void dropout_pair(uint32_t thr, float keep, uint32_t key, uint64_t idx, float& m0,
                                              float& m1) {
-  const uint32_t h = attn_mix((uint32_t)(idx >> 1) ^ key);
+  const uint32_t h = attn_mix((uint32_t)(idx >> 1) + key);
   m0 = (h & 0xFFFFu) >= thr ? keep : 0.f;
   m1 = (h >> 16) >= thr ? keep : 0.f;
 }
@@ -43,7 +43,7 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 // the same with the pair's hash index j = (idx >> 1) mod 2^32 supplied in 32 bits (idx < 2^33)
 __device__ __forceinline__ void dropout_pair32(uint32_t thr, float keep, uint32_t key, uint32_t j, float& m0,
                                                float& m1) {
-  const uint32_t h = attn_mix(j ^ key);
+  const uint32_t h = attn_mix(j + key);
   m0 = (h & 0xFFFFu) >= thr ? keep : 0.f;
   m1 = (h >> 16) >= thr ? keep : 0.f;
 }
@@ -208,7 +208,7 @@ __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16&
     for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
       const int k0 = acc_row(r, hh);
       if constexpr (LATE) {
-        const uint32_t h0 = attn_mix((rowj + (k0 >> 1)) ^ dkey), h1 = attn_mix((rowj + (k0 >> 1) + 16) ^ dkey);
+        const uint32_t h0 = attn_mix(rowj + (k0 >> 1) + dkey), h1 = attn_mix(rowj + (k0 >> 1) + 16 + dkey);
         s0[r] = (h0 & 0xFFFFu) >= dthr ? s0[r] : 0.f;
         s0[r + 1] = (h0 >> 16) >= dthr ? s0[r + 1] : 0.f;
         s1[r] = (h1 & 0xFFFFu) >= dthr ? s1[r] : 0.f;

@@ -108,6 +108,8 @@ __device__ __forceinline__ uint32_t cfm_mix32(uint32_t x) {
 // The attention-probability dropout's element hash: two 24-bit multiplies (v_mul_u32_u24, full rate) in place of
 // lowbias32's two 32-bit ones (v_mul_lo_u32, quarter rate) -- the attention kernels hash one pair per two scores
 // and were VALU-bound on it.  Each multiply sees 24 bits, but the xor-shift before it folds the high bits in.
+// The key is ADDED to the pair index (not xor-ed, as for lowbias32), so a lane's base + key folds into one
+// register and each pair costs one add.
 // Over the attention index pattern ((bh T + i) T2 + j/2) its keep rate and lag-1..8 / diagonal correlations
 // of the keep decisions match lowbias32's to within sampling noise (T = 97, 373, 1498).
 __device__ __forceinline__ uint32_t attn_mix(uint32_t x) {
@@ -155,13 +157,13 @@ __device__ __forceinline__ float attn_dropout_scale(float p, uint64_t seed, uint
   if (p <= 0.f) return 1.f;
   const uint32_t thr = drop_thr(p);
   const uint64_t j = idx >> 1;
-  const uint32_t h = attn_mix((uint32_t)j ^ drop_key(seed, (uint32_t)(j >> 32)));
+  const uint32_t h = attn_mix((uint32_t)j + drop_key(seed, (uint32_t)(j >> 32)));
   return ((idx & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thr ? drop_keep_scale(thr) : 0.f;
 }
 // attn_dropout_scale with the per-seed key hoisted (valid for idx < 2^33, where drop_key's high word is 0):
 // bit-identical masks at one mix per element pair (MFMA attention kernels: key = drop_key(seed, 0))
 __device__ __forceinline__ float dropout_keyed(uint32_t thr, float keep, uint32_t key, uint64_t idx) {
-  const uint32_t h = attn_mix((uint32_t)(idx >> 1) ^ key);
+  const uint32_t h = attn_mix((uint32_t)(idx >> 1) + key);
   const uint32_t bits = (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
   return bits >= thr ? keep : 0.f;
 }

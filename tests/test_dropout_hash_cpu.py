@@ -1,5 +1,5 @@
 """Statistical check of the attention-dropout element hash (cfm_common.h attn_mix: two 24-bit multiplies) over
-the index pattern the attention kernels use, ((b H + h) T + i) T2 + j/2 with 16 bits per element: keep rate,
+the index pattern the attention kernels use, ((b H + h) T + i) T2 + j/2 (+ the key) with 16 bits per element: keep rate,
 and the correlation of keep decisions at key lags 1..8, query lags 1..8 and both diagonals, next to lowbias32
 (cfm_mix32, the hash of every other dropout) as the reference quality.  numpy only (CPU)."""
 import numpy as np
@@ -34,7 +34,7 @@ def _keep(f, nbh, T, key, p=0.1):
     bh = np.arange(nbh, dtype=np.uint64)[:, None, None]
     i = np.arange(T, dtype=np.uint64)[None, :, None]
     jp = np.arange(T2, dtype=np.uint64)[None, None, :]
-    h = f(((bh * T + i) * T2 + jp) ^ np.uint64(key))
+    h = f(((bh * T + i) * T2 + jp + np.uint64(key)) & M) if f is _attn_mix else f(((bh * T + i) * T2 + jp) ^ np.uint64(key))
     k = np.stack([(h & 0xFFFF) >= thr, (h >> 16) >= thr], -1).reshape(nbh, T, 2 * T2)[:, :, :T]
     return k.astype(np.float64)
 

@@ -191,7 +191,7 @@ def _attn_mix(x):
 
 def _keep(B, T, H, p, seed):
     """numpy restatement of the attention-dropout keep mask (cfm_common.h attn_mix / drop_key, attn_common.h
-    didx): element (b, h, i, j) keeps iff the 16-bit half (j & 1) of attn_mix(((bh T + i) T2 + j/2) ^ key) >= thr,
+    didx): element (b, h, i, j) keeps iff the 16-bit half (j & 1) of attn_mix(((bh T + i) T2 + j/2) + key) >= thr,
     T2 = (T rounded up to even) / 2, key = lowbias32-derived drop_key(seed, 0).  Returns (B, H, T, T) bool."""
     key = int(_mix32(np.array([(seed & 0xFFFFFFFF) ^ int(_mix32(np.array([((seed >> 32) + 0x9E3779B9) & 0xFFFFFFFF]))[0])]))[0])
     thr = int(np.float32(p) * np.float32(65536.0) + np.float32(0.5))
@@ -199,7 +199,7 @@ def _keep(B, T, H, p, seed):
     bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
     i = np.arange(T, dtype=np.uint64)[None, :, None]
     j = np.arange(T, dtype=np.uint64)[None, None, :]
-    hs = _attn_mix((((bh * T + i) * T2 + j // 2) & 0xFFFFFFFF) ^ key)
+    hs = _attn_mix((((bh * T + i) * T2 + j // 2) + key) & 0xFFFFFFFF)
     half = np.where(j % 2 == 0, hs & 0xFFFF, hs >> 16)
     return (half >= thr).reshape(B, H, T, T)
 
