@@ -666,7 +666,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
 #pragma unroll
       for (int s = 0; s < 4; ++s)
         x2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk[2], 0, 16 * s, lane), qu[s], x2, 0, 0, 0);
-    add_band_c(x2, cbk[2], hh);
+      add_band_c(x2, cbk[2], hh);
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int r = 0; r < 16; ++r) s0[r] += sk[(r & 3) + 8 * (r >> 2)];
@@ -727,7 +727,10 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
-      const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(bcol + 16 * s + 8 * hh);
+      // (B element j <-> band row 16s + 8(j >> 2) + 4hh + (j & 3): the k order trfrag_perm's A fragment expects)
+      const uint2 lo = *reinterpret_cast<const uint2*>(bcol + 16 * s + 4 * hh);
+      const uint2 hi = *reinterpret_cast<const uint2*>(bcol + 16 * s + 8 + 4 * hh);
+      const bf16x8 bfr = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
       const bf16* bk = blk[s >> 1];
       e0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(bk, 16 * (s & 1), 0, lane), bfr, e0, 0, 0, 0);
       e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(bk, 16 * (s & 1), 32, lane), bfr, e1, 0, 0, 0);
