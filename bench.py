@@ -417,6 +417,7 @@ class Harness:
     sync per step): the bench reports it as `nonfinite_steps` and exits non-zero when it is not 0."""
 
     def __init__(self, cfg, dev, rank=0, world=1, *, dropout=0.1, fp8=False, specaug=False, dp_overlap=False,
+                 chunk_layers=4,
                  eager=False, no_optimizer=False, probe_inline=False, lr=2e-5, seed=1234, grad_bf16=False):
         self.cfg = cfg
         name, L, d, H, ffn, K, B, secs, pos_enc = cfg
@@ -437,7 +438,8 @@ class Harness:
         # backward itself; graph: the step is captured as a chain of graphs cut at the chunk boundaries and the
         # reduces are issued between replays, cdist.SegmentedStepGraph).  grad_bf16: bf16 reduce copies
         self.reducer = cdist.GradAllReducer(self.params, model=self.model, overlap=bool(dp_overlap),
-                                            grad_dtype=torch.bfloat16 if grad_bf16 else torch.float32)
+                                            grad_dtype=torch.bfloat16 if grad_bf16 else torch.float32,
+                                            chunk_layers=chunk_layers)
         self.seg = None
         self.opt = Adafactor(self.params, lr=lr, beta1=0.9, scale_parameter=False, relative_step=False)
         # synthetic data: per-utterance min-max-normalised uniform mels, full lengths
@@ -619,6 +621,8 @@ def main():
                     help="N>1: one graph for fwd+bwd, every bucket reduced after the replay")
     ap.add_argument("--grad-bf16", action="store_true",
                     help="N>1: reduce the gradient buckets through bf16 copies (half the xGMI bytes)")
+    ap.add_argument("--dp-chunk-layers", type=int, default=4,
+                    help="layers per gradient bucket chunk (overlap mode: one graph cut + grouped-wgrad flush each)")
     ap.add_argument("--probe-inline", action="store_true",
                     help="put the roofline probe kernels inside the timed graph (default: a separate probed graph)")
     ap.add_argument("--poison", action="store_true",
@@ -656,6 +660,7 @@ def main():
 
     h = Harness(cfg, dev, rank, world, dropout=args.dropout, fp8=args.fp8, specaug=args.specaug,
                 dp_overlap=args.dp_overlap or (world > 1 and not args.no_dp_overlap), eager=args.eager,
+                chunk_layers=args.dp_chunk_layers,
                 no_optimizer=args.no_optimizer, probe_inline=args.probe_inline, grad_bf16=args.grad_bf16)
     model, T2, T_in = h.model, h.T2, h.T_in
 
@@ -785,7 +790,8 @@ def main():
                    "launch": "eager" if h.eager else (f"hip-graph chain ({len(h.seg)} segments, bucket all-reduce "
                                                       "between replays)" if h.seg is not None
                                                       else "hip-graph (fwd+bwd)"),
-                   "grad_reduce_dtype": "bf16" if h.reducer.grad_dtype == torch.bfloat16 else "fp32"},
+                   "grad_reduce_dtype": "bf16" if h.reducer.grad_dtype == torch.bfloat16 else "fp32",
+                   **({"dp_chunk_layers": args.dp_chunk_layers} if h.seg is not None else {})},
         "per_gpu_value": round(value / world, 1),
         # FLOPs the step executes (encoder + the folded front-end GEMMs; CTC head excluded), and the reference
         # composition's count (conv1 + conv2 + projection as the reference computes them) beside it

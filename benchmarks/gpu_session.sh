@@ -29,7 +29,7 @@ for s in "$@"; do
     ktests) run ktests 900 "$PYT -q tests/test_gpu_kernels.py tests/test_gpu_attention.py tests/test_gpu_conformer.py tests/test_gpu_fulldepth.py tests/test_gpu_frontfold.py tests/test_gpu_graph.py" ;;
     bench) run bench 600 "python -u bench.py --gpus 1 --steps 20 --warmup 5" ;;
     benchL60) run benchL60 600 "python -u bench.py --config L60 --steps 10 --warmup 3 --no-cpu-baseline" ;;
-    dp) run dp 900 "for f in '' '--dp-overlap' '--dp-overlap --grad-bf16' ''; do python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline \$f || exit 1; done" ;;
+    dp) run dp 900 "for f in '' '--dp-overlap' '--dp-overlap --grad-bf16' '--dp-overlap --dp-chunk-layers 17' ''; do python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline \$f || exit 1; done" ;;
     pmc_dgemm) run pmc_dgemm 900 "bash benchmarks/pmc_dgemm.sh $OUT 5" ;;
     ktrace) run ktrace 600 "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline && python3 $R/profiles/summarize.py \$(find $OUT/ktrace -name '*kernel_stats.csv' | head -1) auto 45 > $OUT/kernel_summary.txt" ;;
     *) run custom 900 "$s" ;;
