@@ -48,7 +48,10 @@ def _worker(rank, world, port, q):
     random.seed(42)
     draws = psa.draw(8, 40, tau, hp)
     local = psa.pack(draws, tau, lo, hi)
-    q.put((r, w0, grads, (lo, hi), local, len(red.buckets), grads16))
+    # numpy arrays travel by value: a torch tensor goes through a shared-memory handle the receiver fetches from
+    # this process's resource sharer, which races with this process exiting (FileNotFoundError in the parent)
+    q.put((r, w0.numpy(), [g.numpy() for g in grads], (lo, hi), local.numpy(), len(red.buckets),
+           [g.numpy() for g in grads16]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -66,6 +69,8 @@ def test_dp_allreduce_broadcast_and_slicing():
         p.join(timeout=60)
         assert p.exitcode == 0
     out.sort(key=lambda t: t[0])
+    T = torch.from_numpy
+    out = [(r, T(w0), [T(g) for g in gr], sl, T(loc), nb, [T(g) for g in g16]) for r, w0, gr, sl, loc, nb, g16 in out]
     (_, w0a, ga, sa, la, nb, g16a), (_, w0b, gb, sb, lb, _, g16b) = out
     for x, y in zip(g16a, g16b):
         assert x.dtype == torch.float32 and torch.equal(x, torch.full_like(x, 1.875)) and torch.equal(x, y)
