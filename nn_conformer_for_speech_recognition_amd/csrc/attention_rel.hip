@@ -19,9 +19,9 @@
 //              MFMA over the band once dS^T is scattered into the stage in band coordinates;
 //              per-wave column sums of both terms -> du, dv partials (one reduction launch).
 //   dK/dV kernel (keys on the lanes, streams query tiles): recomputes S with the band in the
-//              transposed role, dV += dO^T P~, dK += (q+u)^T dS, and writes scale*dS (bf16,
+//              transposed role, dV += dO^T P~, dK += (q+u)^T dS, and writes dS (bf16,
 //              query-major) for the dpos pass.
-//   dpos kernel: dpos_r = sum_{b,i} scale*dS[i, i+r-(T-1)] (q_i+v) -- in (i, r) coordinates a plain
+//   dpos kernel: dpos_r = scale * sum_{b,i} dS[i, i+r-(T-1)] (q_i+v) -- in (i, r) coordinates a plain
 //              GEMM over i whose dS operand rows are contiguous runs of the stored dS rows.
 #include "attn_common.h"
 
@@ -772,7 +772,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
 // staged in LDS as q+u, q+v, dO (+ lse, D).  The band for (query tile qt, 128 keys) is 192 rows
 // starting at relative row T-64-64qt+J0; it moves DOWN one chunk per query tile (ring chunk kc holds
 // rows T-64+J0-64(kc-2) ..+63, tile qt uses chunks qt, qt+1, qt+2).
-// dsbuf: (B, H, T, ldS) bf16, scale * dS, query-major.
+// dsbuf: (B, H, T, ldS) bf16, dS (unscaled: the dpos pass applies the scale), query-major.
 template <bool VEC>
 __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp, const bf16* __restrict__ dout,
                                                                 const float* __restrict__ lse,
@@ -957,13 +957,13 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
         pd[r] = pa * mk[r];
         sa[r] = pa * (ga[r] * mk[r] - td[r]);
       }
-      // scale * dS -> dsbuf[i][j] (query-major): the 32 x 32 block goes through the wave's stage (free after
+      // dS -> dsbuf[i][j] (query-major, unscaled): the 32 x 32 block goes through the wave's stage (free after
       // the skew reads) as bf16 [query][40] and out as 16-B row chunks, 2 stores per lane instead of 16
       // 2-byte ones.  Keys >= T (zero dS) land in the row's padding [T, ldS); chunks past ldS are skipped.
       {
         bf16* sd = reinterpret_cast<bf16*>(st);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sd[acc_row(r, hh) * 40 + jj] = (bf16)(sa[r] * p.scale);
+        for (int r = 0; r < 16; ++r) sd[acc_row(r, hh) * 40 + jj] = (bf16)sa[r];
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
@@ -1165,18 +1165,26 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e;
-          const float e2 = fast_exp2(__builtin_fmaf(sa[r], c, -Lr[e]));   // lse = +inf for q >= T: 0
-          const float pa = kvalid ? e2 : 0.f;
+          // P of keys >= len is not zeroed here: it only reaches this lane's own dK / dV column (zeroed at the
+          // store) and dS entries the dpos pass masks out (lse = +inf for q >= T: P = 0)
+          const float pa = fast_exp2(__builtin_fmaf(sa[r], c, -Lr[e]));
           const float pk = kp[e] ? pa : 0.f;
           pd[r] = pk;                                                     // keep scale applied to dV once
           sa[r] = pa * __builtin_fmaf(kp[e] ? ga[r] : 0.f, drop ? dkeep : 1.f, -Dr[e]);
         }
       }
-      // scale * dS -> dsbuf[i][j] (query-major) through the wave's stage as bf16 [query][40], 16-B row chunks
+      bf16x8 pf[2], sf[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        pf[s2] = acc2frag(pd, s2);
+        sf[s2] = acc2frag(sa, s2);
+      }
+      // dS -> dsbuf[i][j] (query-major, unscaled: the dpos pass applies the scale) through the wave's stage as
+      // bf16 [query][40] from the MFMA fragments (no second conversion), out as 16-B row chunks
       {
         bf16* sd = reinterpret_cast<bf16*>(st);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sd[acc_row(r, hh) * 40 + jj] = (bf16)(sa[r] * p.scale);
+        for (int r = 0; r < 16; ++r) sd[acc_row(r, hh) * 40 + jj] = sf[r >> 3][r & 7];
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
@@ -1189,12 +1197,10 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pf = acc2frag(pd, s2);
-        const bf16x8 sf = acc2frag(sa, s2);
-        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 0, lane), pf, dv0, 0, 0, 0);
-        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 32, lane), pf, dv1, 0, 0, 0);
-        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 0, lane), sf, dk0, 0, 0, 0);
-        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 32, lane), sf, dk1, 0, 0, 0);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 0, lane), pf[s2], dv0, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 32, lane), pf[s2], dv1, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 0, lane), sf[s2], dk0, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 32, lane), sf[s2], dk1, 0, 0, 0);
       }
     }
     if (qt + 1 < nqt) {
@@ -1207,16 +1213,18 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
   __syncthreads();
   const int nvalid = min(32, p.T - k0w);
   if (nvalid > 0) {
+    // keys >= len: zero gradients (their P was not masked in the loop); the accumulator column is the lane's key
+    const float kz = kvalid ? 1.f : 0.f;
     bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
-    store_transposed(st, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
-    store_transposed(st, dv0, dv1, drop ? dkeep : 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
+    store_transposed(st, dk0, dk1, p.scale * kz, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);       // (per-lane mul)
+    store_transposed(st, dv0, dv1, (drop ? dkeep : 1.f) * kz, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
   }
 }
 
 // ------------------------------------------------------------------------------------ dpos
 // grid (ceil((2T-1)/64), H, B): 64 relative rows R0.. of head h for utterance b -> part[b] (the per-utterance
 // partials are summed by one deterministic column reduction); 4 waves = (d half, r half).
-// part[b][r][h*dk+d] = sum_i dsbuf[b,h,i, i+r-(T-1)] * (q_i + v)[d]   (keys j < len[b] only)
+// part[b][r][h*dk+d] = scale * sum_i dsbuf[b,h,i, i+r-(T-1)] * (q_i + v)[d]   (keys j < len[b] only)
 // The next 64-query tile is loaded into registers while the current one runs through the MFMAs.
 template <bool VEC>
 __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp, const bf16* __restrict__ dsbuf,
@@ -1329,7 +1337,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp
   // acc: rows d (32 dh + acc_row), lanes rr (32 rh + lane&31) -> sO[rr][d] -> this utterance's partial rows
   const int hh = lane >> 5;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) sO[(32 * rh + (lane & 31)) * 65 + 32 * dh + acc_row(r, hh)] = acc[r];
+  for (int r = 0; r < 16; ++r) sO[(32 * rh + (lane & 31)) * 65 + 32 * dh + acc_row(r, hh)] = acc[r] * p.scale;
   __syncthreads();
   float* dst = part + (long)b * nrel * p.HD;
   for (int idx = tid; idx < TILE * 64; idx += 256) {
@@ -1342,7 +1350,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp
 
 namespace cfm {
 
-// workspace of the rel-pos MFMA backward: [D (B*H*T f32)] [du/dv partials] [scale*dS (B*H*T*ldS bf16)]
+// workspace of the rel-pos MFMA backward: [D (B*H*T f32)] [du/dv partials] [dS (B*H*T*ldS bf16)]
 // [per-utterance dpos partials (B*(2T-1)*H*dk f32)]
 static inline int rel_ldS(int T) { return (T + 7) & ~7; }
 static inline size_t rel_part_floats(int B, int T, int H, int dk) { return (size_t)B * 4 * cdiv(T, 128) * 2 * H * dk; }
