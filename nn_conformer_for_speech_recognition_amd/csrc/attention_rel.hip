@@ -1213,11 +1213,18 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
   __syncthreads();
   const int nvalid = min(32, p.T - k0w);
   if (nvalid > 0) {
-    // keys >= len: zero gradients (their P was not masked in the loop); the accumulator column is the lane's key
-    const float kz = kvalid ? 1.f : 0.f;
+    // keys >= len: zero gradients (their P was not masked in the loop and may be large or inf: a select, not a
+    // multiply); the accumulator column is the lane's key
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dk0[r] = kvalid ? dk0[r] : 0.f;
+      dk1[r] = kvalid ? dk1[r] : 0.f;
+      dv0[r] = kvalid ? dv0[r] : 0.f;
+      dv1[r] = kvalid ? dv1[r] : 0.f;
+    }
     bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
-    store_transposed(st, dk0, dk1, p.scale * kz, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);       // (per-lane mul)
-    store_transposed(st, dv0, dv1, (drop ? dkeep : 1.f) * kz, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
+    store_transposed(st, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
+    store_transposed(st, dv0, dv1, drop ? dkeep : 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
   }
 }
 
