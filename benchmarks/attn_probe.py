@@ -1,6 +1,6 @@
 """Attention timing experiments at L15 (B 32, T 373, 8 heads, dk 64, dropout 0.1): the forward under the
-cfm_attn_set_mode dbg bits (0 full, 2 staging only, 4 no epilogue stores, 8 unpipelined order) and the backward
-(dQ + dK/dV; mode 8: unpipelined), HIP-event medians of interleaved rounds.
+cfm_attn_set_mode dbg bits (0 full, 2 staging only, 4 no epilogue stores) and the backward (dQ + dK/dV), HIP-event
+medians of interleaved rounds.
     python benchmarks/attn_probe.py [--reps 5]"""
 import argparse
 import json
@@ -39,10 +39,9 @@ def main():
     o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=0.1, seed=3)
     do = torch.randn(B * T, H * dk, device="cuda", generator=g).to(torch.bfloat16)
     cases = {}
-    for mode, tag in ((0, "fwd"), (8, "fwd unpipelined"), (2, "fwd staging only"), (4, "fwd no stores")):
+    for mode, tag in ((0, "fwd"), (2, "fwd staging only"), (4, "fwd no stores")):
         cases[tag] = (mode, lambda: ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=0.1, seed=3))
     cases["bwd (D + dQ + dK/dV)"] = (0, lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=0.1, seed=3))
-    cases["bwd unpipelined"] = (8, lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=0.1, seed=3))
     cases["fwd p=0"] = (0, lambda: ops.attn_fwd(qkv, lens, B, T, H, dk, drop_p=0.0, seed=3))
     cases["bwd p=0"] = (0, lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, drop_p=0.0, seed=3))
     res = {k: [] for k in cases}

@@ -1,6 +1,6 @@
 """The grouped weight-gradient launch of one L15 backward (17 layers x 8 GEMMs, M = 11,936 tokens) under several
 cfm_gemm_set_mode values (interleaved rounds, HIP events).
-    python benchmarks/wgrad_modes.py [--modes 3,8388611] [--layers 17]"""
+    python benchmarks/wgrad_modes.py [--modes 3] [--layers 17]"""
 import argparse
 import json
 import os
@@ -14,7 +14,7 @@ from nn_conformer_for_speech_recognition_amd import _lib, ops  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="3,8388611")
+    ap.add_argument("--modes", default="3")
     ap.add_argument("--layers", type=int, default=17)
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()

@@ -221,10 +221,9 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
   float m = -INFINITY, l = 0.f;
   const float c = p.scale * LOG2E;
   const int qi = q0 + (lane & 31);
-  // Software-pipelined over key tiles: the S = K Q^T MFMAs of tile kt + 1 are issued before tile kt's softmax
-  // VALU, so they run on the matrix pipe while the wave works through the exponentials and the dropout hashes
-  // (the loop is unrolled by two so the two score buffers keep static register names).  The dropout keep scale
-  // is applied once to the output (o * keep / l), not to every P entry.
+  // The dropout keep scale is applied once to the output (o * keep / l), not to every P entry.  (Round 4: issuing
+  // tile kt+1's S MFMAs before tile kt's softmax VALU, unrolled by two, measured 27.08 vs 26.86 us at L15 --
+  // three waves per SIMD already overlap one wave's VALU with another's MFMAs -- and was removed.)
   const bool late = p.drop_p > 0.f;
   auto qk = [&](int kt, f32x16& s0, f32x16& s1) {
     const bf16* sK = sKall + kt * TILE * KS;
@@ -248,31 +247,13 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
       }
     }
   };
-  f32x16 sa0, sa1, sb0, sb1;
-  if (p.dbg & 8) {   // A/B: the unpipelined order
-    for (int kt = 0; kt < nkt; ++kt) {
-      qk(kt, sa0, sa1);
-      __builtin_amdgcn_sched_barrier(0);
-      softmax_tile<true>(p, sa0, sa1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
-      pv(kt, sa0, sa1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-  qk(0, sa0, sa1);
-  for (int kt = 0; kt < nkt; kt += 2) {
-    const bool n1 = kt + 1 < nkt;
-    if (n1) qk(kt + 1, sb0, sb1);
+  f32x16 sa0, sa1;
+  for (int kt = 0; kt < nkt; ++kt) {
+    qk(kt, sa0, sa1);
     __builtin_amdgcn_sched_barrier(0);
     softmax_tile<true>(p, sa0, sa1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
     pv(kt, sa0, sa1);
-    if (n1) {
-      if (kt + 2 < nkt) qk(kt + 2, sa0, sa1);
-      __builtin_amdgcn_sched_barrier(0);
-      softmax_tile<true>(p, sb0, sb1, o0, o1, m, l, c, (kt + 1) * TILE, len, kt + 1 == nkt - 1, b, h, qi, hh, dthr,
-                         dkeep, dkey);
-      pv(kt + 1, sb0, sb1);
-    }
-  }
+    __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();     // every wave is done with K/V: the images become the epilogue staging
   float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
@@ -325,8 +306,6 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
   const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
   const uint32_t hq = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)qi) * T2 + (uint32_t)(2 * hh);
   const float keep = p.drop_p > 0.f ? dkeep : 1.f;
-  // Software-pipelined as the forward: the S^T / dP^T MFMAs of key step ks + 1 are issued before step ks's
-  // VALU (exponentials, dropout hashes), unrolled by two so both score buffers keep static register names.
   auto sd = [&](int ks, f32x16& s0, f32x16& d0) {
     const int k0 = ks * 32;
     s0 = (f32x16){0};
@@ -364,27 +343,12 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
       a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sKall, k0 + 16 * s, 32, lane), pf, a1, 0, 0, 0);
     }
   };
-  f32x16 sa, da, sb, db;
-  if (p.dbg & 8) {   // A/B: the unpipelined order
-    for (int ks = 0; ks < nks; ++ks) {
-      sd(ks, sa, da);
-      __builtin_amdgcn_sched_barrier(0);
-      ds(ks, sa, da);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-  if (nks > 0) sd(0, sa, da);
-  for (int ks = 0; ks < nks; ks += 2) {
-    const bool n1 = ks + 1 < nks;
-    if (n1) sd(ks + 1, sb, db);
+  f32x16 sa, da;
+  for (int ks = 0; ks < nks; ++ks) {
+    sd(ks, sa, da);
     __builtin_amdgcn_sched_barrier(0);
     ds(ks, sa, da);
-    if (n1) {
-      if (ks + 2 < nks) sd(ks + 2, sa, da);
-      __builtin_amdgcn_sched_barrier(0);
-      ds(ks + 1, sb, db);
-    }
-  }
+    __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();
   float* stage = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
@@ -471,10 +435,6 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
   const int nvalid = min(32, p.T - k0w);
   const bool v8 = p.vec && ((uintptr_t)dqkv & 7) == 0;
 
-  // Both passes are software-pipelined as the forward: the next query step's score MFMAs are issued before the
-  // current step's VALU (exponentials, dropout hashes), unrolled by two for static register names; cfm_attn_set_mode
-  // bit 3 runs the unpipelined order (A/B).
-  const bool pipe = !(p.dbg & 8);
   // ---- pass 1: P, dV^T += dO^T P
   {
     f32x16 dv0 = (f32x16){0}, dv1 = (f32x16){0};
@@ -523,27 +483,12 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
         dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sGall, q0 + 16 * s2, 32, lane), pf[s2], dv1, 0, 0, 0);
       }
     };
-    f32x16 sa, sb;
-    if (!pipe) {
-      for (int qt = 0; qt < nqs; ++qt) {
-        sc(qt, sa);
-        __builtin_amdgcn_sched_barrier(0);
-        pdv(qt, sa);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-      if (nqs > 0) sc(0, sa);
-      for (int qt = 0; qt < nqs; qt += 2) {
-        const bool n1 = qt + 1 < nqs;
-        if (n1) sc(qt + 1, sb);
-        __builtin_amdgcn_sched_barrier(0);
-        pdv(qt, sa);
-        if (n1) {
-          if (qt + 2 < nqs) sc(qt + 2, sa);
-          __builtin_amdgcn_sched_barrier(0);
-          pdv(qt + 1, sb);
-        }
-      }
+    f32x16 sa;
+    for (int qt = 0; qt < nqs; ++qt) {
+      sc(qt, sa);
+      __builtin_amdgcn_sched_barrier(0);
+      pdv(qt, sa);
+      __builtin_amdgcn_sched_barrier(0);
     }
     store_acc_rows(dv0, dv1, 1.f, obase + 2 * p.HD, p.D3, k0w, nvalid, p.dk, v8, lane);
   }
@@ -584,27 +529,12 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
         dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 32, lane), sf[s2], dk1, 0, 0, 0);
       }
     };
-    f32x16 sa, ga, sb, gb;
-    if (!pipe) {
-      for (int qt = 0; qt < nqs; ++qt) {
-        sg(qt, sa, ga);
-        __builtin_amdgcn_sched_barrier(0);
-        dsk(qt, sa, ga);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-      if (nqs > 0) sg(0, sa, ga);
-      for (int qt = 0; qt < nqs; qt += 2) {
-        const bool n1 = qt + 1 < nqs;
-        if (n1) sg(qt + 1, sb, gb);
-        __builtin_amdgcn_sched_barrier(0);
-        dsk(qt, sa, ga);
-        if (n1) {
-          if (qt + 2 < nqs) sg(qt + 2, sa, ga);
-          __builtin_amdgcn_sched_barrier(0);
-          dsk(qt + 1, sb, gb);
-        }
-      }
+    f32x16 sa, ga;
+    for (int qt = 0; qt < nqs; ++qt) {
+      sg(qt, sa, ga);
+      __builtin_amdgcn_sched_barrier(0);
+      dsk(qt, sa, ga);
+      __builtin_amdgcn_sched_barrier(0);
     }
     store_acc_rows(dk0, dk1, p.scale, obase + p.HD, p.D3, k0w, nvalid, p.dk, v8, lane);
   }
@@ -866,7 +796,7 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   if (pos)
     return cfm::attn_rel_fwd_launch(qkv, o, lse, lengths, pos, pos_u, pos_v, B, T, H, dk, drop_p, seed, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
-          ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 14,
+          ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 6,
           cfm::g_rng_salt};
   if (use_head(T)) {
     // LDS sized for the full padded length (lengths are device data; len <= T)
@@ -899,7 +829,7 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
                                      T, H, dk, dtype, drop_p, seed, ws, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0),
-          g_attn_mode & 14, cfm::g_rng_salt};
+          g_attn_mode & 6, cfm::g_rng_salt};
   const long nrow = (long)B * H * T;
   (void)nrow;
   CFM_REQUIRE(H * dk <= 1024, CFM_ERR_UNSUPPORTED, "H*dk must be <= 1024");

@@ -1152,169 +1152,6 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
   probe_end(p.probe);
 }
 
-// XCD-contiguous position of workgroup L among G (blocks b, b + 8 share an XCD; bijective for any G)
-__device__ __forceinline__ int xcd_id_any(int L, int G) {
-  if (G <= 8) return L;
-  const int xcd = L & 7, q = G >> 3, r = G & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
-}
-
-// ---------------------------------------------------------------- persistent warp-specialised K-major GEMM
-// For the wide outputs of short reductions (FFN-up forward / FFN-down data gradient N 2048, QKV N 1536, pointwise-
-// conv-1 N 1024; K 512): one workgroup per CU walks tiles t = pos, pos + grid, ... (row-major tile order, XCD-
-// contiguous positions: the WGs of one XCD hold neighbouring tiles of the same A rows).  The 4 loader waves stream
-// the stages of ALL its tiles through one 3-deep ring (global stage index g = tile * nk + kt), so the next tile's
-// first stages land while the current tile's epilogue runs; the 8 compute waves run the ws kernel's pipelined
-// K loop.  The epilogue stages the f32 tile in 64-row chunks in an LDS area of its own (the ring stays live) and
-// the compute waves finish 8-column chunks through epilogue_store8 (the loaders issue no stores, so their vmcnt
-// counts only their DMA).  All waves pass the same barrier sequence: one per stage (where stage g + 1 becomes
-// visible) + two per epilogue chunk.
-template <int BMt, int WM, int WN, int NL, int NST>
-__global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_wsp_kernel(GemmP p, PipeOp oa, PipeOp ob, int ntm, int ntn) {
-  constexpr int BKt = 64, BNt = BN, NC = WM * WN;
-  constexpr int ABYTES = BMt * BKt * 2, BBYTES = BNt * BKt * 2, STAGE = ABYTES + BBYTES;
-  constexpr int AP = ABYTES / 1024, BP = BBYTES / 1024, PW = (AP + BP) / NL;
-  static_assert(PW * NL == AP + BP && AP * 1024 == ABYTES && BP * 1024 == BBYTES, "whole DMA pieces per loader");
-  constexpr int FM = BMt / WM / 16, FN = BNt / WN / 16;
-  static_assert(FM * WM * 16 == BMt && FN * WN * 16 == BNt, "wave tiling");
-  constexpr int EPS = BNt + 4, CPW = BNt / 8, CR = 64;                 // staging: CR-row chunks of the f32 tile
-  static_assert(BMt % CR == 0 && (CR * CPW) % 64 == 0, "chunking");
-  constexpr int RING = NST * STAGE, STG = CR * EPS * 4;
-  static_assert(NST == 3, "the slot refilled after stage g+1's barrier is g-1's: NST - 1 = 2 stages ahead");
-  __shared__ __attribute__((aligned(1024))) char lds[RING + STG];
-  probe_begin(p.probe);
-  gemm_drop_prep(p);
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntiles = ntm * ntn, G = gridDim.x;
-  const int pos = xcd_id_any(blockIdx.x, G);
-  const int my_tiles = pos < ntiles ? (ntiles - 1 - pos) / G + 1 : 0;
-  const int nk = p.K / BKt;
-  const int gtot = my_tiles * nk;                 // this workgroup's stages
-  float* st = reinterpret_cast<float*>(lds + RING);
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const bool loader = wid >= NC;
-  // ---- loader state: piece i of a stage is 1-KiB piece q = lw + NL i of the [A | B] stage image
-  const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, 0), rb = pipe_rsrc(ob, 0);
-  auto stage_src = [&](int i, int g) {             // source byte offset of loader piece i of global stage g
-    const int t = pos + (g / nk) * G, kt = g % nk;
-    const int tm = t / ntn, tn = t % ntn;
-    const int q = (wid - NC) + NL * i;
-    return (q < AP ? pipe_src<true, BMt, BKt>(oa, q * 64 + lane, tm * BMt, 0)
-                   : pipe_src<true, BNt, BKt>(ob, (q - AP) * 64 + lane, tn * BNt, 0)) + (unsigned)(kt * BKt * 2);
-  };
-  auto issue = [&](int g) {
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int q = (wid - NC) + NL * i;
-      dma16(q < AP ? ra : rb, lds + (g % NST) * STAGE + q * 1024, stage_src(i, g));
-    }
-  };
-  auto wait_stage = [&](int s, int last) {       // stage s landed: only stages issued after it outstanding
-    if (last - s >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-  // ---- compute state
-  const int wm = wid / WN, wn = wid % WN;
-  bf16x8 af[2][FM], bfr[2][FN];
-  auto read = [&](bf16x8 (&fa)[FM], bf16x8 (&fb)[FN], int g, int sub) {
-    const char* sa = lds + (g % NST) * STAGE;
-    const char* sb = sa + ABYTES;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) fb[j] = pipe_frag16k<BKt>(sb, wn * FN * 16 + 16 * j, 32 * sub, lane);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) fa[i] = pipe_frag16k<BKt>(sa, wm * FM * 16 + 16 * i, 32 * sub, lane);
-  };
-  auto mma = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN]) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-  };
-  int last = -1;
-  if (loader && gtot > 0) {
-    for (int s = 0; s < NST - 1 && s < gtot; ++s) issue(s);
-    last = min(NST - 2, gtot - 1);
-    wait_stage(0, last);
-  }
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (!loader && gtot > 0) read(af[0], bfr[0], 0, 0);
-  for (int lt = 0; lt < my_tiles; ++lt) {
-    const int t = pos + lt * G;
-    const int m0 = (t / ntn) * BMt, n0 = (t % ntn) * BNt;
-    for (int kt = 0; kt < nk; ++kt) {
-      const int g = lt * nk + kt;
-      const bool more = g + 1 < gtot;
-      if (!loader) {
-        read(af[1], bfr[1], g, 1);
-        mma(af[0], bfr[0]);
-      }
-      if (more) {
-        if (loader) wait_stage(g + 1, last);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (loader) {
-          const int gn = g + NST - 1;            // refills the slot of stage g - 1
-          if (gn < gtot) {
-            issue(gn);
-            last = gn;
-          }
-        } else {
-          read(af[0], bfr[0], g + 1, 0);
-        }
-      }
-      if (!loader) mma(af[1], bfr[1]);
-    }
-    // ---- epilogue of tile t: CR-row chunks through the staging area, every wave finishes 8-column chunks
-#pragma nounroll
-    for (int c = 0; c < BMt / CR; ++c) {
-      if (!loader) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int r16 = wm * FM * 16 + 16 * i;          // first row of accumulator block i (wave-uniform)
-          if (r16 >= c * CR && r16 < (c + 1) * CR) {
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                st[(r16 - c * CR + 4 * (lane >> 4) + e) * EPS + wn * FN * 16 + 16 * j + (lane & 15)] = acc[i][j][e];
-          }
-        }
-      }
-      // raw barriers: the loaders' prefetch DMA of the next tile stays in flight (a __syncthreads would drain it)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (!loader) {     // (the loaders issue no stores: their vmcnt counts their DMA only)
-        static_assert((CR * CPW) % (NC * 64) == 0, "whole items per compute thread");
-#pragma unroll
-        for (int it = 0; it < CR * CPW / (NC * 64); ++it) {
-          const int item = it * NC * 64 + tid;
-          const int row = item / CPW, c8 = (item % CPW) * 8;
-          const float4 lo = *reinterpret_cast<const float4*>(st + row * EPS + c8);
-          const float4 hi = *reinterpret_cast<const float4*>(st + row * EPS + c8 + 4);
-          float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-          epilogue_store8(p, 0, 0, m0 + c * CR + row, n0 + c8, v);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    if (!loader) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  probe_end(p.probe);
-}
-
 extern int g_gemm_mode;
 // ---------------------------------------------------------------- grouped weight gradients
 // All weight-gradient GEMMs dW_i = dY_iᵀ X_i (+ bias gradient sum_rows dY_i) of a backward pass in ONE
@@ -1581,30 +1418,16 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
   const int sel = (g_gemm_mode >> 4) & 7;
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k);
   int v = sel;
-  if constexpr (AK && BKM) {
-    // wide outputs (N > 512; cfm_gemm_set_mode bit 22 also the d-wide ones) on the persistent warp-specialised kernel:
-    // 192 x 128 tiles, one workgroup per CU, the next tile's stages prefetched under the epilogue (bit 21: off, A/B)
-    const bool wide = p.N > 512 || (g_gemm_mode & 4194304);
-    if (v == 0 && wide && p.split_k == 1 && batch == 1 && !(g_gemm_mode & 2097152)) {
-      const int ntm = cdiv(p.M, 192), ntn = cdiv(p.N, BN);
-      const int grid = min(ntm * ntn, num_cus());
-      hipLaunchKernelGGL((gemm_wsp_kernel<192, 2, 4, 4, 3>), dim3(grid), dim3(768), 0, s, p, oa, ob, ntm, ntn);
-      return;
-    }
-  }
   if constexpr (AK) {
     // auto: outputs <= 512 columns (the encoder's d-wide outputs) take the 192-row tiles: 63 x 4 = 252
     // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
     if (v == 5 || (v == 0 && p.N <= 512 && p.split_k == 1 && (long)p.M * batch >= 4096)) {
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
       if constexpr (BKM) {
-        // warp-specialised loading (cfm_gemm_set_mode bit 19 keeps the shared-DMA kernel below for A/B; bit 20
-        // selects 4 compute waves of 96 x 64 instead of 8 of 96 x 32)
+        // warp-specialised loading (cfm_gemm_set_mode bit 19 keeps the shared-DMA kernel below for A/B): d-wide
+        // layer family 266.6 -> 240.2 us same box (gpurun_out r04b dgemm; 4 compute waves of 96 x 64: 244.4 us)
         if (!(g_gemm_mode & 524288) && p.split_k == 1) {
-          if (g_gemm_mode & 1048576)
-            hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 2, 4, 4>), g192, dim3(512), 0, s, p, oa, ob);
-          else
-            hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 4, 4, 4>), g192, dim3(768), 0, s, p, oa, ob);
+          hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 4, 4, 4>), g192, dim3(768), 0, s, p, oa, ob);
           return;
         }
       }
@@ -1783,181 +1606,15 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   return cfm::check_launch("cfm_gemm");
 }
 
-// ---------------------------------------------------------------- warp-specialised grouped weight gradients
-// The grouped weight-gradient launch (dW = dY^T X over the tokens, MN-major operands read through
-// ds_read_b64_tr_b16) with the ws kernel's roles: 4 loader waves issue every stage's LDS-DMA and, while the
-// compute waves run, fold the staged dY tile into the bias-gradient column sums (they idle otherwise); 8 compute
-// waves of 64 x 64 (32x32x16 MFMA) read the next 16-deep step's fragments while the current MFMAs run.  256 x 128
-// tiles (a 64 x 128 wave tile would not fit the 12-wave register budget), BK 32, 4-deep ring.  cfm_gemm_set_mode
-// bit 23 (A/B against the 256 x 256 shared-DMA kernel).
-constexpr int WSG_BN = 128;
-template <int NST>
-__global__ __launch_bounds__(12 * 64) void gemm_wsg_kernel(GemmP p0, GatherA ga) {
-  constexpr int BMt = 256, BNt = WSG_BN, BKt = 32, WM = 4, WN = 2, NC = WM * WN, NL = 4;
-  constexpr int ABYTES = BMt * BKt * 2, BBYTES = BNt * BKt * 2, STAGE = ABYTES + BBYTES;
-  constexpr int AP = ABYTES / 1024, BP = BBYTES / 1024, PW = (AP + BP) / NL;
-  static_assert(PW * NL == AP + BP, "whole DMA pieces per loader");
-  constexpr int FM = BMt / WM / 32, FN = BNt / WN / 32;
-  constexpr int EPS = BNt + 4, CPW = BNt / 8, CR = 128;             // epilogue: 128-row chunks
-  constexpr int RING = NST * STAGE, EPI = CR * EPS * 4;
-  constexpr int ACH = BMt / 8, RG = NL * 64 / ACH;                    // column sums: 8-column chunk x row group
-  constexpr int RED = EPI;                                            // their partials: after the staging
-  static_assert(RED + RG * BMt * 4 <= (RING > EPI ? RING : EPI), "column-sum partials fit");
-  __shared__ __attribute__((aligned(1024))) char lds[RING > EPI ? RING : EPI];
-  GemmP p = p0;
-  PipeOp oa, ob;
-  int tm, tn;
-  group_task(ga, p, oa, ob, tm, tn);
-  p.probe = p0.probe;
-  probe_begin(p.probe);
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int m0 = tm * BMt, n0 = tn * BNt;
-  const int nk = (p.K + BKt - 1) / BKt;
-  const bool loader = wid >= NC;
-  const bool acs = p.acs_slab != nullptr && tn == 0;
-  f32x16 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x16){0};
-  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int acs_c = (tid - NC * 64) % ACH, acs_r = (tid - NC * 64) / ACH;
-  if (loader) {
-    const int lw = wid - NC;
-    const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, 0), rb = pipe_rsrc(ob, 0);
-    unsigned off[PW];
-    int ldo[PW];
-    bool isa[PW];
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int q = lw + NL * i;
-      isa[i] = q < AP;
-      const int qq = isa[i] ? q : q - AP;
-      off[i] = isa[i] ? pipe_src<false, BMt, BKt>(oa, qq * 64 + lane, m0, 0)
-                      : pipe_src<false, BNt, BKt>(ob, qq * 64 + lane, n0, 0);
-      ldo[i] = (isa[i] ? 0 : ABYTES) + qq * 1024;
-    }
-    const unsigned stepa = (unsigned)(BKt * oa.ld * 2), stepb = (unsigned)(BKt * ob.ld * 2);
-    auto issue = [&](int kt) {
-#pragma unroll
-      for (int i = 0; i < PW; ++i)
-        dma16(isa[i] ? ra : rb, lds + (kt % NST) * STAGE + ldo[i], off[i] + kt * (isa[i] ? stepa : stepb));
-    };
-    auto wait_stage = [&](int s, int last) {
-      const int younger = min(NST - 2, last - s);
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW) : "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    };
-    auto colsum = [&](int kt) {       // the staged dY tile's column sums (chunk c of k-row k at slot c ^ 4(k & 3))
-      const char* sa = lds + (kt % NST) * STAGE;
-#pragma unroll
-      for (int kq = 0; kq < BKt / RG; ++kq) {
-        const int k = acs_r + kq * RG;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + k * (BMt * 2) + 16 * (acs_c ^ (4 * (k & 3))));
-#pragma unroll
-        for (int e = 0; e < 8; ++e) csum[e] += (float)v[e];
-      }
-    };
-    for (int s = 0; s < NST - 1 && s < nk; ++s) issue(s);
-    int last = min(NST - 2, nk - 1);
-    wait_stage(0, last);
-    __builtin_amdgcn_s_barrier();
-    for (int kt = 0; kt + 1 < nk; ++kt) {
-      wait_stage(kt + 1, last);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      const int kn = kt + NST - 1;
-      if (kn < nk) {
-        issue(kn);
-        last = kn;
-      }
-      if (acs) colsum(kt);          // stage kt stays resident until the barrier after stage kt + NST - 2
-    }
-    if (acs) colsum(nk - 1);
-  } else {
-    const int wm = wid / WN, wn = wid % WN;
-    bf16x8 af[2][FM], bfr[2][FN];
-    auto read = [&](bf16x8 (&fa)[FM], bf16x8 (&fb)[FN], int kt, int sub) {
-      const char* sa = lds + (kt % NST) * STAGE;
-      const char* sb = sa + ABYTES;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = pipe_frag<false, BNt, BKt>(sb, wn * FN * 32 + 32 * j, 16 * sub, lane);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) fa[i] = pipe_frag<false, BMt, BKt>(sa, wm * FM * 32 + 32 * i, 16 * sub, lane);
-    };
-    auto mma = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN]) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    };
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    read(af[0], bfr[0], 0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      read(af[1], bfr[1], kt, 1);
-      mma(af[0], bfr[0]);
-      if (kt + 1 < nk) {
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        read(af[0], bfr[0], kt + 1, 0);
-      }
-      mma(af[1], bfr[1]);
-    }
-  }
-  __syncthreads();   // every DMA landed (the loaders' last wait was vmcnt(0)), every fragment read consumed
-  float* st = reinterpret_cast<float*>(lds);
-  float* red = reinterpret_cast<float*>(lds + RED);
-  const int wm = wid / WN, wn = wid % WN;
-#pragma nounroll
-  for (int c = 0; c < BMt / CR; ++c) {
-    if (!loader && (wm * FM * 32) / CR == c) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            st[(wm * FM * 32 - c * CR + 32 * i + accr<false>(r, lane)) * EPS + wn * FN * 32 + 32 * j + accc<false>(r, lane)] =
-                acc[i][j][r];
-    }
-    if (c == 0 && loader && acs) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) red[acs_r * BMt + acs_c * 8 + e] = csum[e];
-    }
-    __syncthreads();
-    if (!loader) {
-#pragma unroll
-      for (int it = 0; it < CR * CPW / (NC * 64); ++it) {
-        const int item = it * NC * 64 + tid;
-        const int row = item / CPW, c8 = (item % CPW) * 8;
-        const float4 lo = *reinterpret_cast<const float4*>(st + row * EPS + c8);
-        const float4 hi = *reinterpret_cast<const float4*>(st + row * EPS + c8 + 4);
-        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        epilogue_store8(p, 0, 0, m0 + c * CR + row, n0 + c8, v);
-      }
-    } else if (c == 0 && acs) {
-      const int t = tid - NC * 64;
-      if (t < BMt && m0 + t < p.M) {
-        float s = 0.f;
-        for (int g = 0; g < RG; ++g) s += red[g * BMt + t];
-        p.acs_slab[m0 + t] = s;
-      }
-    }
-    __syncthreads();
-  }
-  probe_end(p.probe);
-}
-
 CFM_EXPORT size_t cfm_wgrad_group_task_bytes(void) { return sizeof(WgTask); }
 // grouped weight-gradient launch: 256 x 256 output tiles, BK 32, 4-deep ring (half the dY panel re-reads of
 // 256 x 128; 17 layers 5.46 -> 4.89 ms, L15 step -0.8 ms same-box; 256 x 128 BK 32 two per CU, 256 x 128 BK 64 and
 // plain dispatch order measured slower and were removed in round 4; a 256 x 256 BK 64 double-buffered form spilled
 // and ran 2.4x slower)
+// (round 4: a warp-specialised 256 x 128 form -- 4 loader waves folding the bias sums, 8 compute waves -- ran
+// 2.889 vs 2.870 ms for the 17-layer launch, gpurun_out r04b wgrad, and was removed)
 constexpr int WG_BN = 256;
-int wg_bn() { return (g_gemm_mode & 8388608) ? WSG_BN : WG_BN; }
-CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, wg_bn()); }
+CFM_EXPORT long cfm_wgrad_group_tiles(int N, int K) { return (long)cdiv(N, 256) * cdiv(K, WG_BN); }
 
 // fill task i of a HOST table: dW (N x K, fp32) = dYᵀ X over M tokens, dY (M x N) / X (M x K) bf16
 // row-major; db (N, fp32, may be NULL) = sum_rows dY; tile0 = first workgroup id of the task
@@ -1976,7 +1633,7 @@ CFM_EXPORT int cfm_wgrad_group_fill(void* host_tab, int i, const void* dy, const
   t.oa = PipeOp{(const bf16*)dy, N, 0, N, (unsigned)((long)M * N * 2)};
   t.ob = PipeOp{(const bf16*)x, K, 0, K, (unsigned)((long)M * K * 2)};
   t.tile0 = tile0;
-  t.tiles_n = cdiv(K, wg_bn());
+  t.tiles_n = cdiv(K, WG_BN);
   reinterpret_cast<WgTask*>(host_tab)[i] = t;
   return CFM_OK;
 }
@@ -1989,11 +1646,8 @@ CFM_EXPORT int cfm_wgrad_group_probed(const void* dev_tab, int ntasks, long tota
   GatherA ga{};
   ga.group_tab = dev_tab;
   ga.group_n = ntasks;
-  if (g_gemm_mode & 8388608)   // (tables filled under the same mode: 256 x WSG_BN tiles)
-    hipLaunchKernelGGL((gemm_wsg_kernel<4>), dim3((unsigned)total_tiles), dim3(768), 0, cfm::as_stream(stream), gp, ga);
-  else
-    hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 4, 1, false, false, 8, 2, false, true, false, WG_BN>),
-                       dim3((unsigned)total_tiles), dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
+  hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 4, 1, false, false, 8, 2, false, true, false, WG_BN>),
+                     dim3((unsigned)total_tiles), dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
   return cfm::check_launch("cfm_wgrad_group");
 }
 
