@@ -26,7 +26,7 @@ for s in "$@"; do
     wgrad) run wgrad 300 "python -u benchmarks/wgrad_modes.py --modes 3" ;;
     attn) run attn 300 "python -u benchmarks/attn_probe.py" ;;
     rel) run rel 300 "python -u benchmarks/rel_modes.py" ;;
-    relprof) run relprof 600 "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/relprof -o run -- python3 $R/benchmarks/rel_modes.py --reps 2 && python3 $R/profiles/summarize.py \$(find $OUT/relprof -name '*kernel_stats.csv' | head -1) auto 25 > $OUT/rel_kernel_summary.txt" ;;
+    relprof) run relprof 600 "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/relprof -o run -- python3 $R/benchmarks/rel_modes.py --reps 2 && python3 $R/profiles/summarize.py \$(find $OUT/relprof -name '*kernel_stats.csv' | head -1) 1 25 > $OUT/rel_kernel_summary.txt" ;;
     ktests) run ktests 900 "$PYT -q tests/test_gpu_kernels.py tests/test_gpu_attention.py tests/test_gpu_conformer.py tests/test_gpu_fulldepth.py tests/test_gpu_frontfold.py tests/test_gpu_graph.py" ;;
     bench) run bench 600 "python -u bench.py --gpus 1 --steps 20 --warmup 5" ;;
     benchL60) run benchL60 600 "python -u bench.py --config L60 --steps 10 --warmup 3 --no-cpu-baseline" ;;

@@ -737,11 +737,13 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
     }
     __builtin_amdgcn_wave_barrier();
     if (kt + 1 < nkt) {
-      __syncthreads();
+      // the next tile's loads are issued before the barrier (this tile's registers are dead): their latency
+      // overlaps the wait for the other waves
       tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
       tile_load<VEC>(p, b, (kt + 1) * TILE, vcol, rv, tid);
 #pragma unroll
       for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
+      __syncthreads();
       tile_store(skv, rk, tid);
       tile_store(skv + TILE * KS, rv, tid);
       ring_chunk_store(sring + (kt % 3) * TILE * KS, rq, tid);
@@ -1048,10 +1050,11 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
     pu8[e] = d < p.dk ? rp.pu[h * p.dk + d] : 0.f;
   }
   load_dvu8(p, rp, h, tid, dvu);
-  // query tile qt -> LDS (Q + u, dO, lse * log2 e, D); VEC: clamped branch-free rows
-  auto qtile = [&](int qt) {
+  // query tile qt -> registers (qload) -> LDS as Q + u, dO, lse * log2 e, D (qstore); VEC: clamped branch-free rows
+  uint4 rq[2], rg[2], rr[2];
+  float rl = 0.f, rd = 0.f;
+  auto qload = [&](int qt, int ch) {
     const int r0 = qt * TILE;
-    uint4 rq[2], rg[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int v = tid + 256 * i;
@@ -1063,13 +1066,16 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
         rg[i] = ld8(gbase, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
       }
     }
-    float rl = 0.f, rd = 0.f;
-    const int qi = r0 + (tid & 63);
     if (tid < TILE) {
-      const long li = ((long)b * p.H + h) * p.T + min(qi, p.T - 1);
+      const long li = ((long)b * p.H + h) * p.T + min(r0 + tid, p.T - 1);
       rl = lse[li];
       rd = Dg[li];
     }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load<VEC>(p, rp, h, cb - 64 * (ch - 2), tid + 256 * i);
+  };
+  auto qstore = [&](int qt, int slot) {
+    const int qi = qt * TILE + (tid & 63);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int v = tid + 256 * i;
@@ -1085,18 +1091,20 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
       sLD[0][tid] = qi < p.T ? rl * LOG2E : INFINITY;   // lse = +inf for q >= T: P = 0
       sLD[1][tid] = qi < p.T ? rd : 0.f;
     }
+    ring_chunk_store(sring + slot * TILE * KS, rr, tid);
+    ring_c_store(scr + slot * TILE, rr, dvu, tid);
   };
   auto rchunk = [&](int ch, int slot) {
-    uint4 rr[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load<VEC>(p, rp, h, cb - 64 * (ch - 2), tid + 256 * i);
     ring_chunk_store(sring + slot * TILE * KS, rr, tid);
     ring_c_store(scr + slot * TILE, rr, dvu, tid);
   };
   if (nqt > 0) {
-    qtile(0);
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) rchunk(ch, ch);
+    for (int ch = 0; ch < 2; ++ch) rchunk(ch, ch);
+    qload(0, 2);
+    qstore(0, 2);
     __syncthreads();
   }
   bf16* dsb = dsbuf + ((long)b * p.H + h) * p.T * (long)ldS;
@@ -1204,9 +1212,9 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
       }
     }
     if (qt + 1 < nqt) {
+      qload(qt + 1, qt + 3);    // issued before the barrier: the latency overlaps the wait for the other waves
       __syncthreads();          // every wave is done with query tile qt and with band chunk qt
-      qtile(qt + 1);
-      rchunk(qt + 3, qt % 3);
+      qstore(qt + 1, qt % 3);
       __syncthreads();
     }
   }

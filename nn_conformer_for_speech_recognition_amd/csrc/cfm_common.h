@@ -95,8 +95,9 @@ __device__ __forceinline__ void st8_dyn(void* p, int dt, long idx, const float (
 
 // ----------------------------------------------------------------------------- dropout RNG
 // Counter-based dropout: element idx of a call keyed by `seed` draws 16 uniform bits; elements
-// 2j and 2j+1 share one 32-bit hash of j (lowbias32 mixer, two 32-bit multiplies), so the mask
-// costs a few VALU ops per element and is regenerated bit-identically in the backward kernels.
+// 2j and 2j+1 share one 32-bit hash of j + key (attn_mix below: two full-rate 24-bit multiplies; the key itself
+// comes from lowbias32), so the mask costs a few VALU ops per element and is regenerated bit-identically in the
+// backward kernels.
 __device__ __forceinline__ uint32_t cfm_mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -105,9 +106,9 @@ __device__ __forceinline__ uint32_t cfm_mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// The attention-probability dropout's element hash: two 24-bit multiplies (v_mul_u32_u24, full rate) in place of
-// lowbias32's two 32-bit ones (v_mul_lo_u32, quarter rate) -- the attention kernels hash one pair per two scores
-// and were VALU-bound on it.  Each multiply sees 24 bits, but the xor-shift before it folds the high bits in.
+// The dropout element hash (every dropout: attention probabilities, GEMM epilogues, scale_dropout, the LayerNorm
+// backward's g2): two 24-bit multiplies (v_mul_u32_u24, full rate) in place of lowbias32's two 32-bit ones
+// (v_mul_lo_u32, quarter rate) -- the attention kernels hash one pair per two scores and were VALU-bound on it.  Each multiply sees 24 bits, but the xor-shift before it folds the high bits in.
 // The key is ADDED to the pair index (not xor-ed, as for lowbias32), so a lane's base + key folds into one
 // register and each pair costs one add.
 // Over the attention index pattern ((bh T + i) T2 + j/2) its keep rate and lag-1..8 / diagonal correlations
@@ -125,7 +126,7 @@ __device__ __forceinline__ uint32_t drop_key(uint64_t seed, uint32_t jhi) {
 }
 __device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t idx) {
   const uint64_t j = idx >> 1;
-  const uint32_t h = cfm_mix32((uint32_t)j ^ drop_key(seed, (uint32_t)(j >> 32)));
+  const uint32_t h = attn_mix((uint32_t)j + drop_key(seed, (uint32_t)(j >> 32)));
   return (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
 }
 // dropped iff the 16 bits fall below round(p * 65536); kept elements scale by the exact inverse
@@ -152,13 +153,9 @@ __device__ __forceinline__ float dropout_scale(float p, uint64_t seed, uint64_t 
   const uint32_t thr = drop_thr(p);
   return drop_bits(seed, idx) >= thr ? drop_keep_scale(thr) : 0.f;
 }
-// the attention-dropout keep scale of element idx (attn_mix; the SIMT attention kernels)
+// the attention-dropout keep scale of element idx (the SIMT attention kernels): the same element hash
 __device__ __forceinline__ float attn_dropout_scale(float p, uint64_t seed, uint64_t idx) {
-  if (p <= 0.f) return 1.f;
-  const uint32_t thr = drop_thr(p);
-  const uint64_t j = idx >> 1;
-  const uint32_t h = attn_mix((uint32_t)j + drop_key(seed, (uint32_t)(j >> 32)));
-  return ((idx & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thr ? drop_keep_scale(thr) : 0.f;
+  return dropout_scale(p, seed, idx);
 }
 // attn_dropout_scale with the per-seed key hoisted (valid for idx < 2^33, where drop_key's high word is 0):
 // bit-identical masks at one mix per element pair (MFMA attention kernels: key = drop_key(seed, 0))
@@ -176,9 +173,10 @@ __device__ __forceinline__ void dropout_scale8(float p, uint64_t seed, uint64_t 
   if (lo0 <= 0xFFFFFFFBu) {
     const uint32_t key = drop_key(seed, (uint32_t)(j0 >> 32));
     uint32_t h[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) h[q] = cfm_mix32((lo0 + q) ^ key);
     const int odd = (int)(base & 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h[q] = attn_mix(lo0 + q + key);
+    h[4] = odd ? attn_mix(lo0 + 4 + key) : 0u;   // (an even base needs 4 pair hashes)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int q = (odd + e) >> 1;

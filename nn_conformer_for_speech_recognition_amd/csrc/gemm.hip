@@ -309,9 +309,10 @@ __device__ __forceinline__ void epilogue_store8(const GemmP& p, int z, int zs, i
     const uint64_t j0 = base >> 1;
     if ((j0 >> 32) == 0 && (uint32_t)j0 <= 0xFFFFFFFBu && !(p.dbg & 2)) {   // (always, below 2^33 elements)
       uint32_t h[5];
-#pragma unroll
-      for (int q = 0; q < 5; ++q) h[q] = cfm_mix32(((uint32_t)j0 + q) ^ p.dkey0);
       const int odd = (int)(base & 1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) h[q] = attn_mix((uint32_t)j0 + q + p.dkey0);
+      h[4] = odd ? attn_mix((uint32_t)j0 + 4 + p.dkey0) : 0u;   // (an even base needs 4 pair hashes)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int q = (odd + e) >> 1;
