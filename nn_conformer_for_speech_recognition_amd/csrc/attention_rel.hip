@@ -250,9 +250,11 @@ __global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf1
 
 // ------------------------------------------------------------------------------------ band bias column
 // (q + v) . p_r = (q + u) . p_r + c_r with c_r = (v - u) . p_r: the two-waves kernels form the band product from
-// the (q + u) operand they already hold and add c_r (fp32, per relative row) -- no (q + v) operand in registers or
-// LDS (dQ: 16 registers, dK/dV: a 9-KiB Q + v image; the forward has the registers and keeps (q + v), as the
-// c_r path costs ~80 VALU per tile).  c of a ring chunk is computed from the chunk's staged rows: the 8 threads that store one row's 8 16-B
+// the (q + u) operand they already hold and add c_r (fp32, per relative row) -- no (q + v) operand in registers
+// (dQ: 16 registers; the forward has the registers and keeps (q + v), as the c_r path costs ~80 VALU per tile).
+// (Round 4: a two-waves dK/dV built the same way -- 81 KiB, Q+u / dO single-buffered, loads between two barriers --
+// ran 351 vs 302 us per layer at L60, profiles/r04/rel_l60_kernels_s2.txt, and was removed: the one-wave kernel's
+// double-buffered register prefetch hides the tile loads that the single-buffered form exposes twice per tile.)  c of a ring chunk is computed from the chunk's staged rows: the 8 threads that store one row's 8 16-B
 // pieces each dot 8 columns with (v - u) and sum over the 8 lanes (three xor shuffles).
 __device__ __forceinline__ void load_dvu8(const AttnM& p, const RelP& rp, int h, int tid, float (&dvu)[8]) {
 #pragma unroll
@@ -954,232 +956,11 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
       f32x16 pd;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float e2 = fast_exp2(__builtin_fmaf(sa[r], c, -tl[r]));   // lse = +inf for q >= T: 0
-        const float pa = kvalid ? e2 : 0.f;
+        // (keys >= len are not masked here: their P only reaches this lane's own dK / dV column, zeroed at the
+        // store, and dS entries the dpos pass masks out)
+        const float pa = fast_exp2(__builtin_fmaf(sa[r], c, -tl[r]));   // lse = +inf for q >= T: 0
         pd[r] = pa * mk[r];
         sa[r] = pa * (ga[r] * mk[r] - td[r]);
-      }
-      // dS -> dsbuf[i][j] (query-major, unscaled): the 32 x 32 block goes through the wave's stage (free after
-      // the skew reads) as bf16 [query][40] and out as 16-B row chunks, 2 stores per lane instead of 16
-      // 2-byte ones.  Keys >= T (zero dS) land in the row's padding [T, ldS); chunks past ldS are skipped.
-      {
-        bf16* sd = reinterpret_cast<bf16*>(st);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sd[acc_row(r, hh) * 40 + jj] = (bf16)sa[r];
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-          const int idx = 64 * it + lane, qr = idx >> 2, kc = k0w + 8 * (idx & 3);
-          const int qia = qt * TILE + 32 * t + qr;
-          const uint4 v = *reinterpret_cast<const uint4*>(sd + qr * 40 + 8 * (idx & 3));
-          if (qia < p.T && kc < ldS) *reinterpret_cast<uint4*>(dsb + (long)qia * ldS + kc) = v;
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pf = acc2frag(pd, s2);
-        const bf16x8 sf = acc2frag(sa, s2);
-        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 0, lane), pf, dv0, 0, 0, 0);
-        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sG, 32 * t + 16 * s2, 32, lane), pf, dv1, 0, 0, 0);
-        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 0, lane), sf, dk0, 0, 0, 0);
-        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQu, 32 * t + 16 * s2, 32, lane), sf, dk1, 0, 0, 0);
-      }
-    }
-    if (qt + 1 < nqt) {
-      sstore(cur ^ 1);
-      ring_chunk_store(sring + ((qt + 3) & (RING - 1)) * TILE * KS, rr, tid);
-    }
-    __syncthreads();
-  }
-  float* stage = sst + wv * 32 * SS2;    // 32 x 68 >= 32 x 65 floats
-  const int nvalid = min(32, p.T - k0w);
-  if (nvalid > 0) {
-    bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
-    store_transposed(stage, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
-    store_transposed(stage, dv0, dv1, 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
-  }
-}
-
-// ------------------------------------------------------------------------------------ dK, dV, two waves per SIMD
-// attn_rel_bwd_dkdv_kernel's work in <= 80 KiB of LDS and <= 256 registers: one query tile staged as Q + u and dO
-// (no Q + v image: the band product uses Q + u and adds c_r, as the other two-waves kernels), lse / D of the tile,
-// a ring of 3 band chunks with their c, and per wave a 64-row f32 skew stage of column stride 66 (the budget's
-// last KiB; 68 would not fit).  The next query tile is loaded between two barriers.
-constexpr int SD = 66;      // dK/dV skew stage column stride (floats)
-template <bool VEC>
-__global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, RelP rp, const bf16* __restrict__ dout,
-                                                                    const float* __restrict__ lse,
-                                                                    const float* __restrict__ Dg,
-                                                                    bf16* __restrict__ dqkv, bf16* __restrict__ dsbuf,
-                                                                    int ldS) {
-  const bool drop = p.drop_p > 0.f;
-  if (drop) p.seed = salted_seed(p.seed, p.salt);
-  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
-  const float dkeep = drop_keep_scale(dthr);
-  __shared__ __attribute__((aligned(16))) bf16 sq[2 * TILE * KS];         // [Qu, dO][64][72]        18 KiB
-  __shared__ __attribute__((aligned(16))) bf16 sring[3 * TILE * KS];      // band ring                27 KiB
-  __shared__ __attribute__((aligned(16))) float scr[3 * TILE];             // c of the ring's rows
-  __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SD];          // skew stages              33 KiB
-  __shared__ __attribute__((aligned(16))) float sLD[2][TILE];              // lse * log2 e, D
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, jj = lane & 31;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int J0 = blockIdx.x * 128;
-  const int k0w = J0 + wv * 32;
-  const int kj = k0w + jj;
-  const int len = p.len[b];
-  const bool kvalid = kj < len;
-  const int odd = lane & 1, sh = 16 * odd;
-  const uint32_t T2 = (uint32_t)(p.T + (p.T & 1)) >> 1;
-  const uint32_t hbase = ((uint32_t)(b * p.H + h) * (uint32_t)p.T + (uint32_t)(4 * hh + odd)) * T2 + (uint32_t)(kj >> 1);
-  bf16x8 kf[4], vf[4];
-  load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + p.HD + h * p.dk, p.D3, kj, p.T, kf, lane);
-  load_bfrags(p, p.qkv + (long)b * p.T * p.D3 + 2 * p.HD + h * p.dk, p.D3, kj, p.T, vf, lane);
-  const float c = p.scale * LOG2E;
-  f32x16 dk0 = (f32x16){0}, dk1 = (f32x16){0}, dv0 = (f32x16){0}, dv1 = (f32x16){0};
-  const bool block_live = J0 < len;
-  const int nqt = block_live ? (p.T + TILE - 1) / TILE : 0;
-  const int cb = p.T - 64 + J0;                  // relative row of band row 0 at query tile 0
-  float* st = sst + wv * 32 * SD;
-  const bf16* qbase = p.qkv + (long)b * p.T * p.D3 + h * p.dk;
-  const bf16* gbase = dout + (long)b * p.T * p.HD + h * p.dk;
-  float pu8[8], dvu[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int d = (tid & 7) * 8 + e;
-    pu8[e] = d < p.dk ? rp.pu[h * p.dk + d] : 0.f;
-  }
-  load_dvu8(p, rp, h, tid, dvu);
-  // query tile qt -> registers (qload) -> LDS as Q + u, dO, lse * log2 e, D (qstore); VEC: clamped branch-free rows
-  uint4 rq[2], rg[2], rr[2];
-  float rl = 0.f, rd = 0.f;
-  auto qload = [&](int qt, int ch) {
-    const int r0 = qt * TILE;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int v = tid + 256 * i;
-      if constexpr (VEC) {
-        rq[i] = ld8c(qbase, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8);
-        rg[i] = ld8c(gbase, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8);
-      } else {
-        rq[i] = ld8(qbase, p.D3, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
-        rg[i] = ld8(gbase, p.HD, r0 + (v >> 3), p.T, (v & 7) * 8, p.dk, p.vec);
-      }
-    }
-    if (tid < TILE) {
-      const long li = ((long)b * p.H + h) * p.T + min(r0 + tid, p.T - 1);
-      rl = lse[li];
-      rd = Dg[li];
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load<VEC>(p, rp, h, cb - 64 * (ch - 2), tid + 256 * i);
-  };
-  auto qstore = [&](int qt, int slot) {
-    const int qi = qt * TILE + (tid & 63);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int v = tid + 256 * i;
-      const int row = v >> 3, c8 = (v & 7) * 8;
-      const bf16x8 q = __builtin_bit_cast(bf16x8, rq[i]);
-      bf16x8 qu;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) qu[e] = (bf16)((float)q[e] + pu8[e]);
-      *reinterpret_cast<bf16x8*>(sq + row * KS + c8) = qu;
-      *reinterpret_cast<uint4*>(sq + TILE * KS + row * KS + c8) = rg[i];
-    }
-    if (tid < TILE) {
-      sLD[0][tid] = qi < p.T ? rl * LOG2E : INFINITY;   // lse = +inf for q >= T: P = 0
-      sLD[1][tid] = qi < p.T ? rd : 0.f;
-    }
-    ring_chunk_store(sring + slot * TILE * KS, rr, tid);
-    ring_c_store(scr + slot * TILE, rr, dvu, tid);
-  };
-  auto rchunk = [&](int ch, int slot) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) rr[i] = ring_chunk_load<VEC>(p, rp, h, cb - 64 * (ch - 2), tid + 256 * i);
-    ring_chunk_store(sring + slot * TILE * KS, rr, tid);
-    ring_c_store(scr + slot * TILE, rr, dvu, tid);
-  };
-  if (nqt > 0) {
-#pragma unroll
-    for (int ch = 0; ch < 2; ++ch) rchunk(ch, ch);
-    qload(0, 2);
-    qstore(0, 2);
-    __syncthreads();
-  }
-  bf16* dsb = dsbuf + ((long)b * p.H + h) * p.T * (long)ldS;
-  const bf16* sQu = sq;
-  const bf16* sG = sq + TILE * KS;
-  const float* skw = st + jj + 31 + 4 * hh * (SD - 1);   // bd of (query acc_row(r, hh), key jj): skw[((r & 3) + 8 (r >> 2)) (SD - 1)]
-  float* colw = st + jj * SD + 4 * hh;                   // the lane's column (query jj), rows 8g + 4hh .. +3
-  for (int qt = 0; qt < nqt; ++qt) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      // S[q][key], dP[q][key] of queries 32t..32t+31 of the tile (accumulator rows) x the wave's 32 keys
-      f32x16 sa = (f32x16){0}, ga = (f32x16){0};
-      const int o = 32 * (1 + wv - t);           // band offset of the wave's 64 rows in the tile window
-      const int sl0 = (qt + 2 - (o >> 6)) % 3, sl1 = (qt + 2 - ((o + 32) >> 6)) % 3;
-      const bf16* blk0 = sring + sl0 * TILE * KS + (o & 63) * KS;
-      const bf16* blk1 = sring + sl1 * TILE * KS + ((o + 32) & 63) * KS;
-      {
-        f32x16 x0 = (f32x16){0}, x1 = (f32x16){0};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const bf16x8 qf = rowfrag(sQu, 32 * t, 16 * s, lane);     // A of S, B of the band product
-          sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf, kf[s], sa, 0, 0, 0);
-          x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk0, 0, 16 * s, lane), qf, x0, 0, 0, 0);
-          x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(blk1, 0, 16 * s, lane), qf, x1, 0, 0, 0);
-        }
-        add_band_c(x0, scr + sl0 * TILE + (o & 63), hh);
-        add_band_c(x1, scr + sl1 * TILE + ((o + 32) & 63), hh);
-        // X[r'][i] (lanes = queries) -> stage[i][r']; bd[i][j] = X[j - i + 31][i]
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          *reinterpret_cast<float4*>(colw + 8 * g) = make_float4(x0[4 * g], x0[4 * g + 1], x0[4 * g + 2], x0[4 * g + 3]);
-          *reinterpret_cast<float4*>(colw + 32 + 8 * g) =
-              make_float4(x1[4 * g], x1[4 * g + 1], x1[4 * g + 2], x1[4 * g + 3]);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sG, 32 * t, 16 * s, lane), vf[s], ga, 0, 0, 0);
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sa[r] += skw[((r & 3) + 8 * (r >> 2)) * (SD - 1)];
-      __builtin_amdgcn_wave_barrier();
-      const float* tL = sLD[0] + 32 * t + 4 * hh;
-      const float* tD = sLD[1] + 32 * t + 4 * hh;
-      f32x16 pd;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 Lg = *reinterpret_cast<const float4*>(tL + 8 * g);
-        const float4 Dq = *reinterpret_cast<const float4*>(tD + 8 * g);
-        const float Lr[4] = {Lg.x, Lg.y, Lg.z, Lg.w}, Dr[4] = {Dq.x, Dq.y, Dq.z, Dq.w};
-        bool kp[4] = {true, true, true, true};
-        if (drop) {
-#pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            // dropout of (query of register r / r+1, key kj): lanes kj, kj^1 share one 32-bit hash per query
-            // (index (didx >> 1) mod 2^32 = (bh T + q) T2 + kj/2); the even lane hashes register r's query,
-            // the odd lane register r+1's, and a DPP swap hands each lane its partner's
-            const uint32_t hm = attn_mix(
-                hbase + dkey + __builtin_amdgcn_readfirstlane((qt * TILE + 32 * t + 8 * g + e) * (int)T2));
-            const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
-            const uint32_t h0 = odd ? ho : hm, h1 = odd ? hm : ho;
-            kp[e] = ((h0 >> sh) & 0xFFFFu) >= dthr;
-            kp[e + 1] = ((h1 >> sh) & 0xFFFFu) >= dthr;
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * g + e;
-          // P of keys >= len is not zeroed here: it only reaches this lane's own dK / dV column (zeroed at the
-          // store) and dS entries the dpos pass masks out (lse = +inf for q >= T: P = 0)
-          const float pa = fast_exp2(__builtin_fmaf(sa[r], c, -Lr[e]));
-          const float pk = kp[e] ? pa : 0.f;
-          pd[r] = pk;                                                     // keep scale applied to dV once
-          sa[r] = pa * __builtin_fmaf(kp[e] ? ga[r] : 0.f, drop ? dkeep : 1.f, -Dr[e]);
-        }
       }
       bf16x8 pf[2], sf[2];
 #pragma unroll
@@ -1187,8 +968,9 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
         pf[s2] = acc2frag(pd, s2);
         sf[s2] = acc2frag(sa, s2);
       }
-      // dS -> dsbuf[i][j] (query-major, unscaled: the dpos pass applies the scale) through the wave's stage as
-      // bf16 [query][40] from the MFMA fragments (no second conversion), out as 16-B row chunks
+      // dS -> dsbuf[i][j] (query-major, unscaled): the 32 x 32 block goes through the wave's stage (free after
+      // the skew reads) as bf16 [query][40] and out as 16-B row chunks, 2 stores per lane instead of 16
+      // 2-byte ones.  Keys >= T (zero dS) land in the row's padding [T, ldS); chunks past ldS are skipped.
       {
         bf16* sd = reinterpret_cast<bf16*>(st);
 #pragma unroll
@@ -1212,27 +994,24 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dkdv2_kernel(AttnM p, Rel
       }
     }
     if (qt + 1 < nqt) {
-      qload(qt + 1, qt + 3);    // issued before the barrier: the latency overlaps the wait for the other waves
-      __syncthreads();          // every wave is done with query tile qt and with band chunk qt
-      qstore(qt + 1, qt % 3);
-      __syncthreads();
+      sstore(cur ^ 1);
+      ring_chunk_store(sring + ((qt + 3) & (RING - 1)) * TILE * KS, rr, tid);
     }
+    __syncthreads();
   }
-  __syncthreads();
+  float* stage = sst + wv * 32 * SS2;    // 32 x 68 >= 32 x 65 floats
   const int nvalid = min(32, p.T - k0w);
   if (nvalid > 0) {
-    // keys >= len: zero gradients (their P was not masked in the loop and may be large or inf: a select, not a
-    // multiply); the accumulator column is the lane's key
+    bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int r = 0; r < 16; ++r) {      // keys >= len: zero gradients (a select: their unmasked P may overflow)
       dk0[r] = kvalid ? dk0[r] : 0.f;
       dk1[r] = kvalid ? dk1[r] : 0.f;
       dv0[r] = kvalid ? dv0[r] : 0.f;
       dv1[r] = kvalid ? dv1[r] : 0.f;
     }
-    bf16* base = dqkv + (long)b * p.T * p.D3 + h * p.dk;
-    store_transposed(st, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
-    store_transposed(st, dv0, dv1, drop ? dkeep : 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
+    store_transposed(stage, dk0, dk1, p.scale, base + p.HD, p.D3, k0w, nvalid, p.dk, lane);
+    store_transposed(stage, dv0, dv1, 1.f, base + 2 * p.HD, p.D3, k0w, nvalid, p.dk, lane);
   }
 }
 
@@ -1423,12 +1202,8 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
   const int ldS = rel_ldS(p.T);
   const dim3 grid(cdiv(p.T, 128), p.H, p.B);
   if (rel_vec(p, rp)) {
-    if (g_rel_mode & 32)
-      hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                         (bf16*)dqkv, dsbuf, ldS);
-    else
-      hipLaunchKernelGGL(attn_rel_bwd_dkdv2_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                         (bf16*)dqkv, dsbuf, ldS);
+    hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                       (bf16*)dqkv, dsbuf, ldS);
     if (g_rel_mode & 32)
       hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                          (bf16*)dqkv, part);
@@ -1436,12 +1211,8 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
       hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                          (bf16*)dqkv, part);
   } else {
-    if (g_rel_mode & 32)
-      hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                         (bf16*)dqkv, dsbuf, ldS);
-    else
-      hipLaunchKernelGGL(attn_rel_bwd_dkdv2_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                         (bf16*)dqkv, dsbuf, ldS);
+    hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                       (bf16*)dqkv, dsbuf, ldS);
     if (g_rel_mode & 32)
       hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                          (bf16*)dqkv, part);
