@@ -248,7 +248,8 @@ class WgradGroup:
             PROBE("wgroup", (n, hit[2]), desc, launch)
         else:
             launch()
-        self.tasks = []
+        flushed, self.tasks = self.tasks, []
+        return flushed
 
 
 class ReduceGroup(WgradGroup):
