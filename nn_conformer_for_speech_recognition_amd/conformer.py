@@ -146,9 +146,6 @@ class _Side:
 # and the small column reductions (LayerNorm dgamma|dbeta, depthwise conv dw|db) to one more
 _WGRAD_GROUPS = {}
 _RED_GROUPS = {}
-_WGSIDE_LAYERS = 4       # CFM_ENABLE=wgside: layers per side-stream grouped flush
-_WGSIDE_KEEP = []        # operands of side-stream flushes, referenced until layer 0 joins the side stream
-_WGSIDE_STREAMS = {}
 
 
 def _has_grad_hooks(p):
@@ -430,26 +427,12 @@ class _ConformerLayerFn(torch.autograd.Function):
         side.join()
         if cfg.on_routed is not None and side.dest and side.routed == len(side.dest):
             cfg.on_routed(cfg.layer_index)       # (data-parallel reducer: this layer's buckets are final at flush)
-        side_chunk = _WGSIDE_LAYERS if ("wgside" in ops.ENABLED and cfg.on_flushed is None) else 0
-        if side_chunk and cfg.layer_index % side_chunk == 0 and cfg.layer_index != 0:
-            # (opt-in A/B, CFM_ENABLE=wgside) the grouped weight gradients of the last `side_chunk` layers on the
-            # side stream, concurrent with the remaining data-gradient chain; their operands stay referenced
-            # until layer 0 joins the side stream (the allocator may not recycle them under a running kernel)
-            grp = _WGRAD_GROUPS.get(str(gout.device))
-            if grp is not None and len(grp):
-                ws = _WGSIDE_STREAMS.setdefault(str(gout.device), torch.cuda.Stream(gout.device))
-                ws.wait_stream(side.main)      # (its own stream: the per-layer _Side joins must not wait for it)
-                with torch.cuda.stream(ws):
-                    _WGSIDE_KEEP.extend(grp.flush())
         if cfg.layer_index == 0 or cfg.flush_here:
             # layer 0 runs backward last: everything deferred is flushed; data-parallel runs also flush at
             # bucket boundaries so the bucket's all-reduce (on_flushed) overlaps the remaining backward
             grp = _WGRAD_GROUPS.get(str(gout.device))
             if grp is not None:
                 grp.flush()
-            if _WGSIDE_KEEP:
-                side.main.wait_stream(_WGSIDE_STREAMS[str(gout.device)])
-                _WGSIDE_KEEP.clear()
             rgrp = _RED_GROUPS.get(str(gout.device))
             if rgrp is not None:
                 rgrp.flush()

@@ -248,8 +248,7 @@ class WgradGroup:
             PROBE("wgroup", (n, hit[2]), desc, launch)
         else:
             launch()
-        flushed, self.tasks = self.tasks, []
-        return flushed
+        self.tasks = []
 
 
 class ReduceGroup(WgradGroup):
