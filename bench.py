@@ -809,7 +809,7 @@ def main():
         "params_finite": params_ok, "valid": valid,
         # the dominant kernel family: d-wide-output GEMMs (mean FLOP / mean launch; bytes: A + B read, C written
         # in its dtype -- bf16 data gradients, fp32 residual-stream forwards read + written -- averaged likewise)
-        "roofline": roofline_entry(f"gemm_pipe d-wide outputs (N={d}, M={M_ffn} tokens): FFN-down / out-proj / pw2 "
+        "roofline": roofline_entry(f"gemm_ws (warp-specialised) d-wide outputs (N={d}, M={M_ffn} tokens): FFN-down / out-proj / pw2 "
                                    f"forward + every d-wide data gradient + the front-end fold, {dg_n // max(1, args.steps)}"
                                    f" launches per step", dg_flops, dgemm_bytes(dprobe, M_ffn, d), dg_ms, dg_n,
                                    "gemm_dwide_pmc.json"),
