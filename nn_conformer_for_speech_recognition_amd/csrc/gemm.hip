@@ -47,7 +47,6 @@ struct GemmP {
   const float* alpha_b;
   uint32_t dkey0, dthr;        // dropout constants hoisted out of the epilogue (gemm_drop_prep)
   float dkeep;
-  int stagger, stagger_lo, stagger_hi;   // A/B (cfm_gemm_set_mode bits 24-27): workgroups [lo, hi) start late
 };
 
 // salt the dropout seed and hoist the per-launch constants (hash key of the low 2^33 index range,
@@ -753,11 +752,6 @@ template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt /
           bool GROUP = false, bool F8 = false, int BNt = BN, bool M16 = false>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(OCC * NWV / 4)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
-  if (p.stagger) {   // (A/B) the second resident workgroup of each CU starts late, out of phase with the first
-    const int L = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    if (L >= p.stagger_lo && L < p.stagger_hi)
-      for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(32);
-  }
   static_assert(!F8 || (AK && BKM && !GA && !GROUP && BKt % 32 == 0), "fp8: K-major plain operands");
   static_assert(!M16 || (AK && BKM && !GA && !GROUP && !F8 && BKt % 32 == 0), "16x16x32: K-major plain bf16");
   typedef PipeGeo<BMt, BKt, NST, NWV, BNt> G;
@@ -1420,11 +1414,7 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 int num_cus();
 
 template <bool AK, bool BKM, bool M16 = false>
-void launch_pipe_t(const GemmP& p0, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
-  GemmP p = p0;
-  p.stagger = (g_gemm_mode >> 24) & 15;     // (A/B: units of s_sleep 32 ~ 2k cycles)
-  p.stagger_lo = num_cus();
-  p.stagger_hi = 2 * num_cus();
+void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
   // 0 auto, 1 V256, 2 V256S, 5 V192, 7 V192S8
   const int sel = (g_gemm_mode >> 4) & 7;
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k);
