@@ -3,7 +3,7 @@ FFN-up forward (N 2048: bias + SiLU + pre-activation + dropout, two bf16 outputs
 silu'(pre) + dropout), QKV forward (N 1536, bias) and pointwise-conv-1 forward (N 1024, bias), timed under several
 cfm_gemm_set_mode values in one process (interleaved rounds).
 
-    python benchmarks/wide_gemm.py [--modes 3,11,83] [--reps 5]"""
+    python benchmarks/wide_gemm.py [--modes 3,11,83] [--reps 5] [--variants]"""
 import argparse
 import json
 import os
@@ -32,6 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--modes", default="3,11")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", action="store_true")
     a = ap.parse_args()
     modes = [int(m) for m in a.modes.split(",")]
     M, d, F = 32 * 373, 512, 2048
@@ -58,6 +59,14 @@ def main():
         "qkv_fwd": (2 * M * 3 * d * d, lambda: ops.linear(x, w_qkv, b_qkv, out=qkv)),
         "pw1_fwd": (2 * M * 2 * d * d, lambda: ops.linear(x, w_pw1, b_pw1, out=a1)),
     }
+    if a.variants:   # the FFN-up epilogue taken apart: bias only, + SiLU, + pre-activation store, + dropout
+        cases.update({
+            "up_bias": (2 * M * F * d, lambda: ops.linear(x, w_up, b_up, out=y)),
+            "up_silu": (2 * M * F * d, lambda: ops.linear(x, w_up, b_up, act=ops.ACT_SILU, out=y)),
+            "up_silu_pre": (2 * M * F * d, lambda: ops.linear(x, w_up, b_up, act=ops.ACT_SILU, pre=pre, out=y)),
+            "up_silu_drop": (2 * M * F * d, lambda: ops.linear(x, w_up, b_up, act=ops.ACT_SILU, drop_p=0.1, seed=1,
+                                                                out=y)),
+        })
     res = {m: {k: [] for k in cases} for m in modes}
     for _ in range(a.reps):
         for m in modes:

@@ -37,7 +37,7 @@ struct GemmP {
   // output row remap for the conv2 data-grad parity classes: row m = (b, i, j) of the class
   // -> dh1 row (b, 2i+pf, 2j+pt)
   int cmap, cm_F1c, cm_T1c, cm_pf, cm_pt, cm_F1, cm_T1;
-  int dbg;     // timing experiments only (cfm_gemm_set_mode bit 3): skip the epilogue's stores
+  int dbg;     // timing experiments only (cfm_gemm_set_mode bit 3: skip the epilogue's stores; bit 13: the main loop)
   unsigned long long* probe;   // optional timing slot (cfm_gemm_desc.probe)
   float* acs_slab;             // A column-sum partials [split][M] (cfm_gemm_desc.a_colsum) or nullptr
   const bf16* rd_with;         // per-64-column-group row dots with C (cfm_gemm_desc.rowdot_*) or nullptr
@@ -47,6 +47,7 @@ struct GemmP {
   const float* alpha_b;
   uint32_t dkey0, dthr;        // dropout constants hoisted out of the epilogue (gemm_drop_prep)
   float dkeep;
+  int efast;                   // staged-epilogue fast path (epi_fast_kind; 0: the generic epilogue_store8 rows)
 };
 
 // salt the dropout seed and hoist the per-launch constants (hash key of the low 2^33 index range,
@@ -510,7 +511,164 @@ template <bool M16> __device__ __forceinline__ int accc(int r, int lane) {
   return M16 ? 16 * ((r >> 2) & 1) + (lane & 15) : (lane & 31);
 }
 
-template <int FM, int FN, int WM, int WN, int NTt, int BNt = BN, bool M16 = false, int ROWS = 128>
+// Staged-epilogue fast path (the encoder's launches; host-side selection in epi_fast_kind): split-K 1, vectorised
+// C with N % 8 == 0, bf16 pre-activation, f32 residual, the 32-bit dropout hash range, and a feature set fixed
+// at compile time per kind (EK, a kernel template parameter: each kernel carries one epilogue body -- the generic
+// body's registers spilled in the 128-register two-per-CU kernels, one accumulator inside the MFMA loop):
+//   EF_BF16      bf16 C; alpha, bias, SiLU + bf16 pre-activation store, dropout, out_scale (FFN-up, QKV, pw1 fwd)
+//   EF_BF16_ACTG bf16 C; silu'(pre) * dropout (FFN-down data gradient)
+//   EF_BF16_RD   bf16 C; rowdot with rd_with (attention out-projection data gradient)
+//   EF_F32       f32 C; as EF_BF16
+//   EF_F32_RES   f32 C; alpha, bias, dropout, out_scale, f32 residual (the d-wide residual-stream outputs)
+// A thread's 8-column chunk is the same on every row it finishes, so its bias is loaded once, and each row's global
+// input (the bf16 pre-activation / rd_with, or the f32 residual) is issued ahead of the previous rows' stores:
+// vmcnt counts loads and stores in one in-order queue, and the generic rows, which load bias / pre / residual
+// between the previous row's stores, waited for every previous row's write acknowledgements (bias-only FFN-up
+// epilogue without the main loop: 49 MB in 21.9 us = 2.2 TB/s).  Arithmetic and its order are epilogue_store8's
+// (bit-identical outputs).
+enum { EF_GENERIC = 0, EF_BF16 = 1, EF_BF16_ACTG = 2, EF_BF16_RD = 3, EF_F32 = 4, EF_F32_RES = 5 };
+
+__device__ __forceinline__ void epi_bias8(const GemmP& p, int n, float (&b)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b[e] = 0.f;
+  if (p.efast && p.bias && n < p.N) {
+    const float4 a = *reinterpret_cast<const float4*>(p.bias + n);
+    const float4 c = *reinterpret_cast<const float4*>(p.bias + n + 4);
+    b[0] = a.x; b[1] = a.y; b[2] = a.z; b[3] = a.w; b[4] = c.x; b[5] = c.y; b[6] = c.z; b[7] = c.w;
+  }
+}
+
+template <int EK, int IT, int NTt, int CPW, int EPS>
+__device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, int z, int mbase, int n0, int tid,
+                                              const float (&b)[8]) {
+  static_assert(EK > EF_GENERIC && EK <= EF_F32_RES, "fast epilogue kind");
+  constexpr bool CF32 = EK == EF_F32 || EK == EF_F32_RES, ACTG = EK == EF_BF16_ACTG, RD = EK == EF_BF16_RD;
+  constexpr bool RES = EK == EF_F32_RES, BIAS = !ACTG && !RD, SILU = EK == EF_BF16 || EK == EF_F32;
+  constexpr bool DROP = !RD;
+  constexpr int NW = RES ? 8 : (ACTG || RD) ? 4 : 0;   // input dwords per row
+  constexpr int RPI = NTt / CPW;                       // rows per pass
+  const int c8 = (tid % CPW) * 8, n = n0 + c8, r0 = tid / CPW;
+  const bool nok = n < p.N;
+  // row it's input is issued PD rows ahead, before the stores of row it - PD (all rows up front for the f32
+  // residual: the one-per-CU warp-specialised kernel has the registers; two rows ahead in the 128-register kernels)
+  constexpr int PD = NW == 8 && NTt >= 768 ? IT : (IT < 2 ? IT : 2);
+  uint4 in[IT][NW == 8 ? 2 : 1];
+  auto load_in = [&](int it) {
+    const int m = mbase + it * RPI + r0;
+    if (m < p.M && nok) {
+      if constexpr (RES) {
+        const uint4* s = reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(p.res) + (long)z * p.sc +
+                                                        (long)m * p.ldr + n);
+        in[it][0] = s[0];
+        in[it][1] = s[1];
+      } else if constexpr (ACTG) {
+        in[it][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.pre) + (long)z * p.sc +
+                                                    out_row(p, m) * p.ldc + n);
+      } else if constexpr (RD) {
+        in[it][0] = *reinterpret_cast<const uint4*>(p.rd_with + (long)m * p.ldc + n);
+      }
+    }
+  };
+  if constexpr (NW > 0) {
+#pragma unroll
+    for (int it = 0; it < PD; ++it) load_in(it);
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    if constexpr (NW > 0) {
+      if (it + PD < IT) load_in(it + PD);
+    }
+    const int row = it * RPI + r0, m = mbase + row;
+    const float4 lo = *reinterpret_cast<const float4*>(st + row * EPS + c8);
+    const float4 hi = *reinterpret_cast<const float4*>(st + row * EPS + c8 + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const bool ok = m < p.M && nok;
+    if (ok) {
+      const long cidx = (long)z * p.sc + out_row(p, m) * p.ldc + n;
+      if (p.alpha != 1.f) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+      }
+      if constexpr (BIAS) {
+        if (p.bias) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += b[e];
+        }
+      }
+      if constexpr (ACTG) {
+        const bf16x8 pr = __builtin_bit_cast(bf16x8, in[it][0]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= silu_grad_f((float)pr[e]);
+      }
+      if constexpr (SILU) {
+        if (p.act == CFM_ACT_SILU) {
+          if (p.pre) {
+            bf16x8 q;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q[e] = (bf16)v[e];
+            *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.pre) + cidx) = __builtin_bit_cast(uint4, q);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
+        }
+      }
+      if constexpr (DROP) {
+        if (p.drop_p > 0.f) {
+          const uint64_t base = p.doff + (uint64_t)((long)z * p.M * p.N + (long)m * p.N + n);
+          const uint32_t j0 = (uint32_t)(base >> 1);
+          const int odd = (int)(base & 1);
+          uint32_t h[5];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) h[q] = attn_mix(j0 + q + p.dkey0);
+          h[4] = odd ? attn_mix(j0 + 4 + p.dkey0) : 0u;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int q = (odd + e) >> 1;
+            const uint32_t bits = ((odd + e) & 1) ? (h[q] >> 16) : (h[q] & 0xFFFFu);
+            v[e] *= bits >= p.dthr ? p.dkeep : 0.f;
+          }
+        }
+      }
+      if constexpr (!RD) {
+        if (p.out_scale != 1.f) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
+        }
+      }
+      if constexpr (RES) {
+        const float4 ra = __builtin_bit_cast(float4, in[it][0]), rb = __builtin_bit_cast(float4, in[it][1]);
+        v[0] += ra.x; v[1] += ra.y; v[2] += ra.z; v[3] += ra.w; v[4] += rb.x; v[5] += rb.y; v[6] += rb.z; v[7] += rb.w;
+      }
+      if constexpr (CF32) {
+        float* d = reinterpret_cast<float*>(p.C) + cidx;
+        *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        bf16x8 q;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q[e] = (bf16)v[e];
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.C) + cidx) = __builtin_bit_cast(uint4, q);
+      }
+    }
+    if constexpr (RD) {   // 8-lane group = 64 columns (as tile_epilogue_g's generic rows)
+      float t = 0.f;
+      if (ok) {
+        const bf16x8 w = __builtin_bit_cast(bf16x8, in[it][0]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t += (float)(bf16)v[e] * (float)w[e];
+      }
+      t += __shfl_xor(t, 1, 64);
+      t += __shfl_xor(t, 2, 64);
+      t += __shfl_xor(t, 4, 64);
+      if ((tid & 7) == 0 && ok) {
+        const int bb = m / p.rd_T, tt = m - bb * p.rd_T, g = n >> 6;
+        p.rd_out[((long)bb * (p.N >> 6) + g) * p.rd_T + tt] = t;
+      }
+    }
+  }
+}
+
+template <int FM, int FN, int WM, int WN, int NTt, int BNt = BN, bool M16 = false, int ROWS = 128, int EK = EF_GENERIC>
 __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM][FN], float* st, int z, int zs,
                                                 int m0, int n0, int wm, int wn, int lane, int tid) {
   // ROWS: the staging rows `st` holds (ROWS x (BNt + 4) floats)
@@ -520,7 +678,7 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
   constexpr int EPS = BNt + 4;         // staging row stride (floats): = 4 mod 32 for both widths
   constexpr int CPW = BNt / 8;         // 8-column chunks per row
   static_assert(WN * FN * 32 == BNt, "tile width");
-  if (p.split_k > 1 && !p.slab) {
+  if (EK == EF_GENERIC && p.split_k > 1 && !p.slab) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -533,6 +691,8 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
         }
     return;
   }
+  float bias8[8];
+  if constexpr (EK != EF_GENERIC) epi_bias8(p, n0 + (tid % CPW) * 8, bias8);
   // (one pass per band chunk; not unrolled -- the epilogue body is large and nothing in it is indexed by hf)
 #pragma nounroll
   for (int hf = 0; hf < WM / CHB; ++hf) {
@@ -549,6 +709,12 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
           }
     }
     __syncthreads();
+    static_assert((RC * CPW) % NTt == 0 && NTt % CPW == 0, "whole rows per pass");
+    if constexpr (EK != EF_GENERIC) {
+      epi_rows_fast<EK, RC * CPW / NTt, NTt, CPW, EPS>(p, st, z, m0 + RC * hf, n0, tid, bias8);
+      if (hf + 1 < WM / CHB) __syncthreads();
+      continue;
+    }
 #pragma unroll 2
     for (int it = 0; it < RC * CPW / NTt; ++it) {
       const int row = it * (NTt / CPW) + tid / CPW, c8 = (tid % CPW) * 8;
@@ -749,7 +915,7 @@ __device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& 
 // LDS images, fragments per k and accumulator registers) -- K-major plain operands only.  On random data the
 // chip holds a higher clock under the 16x16 shape than under 32x32x16 (MI355X_MICROARCH.md, DVFS item 7).
 template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2, bool GA = false,
-          bool GROUP = false, bool F8 = false, int BNt = BN, bool M16 = false>
+          bool GROUP = false, bool F8 = false, int BNt = BN, bool M16 = false, int EK = EF_GENERIC>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(OCC * NWV / 4)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   static_assert(!F8 || (AK && BKM && !GA && !GROUP && BKt % 32 == 0), "fp8: K-major plain operands");
@@ -779,7 +945,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, z), rb = pipe_rsrc(ob, z);
   const int kbeg = __builtin_amdgcn_readfirstlane(ks * p.k_per_split);
   const int kend = __builtin_amdgcn_readfirstlane(min(p.K, kbeg + p.k_per_split));
-  const int nk = kend > kbeg ? (kend - kbeg + BKt - 1) / BKt : 0;
+  const int nk = kend > kbeg && !(p.dbg & 4) ? (kend - kbeg + BKt - 1) / BKt : 0;   // (dbg 4: epilogue only)
 
   // per-lane source offsets of stage 0; later stages add k0 * (row stride) (MN-major) or k0 * 2
   unsigned offa[G::AI], offb[G::BI];
@@ -987,7 +1153,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     if (p.alpha_a) p.alpha *= p.alpha_a[0];
     if (p.alpha_b) p.alpha *= p.alpha_b[0];
   }
-  tile_epilogue_g<FM, FN, WM, WN, G::NTt, BNt, M16>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane,
+  tile_epilogue_g<FM, FN, WM, WN, G::NTt, BNt, M16, 128, EK>(p, acc, reinterpret_cast<float*>(lds), z, zz, m0, n0, wm, wn, lane,
                                                       tid);
   probe_end(p.probe);
 }
@@ -1002,7 +1168,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
 // stages issued ahead).  Gemm lab (benchmarks/gemm_lab, M 11,936 N 512 K 2048, naive stores): 33.9 -> 27.0 us.
 // Epilogue: the whole f32 tile staged in the ring's LDS, then every wave (loaders included) finishes 8-column
 // chunks through epilogue_store8 (+ rowdot), as tile_epilogue_g does.
-template <int BMt, int WM, int WN, int NL, int NST>
+template <int BMt, int WM, int WN, int NL, int NST, int EK = EF_GENERIC>
 __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, PipeOp oa, PipeOp ob) {
   constexpr int BKt = 64, BNt = BN, NC = WM * WN, NTt = (NC + NL) * 64;
   constexpr int ABYTES = BMt * BKt * 2, BBYTES = BNt * BKt * 2, STAGE = ABYTES + BBYTES;
@@ -1021,7 +1187,7 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
   xcd_tile3(tm, tn, zz);
   const int m0 = tm * BMt, n0 = tn * BNt;
   const int z = zz;                       // split_k == 1: the batch index
-  const int nk = p.K / BKt;
+  const int nk = (p.dbg & 4) ? 0 : p.K / BKt;   // (dbg 4: epilogue only)
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -1111,6 +1277,8 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
     if (t == -1234.5f) reinterpret_cast<float*>(p.C)[tid] = t;
     return;
   }
+  float bias8[8];
+  if constexpr (EK != EF_GENERIC) epi_bias8(p, n0 + (tid % CPW) * 8, bias8);
   __syncthreads();   // every DMA landed (the loaders' last wait was vmcnt(0)), every fragment read consumed
   float* st = reinterpret_cast<float*>(lds);
   if (wid < NC) {
@@ -1125,6 +1293,11 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
   }
   __syncthreads();
   static_assert((BMt * CPW) % NTt == 0 && NTt % CPW == 0, "whole rows per pass");
+  if constexpr (EK != EF_GENERIC) {
+    epi_rows_fast<EK, BMt * CPW / NTt, NTt, CPW, EPS>(p, st, z, m0, n0, tid, bias8);
+    probe_end(p.probe);
+    return;
+  }
 #pragma unroll 2
   for (int it = 0; it < BMt * CPW / NTt; ++it) {
     const int row = it * (NTt / CPW) + tid / CPW, c8 = (tid % CPW) * 8;
@@ -1413,6 +1586,23 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
 //  main loops for K-major operands, a 3-deep 192-row ring)
 int num_cus();
 
+// f(std::integral_constant<int, EK>) for the launch's epilogue kind (K-major x K-major launches only: the other
+// operand layouts keep the generic epilogue, so their kernels are instantiated once)
+template <bool KK, class F>
+void ek_dispatch(int ek, F&& f) {
+  if constexpr (KK) {
+    switch (ek) {
+      case EF_BF16: f(std::integral_constant<int, EF_BF16>{}); return;
+      case EF_BF16_ACTG: f(std::integral_constant<int, EF_BF16_ACTG>{}); return;
+      case EF_BF16_RD: f(std::integral_constant<int, EF_BF16_RD>{}); return;
+      case EF_F32: f(std::integral_constant<int, EF_F32>{}); return;
+      case EF_F32_RES: f(std::integral_constant<int, EF_F32_RES>{}); return;
+      default: break;
+    }
+  }
+  f(std::integral_constant<int, EF_GENERIC>{});
+}
+
 template <bool AK, bool BKM, bool M16 = false>
 void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch, hipStream_t s) {
   // 0 auto, 1 V256, 2 V256S, 5 V192, 7 V192S8
@@ -1428,7 +1618,9 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
         // warp-specialised loading (cfm_gemm_set_mode bit 19 keeps the shared-DMA kernel below for A/B): d-wide
         // layer family 266.6 -> 240.2 us same box (gpurun_out r04b dgemm; 4 compute waves of 96 x 64: 244.4 us)
         if (!(g_gemm_mode & 524288) && p.split_k == 1) {
-          hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 4, 4, 4>), g192, dim3(768), 0, s, p, oa, ob);
+          ek_dispatch<true>(p.efast, [&](auto ek) {
+            hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 4, 4, 4, decltype(ek)::value>), g192, dim3(768), 0, s, p, oa, ob);
+          });
           return;
         }
       }
@@ -1446,8 +1638,11 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
       v = 7;
     if (v == 7) {   // 192 x 128 tiles, 8 waves of 96 x 32, BK 32 (uneven A DMA split): two per CU
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
-      hipLaunchKernelGGL((gemm_pipe_kernel<192, 32, 3, 2, AK, BKM, 8, 4, false, false, false, BN, M16>), g192, dim3(512),
-                         0, s, p, oa, ob, GatherA{});
+      ek_dispatch<AK && BKM>(p.efast, [&](auto ek) {
+        hipLaunchKernelGGL((gemm_pipe_kernel<192, 32, 3, 2, AK, BKM, 8, 4, false, false, false, BN, M16,
+                                             decltype(ek)::value>),
+                           g192, dim3(512), 0, s, p, oa, ob, GatherA{});
+      });
       return;
     }
   }
@@ -1461,8 +1656,10 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
     hipLaunchKernelGGL((gemm_pipe_kernel<256, 64, 3, 1, AK, BKM, 8, 2, false, false, false, BN, M16>), g256, dim3(512), 0,
                        s, p, oa, ob, GatherA{});
   else
-    hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, AK, BKM, 8, 2, false, false, false, BN, M16>), g256, dim3(512), 0,
-                       s, p, oa, ob, GatherA{});
+    ek_dispatch<AK && BKM>(p.efast, [&](auto ek) {
+      hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, AK, BKM, 8, 2, false, false, false, BN, M16, decltype(ek)::value>),
+                         g256, dim3(512), 0, s, p, oa, ob, GatherA{});
+    });
 }
 
 int num_cus() {
@@ -1475,9 +1672,27 @@ int num_cus() {
   return n;
 }
 
+// the staged-epilogue fast path a launch can take (EF_*, epi_rows_fast; EF_GENERIC: the epilogue_store8 rows)
+int epi_fast_kind(const GemmP& p, int batch) {
+  if (p.split_k != 1 || !p.vec_c || p.N % 8 || (p.dbg & 2) || (g_gemm_mode & 16384)) return EF_GENERIC;
+  if (p.drop_p > 0.f && (p.doff + (uint64_t)batch * p.M * p.N) / 2 + 8 > 0xFFFFFFFBull) return EF_GENERIC;
+  const bool f32 = p.dtc == CFM_F32, silu = p.act == CFM_ACT_SILU;
+  if (!f32 && p.dtc != CFM_BF16) return EF_GENERIC;
+  if (p.res)
+    return f32 && p.dtr == CFM_F32 && !silu && !p.act_grad && !p.rd_out ? EF_F32_RES : EF_GENERIC;
+  if (p.act_grad)
+    return !f32 && p.dtpre == CFM_BF16 && !silu && !p.rd_out && !p.bias ? EF_BF16_ACTG : EF_GENERIC;
+  if (p.rd_out)
+    return !f32 && !silu && !p.bias && p.drop_p <= 0.f && p.out_scale == 1.f ? EF_BF16_RD : EF_GENERIC;
+  if (silu && p.pre && p.dtpre != CFM_BF16) return EF_GENERIC;
+  return f32 ? EF_F32 : EF_BF16;
+}
+
 int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   p.vec_c = vec_epilogue_ok(p);
-  p.dbg = ((g_gemm_mode & 8) ? 1 : 0) | ((g_gemm_mode & 1024) ? 2 : 0);   // bit 10: generic dropout path (A/B)
+  p.dbg = ((g_gemm_mode & 8) ? 1 : 0) | ((g_gemm_mode & 1024) ? 2 : 0)    // bit 10: generic dropout path (A/B)
+          | ((g_gemm_mode & 8192) ? 4 : 0);                                     // bit 13: skip the main loop (timing)
+  p.efast = d.a_kmajor && d.b_kmajor ? epi_fast_kind(p, d.batch) : EF_GENERIC;                                  // bit 14: generic epilogue rows (A/B)
   if (cdiv(p.M, 128) > 65535 || (long)d.batch * p.split_k > 65535) return cfm::fail(CFM_ERR_SHAPE, "gemm: grid too large");
   const long ea = pipe_extent(d.a_kmajor, d.M, d.K, d.lda), eb = pipe_extent(d.b_kmajor, d.N, d.K, d.ldb);
   const PipeOp oa{(const bf16*)d.A, d.lda, d.stride_a, d.M, (unsigned)(ea * 2)};

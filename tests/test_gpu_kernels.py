@@ -437,6 +437,69 @@ def test_gemm_warp_specialised_matches_shared_dma(gemm_mode, M, K, epi):
         assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("M", [11936, 1000, 385])
+@pytest.mark.parametrize("epi,N", [("silu_pre_drop", 2048), ("actg_drop", 2048), ("bias", 1536), ("bias", 1024),
+                                   ("f32_bias", 2048), ("res_drop", 512), ("res_drop", 2048), ("rowdot", 512),
+                                   ("plain", 512), ("silu_pre_drop", 512)])
+def test_gemm_fast_epilogue_matches_generic(gemm_mode, M, epi, N):
+    """The compile-time epilogue kinds (epi_rows_fast: inputs issued ahead of the stores, bias loaded once) against
+    the generic per-row epilogue_store8 path (cfm_gemm_set_mode bit 14) on the same kernels: the same arithmetic in
+    the same order -> bit-identical outputs, for every kind the encoder launches, on the 256-row two-per-CU tiles
+    (2048 wide), the 192-row tiles (1024 / 1536) and the warp-specialised d-wide kernel (512), ragged M."""
+    K = 512
+    g = torch.Generator().manual_seed(M + N + len(epi))
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV)
+    pre_in = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    with_ = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    T = M // 8 if M % 8 == 0 else M
+    outs = []
+    for mode in (3, 3 | 16384):
+        gemm_mode(mode)
+        if epi == "silu_pre_drop":
+            y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.linear(x, w, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=5, out=y)
+            outs.append((y.clone(), pre.clone()))
+        elif epi == "actg_drop":
+            y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(x, w, y, M, N, K, pre=pre_in, act_grad=True, drop_p=0.1, seed=6)
+            outs.append((y.clone(),))
+        elif epi == "bias":
+            y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.linear(x, w, b, out=y)
+            outs.append((y.clone(),))
+        elif epi == "f32_bias":
+            y = torch.empty(M, N, device=DEV, dtype=torch.float32)
+            ops.linear(x, w, b, out=y, out_scale=0.5)
+            outs.append((y.clone(),))
+        elif epi == "res_drop":
+            y = torch.empty(M, N, device=DEV, dtype=torch.float32)
+            ops.linear(x, w, b, out=y, drop_p=0.1, seed=7, out_scale=0.5, residual=res)
+            outs.append((y.clone(),))
+        elif epi == "rowdot":
+            y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            D = torch.empty(M * N // 64, device=DEV, dtype=torch.float32)
+            ops.gemm(x, w, y, M, N, K, rowdot=(with_, D, T))
+            outs.append((y.clone(), D.clone()))
+        else:
+            y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(x, w, y, M, N, K)
+            outs.append((y.clone(),))
+    torch.cuda.synchronize()
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    if epi == "silu_pre_drop":   # and the values themselves (fp32 reference of the same epilogue)
+        pre_ref = (x.float() @ w.float().T + b)
+        assert _rel(outs[0][1].float(), pre_ref) < 1e-2
+        kept = outs[0][0] != 0
+        assert 0.87 < kept.float().mean().item() < 0.93
+        act = torch.nn.functional.silu(pre_ref) / 0.9
+        assert _rel(outs[0][0].float()[kept], act[kept]) < 1e-2
+
+
 @pytest.mark.parametrize("training", [True, False])
 @pytest.mark.parametrize("sync", [False, True])
 @pytest.mark.parametrize("B,T,C,K,dt", [(2, 37, 64, 31, torch.bfloat16), (3, 100, 96, 3, torch.float32),
