@@ -538,6 +538,22 @@ __device__ __forceinline__ void epi_bias8(const GemmP& p, int n, float (&b)[8]) 
   }
 }
 
+// dropout of 8 consecutive elements starting at an index of parity ODD whose pair index is j0 (epilogue_store8's
+// hash path: element i draws the (i & 1) half of attn_mix(i / 2 + key))
+template <bool ODD>
+__device__ __forceinline__ void drop8_fast(float (&v)[8], uint32_t j0, const GemmP& p) {
+  constexpr int NH = ODD ? 5 : 4;
+  uint32_t h[NH];
+#pragma unroll
+  for (int q = 0; q < NH; ++q) h[q] = attn_mix(j0 + q + p.dkey0);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int q = (ODD + e) >> 1;
+    const uint32_t bits = ((ODD + e) & 1) ? (h[q] >> 16) : (h[q] & 0xFFFFu);
+    v[e] *= bits >= p.dthr ? p.dkeep : 0.f;
+  }
+}
+
 template <int EK, int IT, int NTt, int CPW, int EPS>
 __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, int z, int mbase, int n0, int tid,
                                               const float (&b)[8]) {
@@ -563,7 +579,7 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
         in[it][1] = s[1];
       } else if constexpr (ACTG) {
         in[it][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.pre) + (long)z * p.sc +
-                                                    out_row(p, m) * p.ldc + n);
+                                                    (long)m * p.ldc + n);
       } else if constexpr (RD) {
         in[it][0] = *reinterpret_cast<const uint4*>(p.rd_with + (long)m * p.ldc + n);
       }
@@ -584,7 +600,7 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     const bool ok = m < p.M && nok;
     if (ok) {
-      const long cidx = (long)z * p.sc + out_row(p, m) * p.ldc + n;
+      const long cidx = (long)z * p.sc + (long)m * p.ldc + n;   // (no row remap: epi_fast_kind)
       if (p.alpha != 1.f) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
@@ -614,19 +630,11 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
       }
       if constexpr (DROP) {
         if (p.drop_p > 0.f) {
-          const uint64_t base = p.doff + (uint64_t)((long)z * p.M * p.N + (long)m * p.N + n);
-          const uint32_t j0 = (uint32_t)(base >> 1);
-          const int odd = (int)(base & 1);
-          uint32_t h[5];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) h[q] = attn_mix(j0 + q + p.dkey0);
-          h[4] = odd ? attn_mix(j0 + 4 + p.dkey0) : 0u;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int q = (odd + e) >> 1;
-            const uint32_t bits = ((odd + e) & 1) ? (h[q] >> 16) : (h[q] & 0xFFFFu);
-            v[e] *= bits >= p.dthr ? p.dkeep : 0.f;
-          }
+          // n and N are multiples of 8: the element index's parity is the offset's (uniform), so the hash-half
+          // selection is static in each branch (a per-lane parity cost ~48 selects per row)
+          const uint32_t j0 = (uint32_t)((p.doff + (uint64_t)(((long)z * p.M + m) * p.N + n)) >> 1);
+          if (p.doff & 1) drop8_fast<true>(v, j0, p);
+          else drop8_fast<false>(v, j0, p);
         }
       }
       if constexpr (!RD) {
@@ -1674,7 +1682,7 @@ int num_cus() {
 
 // the staged-epilogue fast path a launch can take (EF_*, epi_rows_fast; EF_GENERIC: the epilogue_store8 rows)
 int epi_fast_kind(const GemmP& p, int batch) {
-  if (p.split_k != 1 || !p.vec_c || p.N % 8 || (p.dbg & 2) || (g_gemm_mode & 16384)) return EF_GENERIC;
+  if (p.split_k != 1 || !p.vec_c || p.N % 8 || p.cmap || (p.dbg & 2) || (g_gemm_mode & 16384)) return EF_GENERIC;
   if (p.drop_p > 0.f && (p.doff + (uint64_t)batch * p.M * p.N) / 2 + 8 > 0xFFFFFFFBull) return EF_GENERIC;
   const bool f32 = p.dtc == CFM_F32, silu = p.act == CFM_ACT_SILU;
   if (!f32 && p.dtc != CFM_BF16) return EF_GENERIC;
