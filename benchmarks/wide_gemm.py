@@ -16,16 +16,23 @@ from nn_conformer_for_speech_recognition_amd import _lib, ops  # noqa: E402
 
 
 def timeit(fn, n=20, warm=3):
+    """Device time per call: n calls captured in one HIP graph and replayed (the Python / ctypes launch path costs
+    ~12 us per call, more than the short-K GEMMs themselves: event timing of eager launches floors there)."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(n):
-        fn()
+    g.replay()
     e.record()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) / n * 1e3
+    return s.elapsed_time(e) / n * 1e3        # us
 
 
 def main():

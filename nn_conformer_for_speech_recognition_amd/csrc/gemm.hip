@@ -554,45 +554,62 @@ __device__ __forceinline__ void drop8_fast(float (&v)[8], uint32_t j0, const Gem
   }
 }
 
-template <int EK, int IT, int NTt, int CPW, int EPS>
+// per-row global inputs of a fast epilogue kind: dwords per row, and the holder (IT rows of one thread)
+template <int EK> constexpr int epi_nw() {
+  return EK == EF_F32_RES ? 8 : (EK == EF_BF16_ACTG || EK == EF_BF16_RD) ? 4 : 0;
+}
+template <int EK, int IT> struct EpiIn { uint4 v[IT][epi_nw<EK>() == 8 ? 2 : 1]; };
+
+template <int EK, int IT, int NTt, int CPW>
+__device__ __forceinline__ void epi_load_row(const GemmP& p, int z, int mbase, int n0, int tid, int it,
+                                             EpiIn<EK, IT>& in) {
+  const int n = n0 + (tid % CPW) * 8, m = mbase + it * (NTt / CPW) + tid / CPW;
+  if (m < p.M && n < p.N) {
+    if constexpr (EK == EF_F32_RES) {
+      const uint4* s = reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(p.res) + (long)z * p.sc +
+                                                      (long)m * p.ldr + n);
+      in.v[it][0] = s[0];
+      in.v[it][1] = s[1];
+    } else if constexpr (EK == EF_BF16_ACTG) {
+      in.v[it][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.pre) + (long)z * p.sc +
+                                                    (long)m * p.ldc + n);
+    } else if constexpr (EK == EF_BF16_RD) {
+      in.v[it][0] = *reinterpret_cast<const uint4*>(p.rd_with + (long)m * p.ldc + n);
+    }
+  }
+}
+
+// every row's input, issued up front (the warp-specialised kernel: before its main loop, which hides the latency)
+template <int EK, int IT, int NTt, int CPW>
+__device__ __forceinline__ void epi_load_all(const GemmP& p, int z, int mbase, int n0, int tid, EpiIn<EK, IT>& in) {
+  if constexpr (epi_nw<EK>() > 0) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) epi_load_row<EK, IT, NTt, CPW>(p, z, mbase, n0, tid, it, in);
+  }
+}
+
+// PRE: `in` already holds every row's input (epi_load_all); otherwise row it's input is issued PD rows ahead,
+// before the stores of row it - PD (two rows ahead: the 128-register two-per-CU kernels)
+template <int EK, int IT, int NTt, int CPW, int EPS, bool PRE = false>
 __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, int z, int mbase, int n0, int tid,
-                                              const float (&b)[8]) {
+                                              const float (&b)[8], EpiIn<EK, IT>& in) {
   static_assert(EK > EF_GENERIC && EK <= EF_F32_RES, "fast epilogue kind");
   constexpr bool CF32 = EK == EF_F32 || EK == EF_F32_RES, ACTG = EK == EF_BF16_ACTG, RD = EK == EF_BF16_RD;
   constexpr bool RES = EK == EF_F32_RES, BIAS = !ACTG && !RD, SILU = EK == EF_BF16 || EK == EF_F32;
   constexpr bool DROP = !RD;
-  constexpr int NW = RES ? 8 : (ACTG || RD) ? 4 : 0;   // input dwords per row
+  constexpr int NW = epi_nw<EK>();
   constexpr int RPI = NTt / CPW;                       // rows per pass
   const int c8 = (tid % CPW) * 8, n = n0 + c8, r0 = tid / CPW;
   const bool nok = n < p.N;
-  // row it's input is issued PD rows ahead, before the stores of row it - PD (all rows up front for the f32
-  // residual: the one-per-CU warp-specialised kernel has the registers; two rows ahead in the 128-register kernels)
-  constexpr int PD = NW == 8 && NTt >= 768 ? IT : (IT < 2 ? IT : 2);
-  uint4 in[IT][NW == 8 ? 2 : 1];
-  auto load_in = [&](int it) {
-    const int m = mbase + it * RPI + r0;
-    if (m < p.M && nok) {
-      if constexpr (RES) {
-        const uint4* s = reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(p.res) + (long)z * p.sc +
-                                                        (long)m * p.ldr + n);
-        in[it][0] = s[0];
-        in[it][1] = s[1];
-      } else if constexpr (ACTG) {
-        in[it][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.pre) + (long)z * p.sc +
-                                                    (long)m * p.ldc + n);
-      } else if constexpr (RD) {
-        in[it][0] = *reinterpret_cast<const uint4*>(p.rd_with + (long)m * p.ldc + n);
-      }
-    }
-  };
-  if constexpr (NW > 0) {
+  constexpr int PD = PRE ? IT : (IT < 2 ? IT : 2);
+  if constexpr (NW > 0 && !PRE) {
 #pragma unroll
-    for (int it = 0; it < PD; ++it) load_in(it);
+    for (int it = 0; it < PD; ++it) epi_load_row<EK, IT, NTt, CPW>(p, z, mbase, n0, tid, it, in);
   }
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    if constexpr (NW > 0) {
-      if (it + PD < IT) load_in(it + PD);
+    if constexpr (NW > 0 && !PRE) {
+      if (it + PD < IT) epi_load_row<EK, IT, NTt, CPW>(p, z, mbase, n0, tid, it + PD, in);
     }
     const int row = it * RPI + r0, m = mbase + row;
     const float4 lo = *reinterpret_cast<const float4*>(st + row * EPS + c8);
@@ -612,7 +629,7 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
         }
       }
       if constexpr (ACTG) {
-        const bf16x8 pr = __builtin_bit_cast(bf16x8, in[it][0]);
+        const bf16x8 pr = __builtin_bit_cast(bf16x8, in.v[it][0]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] *= silu_grad_f((float)pr[e]);
       }
@@ -644,7 +661,7 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
         }
       }
       if constexpr (RES) {
-        const float4 ra = __builtin_bit_cast(float4, in[it][0]), rb = __builtin_bit_cast(float4, in[it][1]);
+        const float4 ra = __builtin_bit_cast(float4, in.v[it][0]), rb = __builtin_bit_cast(float4, in.v[it][1]);
         v[0] += ra.x; v[1] += ra.y; v[2] += ra.z; v[3] += ra.w; v[4] += rb.x; v[5] += rb.y; v[6] += rb.z; v[7] += rb.w;
       }
       if constexpr (CF32) {
@@ -661,7 +678,7 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
     if constexpr (RD) {   // 8-lane group = 64 columns (as tile_epilogue_g's generic rows)
       float t = 0.f;
       if (ok) {
-        const bf16x8 w = __builtin_bit_cast(bf16x8, in[it][0]);
+        const bf16x8 w = __builtin_bit_cast(bf16x8, in.v[it][0]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) t += (float)(bf16)v[e] * (float)w[e];
       }
@@ -719,7 +736,8 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
     __syncthreads();
     static_assert((RC * CPW) % NTt == 0 && NTt % CPW == 0, "whole rows per pass");
     if constexpr (EK != EF_GENERIC) {
-      epi_rows_fast<EK, RC * CPW / NTt, NTt, CPW, EPS>(p, st, z, m0 + RC * hf, n0, tid, bias8);
+      EpiIn<EK, RC * CPW / NTt> ein;
+      epi_rows_fast<EK, RC * CPW / NTt, NTt, CPW, EPS>(p, st, z, m0 + RC * hf, n0, tid, bias8, ein);
       if (hf + 1 < WM / CHB) __syncthreads();
       continue;
     }
@@ -1196,6 +1214,11 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
   const int m0 = tm * BMt, n0 = tn * BNt;
   const int z = zz;                       // split_k == 1: the batch index
   const int nk = (p.dbg & 4) ? 0 : p.K / BKt;   // (dbg 4: epilogue only)
+  // the epilogue rows' global inputs (f32 residual / bf16 rd_with / pre-activation), issued before the main loop
+  // so their latency hides under it (the loaders' counted stage waits see them as older, completed first)
+  constexpr int EIT = BMt * CPW / NTt;
+  EpiIn<EK == EF_GENERIC ? EF_BF16 : EK, EIT> ein;
+  if constexpr (EK != EF_GENERIC) epi_load_all<EK, EIT, NTt, CPW>(p, z, m0, n0, tid, ein);
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -1302,7 +1325,7 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
   __syncthreads();
   static_assert((BMt * CPW) % NTt == 0 && NTt % CPW == 0, "whole rows per pass");
   if constexpr (EK != EF_GENERIC) {
-    epi_rows_fast<EK, BMt * CPW / NTt, NTt, CPW, EPS>(p, st, z, m0, n0, tid, bias8);
+    epi_rows_fast<EK, EIT, NTt, CPW, EPS, true>(p, st, z, m0, n0, tid, bias8, ein);
     probe_end(p.probe);
     return;
   }
