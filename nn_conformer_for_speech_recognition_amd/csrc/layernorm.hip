@@ -145,25 +145,11 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TDY* __restrict__ dy, co
   ldv<V>(gamma + lane * V, gm);
 #pragma unroll
   for (int i = 0; i < V; ++i) pg[i] = pb[i] = 0.f;
-  // the next row's loads are issued before this row's stores: vmcnt counts loads and stores in one in-order queue,
-  // so a load issued after the stores could not be waited for without waiting for their write acknowledgements
-  float d[V], xh[V], o[V], mean = 0.f, rstd = 0.f;
-  auto load_row = [&](long row, float (&d_)[V], float (&x_)[V], float (&o_)[V], float& mean_, float& rstd_) {
-    mean_ = mean_in[row];
-    rstd_ = rstd_in[row];
-    ldv<V>(dy + row * D + lane * V, d_);
-    ldv<V>(x + row * D + lane * V, x_);
-    if (dres) ldv<V>(dres + row * D + lane * V, o_);
-    else {
-#pragma unroll
-      for (int i = 0; i < V; ++i) o_[i] = 0.f;
-    }
-  };
-  if (wglob < M) load_row(wglob, d, xh, o, mean, rstd);
   for (long row = wglob; row < M; row += nwaves) {
-    float dn[V], xn[V], on[V], mean_n = 0.f, rstd_n = 0.f;
-    if (row + nwaves < M) load_row(row + nwaves, dn, xn, on, mean_n, rstd_n);
-    float g[V];
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float d[V], xh[V], g[V];
+    ldv<V>(dy + row * D + lane * V, d);
+    ldv<V>(x + row * D + lane * V, xh);
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
@@ -176,6 +162,12 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TDY* __restrict__ dy, co
     }
     sg = wave_sum(sg) * (1.f / D);
     sgx = wave_sum(sgx) * (1.f / D);
+    float o[V];
+    if (dres) ldv<V>(dres + row * D + lane * V, o);
+    else {
+#pragma unroll
+      for (int i = 0; i < V; ++i) o[i] = 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < V; ++i) o[i] += rstd * (g[i] - sg - xh[i] * sgx);
     stv<V>(dx + row * D + lane * V, o);
@@ -191,14 +183,6 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TDY* __restrict__ dy, co
         st8_dyn(dr.g2, CFM_BF16, row * D + lane * V, q);
       }
     }
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-      d[i] = dn[i];
-      xh[i] = xn[i];
-      o[i] = on[i];
-    }
-    mean = mean_n;
-    rstd = rstd_n;
   }
 #pragma unroll
   for (int i = 0; i < V; ++i) {

@@ -71,16 +71,27 @@ __global__ __launch_bounds__(EB) void ada_colpart(const AdaP* __restrict__ t, in
   if (q.C % 4 == 0 && ((uintptr_t)q.g & 15) == 0) {
     // float4 columns: lane owns columns 4 lane + 256 k4 .. +3 (k4 < nk4); cacc[4 k4 + e] = column 4 lane + 256 k4 + e
     const int nk4 = (q.C + 255) / 256;
+    // the wave's next row is loaded while this one is summed (one row per round trip otherwise)
+    float4 cur[KMAX / 4], nxt[KMAX / 4];
+    auto load_row = [&](int r, float4 (&dst)[KMAX / 4]) {
+      const float* g = q.g + ((long)b * q.R + r) * q.C;
+#pragma unroll
+      for (int k4 = 0; k4 < KMAX / 4; ++k4) {
+        const int c = 4 * lane + 256 * k4;
+        if (k4 < nk4 && c < q.C) dst[k4] = *reinterpret_cast<const float4*>(g + c);
+      }
+    };
+    if (r0 + wv < r1) load_row(r0 + wv, cur);
     for (int j = 0; j < RB / 4; ++j) {
       const int r = r0 + wv + 4 * j;
       if (r >= r1) break;
-      const float* g = q.g + ((long)b * q.R + r) * q.C;
+      if (j + 1 < RB / 4 && r + 4 < r1) load_row(r + 4, nxt);
       float s = 0.f;
 #pragma unroll
       for (int k4 = 0; k4 < KMAX / 4; ++k4) {
         const int c = 4 * lane + 256 * k4;
         if (k4 < nk4 && c < q.C) {
-          const float4 v = *reinterpret_cast<const float4*>(g + c);
+          const float4 v = cur[k4];
           const float e0 = v.x * v.x + eps1, e1 = v.y * v.y + eps1, e2 = v.z * v.z + eps1, e3 = v.w * v.w + eps1;
           s += (e0 + e1) + (e2 + e3);
           cacc[4 * k4] += e0; cacc[4 * k4 + 1] += e1; cacc[4 * k4 + 2] += e2; cacc[4 * k4 + 3] += e3;
@@ -88,6 +99,8 @@ __global__ __launch_bounds__(EB) void ada_colpart(const AdaP* __restrict__ t, in
       }
       s = wave_sum(s);
       rsum = lane == j ? s : rsum;
+#pragma unroll
+      for (int k4 = 0; k4 < KMAX / 4; ++k4) cur[k4] = nxt[k4];
     }
 #pragma unroll
     for (int k4 = 0; k4 < KMAX / 4; ++k4)
@@ -126,7 +139,10 @@ __global__ __launch_bounds__(EB) void ada_colpart(const AdaP* __restrict__ t, in
   for (int c = threadIdx.x; c < q.C; c += EB) dst[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
-// row tasks of NARROW factored tensors: 64 rows per wave (lane = row)
+// row tasks of NARROW factored tensors: 256 rows per wave (lane = 4 rows; a task per 64 rows left each wave's
+// parameter search -- ~9 dependent table loads -- in front of one 4-byte row: ~18.6 M such rows at L15, the
+// degenerate (O, I, 1) pointwise-conv weights, ran 95 us)
+constexpr int ROWS_PER_TASK = 256;
 __global__ void ada_rows(const AdaP* __restrict__ t, int n, long ntasks, float b2t, float eps1) {
   const int lane = threadIdx.x & 63;
   // wave-uniform task made provably uniform: the parameter search and the table fields become scalar loads
@@ -142,13 +158,29 @@ __global__ void ada_rows(const AdaP* __restrict__ t, int n, long ntasks, float b
     if (lane == 0) row_update(q, lt, s, b2t);
     return;
   }
-  const long lr = lt * 64 + lane;
-  if (lr < (long)q.nb * q.R) {
-    const float* g = q.g + lr * q.C;
-    float s = 0.f;
+  const long nrows = (long)q.nb * q.R, base = lt * ROWS_PER_TASK;
+  if (q.C == 1 && ((uintptr_t)q.g & 15) == 0 && ((uintptr_t)q.row & 15) == 0 && base + ROWS_PER_TASK <= nrows) {
+    // one element per row: lane owns rows base + 4 lane .. +3 (16-B loads of g and of the row state)
+    const long lr = base + 4 * lane;
+    const float4 g = *reinterpret_cast<const float4*>(q.g + lr);
+    float4 v = *reinterpret_cast<const float4*>(q.row + lr);
+    v.x = b2t * v.x + (1.f - b2t) * ((g.x * g.x + eps1) / q.C);
+    v.y = b2t * v.y + (1.f - b2t) * ((g.y * g.y + eps1) / q.C);
+    v.z = b2t * v.z + (1.f - b2t) * ((g.z * g.z + eps1) / q.C);
+    v.w = b2t * v.w + (1.f - b2t) * ((g.w * g.w + eps1) / q.C);
+    *reinterpret_cast<float4*>(q.row + lr) = v;
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < ROWS_PER_TASK / 64; ++k) {
+    const long lr = base + lane + 64 * k;
+    if (lr < nrows) {
+      const float* g = q.g + lr * q.C;
+      float s = 0.f;
 #pragma unroll 8     // independent loads in flight (a serial chain of load latencies otherwise)
-    for (int c = 0; c < q.C; ++c) s += g[c] * g[c] + eps1;
-    row_update(q, lr, s, b2t);
+      for (int c = 0; c < q.C; ++c) s += g[c] * g[c] + eps1;
+      row_update(q, lr, s, b2t);
+    }
   }
 }
 
@@ -170,6 +202,18 @@ __global__ void ada_cols(const AdaP* __restrict__ t, int n, long ncols, float b2
     const float* pp = part + q.part_off + (long)b * nrb * q.C + j;
 #pragma unroll 8     // (fixed order kept: the unrolled adds still run k = 0, 1, 2, ...)
     for (int k = 0; k < nrb; ++k) s += pp[(long)k * q.C];
+  } else if (q.C == 1 && q.R % 4 == 0 && ((uintptr_t)q.g & 15) == 0) {
+    // C == 1 (the pointwise-conv weights (O, I, 1): R = I rows of one element): the column is contiguous, so
+    // 16-B loads, a quarter of the latency rounds; the adds keep the r = 0, 1, 2, ... order (bit-identical)
+    const float4* g4 = reinterpret_cast<const float4*>(q.g + (long)b * q.R);
+#pragma unroll 8
+    for (int r4 = 0; r4 < q.R / 4; ++r4) {
+      const float4 v = g4[r4];
+      s += v.x * v.x + eps1;
+      s += v.y * v.y + eps1;
+      s += v.z * v.z + eps1;
+      s += v.w * v.w + eps1;
+    }
   } else {
     const float* g = q.g + (long)b * q.R * q.C + j;
 #pragma unroll 8
@@ -297,19 +341,34 @@ __global__ __launch_bounds__(EB) void ada_apply(const AdaP* __restrict__ t, int 
   const float rms = sqrtf(sumsq / (float)q.numel);
   const float scale = lr / fmaxf(rms / clip, 1.f);
   if (vec4_ok(q)) {
-    for (long i = start + 4 * threadIdx.x; i < end; i += 4 * EB) {
-      float u[4];
-      ada_u<4>(q, rowmean, (unsigned)i, b2t, eps1, false, u);
-      float4 upd = make_float4(u[0] * scale, u[1] * scale, u[2] * scale, u[3] * scale);
+    // the CHUNK / (4 EB) = 4 steps unrolled with every load (g, factors, m, p) issued before the first store: vmcnt
+    // counts loads and stores in one in-order queue, so step j + 1's loads behind step j's stores waited for them
+    constexpr int NJ = CHUNK / (4 * EB);
+    float u[NJ][4];
+    float4 mv[NJ], pv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const long i = start + 4 * threadIdx.x + (long)j * 4 * EB;
+      if (i < end) {
+        ada_u<4>(q, rowmean, (unsigned)i, b2t, eps1, false, u[j]);
+        if (q.m) mv[j] = *reinterpret_cast<const float4*>(q.m + i);
+        pv[j] = *reinterpret_cast<const float4*>(q.p + i);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const long i = start + 4 * threadIdx.x + (long)j * 4 * EB;
+      if (i >= end) break;
+      float4 upd = make_float4(u[j][0] * scale, u[j][1] * scale, u[j][2] * scale, u[j][3] * scale);
       if (q.m) {
-        const float4 m = *reinterpret_cast<const float4*>(q.m + i);
+        const float4 m = mv[j];
         upd.x = beta1 * m.x + (1.f - beta1) * upd.x;
         upd.y = beta1 * m.y + (1.f - beta1) * upd.y;
         upd.z = beta1 * m.z + (1.f - beta1) * upd.z;
         upd.w = beta1 * m.w + (1.f - beta1) * upd.w;
         *reinterpret_cast<float4*>(q.m + i) = upd;
       }
-      float4 p = *reinterpret_cast<const float4*>(q.p + i);
+      float4 p = pv[j];
       p.x -= upd.x; p.y -= upd.y; p.z -= upd.z; p.w -= upd.w;
       *reinterpret_cast<float4*>(q.p + i) = p;
     }
@@ -348,7 +407,9 @@ CFM_EXPORT int cfm_adafactor_blocks(long numel) { return (int)((numel + CHUNK - 
 
 // number of row tasks / row-mean tasks / column-partial tasks / partial floats a factored tensor
 // contributes (see ada_rows / ada_rowmean / ada_colpart)
-CFM_EXPORT long cfm_adafactor_row_tasks(int nb, int R, int C) { return is_wide(C) ? 0 : ((long)nb * R + 63) / 64; }
+CFM_EXPORT long cfm_adafactor_row_tasks(int nb, int R, int C) {
+  return is_wide(C) ? 0 : ((long)nb * R + ROWS_PER_TASK - 1) / ROWS_PER_TASK;
+}
 CFM_EXPORT long cfm_adafactor_colpart_tasks(int nb, int R, int C) { return is_wide(C) ? (long)nb * ((R + RB - 1) / RB) : 0; }
 CFM_EXPORT long cfm_adafactor_part_floats(int nb, int R, int C) {
   return is_wide(C) ? (long)nb * ((R + RB - 1) / RB) * C : 0;
