@@ -244,6 +244,26 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, const float* __rest
   }
 }
 
+// 8 consecutive elements per thread, one pass (C % 8 == 0, 16-B aligned): the grid-stride kernel above runs ~3
+// iterations per thread whose loads each wait behind the previous iteration's store (one in-order vmcnt queue)
+template <int DTZ>
+__global__ __launch_bounds__(256) void bn_apply_vec8(const float* __restrict__ y, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, const float* __restrict__ mean,
+                                                     const float* __restrict__ invstd, void* __restrict__ z, long M,
+                                                     int C, int act) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= M * C) return;
+  const int c = (int)(i % C);
+  float v[8];
+  ld8_dyn(y, CFM_F32, i, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float u = (v[e] - mean[c + e]) * invstd[c + e] * gamma[c + e] + beta[c + e];
+    v[e] = act ? silu_f(u) : u;
+  }
+  st8_dyn(z, DTZ, i, v);
+}
+
 // row-chunk partial sums (sum, sumsq) of y over (M, C); grid (ceil(C/64), nparts), 4 waves per block
 __global__ __launch_bounds__(256) void bn_stats_rows_kernel(const float* __restrict__ y, long M, int C,
                                                             long rows_per, float* __restrict__ part) {
@@ -696,6 +716,22 @@ int ew_grid(long n) {
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
 }
 
+void bn_apply(const float* y, const float* gamma, const float* beta, const float* mean, const float* invstd, void* z,
+              int dtz, long M, int C, int act, hipStream_t s) {
+  const bool vec = C % 8 == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)z & 15) == 0 &&
+                   (dtz == CFM_BF16 || dtz == CFM_F32) && M * C / 8 / 256 < (1L << 31);
+  if (vec) {
+    const unsigned nb = (unsigned)((M * C / 8 + 255) / 256);
+    if (dtz == CFM_BF16)
+      hipLaunchKernelGGL(bn_apply_vec8<CFM_BF16>, dim3(nb), dim3(256), 0, s, y, gamma, beta, mean, invstd, z, M, C, act);
+    else
+      hipLaunchKernelGGL(bn_apply_vec8<CFM_F32>, dim3(nb), dim3(256), 0, s, y, gamma, beta, mean, invstd, z, M, C, act);
+    return;
+  }
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z, dtz, M, C,
+                     act);
+}
+
 long conv_nparts(int B, int T) { return (long)B * ((T + TT - 1) / TT); }
 
 // fwd stats from [2][nparts][C] partials at ws; scratch (2C) right after them
@@ -783,8 +819,7 @@ CFM_EXPORT int cfm_bn_silu_fwd(const float* y, const float* gamma, const float* 
     hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, running_mean, running_var, C,
                        eps, mean, invstd);
   }
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z, dtz,
-                     M, C, 1);
+  bn_apply(y, gamma, beta, mean, invstd, z, dtz, M, C, 1, s);
   return cfm::check_launch("cfm_bn_silu_fwd");
 }
 
@@ -814,8 +849,7 @@ CFM_EXPORT int cfm_bn_fwd(const float* y, const float* gamma, const float* beta,
     hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, running_mean, running_var, C,
                        eps, mean, invstd);
   }
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z, dtz,
-                     M, C, act);
+  bn_apply(y, gamma, beta, mean, invstd, z, dtz, M, C, act, s);
   return cfm::check_launch("cfm_bn_fwd");
 }
 
@@ -945,8 +979,7 @@ CFM_EXPORT int cfm_bn_silu_fwd_apply(const float* y, const float* gamma, const f
   hipStream_t s = cfm::as_stream(stream);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, sums + C, M_total, C, mean,
                      invstd, running_mean, running_var, momentum, eps);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M * C)), dim3(256), 0, s, y, gamma, beta, mean, invstd, z, dtz,
-                     M, C, 1);
+  bn_apply(y, gamma, beta, mean, invstd, z, dtz, M, C, 1, s);
   return cfm::check_launch("cfm_bn_silu_fwd_apply");
 }
 
