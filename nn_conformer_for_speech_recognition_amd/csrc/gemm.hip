@@ -515,18 +515,24 @@ template <bool M16> __device__ __forceinline__ int accc(int r, int lane) {
 // C with N % 8 == 0, bf16 pre-activation, f32 residual, the 32-bit dropout hash range, and a feature set fixed
 // at compile time per kind (EK, a kernel template parameter: each kernel carries one epilogue body -- the generic
 // body's registers spilled in the 128-register two-per-CU kernels, one accumulator inside the MFMA loop):
-//   EF_BF16      bf16 C; alpha, bias, SiLU + bf16 pre-activation store, dropout, out_scale (FFN-up, QKV, pw1 fwd)
+//   EF_BF16      bf16 C, nothing else (the d-wide data gradients)
+//   EF_BF16_BIAS bf16 C; bias (QKV, pointwise-conv-1 forward)
+//   EF_BF16_SILU bf16 C; bias, SiLU + bf16 pre-activation store, dropout (FFN-up forward)
 //   EF_BF16_ACTG bf16 C; silu'(pre) * dropout (FFN-down data gradient)
 //   EF_BF16_RD   bf16 C; rowdot with rd_with (attention out-projection data gradient)
-//   EF_F32       f32 C; as EF_BF16
-//   EF_F32_RES   f32 C; alpha, bias, dropout, out_scale, f32 residual (the d-wide residual-stream outputs)
+//   EF_F32       f32 C; alpha, bias, SiLU (+ pre), dropout, out_scale as run-time options
+//   EF_F32_RES   f32 C; bias, dropout, out_scale, f32 residual (the d-wide residual-stream outputs)
+// Every option a kind does not list is absent by construction (epi_fast_kind checks): a run-time test on a
+// uniform kernel argument is flattened by the compiler into per-lane selects with BOTH sides computed (the SiLU
+// of the bias-only QKV rows, the alpha and out_scale products), so the encoder's kinds carry no such tests.
 // A thread's 8-column chunk is the same on every row it finishes, so its bias is loaded once, and each row's global
 // input (the bf16 pre-activation / rd_with, or the f32 residual) is issued ahead of the previous rows' stores:
 // vmcnt counts loads and stores in one in-order queue, and the generic rows, which load bias / pre / residual
 // between the previous row's stores, waited for every previous row's write acknowledgements (bias-only FFN-up
 // epilogue without the main loop: 49 MB in 21.9 us = 2.2 TB/s).  Arithmetic and its order are epilogue_store8's
 // (bit-identical outputs).
-enum { EF_GENERIC = 0, EF_BF16 = 1, EF_BF16_ACTG = 2, EF_BF16_RD = 3, EF_F32 = 4, EF_F32_RES = 5 };
+enum { EF_GENERIC = 0, EF_BF16 = 1, EF_BF16_BIAS = 2, EF_BF16_SILU = 3, EF_BF16_ACTG = 4, EF_BF16_RD = 5, EF_F32 = 6,
+       EF_F32_RES = 7 };
 
 __device__ __forceinline__ void epi_bias8(const GemmP& p, int n, float (&b)[8]) {
 #pragma unroll
@@ -595,8 +601,9 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
                                               const float (&b)[8], EpiIn<EK, IT>& in) {
   static_assert(EK > EF_GENERIC && EK <= EF_F32_RES, "fast epilogue kind");
   constexpr bool CF32 = EK == EF_F32 || EK == EF_F32_RES, ACTG = EK == EF_BF16_ACTG, RD = EK == EF_BF16_RD;
-  constexpr bool RES = EK == EF_F32_RES, BIAS = !ACTG && !RD, SILU = EK == EF_BF16 || EK == EF_F32;
-  constexpr bool DROP = !RD;
+  constexpr bool RES = EK == EF_F32_RES, GEN = EK == EF_F32;   // GEN: the run-time options of EF_F32
+  constexpr bool BIAS = EK == EF_BF16_BIAS || EK == EF_BF16_SILU || RES, SILU = EK == EF_BF16_SILU;
+  constexpr bool DROP = EK == EF_BF16_SILU || ACTG || RES || GEN;
   constexpr int NW = epi_nw<EK>();
   constexpr int RPI = NTt / CPW;                       // rows per pass
   const int c8 = (tid % CPW) * 8, n = n0 + c8, r0 = tid / CPW;
@@ -618,24 +625,28 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
     const bool ok = m < p.M && nok;
     if (ok) {
       const long cidx = (long)z * p.sc + (long)m * p.ldc + n;   // (no row remap: epi_fast_kind)
-      if (p.alpha != 1.f) {
+      if constexpr (GEN) {
+        if (p.alpha != 1.f) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
-      }
-      if constexpr (BIAS) {
+          for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+        }
         if (p.bias) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += b[e];
         }
+      }
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += b[e];
       }
       if constexpr (ACTG) {
         const bf16x8 pr = __builtin_bit_cast(bf16x8, in.v[it][0]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] *= silu_grad_f((float)pr[e]);
       }
-      if constexpr (SILU) {
-        if (p.act == CFM_ACT_SILU) {
-          if (p.pre) {
+      if constexpr (SILU || GEN) {
+        if (SILU || p.act == CFM_ACT_SILU) {
+          if (SILU || p.pre) {
             bf16x8 q;
 #pragma unroll
             for (int e = 0; e < 8; ++e) q[e] = (bf16)v[e];
@@ -654,7 +665,10 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
           else drop8_fast<false>(v, j0, p);
         }
       }
-      if constexpr (!RD) {
+      if constexpr (RES) {   // (unconditional: x * 1.0f == x, and no per-lane select for the 1.0 launches)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
+      } else if constexpr (GEN) {
         if (p.out_scale != 1.f) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
@@ -1624,6 +1638,8 @@ void ek_dispatch(int ek, F&& f) {
   if constexpr (KK) {
     switch (ek) {
       case EF_BF16: f(std::integral_constant<int, EF_BF16>{}); return;
+      case EF_BF16_BIAS: f(std::integral_constant<int, EF_BF16_BIAS>{}); return;
+      case EF_BF16_SILU: f(std::integral_constant<int, EF_BF16_SILU>{}); return;
       case EF_BF16_ACTG: f(std::integral_constant<int, EF_BF16_ACTG>{}); return;
       case EF_BF16_RD: f(std::integral_constant<int, EF_BF16_RD>{}); return;
       case EF_F32: f(std::integral_constant<int, EF_F32>{}); return;
@@ -1707,16 +1723,19 @@ int num_cus() {
 int epi_fast_kind(const GemmP& p, int batch) {
   if (p.split_k != 1 || !p.vec_c || p.N % 8 || p.cmap || (p.dbg & 2) || (g_gemm_mode & 16384)) return EF_GENERIC;
   if (p.drop_p > 0.f && (p.doff + (uint64_t)batch * p.M * p.N) / 2 + 8 > 0xFFFFFFFBull) return EF_GENERIC;
-  const bool f32 = p.dtc == CFM_F32, silu = p.act == CFM_ACT_SILU;
-  if (!f32 && p.dtc != CFM_BF16) return EF_GENERIC;
+  const bool f32 = p.dtc == CFM_F32, bf = p.dtc == CFM_BF16, silu = p.act == CFM_ACT_SILU;
+  const bool a1 = p.alpha == 1.f, s1 = p.out_scale == 1.f;
+  if (!f32 && !bf) return EF_GENERIC;
   if (p.res)
-    return f32 && p.dtr == CFM_F32 && !silu && !p.act_grad && !p.rd_out ? EF_F32_RES : EF_GENERIC;
+    return f32 && p.dtr == CFM_F32 && p.bias && a1 && !silu && !p.act_grad && !p.rd_out ? EF_F32_RES : EF_GENERIC;
   if (p.act_grad)
-    return !f32 && p.dtpre == CFM_BF16 && !silu && !p.rd_out && !p.bias ? EF_BF16_ACTG : EF_GENERIC;
+    return bf && p.dtpre == CFM_BF16 && !p.bias && a1 && s1 && !silu && !p.rd_out ? EF_BF16_ACTG : EF_GENERIC;
   if (p.rd_out)
-    return !f32 && !silu && !p.bias && p.drop_p <= 0.f && p.out_scale == 1.f ? EF_BF16_RD : EF_GENERIC;
-  if (silu && p.pre && p.dtpre != CFM_BF16) return EF_GENERIC;
-  return f32 ? EF_F32 : EF_BF16;
+    return bf && !p.bias && a1 && s1 && !silu && p.drop_p <= 0.f ? EF_BF16_RD : EF_GENERIC;
+  if (f32) return silu && p.pre && p.dtpre != CFM_BF16 ? EF_GENERIC : EF_F32;
+  if (silu) return p.pre && p.dtpre == CFM_BF16 && p.bias && a1 && s1 ? EF_BF16_SILU : EF_GENERIC;
+  if (p.drop_p > 0.f || !a1 || !s1) return EF_GENERIC;
+  return p.bias ? EF_BF16_BIAS : EF_BF16;
 }
 
 int launch_pipe(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
