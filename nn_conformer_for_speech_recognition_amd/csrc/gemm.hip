@@ -1912,6 +1912,7 @@ CFM_EXPORT int cfm_wgrad_group_probed(const void* dev_tab, int ntasks, long tota
   GatherA ga{};
   ga.group_tab = dev_tab;
   ga.group_n = ntasks;
+  // (round 4: a 5-deep ring -- 5 x 32 KiB, the whole 160 KiB LDS -- ran 3.132 vs 2.896 ms, gpurun_out r04u)
   hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 4, 1, false, false, 8, 2, false, true, false, WG_BN>),
                      dim3((unsigned)total_tiles), dim3(512), 0, cfm::as_stream(stream), gp, PipeOp{}, PipeOp{}, ga);
   return cfm::check_launch("cfm_wgrad_group");
