@@ -965,7 +965,8 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   static_assert(WM * FM * 32 == BMt && WN * FN * 32 == BNt, "wave tiling");
   static_assert(G::EVEN || (!GA && !GROUP), "uneven DMA split: plain operands only");
   probe_begin(p.probe);
-  gemm_drop_prep(p);
+  // (the dropout constants are prepared right before the epilogue: gemm_drop_prep loads the bound step counter,
+  // and waiting for that load at the top held back the first DMA stage by one memory round trip)
   static_assert(NST >= 3 && NST <= 6, "ring depth");
   __shared__ __attribute__((aligned(1024))) char lds[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1188,6 +1189,7 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
     if (t == -1234.5f) reinterpret_cast<float*>(p.C)[tid] = t;
     return;
   }
+  if constexpr (!GROUP) gemm_drop_prep(p);
   __syncthreads();   // every wave done with the ring (no DMA outstanding) -> reuse it for the epilogue
   if constexpr (F8) {   // per-tensor dequantisation of the fp8 operands (device scalars)
     if (p.alpha_a) p.alpha *= p.alpha_a[0];
@@ -1221,7 +1223,6 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
   static_assert(NST >= 3 && NST <= 5, "ring depth");
   __shared__ __attribute__((aligned(1024))) char lds[RING > EPI ? RING : EPI];
   probe_begin(p.probe);
-  gemm_drop_prep(p);
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   int tm, tn, zz;
   xcd_tile3(tm, tn, zz);
@@ -1322,6 +1323,7 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
     if (t == -1234.5f) reinterpret_cast<float*>(p.C)[tid] = t;
     return;
   }
+  gemm_drop_prep(p);   // (here, not at the top: its counter load would hold back the loaders' first stage)
   float bias8[8];
   if constexpr (EK != EF_GENERIC) epi_bias8(p, n0 + (tid % CPW) * 8, bias8);
   __syncthreads();   // every DMA landed (the loaders' last wait was vmcnt(0)), every fragment read consumed
