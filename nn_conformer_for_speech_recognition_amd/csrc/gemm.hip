@@ -1685,6 +1685,18 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
     if (v == 0 && p.N > 512 && p.N <= 1536 && p.k_per_split <= 512 && p.split_k == 1 && p.M >= 4096 &&
         !(g_gemm_mode & 4096))
       v = 7;
+    // 1024- / 1536-wide K-major x K-major outputs (QKV, pointwise-conv-1 forward) on the warp-specialised kernel:
+    // QKV 32.41 -> 30.97 us, pw1 22.53 -> 21.41 us same box, bit-identical (gpurun_out r04y; the 2048-wide ones
+    // stay on the two-per-CU 256-row tiles: 45.5 vs 57.3 us).  cfm_gemm_set_mode bit 21 keeps the 192-row pipeline.
+    if constexpr (BKM) {
+      if (v == 7 && sel == 0 && !(g_gemm_mode & 2097152)) {
+        const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
+        ek_dispatch<true>(p.efast, [&](auto ek) {
+          hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 4, 4, 4, decltype(ek)::value>), g192, dim3(768), 0, s, p, oa, ob);
+        });
+        return;
+      }
+    }
     if (v == 7) {   // 192 x 128 tiles, 8 waves of 96 x 32, BK 32 (uneven A DMA split): two per CU
       const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
       ek_dispatch<AK && BKM>(p.efast, [&](auto ek) {

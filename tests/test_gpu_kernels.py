@@ -437,6 +437,32 @@ def test_gemm_warp_specialised_matches_shared_dma(gemm_mode, M, K, epi):
         assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("M", [11936, 4100])
+@pytest.mark.parametrize("N", [1024, 1536, 640])
+def test_gemm_wide_ws_matches_pipe(gemm_mode, M, N):
+    """1024- / 1536-wide K-major x K-major outputs (QKV, pointwise-conv-1 forward) run on the warp-specialised kernel;
+    cfm_gemm_set_mode bit 21 keeps the two-per-CU 192-row pipeline.  Same 16x16x32 MFMAs in the same k order and the
+    same epilogue kinds -> bit-identical (bias-only and SiLU + pre-activation + dropout rows, ragged M)."""
+    K = 512
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    outs = []
+    for mode in (3, 3 | 2097152):
+        gemm_mode(mode)
+        y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.linear(x, w, b, out=y)
+        ys = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.linear(x, w, b, act=ops.ACT_SILU, pre=pre, drop_p=0.1, seed=9, out=ys)
+        outs.append((y.clone(), ys.clone(), pre.clone()))
+    torch.cuda.synchronize()
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    assert _rel(outs[0][0].float(), x.float() @ w.float().T + b) < 1e-2
+
+
 @pytest.mark.parametrize("M", [11936, 1000, 385])
 @pytest.mark.parametrize("epi,N", [("silu_pre_drop", 2048), ("actg_drop", 2048), ("bias", 1536), ("bias", 1024),
                                    ("f32_bias", 2048), ("res_drop", 512), ("res_drop", 2048), ("rowdot", 512),
