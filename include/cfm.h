@@ -219,9 +219,13 @@ int cfm_colreduce_group(const void* dev_table, int ntasks, long total_blocks, vo
 int cfm_wgrad_group_probed(const void* dev_table, int ntasks, long total_tiles, unsigned long long* probe,
                            void* stream);
 /* kernel-selection switch for A/B measurements: bit 0 = 256-row register-staged tiles allowed,
-   bit 1 = LDS-DMA pipelined kernel allowed, bit 3 = timing experiment (pipelined kernel skips its
-   stores), bits 4-5 = pipelined variant (0 auto, 1 256x128/BK64, 2 256x128/BK32 two per CU,
-   3 128x128/BK64); default 3. */
+   bit 1 = LDS-DMA pipelined kernel allowed, bit 3 = timing experiment (pipelined kernels skip their
+   stores), bits 4-6 = pipelined variant (0 auto, 1 256x128/BK64, 2 256x128/BK32 two per CU,
+   5 192x128, 7 192x128/BK32 two per CU), bit 10 = generic dropout hash path, bit 12 = no 192-row rule for
+   1024/1536-wide outputs, bit 13 = timing experiment (main loop skipped: epilogue only), bit 14 = generic
+   epilogue rows instead of the compile-time epilogue kinds, bit 19 = shared-DMA pipeline instead of the
+   warp-specialised kernel for d-wide outputs, bit 21 = 192-row pipeline instead of the warp-specialised kernel
+   for 1024/1536-wide outputs; default 3. */
 int cfm_gemm_set_mode(int mode);
 
 /* out[n] (+)= sum_m x[m*ld + n]  — bias gradients (sum over tokens).  ws: >= 4*N*256 bytes. */
