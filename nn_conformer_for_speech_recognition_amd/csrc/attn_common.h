@@ -187,20 +187,32 @@ __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16&
   mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
   const float mn = fmaxf(m, mloc * c);
   const float alpha = fast_exp2(m - mn);
+  // the scale-and-shift and the o rescale on packed FP32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth per
+  // instruction, the same IEEE operations per element); the sum keeps its order
+  typedef float f32x2v __attribute__((ext_vector_type(2)));
+  const f32x2v c2 = {c, c}, nm2 = {-mn, -mn}, a2 = {alpha, alpha};
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    const f32x2v x0 = __builtin_elementwise_fma((f32x2v){s0[r], s0[r + 1]}, c2, nm2);
+    const f32x2v x1 = __builtin_elementwise_fma((f32x2v){s1[r], s1[r + 1]}, c2, nm2);
+    s0[r] = x0.x; s0[r + 1] = x0.y;
+    s1[r] = x1.x; s1[r + 1] = x1.y;
+  }
   float ls = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    s0[r] = fast_exp2(__builtin_fmaf(s0[r], c, -mn));
-    s1[r] = fast_exp2(__builtin_fmaf(s1[r], c, -mn));
+    s0[r] = fast_exp2(s0[r]);
+    s1[r] = fast_exp2(s1[r]);
     ls += s0[r] + s1[r];
   }
   ls += __shfl_xor(ls, 32, 64);
   l = l * alpha + ls;
   m = mn;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    o0[r] *= alpha;
-    o1[r] *= alpha;
+  for (int r = 0; r < 16; r += 2) {
+    const f32x2v y0 = (f32x2v){o0[r], o0[r + 1]} * a2, y1 = (f32x2v){o1[r], o1[r + 1]} * a2;
+    o0[r] = y0.x; o0[r + 1] = y0.y;
+    o1[r] = y1.x; o1[r + 1] = y1.y;
   }
   if (p.drop_p > 0.f) {
     const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kbase) >> 1);   // even: 32-bit pair indices
