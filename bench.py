@@ -72,7 +72,7 @@ def algorithmic_flops_per_frame(L, d, H, ffn, K, T_in, T2, F2, C1=512, C2=128, r
 
 
 def executed_flops_per_frame(L, d, H, ffn, K, T_in, T2, rel=False, B=1, Kp=1792, T2p=None):
-    """The FLOPs the step EXECUTES per mel frame (fwd+bwd), for step_algorithmic_tflops / step_mfma_frac: the
+    """The FLOPs the step EXECUTES per mel frame (fwd+bwd), for step_executed_tflops / step_mfma_frac: the
     encoder as in algorithmic_flops_per_frame, but the front-end as the folded GEMMs that replace conv1 + conv2 +
     projection: the forward GEMM 2*T2*Kp*d and the weight-gradient GEMM 2*T2p*Kp*d per utterance
     (Kp = 11 frames x 80 mels x hi+lo, padded; no input gradient); the fold's ~1 GFLOP/step of fp32 weight
@@ -181,22 +181,45 @@ def run_nst(args, model, x, lens_i32, dev, cfg, rank, world):
         torch.distributed.destroy_process_group()
 
 
+_ELT = {_lib.F32: 4, _lib.BF16: 2, _lib.FP8: 1}
+
+
+def gemm_desc_bytes(desc):
+    """Algorithmic HBM bytes of one cfm_gemm launch from its descriptor: A (M x K per batch) and B (N x K, per batch
+    when strided) read in dtype_ab, C (M x N per batch) written in dtype_c, the residual (M x N) read in dtype_r --
+    the definition benchmarks/pmc_dgemm_json.py uses for the PMC record's `algorithmic_bytes_per_launch`."""
+    bt = max(1, int(desc.batch))
+    ea, ec = _ELT[int(desc.dtype_ab)], _ELT[int(desc.dtype_c)]
+    b_batches = bt if desc.stride_b else 1
+    n = ea * (desc.M * desc.K * bt + desc.N * desc.K * b_batches) + ec * desc.M * desc.N * bt
+    if desc.residual:
+        n += _ELT[int(desc.dtype_r)] * desc.M * desc.N * bt
+    return float(n)
+
+
 class KernelProbe:
     """Timing of one kernel family, installed as ops.PROBE.  Each matching launch gets a probe slot
-    (cfm_gemm_desc.probe): the kernel itself records its first workgroup's start and its last
-    workgroup's end (s_memrealtime) — the interval rocprofv3 reports as the kernel's duration —
-    and one-lane kernels on the same stream reset the slot before and accumulate it after the
-    launch.  Works eagerly and inside a captured HIP graph (every replay accumulates)."""
+    (cfm_gemm_desc.probe, 8 x u64): a one-lane kernel on the same stream resets the slot and stamps the wall clock
+    right before the launch (cfm_probe_slot mode 2), the kernel itself records its first workgroup's start and its
+    last workgroup's end (s_memrealtime), and a one-lane kernel after it stamps again and accumulates (mode 3):
+    * `busy` = first-workgroup start -> last-workgroup end (the launch's own execution);
+    * `incl` = stamp -> stamp around the launch MINUS the same interval of empty stamp pairs (calibrate(): the
+      two one-lane kernels alone), i.e. the time the launch adds to a serial stream -- its dispatch ramp,
+      execution and end-of-kernel completion, what rocprofv3's kernel trace counts; `frac` uses it.
+    Works eagerly and inside a captured HIP graph (every replay accumulates)."""
 
     MAX_SLOTS = 1024
+    CAL_PAIRS = 32
 
     def __init__(self, match, device):
         self.match = match
         self.active = False
-        self.slots = torch.zeros(self.MAX_SLOTS, 4, dtype=torch.int64, device=device)
+        self.slots = torch.zeros(self.MAX_SLOTS, 8, dtype=torch.int64, device=device)
+        self.cal = torch.zeros(self.CAL_PAIRS, 8, dtype=torch.int64, device=device)
         self.used = 0
         self.khz = _lib.load().cfm_wallclock_khz()
         self.slot_flops = [0.0] * self.MAX_SLOTS    # 2*M*N*K*batch of the launch each slot times (GEMMs)
+        self.slot_bytes = [0.0] * self.MAX_SLOTS    # gemm_desc_bytes of that launch
 
     def __call__(self, kind, shape, desc, launch):
         if not (self.active and self.match(kind, shape, desc)) or self.khz <= 0:
@@ -206,43 +229,75 @@ class KernelProbe:
         if kind == "gemm":
             M, N, K = shape
             self.slot_flops[slot] = 2.0 * M * N * K * max(1, int(desc.batch))
+            self.slot_bytes[slot] = gemm_desc_bytes(desc)
         ptr = _lib.ptr(self.slots[slot])
-        _lib.call("cfm_probe_slot", ptr, 0, _lib.stream())
+        _lib.call("cfm_probe_slot", ptr, 2, _lib.stream())
         desc.probe = ptr
         r = launch()
         desc.probe = None
-        _lib.call("cfm_probe_slot", ptr, 1, _lib.stream())
+        _lib.call("cfm_probe_slot", ptr, 3, _lib.stream())
         return r
+
+    def calibrate(self):
+        """CAL_PAIRS empty (stamp, accumulate) pairs on the current stream -- launched inside the probe graph's
+        capture, so every replay re-measures the one-lane kernels' own interval."""
+        if self.khz <= 0:
+            return
+        for i in range(self.CAL_PAIRS):
+            ptr = _lib.ptr(self.cal[i])
+            _lib.call("cfm_probe_slot", ptr, 2, _lib.stream())
+            _lib.call("cfm_probe_slot", ptr, 3, _lib.stream())
 
     def reset(self):
         self.slots.zero_()
+        self.cal.zero_()
 
-    def mean_ms(self):
+    def empty_pair_ms(self):
+        n = int(self.cal[:, 3].sum().item())
+        return (self.cal[:, 5].double().sum().item() / self.khz / n) if n else None
+
+    def mean_ms(self, incl=False):
+        """(mean ms per timed launch, launches timed): busy, or with incl=True the stamp-to-stamp interval minus
+        the empty pairs' (uncorrected when no calibration ran, e.g. eager runs)."""
         torch.cuda.synchronize()
-        tot = self.slots[:, 2].double().sum().item()
+        tot = self.slots[:, 5 if incl else 2].double().sum().item()
         n = int(self.slots[:, 3].sum().item())
-        return (tot / self.khz / n) if n else float("nan"), n
+        if not n:
+            return float("nan"), 0
+        ms = tot / self.khz / n
+        if incl and self.empty_pair_ms() is not None:
+            ms -= self.empty_pair_ms()
+        return ms, n
+
+    def _mean(self, per_slot):
+        cnt = self.slots[:, 3].double().cpu()
+        n = cnt.sum().item()
+        return (sum(f * c for f, c in zip(per_slot, cnt.tolist())) / n) if n else float("nan")
 
     def mean_flops(self):
         """Launch-weighted mean FLOPs per timed launch (a family of GEMM shapes)."""
-        cnt = self.slots[:, 3].double().cpu()
-        n = cnt.sum().item()
-        return (sum(f * c for f, c in zip(self.slot_flops, cnt.tolist())) / n) if n else float("nan")
+        return self._mean(self.slot_flops)
+
+    def mean_bytes(self):
+        """Launch-weighted mean algorithmic bytes per timed launch (gemm_desc_bytes)."""
+        return self._mean(self.slot_bytes)
 
 
-def dgemm_bytes(probe, M, d):
-    """Mean algorithmic bytes per launch of the d-wide GEMM family: A (M x K) + B (d x K) bf16 read, C (M x d)
-    written (fp32 + an fp32 residual read for the residual-stream forwards, bf16 for data gradients).  Approximated
-    per launch from its FLOPs (K = flops / 2Md) with the bf16-output form; the fp32 forwards (3 of 10 per layer)
-    move 12 more bytes per output element."""
-    cnt = probe.slots[:, 3].double().cpu().tolist()
-    tot = n = 0.0
-    for f, c in zip(probe.slot_flops, cnt):
-        if c and f:
-            Kx = f / (2.0 * M * d)
-            tot += c * (2.0 * (M * Kx + d * Kx) + 2.0 * M * d)
-            n += c
-    return tot / n if n else float("nan")
+def trace_family_ms(summary_file, config, family):
+    """The rocprofv3 kernel-trace figure of a kernel family, read from a committed summary
+    (profiles/summarize_trace.py output: per (kernel, grid) rows of launches per step and mean duration) of a
+    bench.py run of the same config: (mean ms per launch, launches per step, summary path) or None."""
+    path = os.path.join(REPO, summary_file)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f)
+    if rec.get("config") != config:
+        return None
+    fam = rec.get("families", {}).get(family)
+    if not fam:
+        return None
+    return fam["avg_ns"] / 1e6, fam["launches_per_step"], summary_file
 
 
 def time_ctc_head(h, reps=20):
@@ -538,6 +593,8 @@ class Harness:
             for p in probes:
                 p.active = True
             with self.reducer.no_sync(), torch.cuda.graph(self.probe_graph):    # (no reduce / cut inside)
+                for p in probes:
+                    p.calibrate()
                 self.fwd_bwd()
             for p in probes:
                 p.active = False
@@ -720,23 +777,21 @@ def main():
 
     h.probe_replays(args.steps)
     ops.PROBE = None
-    gemm_ms, n_launch = probe.mean_ms()
     if os.environ.get("BENCH_PROBE_DUMP"):
         torch.save(probe.slots.cpu(), os.environ["BENCH_PROBE_DUMP"])
-    if h.probe_graph is not None:
-        timing = ("in-kernel s_memrealtime first-start / last-end of every matching launch over --steps replays "
-                  "of a second capture of the same step that carries the probe kernels, run right after the timed "
-                  "region (the timed graph carries no probes)")
-    else:
-        timing = ("in-kernel s_memrealtime first-start / last-end of every matching launch in the timed "
-                  "region" + (" (graph replays)" if h.graph is not None else ""))
+    where = ("over --steps replays of a second capture of the same step that carries the probe kernels, run right "
+             "after the timed region (the timed graph carries no probes)" if h.probe_graph is not None else
+             "in the timed region" + (" (graph replays)" if h.graph is not None else ""))
+    timing = ("avg_launch_ms: s_memrealtime of a one-lane stamp kernel right before each matching launch to that of "
+              "one right after it, minus the same interval of empty stamp pairs (empty_pair_ms) -- the time the "
+              "launch adds to the serial stream (dispatch ramp + execution + end-of-kernel completion), as "
+              "rocprofv3's kernel trace counts it; avg_launch_ms_busy: first-workgroup start to last-workgroup end; "
+              + where)
     gemm_flops = 2.0 * M_ffn * ffn * d
     # algorithmic bytes of one FFN up-projection launch: A (M x d) + W (ffn x d) bf16 reads, bias fp32,
     # y and the saved pre-activation (M x ffn each, bf16) written
     gemm_bytes = 2.0 * (M_ffn * d + ffn * d) + 4.0 * ffn + 2.0 * 2.0 * M_ffn * ffn
-    wg_ms, wg_n = wprobe.mean_ms()
-    dg_ms, dg_n = dprobe.mean_ms()
-    dg_flops = dprobe.mean_flops()
+    _, dg_n = dprobe.mean_ms(incl=True)
     wg_shapes = [(d, ffn), (ffn, d)] * 2 + [(3 * d, d), (d, d), (2 * d, d), (d, d)]   # (N, K) per layer
     wg_flops = 2.0 * M_ffn * L * sum(n * k for n, k in wg_shapes)
     wg_bytes = L * sum(2.0 * M_ffn * (n + k) + 4.0 * n * k + 4.0 * n for n, k in wg_shapes)
@@ -747,9 +802,16 @@ def main():
     ref_tflops = fpf * B * T_in / (ms_step * 1e-3) / 1e12
     ctc_ms = time_ctc_head(h) if rank == 0 else float("nan")
 
-    def roofline_entry(kernel, flops, nbytes, ms, n_launch, pmc_file):
+    cfg_key = args.config + ("+fp8" if args.fp8 else "") + ("+specaug" if args.specaug else "") + (
+        f"+pos_{args.pos_enc}" if args.pos_enc else "") + (f"+L{args.layers}" if args.layers else "")
+
+    def roofline_entry(kernel, flops, nbytes, pr, pmc_file, family):
         """bound from the kernel's arithmetic intensity against the machine balance (peak FLOP/s over peak
-        HBM B/s); `achieved`/`peak`/`frac` in the bound's unit, both fractions reported."""
+        HBM B/s); `achieved`/`peak`/`frac` in that bound's unit, both fractions reported.  Duration: the probe's
+        dispatch-inclusive mean (KernelProbe); its busy mean and the rocprofv3 kernel-trace mean of the same
+        family (a committed profiles/r05 summary of a bench.py run of this config) are reported beside it."""
+        ms, n_launch = pr.mean_ms(incl=True)
+        ms_busy, _ = pr.mean_ms()
         intensity = flops / nbytes
         balance = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
         tflops = flops / (ms * 1e-3) / 1e12
@@ -761,9 +823,18 @@ def main():
              "frac": round(gbs / PEAK_HBM_GBS if hbm else tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
              "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
              "intensity_flop_per_byte": round(intensity, 1), "machine_balance_flop_per_byte": round(balance, 1),
-             "avg_launch_ms": round(ms, 4), "launches_timed": n_launch, "timing": timing,
-             "flops_per_launch": flops, "algorithmic_bytes": nbytes}
-        for rnd in ("r04", "r03", "r02"):
+             "avg_launch_ms": round(ms, 4), "avg_launch_ms_busy": round(ms_busy, 4),
+             "empty_pair_ms": None if pr.empty_pair_ms() is None else round(pr.empty_pair_ms(), 4),
+             "launches_timed": n_launch,
+             "timing": timing, "flops_per_launch": flops, "algorithmic_bytes": nbytes}
+        tr = trace_family_ms(f"profiles/r05/trace_{cfg_key}.json", cfg_key, family)
+        if tr is not None:
+            e["avg_launch_ms_trace"] = round(tr[0], 4)
+            e["trace_launches_per_step"] = tr[1]
+            e["frac_by_trace"] = round((gbs / PEAK_HBM_GBS if hbm else tflops / PEAK_BF16_TFLOPS) * ms / tr[0], 4)
+            e["trace_source"] = tr[2] + " (rocprofv3 --kernel-trace of a bench.py run of this config: the family's "\
+                                        "mean dispatch duration over the timed graph replays)"
+        for rnd in ("r05", "r04", "r03", "r02"):
             path = os.path.join(REPO, "profiles", rnd, pmc_file)
             if not os.path.exists(path):
                 continue
@@ -772,6 +843,10 @@ def main():
             if rec.get("shape_key") == [M_ffn, d, ffn, L] and rec.get("hbm_bytes_per_launch"):
                 e["traffic"] = rec["hbm_bytes_per_launch"]
                 e["traffic_source"] = f"profiles/{rnd}/{pmc_file} ({rec.get('kernel', '?')[:80]})"
+                if rec.get("algorithmic_bytes_per_launch"):
+                    e["traffic_over_algorithmic"] = round(rec["hbm_bytes_per_launch"] /
+                                                          rec["algorithmic_bytes_per_launch"], 3)
+                    e["pmc_algorithmic_bytes"] = rec["algorithmic_bytes_per_launch"]
                 break
         return e
 
@@ -795,10 +870,11 @@ def main():
         "per_gpu_value": round(value / world, 1),
         # FLOPs the step executes (encoder + the folded front-end GEMMs; CTC head excluded), and the reference
         # composition's count (conv1 + conv2 + projection as the reference computes them) beside it
-        "step_algorithmic_tflops": round(step_tflops, 1),
+        "step_executed_tflops": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
         "step_flops_basis": "executed: encoder (SURVEY.md 8d per-layer MACs) + folded front-end GEMMs; CTC head "
-                            "excluded",
+                            "excluded (rounds 1-4 records named this key step_algorithmic_tflops; since round 4 it "
+                            "is the executed count, the reference composition's is step_ref_composition_tflops)",
         "step_ref_composition_tflops": round(ref_tflops, 1),
         "ctc_head": {"ms": round(ctc_ms, 4), "share_of_step": round(ctc_ms / ms_step, 4),
                      "flops": 3 * 2.0 * B * T2 * d * h.V,
@@ -807,18 +883,19 @@ def main():
         "loss": loss_val,
         "steps_checked": h.steps_run, "nonfinite_steps": nonfinite, "nonfinite_before_timing": bad_before,
         "params_finite": params_ok, "valid": valid,
-        # the dominant kernel family: d-wide-output GEMMs (mean FLOP / mean launch; bytes: A + B read, C written
-        # in its dtype -- bf16 data gradients, fp32 residual-stream forwards read + written -- averaged likewise)
+        # the dominant kernel family: d-wide-output GEMMs (mean FLOP / mean launch; bytes per launch from its
+        # descriptor (gemm_desc_bytes): A + B read, C written in its dtype -- bf16 data gradients, fp32
+        # residual-stream forwards written + residual read -- averaged likewise)
         "roofline": roofline_entry(f"gemm_ws (warp-specialised) d-wide outputs (N={d}, M={M_ffn} tokens): FFN-down / out-proj / pw2 "
                                    f"forward + every d-wide data gradient + the front-end fold, {dg_n // max(1, args.steps)}"
-                                   f" launches per step", dg_flops, dgemm_bytes(dprobe, M_ffn, d), dg_ms, dg_n,
-                                   "gemm_dwide_pmc.json"),
+                                   f" launches per step", dprobe.mean_flops(), dprobe.mean_bytes(), dprobe,
+                                   "gemm_dwide_pmc.json", "dwide"),
         "roofline_ffn_up": roofline_entry(f"gemm_pipe FFN up-projection M={M_ffn} N={ffn} K={d} (+bias+SiLU+dropout, "
-                                          f"y and pre-activation stored)", gemm_flops, gemm_bytes, gemm_ms, n_launch,
-                                          "gemm_ffn_up_pmc.json"),
+                                          f"y and pre-activation stored)", gemm_flops, gemm_bytes, probe,
+                                          "gemm_ffn_up_pmc.json", "ffn_up"),
         "roofline_wgrad": roofline_entry(f"grouped weight gradients (cfm_wgrad_group): {L} layers x 8 GEMMs, "
-                                         f"M={M_ffn} tokens", wg_flops, wg_bytes, wg_ms, wg_n,
-                                         "wgrad_group_pmc.json"),
+                                         f"M={M_ffn} tokens", wg_flops, wg_bytes, wprobe, "wgrad_group_pmc.json",
+                                         "wgrad"),
     }
     if args.poison:
         result["poison"] = True

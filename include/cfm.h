@@ -54,7 +54,13 @@ int cfm_rng_bind(const uint64_t* counter);
    cannot be read back on ROCm).  A probe slot is 4 x u64 {start, end, total, count}: mode 0
    resets start = ~0, end = 0 (before the probed launch, which records its first-start / last-end
    into start / end, see cfm_gemm_desc.probe); mode 1 adds end - start to total and 1 to count
-   (after it).  Ticks of the constant-rate GPU wall clock at cfm_wallclock_khz() kHz. */
+   (after it).  Modes 2 / 3 take an 8 x u64 slot {start, end, total, count, stamp, total_incl, -, -}:
+   mode 2 is mode 0 plus stamp = the wall clock when this one-lane kernel runs, mode 3 is mode 1 plus
+   total_incl += (the wall clock when this one-lane kernel runs) - stamp: stamp-to-stamp around the
+   probed launch.  Minus the same interval of an EMPTY pair (mode 2 directly followed by mode 3:
+   the two one-lane kernels' own dispatch), it is the time the launch adds to a serial stream --
+   its dispatch ramp, execution and end-of-kernel completion, what rocprofv3's kernel trace counts.
+   Ticks of the constant-rate GPU wall clock at cfm_wallclock_khz() kHz. */
 int cfm_probe_slot(unsigned long long* slot, int mode, void* stream);
 int cfm_wallclock_khz(void);
 

@@ -617,7 +617,10 @@ class Conformer(nn.Module):
         """The encoder as torch.ops.cfm.* calls (library.layer_forward): the route torch.compile traces
         (fullgraph=True).  Same kernels as the fused layer node; dropout seeds are fixed per call site unless
         `seed` is given (a device step counter bound with cfm_rng_bind salts them per step, as in HIP-graph
-        replay), so no Python-side step counter is mutated inside the traced region."""
+        replay), so no Python-side step counter is mutated inside the traced region.
+        The guard below sees only THAT a counter is bound, not that it advances: the caller owns advancing it once
+        per step, outside the compiled region (bench.py's Harness adds 1 to its counter before every replay); a
+        bound but frozen counter replays the same masks every step."""
         from . import library, _lib
         if seed is None and self.training and not _lib.RNG_BOUND and any(
                 float(ly.dropout) > 0 for ly in self.conformer_layers):

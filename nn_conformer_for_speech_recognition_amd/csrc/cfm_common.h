@@ -95,7 +95,7 @@ __device__ __forceinline__ void st8_dyn(void* p, int dt, long idx, const float (
 
 // ----------------------------------------------------------------------------- dropout RNG
 // Counter-based dropout: element idx of a call keyed by `seed` draws 16 uniform bits; elements
-// 2j and 2j+1 share one 32-bit hash of j + key (attn_mix below: two full-rate 24-bit multiplies; the key itself
+// 2j and 2j+1 share one 32-bit hash of j + key (attn_mix below: two full-rate 24-bit multiply-adds; the key itself
 // comes from lowbias32), so the mask costs a few VALU ops per element and is regenerated bit-identically in the
 // backward kernels.
 __device__ __forceinline__ uint32_t cfm_mix32(uint32_t x) {
@@ -107,17 +107,22 @@ __device__ __forceinline__ uint32_t cfm_mix32(uint32_t x) {
   return x;
 }
 // The dropout element hash (every dropout: attention probabilities, GEMM epilogues, scale_dropout, the LayerNorm
-// backward's g2): two 24-bit multiplies (v_mul_u32_u24, full rate) in place of lowbias32's two 32-bit ones
-// (v_mul_lo_u32, quarter rate) -- the attention kernels hash one pair per two scores and were VALU-bound on it.  Each multiply sees 24 bits, but the xor-shift before it folds the high bits in.
+// backward's g2): two full-rate 24-bit multiply-adds (v_mad_u32_u24) in place of lowbias32's two 32-bit
+// multiplies (v_mul_lo_u32, quarter rate) -- the attention kernels hash one pair per two scores and were
+// VALU-bound on it.  Each round x += lo24(x) * C with C even is lo24 * (C + 1) + (hi8 << 24): C + 1 odd makes
+// it a bijection of the 32-bit word (two inputs with equal images have equal lo24, since C + 1 is invertible
+// mod 2^24, hence equal hi8), so the whole hash is one-to-one and distinct element pairs never share bits by
+// construction.  (Round 4's form multiplied lo24 alone and dropped the high byte: x and x ^ (d * 0x01000100)
+// collided.)
 // The key is ADDED to the pair index (not xor-ed, as for lowbias32), so a lane's base + key folds into one
 // register and each pair costs one add.
-// Over the attention index pattern ((bh T + i) T2 + j/2) its keep rate and lag-1..8 / diagonal correlations
-// of the keep decisions match lowbias32's to within sampling noise (T = 97, 373, 1498).
+// Over the attention and GEMM-epilogue index patterns its keep rate and lag-1..8 / diagonal correlations of the
+// keep decisions match lowbias32's to within sampling noise (tests/test_dropout_hash_cpu.py).
 __device__ __forceinline__ uint32_t attn_mix(uint32_t x) {
   x ^= x >> 16;
-  x = (x & 0xFFFFFFu) * 0x9E3779u;
+  x += (x & 0xFFFFFFu) * 0x9E3778u;
   x ^= x >> 15;
-  x = (x & 0xFFFFFFu) * 0x85EBCAu;
+  x += (x & 0xFFFFFFu) * 0x85EBCAu;
   x ^= x >> 16;
   return x;
 }

@@ -389,18 +389,20 @@ CFM_EXPORT int cfm_colsum(const void* x, int dtx, long M, int N, long ld, float*
 // after it, on the same stream (so they work as nodes of a captured HIP graph too).
 namespace {
 __global__ void probe_slot_kernel(unsigned long long* s, int mode) {
-  if (mode == 0) {
+  if (mode == 0 || mode == 2) {
     s[0] = ~0ull;
     s[1] = 0ull;
+    if (mode == 2) s[4] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
   } else {
     if (s[1] > s[0]) s[2] += s[1] - s[0];
+    if (mode == 3) s[5] += (unsigned long long)__builtin_amdgcn_s_memrealtime() - s[4];
     s[3] += 1;
   }
 }
 }  // namespace
 
 CFM_EXPORT int cfm_probe_slot(unsigned long long* slot, int mode, void* stream) {
-  CFM_REQUIRE(slot && (mode == 0 || mode == 1), CFM_ERR_ARG, "bad args");
+  CFM_REQUIRE(slot && mode >= 0 && mode <= 3, CFM_ERR_ARG, "bad args");
   hipLaunchKernelGGL(probe_slot_kernel, dim3(1), dim3(1), 0, cfm::as_stream(stream), slot, mode);
   return cfm::check_launch("cfm_probe_slot");
 }

@@ -1,0 +1,94 @@
+"""Summarise a rocprofv3 --kernel-trace CSV of a bench.py run into the per-family figures bench.py's roofline entries
+quote beside their live probes (`avg_launch_ms_trace`).
+
+    python profiles/summarize_trace.py KERNEL_TRACE.csv OUT.json --config L15 --warmup W --steps K
+
+The bench run dispatches, in order: W eager warm-up steps, one graph replay, K timed replays, then K replays of the
+probe graph, where every probed launch sits between two probe_slot_kernel dispatches.  The probe brackets name each
+family's kernel signatures (kernel name + workgroup count); a step ends at the grouped weight-gradient launch (one
+per step).  Family figures are the mean durations (End - Start, the kernel trace's own clock) of those signatures'
+UNBRACKETED dispatches in the K timed replays, i.e. in the timed graph that carries no probe kernels:
+* wgrad  -- the grouped weight-gradient launch (gemm_pipe_kernel<256, 32, 4, 1, ...>);
+* ffn_up -- the FFN up-projection forward (gemm_pipe_kernel<256, 32, 3, 2, ...>, the bracketed signature only);
+* dwide  -- every other bracketed signature (the d-wide GEMM family of bench.py's `roofline`).
+Also written: every signature's launches per timed step and mean duration, and the timed steps' kernel time."""
+import argparse
+import csv
+import json
+import statistics
+
+ap = argparse.ArgumentParser()
+ap.add_argument("trace")
+ap.add_argument("out")
+ap.add_argument("--config", required=True)
+ap.add_argument("--warmup", type=int, required=True)
+ap.add_argument("--steps", type=int, required=True)
+a = ap.parse_args()
+
+WGRAD, FFNUP, PROBE = "gemm_pipe_kernel<256, 32, 4, 1,", "gemm_pipe_kernel<256, 32, 3, 2,", "probe_slot_kernel"
+
+
+def wgs(r):
+    n = 1
+    for ax in "XYZ":
+        n *= max(1, int(r[f"Grid_Size_{ax}"]) // max(1, int(r[f"Workgroup_Size_{ax}"])))
+    return n
+
+
+rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+disp = []
+step = 0
+for r in rows:
+    name = r["Kernel_Name"]
+    disp.append({"name": name, "sig": (name, wgs(r)), "ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                 "start": int(r["Start_Timestamp"]), "end": int(r["End_Timestamp"]), "step": step})
+    if WGRAD in name:
+        step += 1
+# bracketed: the probed launch of a (stamp, launch, accumulate) triple -- parsed left to right, so an unprobed
+# launch between two triples (probe, X, probe) is not taken for a probed one
+for d in disp:
+    d["bracketed"] = False
+i = 0
+while i < len(disp):
+    if (PROBE in disp[i]["name"] and i + 2 < len(disp) and PROBE not in disp[i + 1]["name"]
+            and PROBE in disp[i + 2]["name"]):
+        disp[i + 1]["bracketed"] = True
+        i += 3
+    else:
+        i += 1
+fam_sigs = {"wgrad": set(), "ffn_up": set(), "dwide": set()}
+for d in disp:
+    if d["bracketed"]:
+        n = d["name"]
+        fam_sigs["wgrad" if WGRAD in n else "ffn_up" if FFNUP in n else "dwide"].add(d["sig"])
+t0, t1 = a.warmup + 1, a.warmup + 1 + a.steps          # timed replays: steps [t0, t1)
+timed = [d for d in disp if t0 <= d["step"] < t1 and not d["bracketed"] and PROBE not in d["name"]]
+if not timed:
+    raise SystemExit("no timed steps found (check --warmup / --steps)")
+K = a.steps
+fams = {}
+for f, sigs in fam_sigs.items():
+    ds = [d["ns"] for d in timed if d["sig"] in sigs]
+    if ds:
+        fams[f] = {"avg_ns": sum(ds) / len(ds), "median_ns": statistics.median(ds), "launches_per_step": len(ds) / K,
+                   "ms_per_step": sum(ds) / K / 1e6,
+                   "signatures": sorted(f"{s[0][:110]} [{s[1]} WGs]" for s in sigs)}
+by = {}
+for d in timed:
+    by.setdefault(d["sig"], []).append(d["ns"])
+sigs = sorted(by.items(), key=lambda kv: -sum(kv[1]))
+span = (max(d["end"] for d in timed) - min(d["start"] for d in timed)) / K / 1e6
+rec = {"config": a.config, "source": a.trace, "timed_steps": K, "warmup": a.warmup,
+       "kernel_ms_per_step": sum(d["ns"] for d in timed) / K / 1e6,
+       "first_start_to_last_end_ms_per_step": span,
+       "families": fams,
+       "kernels": [{"name": s[0][:160], "workgroups": s[1], "launches_per_step": len(v) / K,
+                    "avg_us": sum(v) / len(v) / 1e3, "ms_per_step": sum(v) / K / 1e6} for s, v in sigs]}
+with open(a.out, "w") as f:
+    json.dump(rec, f, indent=1)
+print(f"{a.config}: kernel time {rec['kernel_ms_per_step']:.3f} ms/step, span {span:.3f} ms/step over {K} timed steps")
+for f, v in fams.items():
+    print(f"  {f:7s} {v['launches_per_step']:6.1f}/step  avg {v['avg_ns'] / 1e3:8.2f} us  {v['ms_per_step']:.3f} ms/step")
+for k in rec["kernels"][:40]:
+    print(f"  {k['ms_per_step']:8.3f} ms/step  {k['launches_per_step']:6.1f}/step  avg {k['avg_us']:8.1f} us  "
+          f"[{k['workgroups']}] {k['name'][:100]}")

@@ -8,6 +8,7 @@ import pytest
 import torch
 
 from nn_conformer_for_speech_recognition_amd import _lib, ops
+from tests import dropout_hash as dh
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -169,37 +170,17 @@ def test_rel_attention_mfma_matches_simt_under_dropout(attn_mode):
 
 
 # ------------------------------------------------------------------------------------ dropout masks, read back
-def _mix32(x):
-    x = x.astype(np.uint64) & 0xFFFFFFFF
-    x ^= x >> 16
-    x = (x * 0x7FEB352D) & 0xFFFFFFFF
-    x ^= x >> 15
-    x = (x * 0x846CA68B) & 0xFFFFFFFF
-    x ^= x >> 16
-    return x
-
-
-def _attn_mix(x):
-    x = x.astype(np.uint64) & 0xFFFFFFFF
-    x ^= x >> 16
-    x = ((x & 0xFFFFFF) * 0x9E3779) & 0xFFFFFFFF
-    x ^= x >> 15
-    x = ((x & 0xFFFFFF) * 0x85EBCA) & 0xFFFFFFFF
-    x ^= x >> 16
-    return x
-
-
 def _keep(B, T, H, p, seed):
     """numpy restatement of the attention-dropout keep mask (cfm_common.h attn_mix / drop_key, attn_common.h
     didx): element (b, h, i, j) keeps iff the 16-bit half (j & 1) of attn_mix(((bh T + i) T2 + j/2) + key) >= thr,
     T2 = (T rounded up to even) / 2, key = lowbias32-derived drop_key(seed, 0).  Returns (B, H, T, T) bool."""
-    key = int(_mix32(np.array([(seed & 0xFFFFFFFF) ^ int(_mix32(np.array([((seed >> 32) + 0x9E3779B9) & 0xFFFFFFFF]))[0])]))[0])
-    thr = int(np.float32(p) * np.float32(65536.0) + np.float32(0.5))
+    key = dh.drop_key(seed)
+    thr = dh.drop_thr(p)
     T2 = (T + (T & 1)) >> 1
     bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
     i = np.arange(T, dtype=np.uint64)[None, :, None]
     j = np.arange(T, dtype=np.uint64)[None, None, :]
-    hs = _attn_mix((((bh * T + i) * T2 + j // 2) + key) & 0xFFFFFFFF)
+    hs = dh.attn_mix((((bh * T + i) * T2 + j // 2) + key) & 0xFFFFFFFF)
     half = np.where(j % 2 == 0, hs & 0xFFFF, hs >> 16)
     return (half >= thr).reshape(B, H, T, T)
 

@@ -19,7 +19,9 @@ the round-4 MI355X values are quoted here and in DESIGN.md §1):
   NST (bf16, eval, 17 layers): 100 % of the 325 valid frames agree with the oracle's argmax (all have a top-2
     margin > 0.25 nats).
   fp8 (forward GEMMs e4m3, backward bf16, rel-pos, T 373): measured y 4.5 %, dx 3.7 %, worst gradient 9.1 %
-    (layer-16 linear_pos)."""
+    (layer-16 linear_pos); asserted at ~1.5x those.
+  Round 5 adds Conformer-L with relative positions (L60's arithmetic) at T 94 and at L60's T 1498, and the
+  position-free stack at the L15 length T 373, fp32 and bf16 (measured values in DESIGN.md §1)."""
 import json
 
 import pytest
@@ -70,16 +72,23 @@ STACKS = {   # name: (d, H, ffn, K, layers) -- bench.py CONFIGS
 }
 
 
-@pytest.mark.parametrize("T,lens", [(94, [94, 71])])
-@pytest.mark.parametrize("stack", sorted(STACKS))
+CASES = [   # (stack, pos_enc, T_enc, lengths): every benchmarked stack at T 94 (T_in 385); Conformer-L with
+    # relative positions (L60's arithmetic) at T 94 and at L60's own length T 1498 (B 1, 60 s); the L15 length 373
+    ("L17", "none", 94, [94, 71]), ("M16", "none", 94, [94, 71]), ("S16", "none", 94, [94, 71]),
+    ("L17", "rel", 94, [94, 71]), ("L17", "none", 373, [373, 301]), ("L17", "rel", 1498, [1498]),
+]
+
+
+@pytest.mark.parametrize("stack,pos,T,lens", CASES, ids=[f"{c[0]}-{c[1]}-T{c[2]}" for c in CASES])
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
-def test_full_depth_encoder_vs_oracle(stack, cd, T, lens):
-    """Every layer of the benchmarked stack, fwd + bwd, ragged lengths (T_in 385 -> T_enc 94)."""
+def test_full_depth_encoder_vs_oracle(stack, pos, cd, T, lens):
+    """Every layer of the benchmarked stack, fwd + bwd, ragged lengths.  The rel-pos biases' gradients (u, v: a sum
+    over every query of one head) get 3x the gradient tolerance, as in test_gpu_conformer.py."""
     d, H, ffn, K, L = STACKS[stack]
     torch.manual_seed(7)
-    ref = oc.ConformerRef(d, H, ffn, L, K, 0.0).train()
+    ref = oc.ConformerRef(d, H, ffn, L, K, 0.0, pos_enc=pos).train()
     _seed_ref(ref)
-    m = Conformer(d, H, ffn, L, K, 0.0, compute_dtype=cd)
+    m = Conformer(d, H, ffn, L, K, 0.0, pos_enc=pos, compute_dtype=cd)
     m.load_state_dict(ref.state_dict())
     m = m.to(DEV).train()
     x = torch.randn(len(lens), T, d)
@@ -94,13 +103,17 @@ def test_full_depth_encoder_vs_oracle(stack, cd, T, lens):
     ey, ex = rel_err(y.detach(), yr.detach()), rel_err(xd.grad, xr.grad)
     rp = dict(ref.named_parameters())
     eg = {n: rel_err(p.grad, rp[n].grad) for n, p in m.named_parameters() if not _bn_noise(n)}
+    eu = {n: e for n, e in eg.items() if "pos_bias" in n}
+    eg = {n: e for n, e in eg.items() if "pos_bias" not in n}
     worst = max(eg, key=eg.get)
     eb = max(rel_err(b1, b2) for (n, b1), (_, b2) in zip(m.named_buffers(), ref.named_buffers()) if "running" in n)
-    _report(f"encoder {stack} {str(cd)[6:]} T{T}", y=ey, dx=ex, worst_grad=eg[worst], worst_param=worst,
-            median_grad=sorted(eg.values())[len(eg) // 2], bn_running=eb)
+    _report(f"encoder {stack} {pos} {str(cd)[6:]} T{T}", y=ey, dx=ex, worst_grad=eg[worst], worst_param=worst,
+            median_grad=sorted(eg.values())[len(eg) // 2], bn_running=eb,
+            **({"worst_pos_bias_grad": max(eu.values())} if eu else {}))
     ty, tx, tg = TOL[cd]
     assert ey < ty and ex < tx, (ey, ex)
     assert eg[worst] < tg, (worst, eg[worst])
+    assert all(e < 3 * tg for e in eu.values()), eu
     assert eb < ty
 
 
@@ -243,5 +256,6 @@ def test_fp8_L17_vs_oracle():
     worst = max(eg, key=eg.get)
     _report("encoder L17 fp8 rel T373", y=ey, dx=ex, worst_grad=eg[worst], worst_param=worst,
             median_grad=sorted(eg.values())[len(eg) // 2])
-    assert ey < 1e-1 and ex < 1e-1, (ey, ex)
-    assert eg[worst] < 2e-1, (worst, eg[worst])
+    # ~1.5x the measured round-4 errors (y 4.5 %, dx 3.7 %, worst gradient 9.1 %): a doubling of fp8 error fails
+    assert ey < 7e-2 and ex < 6e-2, (ey, ex)
+    assert eg[worst] < 1.4e-1, (worst, eg[worst])
