@@ -283,10 +283,17 @@ class KernelProbe:
         return self._mean(self.slot_bytes)
 
 
+def lib_md5():
+    import hashlib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.md5(f.read()).hexdigest()
+
+
 def trace_family_ms(summary_file, config, family):
     """The rocprofv3 kernel-trace figure of a kernel family, read from a committed summary
     (profiles/summarize_trace.py output: per (kernel, grid) rows of launches per step and mean duration) of a
-    bench.py run of the same config: (mean ms per launch, launches per step, summary path) or None."""
+    bench.py run of the same config: (mean ms per launch, launches per step, summary path, same build) or None;
+    `same build`: the summary's libcfm.so md5 is the md5 of the library this run loaded."""
     path = os.path.join(REPO, summary_file)
     if not os.path.exists(path):
         return None
@@ -297,7 +304,7 @@ def trace_family_ms(summary_file, config, family):
     fam = rec.get("families", {}).get(family)
     if not fam:
         return None
-    return fam["avg_ns"] / 1e6, fam["launches_per_step"], summary_file
+    return fam["avg_ns"] / 1e6, fam["launches_per_step"], summary_file, rec.get("lib_md5") == lib_md5()
 
 
 def time_ctc_head(h, reps=20):
@@ -782,7 +789,7 @@ def main():
     where = ("over --steps replays of a second capture of the same step that carries the probe kernels, run right "
              "after the timed region (the timed graph carries no probes)" if h.probe_graph is not None else
              "in the timed region" + (" (graph replays)" if h.graph is not None else ""))
-    timing = ("avg_launch_ms: s_memrealtime of a one-lane stamp kernel right before each matching launch to that of "
+    timing = ("avg_launch_ms_live: s_memrealtime of a one-lane stamp kernel right before each matching launch to that of "
               "one right after it, minus the same interval of empty stamp pairs (empty_pair_ms) -- the time the "
               "launch adds to the serial stream (dispatch ramp + execution + end-of-kernel completion), as "
               "rocprofv3's kernel trace counts it; avg_launch_ms_busy: first-workgroup start to last-workgroup end; "
@@ -807,11 +814,16 @@ def main():
 
     def roofline_entry(kernel, flops, nbytes, pr, pmc_file, family):
         """bound from the kernel's arithmetic intensity against the machine balance (peak FLOP/s over peak
-        HBM B/s); `achieved`/`peak`/`frac` in that bound's unit, both fractions reported.  Duration: the probe's
-        dispatch-inclusive mean (KernelProbe); its busy mean and the rocprofv3 kernel-trace mean of the same
-        family (a committed profiles/r05 summary of a bench.py run of this config) are reported beside it."""
-        ms, n_launch = pr.mean_ms(incl=True)
+        HBM B/s); `achieved`/`peak`/`frac` in that bound's unit, both fractions reported.  Duration per launch, three
+        ways: live probes (dispatch-inclusive and busy, KernelProbe) and the rocprofv3 kernel-trace mean of the same
+        family from a committed profiles/r05 summary of a bench.py run of this config.  `frac` uses the trace's mean
+        when that summary was taken with THIS libcfm.so build (md5), so it reproduces from profiles/; otherwise the
+        live dispatch-inclusive mean."""
+        ms_live, n_launch = pr.mean_ms(incl=True)
         ms_busy, _ = pr.mean_ms()
+        tr = trace_family_ms(f"profiles/r05/trace_{cfg_key}.json", cfg_key, family)
+        use_trace = tr is not None and tr[3]
+        ms = tr[0] if use_trace else ms_live
         intensity = flops / nbytes
         balance = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
         tflops = flops / (ms * 1e-3) / 1e12
@@ -823,15 +835,18 @@ def main():
              "frac": round(gbs / PEAK_HBM_GBS if hbm else tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
              "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
              "intensity_flop_per_byte": round(intensity, 1), "machine_balance_flop_per_byte": round(balance, 1),
-             "avg_launch_ms": round(ms, 4), "avg_launch_ms_busy": round(ms_busy, 4),
+             "avg_launch_ms": round(ms, 4),
+             "duration_basis": "rocprofv3 kernel trace of this build (avg_launch_ms_trace)" if use_trace else
+                               "live dispatch-inclusive probe (avg_launch_ms_live)",
+             "avg_launch_ms_live": round(ms_live, 4), "avg_launch_ms_busy": round(ms_busy, 4),
              "empty_pair_ms": None if pr.empty_pair_ms() is None else round(pr.empty_pair_ms(), 4),
              "launches_timed": n_launch,
              "timing": timing, "flops_per_launch": flops, "algorithmic_bytes": nbytes}
-        tr = trace_family_ms(f"profiles/r05/trace_{cfg_key}.json", cfg_key, family)
         if tr is not None:
             e["avg_launch_ms_trace"] = round(tr[0], 4)
             e["trace_launches_per_step"] = tr[1]
-            e["frac_by_trace"] = round((gbs / PEAK_HBM_GBS if hbm else tflops / PEAK_BF16_TFLOPS) * ms / tr[0], 4)
+            e["trace_same_build"] = tr[3]
+            e["live_over_trace"] = round(ms_live / tr[0], 4)
             e["trace_source"] = tr[2] + " (rocprofv3 --kernel-trace of a bench.py run of this config: the family's "\
                                         "mean dispatch duration over the timed graph replays)"
         for rnd in ("r05", "r04", "r03", "r02"):

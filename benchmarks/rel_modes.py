@@ -1,6 +1,6 @@
 """Rel-pos attention at the L60 shape (B 8, T 1498, H 8, dk 64, dropout 0.1): forward and backward under
 cfm_attn_set_mode values (interleaved rounds, HIP-event medians).
-    python benchmarks/rel_modes.py [--modes 0,32] [--reps 5]"""
+    python benchmarks/rel_modes.py [--modes 0] [--reps 5]"""
 import argparse
 import json
 import os
@@ -27,7 +27,7 @@ def timeit(fn, n=10, warm=2):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="0,32")
+    ap.add_argument("--modes", default="0")
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     modes = [int(m) for m in a.modes.split(",")]

@@ -175,6 +175,11 @@ typedef struct cfm_gemm_desc {
      view of the packed mels, cfm_ffold_*).  0: lda >= (a_kmajor ? K : M) and ldb >= (b_kmajor ? K : N) are
      enforced (CFM_ERR_SHAPE), so a wrongly transposed view fails instead of reading overlapping rows. */
   int allow_overlap;
+  /* dtype_ab == CFM_FP8 with MX operands (both or neither): the e8m0 block scales of A and B as cfm_quant_mx
+     writes them ([M][K/32] / [N][K/32] bytes, one per 32 consecutive K elements of a row); the block-scaled MFMA
+     applies them per 32-element run (alpha_*_dev must be NULL).  K % 128 == 0, K <= 2048. */
+  const uint8_t* mx_a;
+  const uint8_t* mx_b;
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 /* Per-tensor fp8 (e4m3fn) quantisation for the fp8 GEMM path (configs[4]; no reference counterpart -- the
@@ -200,6 +205,28 @@ int cfm_quant_fp8_batch(const cfm_q8_task* tasks, int ntasks, long nblocks, int 
                         void* stream);
 /* y = float(x) * inv_scale (inv_scale NULL: 1) -- the dequantised view, for tests. */
 int cfm_dequant_fp8(const void* x, long n, const float* inv_scale, float* y, void* stream);
+/* MX e4m3 quantisation (OCP microscaling; configs[4]'s fp8 path, no reference counterpart): every 32
+   consecutive elements of a row share one e8m0 scale byte s = 127 - k, k the largest integer with
+   amax(block) * 2^k <= 448 (0 for an all-zero block), and y = e4m3(x * 2^k) (round to nearest even).
+   x: rows x K (row stride ldx elements, fp32 or bf16, 16-B aligned), K % 32 == 0; y: rows x K bytes
+   (row stride K); s: rows x K/32 bytes (row-major).  One pass, no tensor-wide amax: the operand form of
+   cfm_gemm_desc.mx_a / mx_b. */
+int cfm_quant_mx(const void* x, int dtype_x, long rows, int K, long ldx, void* y, uint8_t* s, void* stream);
+/* Batched cfm_quant_mx over a device table (the per-step MX copies of the forward GEMM weights): ONE launch;
+   blk0 = prefix sum of cfm_quant_mx_batch_blocks(rows, K); rows of each tensor contiguous (ldx = K). */
+typedef struct {
+  const void* x;      /* fp32 or bf16 (dtype_x of the call), 16-B aligned */
+  void* y;            /* e4m3 bytes, 8-B aligned */
+  uint8_t* s;         /* e8m0 block scales, rows x K/32 */
+  long rows;
+  int K;
+  int pad;
+  long blk0;
+} cfm_mx_task;
+long cfm_quant_mx_batch_blocks(long rows, int K);
+int cfm_quant_mx_batch(const cfm_mx_task* tasks, int ntasks, long nblocks, int dtype_x, void* stream);
+/* y[i] = e4m3(x[i]) * 2^(s[i / 32] - 127) -- the dequantised view of an MX tensor (n % 32 == 0), for tests. */
+int cfm_dequant_mx(const void* x, const uint8_t* s, long n, float* y, void* stream);
 /* Grouped weight gradients: every dW_i (N_i x K_i, fp32) = dY_i^T X_i over the same M tokens (dY_i (M x N_i),
    X_i (M x K_i) bf16 row-major) and optionally db_i = sum_rows dY_i, in ONE launch of 256x128 tiles that each
    run the whole token reduction (no split-K).  The caller fills a HOST table (cfm_wgrad_group_fill, one
@@ -224,6 +251,24 @@ int cfm_colreduce_group(const void* dev_table, int ntasks, long total_blocks, vo
 /* the same launch with a timing slot (as cfm_gemm_desc.probe: first-workgroup start / last-workgroup end) */
 int cfm_wgrad_group_probed(const void* dev_table, int ntasks, long total_tiles, unsigned long long* probe,
                            void* stream);
+/* Planned grouped weight gradients (the encoder backward's default): cfm_wgrad_group_plan packs the tasks'
+   tiles (task_tiles[i] = cfm_wgrad_group_tiles(N_i, K_i)) into rounds of one tile per CU per XCD (nxcd XCDs of
+   cus CUs) made of whole tasks -- the tiles sharing a dY or X column slice co-resident on one XCD, which then
+   streams the slice through its L2 once -- and splits the tiles of the ragged last round over K slices
+   (task_split[i] > 1), so that round fills the chip.  It writes one schedule word per workgroup (sched, capacity
+   cap) and returns the grid size (< 0: error).  Fill the table with cfm_wgrad_group_fill_split (split = the
+   plan's task_split[i]; ws = cfm_wgrad_group_ws_floats(N, K, split) floats of fp32 workspace for a split task;
+   red0 = running sum of cfm_wgrad_group_red_blocks), copy table and schedule to the device and launch
+   cfm_wgrad_group_sched (red_blocks = the total): the GEMM launch, then the deterministic slab reduction of the
+   split tasks into dw / db.  probe: optional timing slot (as cfm_wgrad_group_probed). */
+long cfm_wgrad_group_plan(const long* task_tiles, int ntasks, int nxcd, int cus, unsigned* sched, long cap,
+                          int* task_split);
+long cfm_wgrad_group_ws_floats(int N, int K, int split);
+long cfm_wgrad_group_red_blocks(int N, int K, int split);
+int cfm_wgrad_group_fill_split(void* host_table, int i, const void* dy, const void* x, float* dw, float* db, int M,
+                               int N, int K, int split, float* ws, long red0);
+int cfm_wgrad_group_sched(const void* dev_table, int ntasks, const unsigned* dev_sched, long grid, long red_blocks,
+                          unsigned long long* probe, void* stream);
 /* kernel-selection switch for A/B measurements: bit 0 = 256-row register-staged tiles allowed,
    bit 1 = LDS-DMA pipelined kernel allowed, bit 3 = timing experiment (pipelined kernels skip their
    stores), bits 4-6 = pipelined variant (0 auto, 1 256x128/BK64, 2 256x128/BK32 two per CU,
@@ -341,7 +386,10 @@ int cfm_glu_dwconv_bwd_bn(const void* dz, int dtype_dz, const float* y, const fl
  * (saved for backward); lengths: (B) int32 valid keys.  pos (rel only): (2T-1, H*dk) projected
  * table; pos_u / pos_v: (H*dk) fp32.  dtype: CFM_BF16 (MFMA) or CFM_F32. */
 /* A/B switch (measurement only): bit 0 forces the tiled attention kernels instead of the
-   whole-head ones (T <= 384: one workgroup per (b, h) with K/V staged once in LDS). */
+   whole-head ones (T <= 384: one workgroup per (b, h) with K/V staged once in LDS); bits 1-2 timing
+   experiments of the whole-head forward (value 2: staging only, 4: no output stores -- outputs invalid);
+   bit 4 runs bf16 relative-position attention on the SIMT kernels (parity cross-check); bit 6 keeps the
+   rel-pos kernels' zero-filling (non-clamped) tile loads. */
 int cfm_attn_set_mode(int mode);
 int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
                  const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,

@@ -44,6 +44,7 @@ class GemmDesc(ctypes.Structure):
         ("rowdot_with", c_void_p), ("rowdot_out", c_void_p), ("rowdot_T", c_int),
         ("alpha_a_dev", c_void_p), ("alpha_b_dev", c_void_p),
         ("allow_overlap", c_int),
+        ("mx_a", c_void_p), ("mx_b", c_void_p),
     ]
 
 
@@ -75,12 +76,22 @@ _SIGS = {
     "cfm_quant_fp8_batch_blocks": (c_long, [c_long]),
     "cfm_quant_fp8_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_void_p]),
     "cfm_dequant_fp8": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
+    "cfm_quant_mx": (c_int, [c_void_p, c_int, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p]),
+    "cfm_quant_mx_batch_blocks": (c_long, [c_long, c_int]),
+    "cfm_quant_mx_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p]),
+    "cfm_dequant_mx": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
     "cfm_wgrad_group_task_bytes": (c_size_t, []),
     "cfm_wgrad_group_tiles": (c_long, [c_int, c_int]),
     "cfm_wgrad_group_fill": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                      c_long]),
     "cfm_wgrad_group": (c_int, [c_void_p, c_int, c_long, c_void_p]),
     "cfm_wgrad_group_probed": (c_int, [c_void_p, c_int, c_long, c_void_p, c_void_p]),
+    "cfm_wgrad_group_plan": (c_long, [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
+    "cfm_wgrad_group_ws_floats": (c_long, [c_int, c_int, c_int]),
+    "cfm_wgrad_group_red_blocks": (c_long, [c_int, c_int, c_int]),
+    "cfm_wgrad_group_fill_split": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                           c_int, c_int, c_void_p, c_long]),
+    "cfm_wgrad_group_sched": (c_int, [c_void_p, c_int, c_void_p, c_long, c_long, c_void_p, c_void_p]),
     "cfm_colreduce_group_task_bytes": (c_size_t, []),
     "cfm_colreduce_group_blocks": (c_long, [c_long]),
     "cfm_colreduce_group_fill": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_long, c_void_p, c_void_p, c_int,

@@ -18,6 +18,7 @@ activations use the compute dtype (bf16 by default, fp32 for the parity mode).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -105,6 +106,8 @@ class _Cfg:
 _WIDX = (2, 4, 8, 10, 14, 20, 24, 26)
 # weights of the forward GEMMs that run on fp8 in fp8 mode: FFN up/down (both FFNs), QKV, out-projection
 _FP8_W = (2, 4, 8, 10, 24, 26)
+# fp8 scaling: MX block scales (default) or per-tensor current scaling (CFM_FP8_SCALING=tensor, A/B)
+FP8_MX = os.environ.get("CFM_FP8_SCALING", "mx") != "tensor"
 
 
 _SIDE_STREAMS = {}
@@ -184,11 +187,15 @@ def _wt(cfg, i):
 
 def _fp8_linear(x, cfg, i, **kw):
     """Forward GEMM with fp8 (e4m3fn) operands when the layer runs the fp8 path (BASELINE.json configs[4]):
-    x quantised per tensor on the device, weight i from the per-step fp8 shadow; else None.  The backward
-    keeps the bf16 operands (x, the bf16 weight shadow)."""
+    x quantised on the device -- MX block scales (one e8m0 per 32 K-elements, one pass, applied inside the
+    block-scaled MFMA), or per tensor with CFM_FP8_SCALING=tensor (A/B) -- weight i from the per-step fp8 shadow;
+    else None.  The backward keeps the bf16 operands (x, the bf16 weight shadow)."""
     if not cfg.shadow8 or i not in cfg.shadow8 or x.shape[1] % 128:
         return None
     wq, sw = cfg.shadow8[i]
+    if FP8_MX:
+        xq, sx = ops.quant_mx(x)
+        return ops.linear(xq, wq, x_mx=sx, w_mx=sw, **kw)
     xq, sx = ops.quant_fp8(x)
     return ops.linear(xq, wq, x_scale=sx, w_scale=sw, **kw)
 
@@ -567,7 +574,7 @@ class Conformer(nn.Module):
         if getattr(self, "_q8", None) is None or self._q8[0] != key:
             srcs8 = [layer.params()[i].detach().view(layer.params()[i].shape[0], -1)
                      for layer in self.conformer_layers for i in _FP8_W]
-            self._q8 = (key, ops.Quant8Batch(srcs8))
+            self._q8 = (key, ops.QuantMXBatch(srcs8) if FP8_MX else ops.Quant8Batch(srcs8))
         outs = self._q8[1].refresh()
         nw = len(_FP8_W)
         out = []

@@ -171,83 +171,6 @@ __device__ __forceinline__ BandRows band_rows_q(const bf16* ring, int kt, int wv
   return br;
 }
 
-// ------------------------------------------------------------------------------------ forward
-// grid (ceil(T/128), H, B), 4 waves x 32 queries; K/V tiles of 64 keys double-buffered, band ring.
-template <bool VEC>
-__global__ __launch_bounds__(256) void attn_rel_fwd_kernel(AttnM p, RelP rp, bf16* __restrict__ o,
-                                                           float* __restrict__ lse) {
-  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
-  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
-  const float dkeep = drop_keep_scale(dthr);
-  __shared__ __attribute__((aligned(16))) bf16 skv[2 * 2 * TILE * KS];    // [buf][K,V][64][72]   36 KiB
-  __shared__ __attribute__((aligned(16))) bf16 sring[RING * TILE * KS];   // band ring            36 KiB
-  __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SS];          // per-wave skew stage  50 KiB
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int Q0 = blockIdx.x * 128, q0 = Q0 + wv * 32;
-  const int qi = q0 + (lane & 31);
-  const int len = p.len[b];
-  const int rbase = p.T - 1 - Q0 - 127;          // relative row of band row 0 at key tile 0
-  bf16x8 qu[4], qv[4];
-  load_q_uv(p, rp, b, h, qi, qu, qv, lane);
-  float* st = sst + wv * 32 * SS;
-  f32x16 o0 = (f32x16){0}, o1 = (f32x16){0};
-  float m = -INFINITY, l = 0.f;
-  const float c = p.scale * LOG2E;
-  const int nkt = (len + TILE - 1) / TILE;
-  uint4 rk[2], rv[2], rq[2];
-  const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
-  if (nkt > 0) {
-    tile_load<VEC>(p, b, 0, kcol, rk, tid);
-    tile_load<VEC>(p, b, 0, vcol, rv, tid);
-    tile_store(skv, rk, tid);
-    tile_store(skv + TILE * KS, rv, tid);
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
-      ring_chunk_store(sring + ch * TILE * KS, rq, tid);
-    }
-    __syncthreads();
-  }
-  wait_prologue_loads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const bf16* sK = skv + (kt & 1) * 2 * TILE * KS;
-    const bf16* sV = sK + TILE * KS;
-    if (kt + 1 < nkt) {
-      tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
-      tile_load<VEC>(p, b, (kt + 1) * TILE, vcol, rv, tid);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
-    }
-    f32x16 s0, s1;
-    scores_qlanes(sK, band_rows_q(sring, kt, wv), qu, qv, st, s0, s1, lane);
-    // the non-rel kernels' online-softmax step (attn_common.h): masking only on the last key tile, the running max
-    // over raw scores (c > 0), exp2 as one FMA + v_exp, then the same dropout hash as before
-    softmax_tile(p, s0, s1, o0, o1, m, l, c, kt * TILE, len, kt == nkt - 1, b, h, qi, hh, dthr, dkeep, dkey);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
-        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 0, lane), pf, o0, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sV, 32 * t + 16 * s, 32, lane), pf, o1, 0, 0, 0);
-      }
-    }
-    if (kt + 1 < nkt) {
-      bf16* nK = skv + ((kt + 1) & 1) * 2 * TILE * KS;
-      tile_store(nK, rk, tid);
-      tile_store(nK + TILE * KS, rv, tid);
-      ring_chunk_store(sring + ((kt + 3) & (RING - 1)) * TILE * KS, rq, tid);
-    }
-    __syncthreads();
-  }
-  const float inv = 1.f / l;
-  if (q0 < p.T)
-    store_transposed(st, o0, o1, inv, o + (long)b * p.T * p.HD + h * p.dk, p.HD, q0, min(32, p.T - q0), p.dk, lane);
-  if (hh == 0 && qi < p.T) lse[((long)b * p.H + h) * p.T + qi] = (m + __log2f(l)) * LN2;
-}
-
 // ------------------------------------------------------------------------------------ band bias column
 // (q + v) . p_r = (q + u) . p_r + c_r with c_r = (v - u) . p_r: the two-waves kernels form the band product from
 // the (q + u) operand they already hold and add c_r (fp32, per relative row) -- no (q + v) operand in registers
@@ -286,7 +209,8 @@ __device__ __forceinline__ void add_band_c(f32x16& x, const float* cb, int hh) {
 }
 
 // ------------------------------------------------------------------------------------ forward, two waves per SIMD
-// The same tile walk as attn_rel_fwd_kernel in <= 80 KiB of LDS and <= 256 registers, so two workgroups share a
+// grid (ceil(T/128), H, B), 4 waves x 32 queries; K/V tiles of 64 keys, band ring.  <= 80 KiB of LDS and <= 256
+// registers, so two workgroups share a
 // CU (two waves per SIMD: one wave's softmax VALU issues beside the other's MFMAs, and the VALU issue cost per
 // instruction halves -- one wave alone on a SIMD pays 4 cycles per v_fma, two pay 2 each).  LDS: one K/V tile
 // (18 KiB, the next tile prefetched into registers and stored between two barriers), a ring of 3 band chunks
@@ -415,156 +339,9 @@ __global__ __launch_bounds__(256, 2) void attn_rel_fwd2_kernel(AttnM p, RelP rp,
 }
 
 // ------------------------------------------------------------------------------------ dQ (+ du, dv partials)
-// grid (ceil(T/128), H, B).  part: (B * 4*gridDim.x, 2*H*dk) fp32 -- row (b, 32-query block): per-column
-// sums over the block's queries of scale * sum_j dS k_j (u half) and scale * sum_j dS p_r (v half).
-template <bool VEC>
-__global__ __launch_bounds__(256) void attn_rel_bwd_dq_kernel(AttnM p, RelP rp, const bf16* __restrict__ dout,
-                                                              const float* __restrict__ lse,
-                                                              const float* __restrict__ Dg, bf16* __restrict__ dqkv,
-                                                              float* __restrict__ part) {
-  if (p.drop_p > 0.f) p.seed = salted_seed(p.seed, p.salt);
-  const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
-  const float dkeep = drop_keep_scale(dthr);
-  __shared__ __attribute__((aligned(16))) bf16 skv[2 * 2 * TILE * KS];
-  __shared__ __attribute__((aligned(16))) bf16 sring[RING * TILE * KS];
-  __shared__ __attribute__((aligned(16))) float sst[4 * 32 * SS];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, ii = lane & 31;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int Q0 = blockIdx.x * 128, q0 = Q0 + wv * 32;
-  const int qi = q0 + ii;
-  const int len = p.len[b];
-  const int rbase = p.T - 1 - Q0 - 127;
-  bf16x8 qu[4], qv[4], gf[4];
-  load_q_uv(p, rp, b, h, qi, qu, qv, lane);
-  load_bfrags(p, dout + (long)b * p.T * p.HD + h * p.dk, p.HD, qi, p.T, gf, lane);
-  const bool qvalid = qi < p.T;
-  const float L2 = qvalid ? lse[((long)b * p.H + h) * p.T + qi] * LOG2E : INFINITY;   // +inf: P = 0 past T
-  const float Dq = qvalid ? Dg[((long)b * p.H + h) * p.T + qi] : 0.f;
-  const float c = p.scale * LOG2E;
-  float* st = sst + wv * 32 * SS;
-  float* col = st + ii * SS;
-  f32x16 a0 = (f32x16){0}, a1 = (f32x16){0}, e0 = (f32x16){0}, e1 = (f32x16){0};   // K-term, band term
-  const int nkt = (len + TILE - 1) / TILE;
-  uint4 rk[2], rv[2], rq[2];
-  const int kcol = p.HD + h * p.dk, vcol = 2 * p.HD + h * p.dk;
-  if (nkt > 0) {
-    tile_load<VEC>(p, b, 0, kcol, rk, tid);
-    tile_load<VEC>(p, b, 0, vcol, rv, tid);
-    tile_store(skv, rk, tid);
-    tile_store(skv + TILE * KS, rv, tid);
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
-      ring_chunk_store(sring + ch * TILE * KS, rq, tid);
-    }
-    __syncthreads();
-  }
-  wait_prologue_loads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const bf16* sK = skv + (kt & 1) * 2 * TILE * KS;
-    const bf16* sV = sK + TILE * KS;
-    if (kt + 1 < nkt) {
-      tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
-      tile_load<VEC>(p, b, (kt + 1) * TILE, vcol, rv, tid);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
-    }
-    const BandRows br = band_rows_q(sring, kt, wv);
-    f32x16 s0, s1;
-    scores_qlanes(sK, br, qu, qv, st, s0, s1, lane);
-    f32x16 d0 = (f32x16){0}, d1 = (f32x16){0};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 0, 16 * s, lane), gf[s], d0, 0, 0, 0);
-      d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32, 16 * s, lane), gf[s], d1, 0, 0, 0);
-    }
-    if (p.drop_p > 0.f) {
-      const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kt * TILE) >> 1);   // even: 32-bit pair indices
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int k0 = acc_row(r, hh);
-        float m0, m1, m2, m3;
-        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1), m0, m1);
-        dropout_pair32(dthr, dkeep, dkey, rowj + (k0 >> 1) + 16, m2, m3);
-        d0[r] *= m0; d0[r + 1] *= m1;
-        d1[r] *= m2; d1[r + 1] *= m3;
-      }
-    }
-    // P = 2^(c s - lse log2 e) as one FMA + v_exp; key masking only on the utterance's last tile (uniform)
-    const bool tail = kt == nkt - 1 && kt * TILE + TILE > len;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float a0 = __builtin_fmaf(s0[r], c, -L2), a1 = __builtin_fmaf(s1[r], c, -L2);
-      if (tail) {
-        const int k0 = kt * TILE + acc_row(r, hh);
-        a0 = k0 < len ? a0 : -INFINITY;
-        a1 = k0 + 32 < len ? a1 : -INFINITY;
-      }
-      s0[r] = fast_exp2(a0) * (d0[r] - Dq);
-      s1[r] = fast_exp2(a1) * (d1[r] - Dq);
-    }
-    // K-term: dQ^T[d][q] += sum_key K[key][d] dS^T[key][q]
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = acc2frag(t == 0 ? s0 : s1, s);
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 0, lane), pf, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sK, 32 * t + 16 * s, 32, lane), pf, a1, 0, 0, 0);
-      }
-    }
-    // band term: dS^T scattered to band coordinates stage[i][j - i + 31] (zero elsewhere), then
-    // dQ^T[d][q] += sum_r' P_band[r'][d] dS_band^T[r'][q]
-#pragma unroll
-    for (int g = 0; g < 12; ++g) *reinterpret_cast<float4*>(col + 48 * hh + 4 * g) = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int jj = acc_row(r, hh);
-      col[jj - ii + 31] = s0[r];
-      col[jj + 32 - ii + 31] = s1[r];
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const float4 lo = *reinterpret_cast<const float4*>(col + 16 * s + 4 * hh);
-      const float4 hi = *reinterpret_cast<const float4*>(col + 16 * s + 8 + 4 * hh);
-      bf16x8 bfr;
-      bfr[0] = (bf16)lo.x; bfr[1] = (bf16)lo.y; bfr[2] = (bf16)lo.z; bfr[3] = (bf16)lo.w;
-      bfr[4] = (bf16)hi.x; bfr[5] = (bf16)hi.y; bfr[6] = (bf16)hi.z; bfr[7] = (bf16)hi.w;
-      const bf16* blk = br.blk[s >> 1];
-      e0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(blk, 16 * (s & 1), 0, lane), bfr, e0, 0, 0, 0);
-      e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(blk, 16 * (s & 1), 32, lane), bfr, e1, 0, 0, 0);
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (kt + 1 < nkt) {
-      bf16* nK = skv + ((kt + 1) & 1) * 2 * TILE * KS;
-      tile_store(nK, rk, tid);
-      tile_store(nK + TILE * KS, rv, tid);
-      ring_chunk_store(sring + ((kt + 3) & (RING - 1)) * TILE * KS, rq, tid);
-    }
-    __syncthreads();
-  }
-  // per-wave column sums (queries) of both terms -> du / dv partial rows (zeros for blocks past T)
-  const float su = wave_rowsum(st, a0, a1, lane) * p.scale;
-  const float sv = wave_rowsum(st, e0, e1, lane) * p.scale;
-  const long prow = (long)b * (4 * gridDim.x) + blockIdx.x * 4 + wv;
-  if (lane < p.dk) {
-    part[prow * 2 * p.HD + h * p.dk + lane] = su;
-    part[prow * 2 * p.HD + p.HD + h * p.dk + lane] = sv;
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    a0[r] += e0[r];
-    a1[r] += e1[r];
-  }
-  if (q0 < p.T)
-    store_transposed(st, a0, a1, p.scale, dqkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, q0, min(32, p.T - q0),
-                     p.dk, lane);
-}
-
-// ------------------------------------------------------------------------------------ dQ, two waves per SIMD
-// attn_rel_bwd_dq_kernel's work in <= 80 KiB of LDS and <= 256 registers (two workgroups per CU): one K/V tile
+// grid (ceil(T/128), H, B).  part: (B * 4*gridDim.x, 2*H*dk) fp32 -- row (b, 32-query block): per-column sums over
+// the block's queries of scale * sum_j dS k_j (u half) and scale * sum_j dS p_r (v half).
+// Two waves per SIMD: <= 80 KiB of LDS and <= 256 registers (two workgroups per CU): one K/V tile
 // (the next one loaded between two barriers: a register prefetch across the tile spilled, the partner workgroup
 // covers the load), a ring of 3 band chunks, and per wave one 64-row f32 skew
 // stage (as attn_rel_fwd2_kernel) whose bytes also hold the bf16 band-coordinate image of dS^T
@@ -1179,13 +956,8 @@ int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len
   const AttnM p = make_attnm(qkv, qkv, len, B, T, H, dk, drop_p, seed);
   const RelP rp = make_relp(pos, pu, pv, p.dk);
   const dim3 grid(cdiv(p.T, 128), p.H, p.B);
-  if (g_rel_mode & 32) {   // A/B: the one-wave-per-SIMD forward
-    if (rel_vec(p, rp)) hipLaunchKernelGGL(attn_rel_fwd_kernel<true>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
-    else hipLaunchKernelGGL(attn_rel_fwd_kernel<false>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
-  } else {
-    if (rel_vec(p, rp)) hipLaunchKernelGGL(attn_rel_fwd2_kernel<true>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
-    else hipLaunchKernelGGL(attn_rel_fwd2_kernel<false>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
-  }
+  if (rel_vec(p, rp)) hipLaunchKernelGGL(attn_rel_fwd2_kernel<true>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
+  else hipLaunchKernelGGL(attn_rel_fwd2_kernel<false>, grid, dim3(256), 0, s, p, rp, (bf16*)o, lse);
   return check_launch("cfm_attn_fwd(rel)");
 }
 
@@ -1204,21 +976,13 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
   if (rel_vec(p, rp)) {
     hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                        (bf16*)dqkv, dsbuf, ldS);
-    if (g_rel_mode & 32)
-      hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                         (bf16*)dqkv, part);
-    else
-      hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                         (bf16*)dqkv, part);
+    hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                       (bf16*)dqkv, part);
   } else {
     hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                        (bf16*)dqkv, dsbuf, ldS);
-    if (g_rel_mode & 32)
-      hipLaunchKernelGGL(attn_rel_bwd_dq_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                         (bf16*)dqkv, part);
-    else
-      hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                         (bf16*)dqkv, part);
+    hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                       (bf16*)dqkv, part);
   }
   const size_t ds_bytes = ((size_t)p.B * p.H * p.T * ldS * sizeof(bf16) + 255) & ~(size_t)255;
   float* dpos_part = reinterpret_cast<float*>(reinterpret_cast<char*>(dsbuf) + ds_bytes);

@@ -155,7 +155,112 @@ int grid_for(long n) {
   return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
 }
 
+// ---------------------------------------------------------------- MX (OCP microscaling) e4m3
+// Every 32 consecutive elements of a row share one e8m0 scale byte s = 127 - k, k the largest integer with
+// amax(block) * 2^k <= 448 (fp8_scale's rule per block; 0 for an all-zero block), y = e4m3(x * 2^k): the block-scaled
+// MFMA (v_mfma_scale_f32_32x32x64_f8f6f4) multiplies each 32-element product run by 2^(s_a - 127) 2^(s_b - 127).
+// One pass over x (no tensor-wide amax): a thread converts 8 elements, the 4 lanes of a block exchange their maxima
+// by two xor shuffles (lanes 4j .. 4j+3 hold consecutive 8-element chunks of one block).
+__device__ __forceinline__ int mx_k(float a) {
+  if (!(a > 0.f) || !(a < INFINITY)) return 0;
+  int e;
+  const float m = 2.f * frexpf(a, &e);          // a = m * 2^(e-1), m in [1, 2)
+  const int k = (m <= 1.75f ? 8 : 7) - (e - 1);
+  return k < 126 ? (k > -126 ? k : -126) : 126;
+}
+
+__device__ __forceinline__ void mx_chunk(const float (&v)[8], uint8_t* y, uint8_t* s, bool lead) {
+  float m = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+  m = fmaxf(m, __shfl_xor(m, 1, 64));
+  m = fmaxf(m, __shfl_xor(m, 2, 64));
+  const int k = mx_k(m);
+  const float sc = ldexpf(1.f, k);
+  int lo = 0, hi = 0;
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * sc, v[1] * sc, lo, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * sc, v[3] * sc, lo, true);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * sc, v[5] * sc, hi, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * sc, v[7] * sc, hi, true);
+  *reinterpret_cast<uint2*>(y) = make_uint2((unsigned)lo, (unsigned)hi);
+  if (lead) *s = (uint8_t)(127 - k);
+}
+
+// chunks [j * 256 + tid, n8) step nb * 256 of a rows x K tensor (K % 32 == 0: the chunk count is a multiple of 4
+// and a block's 4 chunks sit in one aligned lane quad, so every quad runs the loop together)
+__device__ __forceinline__ void mx_rows(const void* x, int dt, long rows, int K, long ldx, uint8_t* y, uint8_t* s,
+                                        long j, long nb) {
+  const int c8n = K / 8;
+  const long n8 = rows * c8n;
+  for (long i = j * 256 + threadIdx.x; i < n8; i += nb * 256) {
+    const long row = i / c8n;
+    const int c = (int)(i - row * c8n);
+    float v[8];
+    ld8_dyn(x, dt, row * ldx + 8L * c, v);
+    mx_chunk(v, y + row * K + 8L * c, s + row * (K / 32) + c / 4, (c & 3) == 0);
+  }
+}
+
+__global__ __launch_bounds__(256) void quant_mx_kernel(const void* __restrict__ x, int dt, long rows, int K, long ldx,
+                                                       uint8_t* __restrict__ y, uint8_t* __restrict__ s) {
+  mx_rows(x, dt, rows, K, ldx, y, s, blockIdx.x, gridDim.x);
+}
+
+__host__ __device__ inline long mx_blocks(long rows, int K) {
+  const long b = (rows * (K / 8) + 255) / 256;
+  return b > 256 ? 256 : (b < 1 ? 1 : b);
+}
+
+__device__ __forceinline__ int mx_task_of(const cfm_mx_task* t, int n, long blk) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t[mid].blk0 <= blk) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void quant_mx_batch_kernel(const cfm_mx_task* __restrict__ t, int nt, int dt) {
+  const long blk = blockIdx.x;
+  const cfm_mx_task q = t[mx_task_of(t, nt, blk)];
+  mx_rows(q.x, dt, q.rows, q.K, q.K, reinterpret_cast<uint8_t*>(q.y), q.s, blk - q.blk0, mx_blocks(q.rows, q.K));
+}
+
+// e4m3 x e8m0 block scales -> f32 (tests / dequantised views): y = e4m3(x) * 2^(s - 127)
+__global__ __launch_bounds__(256) void dequant_mx_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ s,
+                                                         long n, float* __restrict__ y) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    y[i] = ldexpf(__builtin_amdgcn_cvt_f32_fp8((int)x[i], 0), (int)s[i / 32] - 127);
+}
+
 }  // namespace
+
+CFM_EXPORT int cfm_quant_mx(const void* x, int dtx, long rows, int K, long ldx, void* y, uint8_t* s, void* stream) {
+  CFM_REQUIRE(x && y && s && rows > 0 && K > 0, CFM_ERR_ARG, "null pointer / empty tensor");
+  CFM_REQUIRE(dtx == CFM_F32 || dtx == CFM_BF16, CFM_ERR_DTYPE, "x must be fp32 or bf16");
+  CFM_REQUIRE(K % 32 == 0 && ldx >= K && ldx % 8 == 0, CFM_ERR_SHAPE, "K % 32 == 0, ldx >= K, ldx % 8 == 0");
+  CFM_REQUIRE((uintptr_t)x % 16 == 0 && (uintptr_t)y % 8 == 0, CFM_ERR_ALIGN, "16-B aligned x, 8-B aligned y");
+  hipLaunchKernelGGL(quant_mx_kernel, dim3(grid_for(rows * (long)K)), dim3(256), 0, cfm::as_stream(stream), x, dtx,
+                     rows, K, ldx, (uint8_t*)y, s);
+  return cfm::check_launch("cfm_quant_mx");
+}
+
+CFM_EXPORT long cfm_quant_mx_batch_blocks(long rows, int K) { return mx_blocks(rows, K); }
+
+CFM_EXPORT int cfm_quant_mx_batch(const cfm_mx_task* tasks, int ntasks, long nblocks, int dtx, void* stream) {
+  CFM_REQUIRE(tasks && ntasks > 0 && nblocks > 0, CFM_ERR_ARG, "null table / empty batch");
+  CFM_REQUIRE(dtx == CFM_F32 || dtx == CFM_BF16, CFM_ERR_DTYPE, "x must be fp32 or bf16");
+  hipLaunchKernelGGL(quant_mx_batch_kernel, dim3((unsigned)nblocks), dim3(256), 0, cfm::as_stream(stream), tasks,
+                     ntasks, dtx);
+  return cfm::check_launch("cfm_quant_mx_batch");
+}
+
+CFM_EXPORT int cfm_dequant_mx(const void* x, const uint8_t* s, long n, float* y, void* stream) {
+  CFM_REQUIRE(x && s && y && n > 0 && n % 32 == 0, CFM_ERR_ARG, "null pointer / n % 32");
+  hipLaunchKernelGGL(dequant_mx_kernel, dim3(grid_for(8 * n)), dim3(256), 0, cfm::as_stream(stream),
+                     (const uint8_t*)x, s, n, y);
+  return cfm::check_launch("cfm_dequant_mx");
+}
 
 CFM_EXPORT size_t cfm_quant_fp8_ws_bytes(void) { return AMAX_BLOCKS * sizeof(float); }
 

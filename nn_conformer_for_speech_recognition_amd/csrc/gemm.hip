@@ -14,7 +14,9 @@
 // LDS ring (one barrier per K tile).
 #include "cfm_common.h"
 
+#include <algorithm>
 #include <type_traits>
+#include <vector>
 
 namespace {
 
@@ -48,6 +50,9 @@ struct GemmP {
   uint32_t dkey0, dthr;        // dropout constants hoisted out of the epilogue (gemm_drop_prep)
   float dkeep;
   int efast;                   // staged-epilogue fast path (epi_fast_kind; 0: the generic epilogue_store8 rows)
+  const uint8_t* mxa;          // MX fp8 operands (cfm_gemm_desc.mx_a / mx_b): e8m0 block scales [rows][mxk]
+  const uint8_t* mxb;
+  int mxk;                     // blocks of 32 fp8 per row (K / 32)
 };
 
 // salt the dropout seed and hoist the per-launch constants (hash key of the low 2^33 index range,
@@ -819,6 +824,7 @@ struct GatherA {
   int di[9], dj[9], dR[9];
   const void* group_tab;   // grouped launch (GROUP kernels): device WgTask table, one task per GEMM
   int group_n;
+  const unsigned* group_sched;   // planned grouped launch: one word per workgroup (cfm_wgrad_group_plan) or nullptr
 };
 
 // BMt x 128 tile, BKt-deep K steps, NST-stage ring, NWV waves; the f32 epilogue staging aliases the ring
@@ -856,6 +862,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pipe_rsrc(const PipeOp& o, int
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
   return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
                                            __builtin_amdgcn_readfirstlane((int)o.bytes), 0x00020000);
+}
+
+// buffer resource over `bytes` bytes at p (MX block-scale rows; reads past the range return zero)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mx_rsrc(const uint8_t* p, long bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane((int)(bytes > 0 ? bytes : 0)), 0x00020000);
 }
 
 // one wave-instruction of LDS-DMA: lane l's 16 B from rsrc + voff land at lds_base + 16 l.
@@ -944,7 +959,8 @@ __device__ __forceinline__ void wait_stages(int younger) {
 // 64x64 per wave; (192, 8, 4) -> 96x32 per wave (192-row tiles: 63 x N/128 tiles of the encoder's
 // M = 11,936 fill the 256 CUs in whole rounds); (128, 4, 2) -> 64x64.
 struct WgTask;   // grouped weight-gradient task (below)
-__device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn);
+__device__ __forceinline__ bool group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn,
+                                           int& zz);
 
 // F8: A and B are fp8 e4m3 (OCP), K-major, viewed as bf16 PAIRS by everything up to the LDS image (K, ld and
 // the tile geometry in 2-byte units, so DMA, swizzle and ring are byte-identical to the bf16 kernel); each
@@ -954,11 +970,16 @@ __device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& 
 // M16: the main loop on v_mfma_f32_16x16x32_bf16 (each 32x32 block of a wave's tile as four 16x16 blocks; same
 // LDS images, fragments per k and accumulator registers) -- K-major plain operands only.  On random data the
 // chip holds a higher clock under the 16x16 shape than under 32x32x16 (MI355X_MICROARCH.md, DVFS item 7).
+// MXK > 0 (F8 only): MX operands -- the tile's e8m0 block-scale rows (A rows m0.., B rows n0..: contiguous runs of
+// mxk bytes each, mxk <= MXK) are DMA'd into LDS once, before the ring's first stage (so every stage wait covers
+// them), and each fragment row's scales of a stage are read as one dword (BKt 64: 4 blocks) / short (BKt 32: 2);
+// lane (r, h) of a 64-fp8 k-step q covers block 2q + h of the stage, shifted into the scale register's low byte.
 template <int BMt, int BKt, int NST, int OCC, bool AK, bool BKM, int NWV = BMt / 32, int WN = 2, bool GA = false,
-          bool GROUP = false, bool F8 = false, int BNt = BN, bool M16 = false, int EK = EF_GENERIC>
+          bool GROUP = false, bool F8 = false, int BNt = BN, bool M16 = false, int EK = EF_GENERIC, int MXK = 0>
 __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(OCC * NWV / 4)))
 void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   static_assert(!F8 || (AK && BKM && !GA && !GROUP && BKt % 32 == 0), "fp8: K-major plain operands");
+  static_assert(MXK == 0 || (F8 && (BKt == 64 || BKt == 32) && ((BMt + BNt) * MXK) % 1024 == 0), "MX: fp8 only");
   static_assert(!M16 || (AK && BKM && !GA && !GROUP && !F8 && BKt % 32 == 0), "16x16x32: K-major plain bf16");
   typedef PipeGeo<BMt, BKt, NST, NWV, BNt> G;
   constexpr int WM = NWV / WN, FM = BMt / WM / 32, FN = BNt / WN / 32;
@@ -968,16 +989,16 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
   // (the dropout constants are prepared right before the epilogue: gemm_drop_prep loads the bound step counter,
   // and waiting for that load at the top held back the first DMA stage by one memory round trip)
   static_assert(NST >= 3 && NST <= 6, "ring depth");
-  __shared__ __attribute__((aligned(1024))) char lds[G::LDS];
+  __shared__ __attribute__((aligned(1024))) char lds[G::LDS + (BMt + BNt) * MXK];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   int tm, tn, zz;
   if constexpr (GROUP) {
     unsigned long long* const probe = p.probe;   // the launch's timing slot survives the task's parameters
-    group_task(ga, p, oa, ob, tm, tn);   // this workgroup's GEMM and tile of a grouped launch
+    // this workgroup's GEMM, tile and K slice of a grouped launch (a planned launch's padding workgroups exit)
+    if (!group_task(ga, p, oa, ob, tm, tn, zz)) return;
     p.probe = probe;
     gemm_drop_prep(p);
-    zz = 0;
   } else {
     xcd_tile3(tm, tn, zz);
   }
@@ -1019,6 +1040,18 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
                             : (G::AP / G::NW + (wid < G::AP % G::NW)) + (G::BP / G::NW + (wid < G::BP % G::NW));
   const unsigned stepa = AK ? BKt * 2 : (unsigned)(BKt * oa.ld * 2);
   const unsigned stepb = BKM ? BKt * 2 : (unsigned)(BKt * ob.ld * 2);
+  char* const sca = lds + G::LDS;        // MX: the tile's A / B block-scale rows
+  char* const scb = sca + BMt * MXK;
+  if constexpr (MXK > 0) {
+    const int mk = p.mxk;
+    const __amdgpu_buffer_rsrc_t rsa = mx_rsrc(p.mxa + (long)m0 * mk, (long)(p.M - m0) * mk);
+    const __amdgpu_buffer_rsrc_t rsb = mx_rsrc(p.mxb + (long)n0 * mk, (long)(p.N - n0) * mk);
+    const int pa = (BMt * mk + 1023) / 1024, pb = (BNt * mk + 1023) / 1024;
+    for (int q = wid; q < pa + pb; q += NWV) {   // (rows past M / N read zero through the range check)
+      if (q < pa) dma16(rsa, sca + 1024 * q, (unsigned)(1024 * q + 16 * lane));
+      else dma16(rsb, scb + 1024 * (q - pa), (unsigned)(1024 * (q - pa) + 16 * lane));
+    }
+  }
 
   auto issue = [&](int kt) {
     char* sa = lds + (kt % NST) * G::STAGE;
@@ -1078,6 +1111,20 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
       typedef int i32x8 __attribute__((ext_vector_type(8)));
       constexpr int KS8 = BKt / 32;    // 64-fp8 k-steps per stage
       i32x8 a8[KS8][FM], b8[KS8][FN];
+      unsigned sA[FM], sB[FN];           // MX: this stage's block scales of each fragment row
+      if constexpr (MXK > 0) {
+        const int mk = p.mxk, kb0 = kt * (BKt / 16);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const char* a = sca + (wm * FM * 32 + i * 32 + (lane & 31)) * mk + kb0;
+          sA[i] = BKt == 64 ? *reinterpret_cast<const unsigned*>(a) : *reinterpret_cast<const unsigned short*>(a);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const char* b = scb + (wn * FN * 32 + j * 32 + (lane & 31)) * mk + kb0;
+          sB[j] = BKt == 64 ? *reinterpret_cast<const unsigned*>(b) : *reinterpret_cast<const unsigned short*>(b);
+        }
+      }
       auto frag8 = [&](const char* img, int row0, int q) {
         const int r = row0 + (lane & 31), c = 4 * q + 2 * (lane >> 5);
         const uint4 lo = *reinterpret_cast<const uint4*>(img + r * S::RB + 16 * S::slot(r, c));
@@ -1100,9 +1147,12 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
+          for (int j = 0; j < FN; ++j) {
+            const int sh = 8 * (2 * q + (lane >> 5));
+            const int sa = MXK > 0 ? (int)(sA[i] >> sh) : 127, sb = MXK > 0 ? (int)(sB[j] >> sh) : 127;
             acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8[q][i], b8[q][j], acc[i][j], 0, 0, 0,
-                                                                        127, 0, 127);
+                                                                        sa, 0, sb);
+          }
       continue;
     }
     if constexpr (M16) {
@@ -1380,29 +1430,54 @@ extern int g_gemm_mode;
 // workgroup running the whole K loop (no split-K slabs, no reduce pass), and the ~3000 tiles of the
 // encoder's 17 layers fill the chip in whole rounds.  Workgroup -> (task, tile): XCD-contiguous ids
 // (xcd_tile order), tasks back to back (tile0 ascending), tiles row-major inside a task.
+// Planned form (cfm_wgrad_group_plan, GatherA.group_sched): one schedule word per workgroup -- task, tile, K slice
+// -- laid out so that each XCD (workgroups b, b + 8, ... under round-robin placement) runs whole tasks in rounds of
+// one tile per CU, i.e. every tile that shares a dY or X column slice with another is co-resident on that XCD and
+// streams the slice through its L2 once; the tiles that do not fill whole rounds run split over K slices into fp32
+// slabs (the task's p.split_k / k_per_split / slab / acs_slab), summed by wgrad_split_reduce_kernel.
 struct WgTask {
   GemmP p;
   PipeOp oa, ob;
   long tile0;
   int tiles_n;
-  int pad;
+  int red_blocks;      // split task: blocks of wgrad_split_reduce_kernel (0: not split)
+  long red0;           // first reduce block of this task
+  float* dw;           // split task: the destinations the reduce writes (p.C / p.acs_slab point into the workspace)
+  float* db;
 };
 static_assert(sizeof(WgTask) % 4 == 0, "word-copied task");
+constexpr unsigned WG_SCHED_EMPTY = 0xFFFFFFFFu;   // padding workgroup of a planned launch
+__host__ __device__ constexpr unsigned wg_sched_word(int task, int ks, int tile) {
+  return ((unsigned)task << 20) | ((unsigned)ks << 16) | (unsigned)tile;
+}
 
-__device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn) {
+__device__ __forceinline__ bool group_task(const GatherA& ga, GemmP& p, PipeOp& oa, PipeOp& ob, int& tm, int& tn,
+                                           int& zz) {
   const WgTask* tab = reinterpret_cast<const WgTask*>(ga.group_tab);
-  const int nwg = gridDim.x, L = blockIdx.x;
-  int id = L;
-  if (nwg > 8) {
-    const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
-    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+  int lo, local;
+  zz = 0;
+  if (ga.group_sched) {
+    const unsigned w = __builtin_amdgcn_readfirstlane(ga.group_sched[blockIdx.x]);
+    if (w == WG_SCHED_EMPTY) return false;
+    lo = (int)(w >> 20);
+    zz = (int)((w >> 16) & 15u);
+    local = (int)(w & 0xFFFFu);
+  } else {
+    const int nwg = gridDim.x, L = blockIdx.x;
+    int id = L;
+    if (nwg > 8) {
+      const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
+      id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+    }
+    lo = 0;
+    int hi = ga.group_n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (__builtin_amdgcn_readfirstlane((int)tab[mid].tile0) <= id) lo = mid; else hi = mid - 1;
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    local = id - (int)__builtin_amdgcn_readfirstlane((int)tab[lo].tile0);
   }
-  int lo = 0, hi = ga.group_n - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (__builtin_amdgcn_readfirstlane((int)tab[mid].tile0) <= id) lo = mid; else hi = mid - 1;
-  }
-  lo = __builtin_amdgcn_readfirstlane(lo);
   // copy the task word by word through readfirstlane: the compiler then knows every field (buffer
   // descriptors, loop bounds) is wave-uniform -- SGPRs, no waterfall loops around the buffer loads
   WgTask t;
@@ -1413,9 +1488,41 @@ __device__ __forceinline__ void group_task(const GatherA& ga, GemmP& p, PipeOp& 
   p = t.p;
   oa = t.oa;
   ob = t.ob;
-  const int local = (int)(id - t.tile0);
   tm = local / t.tiles_n;
   tn = local % t.tiles_n;
+  return true;
+}
+
+// sum the K-slice slabs of every split task of a planned grouped launch, in slice order (deterministic):
+// dW (N x K, row-major) = sum_s slab[s], db (N) = sum_s acs_slab[s]; block b of task t: 1024 elements of dW and
+// (b < N / 256) 256 elements of db; task of a block = the last one whose red0 <= b (unsplit tasks own no blocks)
+__global__ __launch_bounds__(256) void wgrad_split_reduce_kernel(const WgTask* __restrict__ tab, int ntasks) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = ntasks - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].red0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const WgTask& t = tab[lo];
+  const int S = t.p.split_k, N = t.p.M, K = t.p.N;
+  const long lb = b - t.red0;
+  const long per = (long)N * K;
+  const long w = (lb * 256 + threadIdx.x) * 4;
+  if (w < per) {
+    const float* src = t.p.slab + w;
+    float4 s = *reinterpret_cast<const float4*>(src);
+    for (int k = 1; k < S; ++k) {
+      const float4 a = *reinterpret_cast<const float4*>(src + k * per);
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+    *reinterpret_cast<float4*>(t.dw + w) = s;
+  }
+  const long n = lb * 256 + threadIdx.x;
+  if (t.db && n < N) {
+    float s = t.p.acs_slab[n];
+    for (int k = 1; k < S; ++k) s += t.p.acs_slab[k * (long)N + n];
+    t.db[n] = s;
+  }
 }
 
 // ---------------------------------------------------------------- fp32 kernel (exact-f32 MFMA)
@@ -1782,6 +1889,29 @@ int launch_fp8(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
   p.alpha_b = d.alpha_b_dev;
   const PipeOp oa{(const bf16*)d.A, d.lda / 2, 0, d.M, (unsigned)((long)d.M * d.lda)};
   const PipeOp ob{(const bf16*)d.B, d.ldb / 2, 0, d.N, (unsigned)((long)d.N * d.ldb)};
+  if (d.mx_a) {
+    // MX operands: block scales applied inside the MFMA, so alpha stays 1 and the fast epilogue kinds apply
+    p.mxa = d.mx_a;
+    p.mxb = d.mx_b;
+    p.mxk = d.K / 32;
+    p.efast = epi_fast_kind(p, 1);
+    if (p.N <= 512 || d.K > 512) {
+      // d-wide outputs, and any K > 512 (the 2048-deep scale rows -- 20 KiB -- do not fit beside a two-per-CU ring)
+      const dim3 g(cdiv(p.N, BN), cdiv(p.M, 192), 1);
+      ek_dispatch<true>(p.efast, [&](auto ek) {
+        hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, true, true, 8, 4, false, false, true, BN, false,
+                                             decltype(ek)::value, 64>), g, dim3(512), 0, s, p, oa, ob, GatherA{});
+      });
+    } else {
+      // K <= 512 (FFN up, QKV): the scale rows (6 KiB) fit beside the 72 KiB ring -- two workgroups per CU
+      const dim3 g(cdiv(p.N, BN), cdiv(p.M, 256), 1);
+      ek_dispatch<true>(p.efast, [&](auto ek) {
+        hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 3, 2, true, true, 8, 2, false, false, true, BN, false,
+                                             decltype(ek)::value, 16>), g, dim3(512), 0, s, p, oa, ob, GatherA{});
+      });
+    }
+    return cfm::check_launch("cfm_gemm(fp8 mx)");
+  }
   if (p.N <= 512) {
     const dim3 g(cdiv(p.N, BN), cdiv(p.M, 192), 1);
     hipLaunchKernelGGL((gemm_pipe_kernel<192, 64, 3, 1, true, true, 8, 4, false, false, true>), g, dim3(512), 0, s, p,
@@ -1834,6 +1964,8 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
                     !d->rowdot_out && !d->a_colsum && (long)d->M * d->lda < (1L << 31) &&
                     (long)d->N * d->ldb < (1L << 31),
                 CFM_ERR_UNSUPPORTED, "fp8: K-major A and B, K % 128 == 0, 16-B aligned rows, no split-K / batch");
+    CFM_REQUIRE(!d->mx_a == !d->mx_b && (!d->mx_a || (d->K <= 2048 && !d->alpha_a_dev && !d->alpha_b_dev)),
+                CFM_ERR_ARG, "fp8 MX: both scale tensors, K <= 2048, no per-tensor alpha");
     return launch_fp8(*d, p, cfm::as_stream(stream));
   }
   const bool bf = d->dtype_ab == CFM_BF16;
@@ -1916,6 +2048,132 @@ CFM_EXPORT int cfm_wgrad_group_fill(void* host_tab, int i, const void* dy, const
   t.tiles_n = cdiv(K, WG_BN);
   reinterpret_cast<WgTask*>(host_tab)[i] = t;
   return CFM_OK;
+}
+
+// the same for a planned launch: task i of the table as cfm_wgrad_group_fill, and when split > 1 (the plan's
+// task_split[i]) its K range cut into `split` slices of whole 32-token steps whose fp32 partials go to the workspace
+// ws (cfm_wgrad_group_ws_floats(N, K, split) floats: split dW slabs, then split db rows), summed into dw / db by the
+// reduce pass; red0 = the task's first reduce block (running sum of cfm_wgrad_group_red_blocks over earlier tasks)
+CFM_EXPORT long cfm_wgrad_group_ws_floats(int N, int K, int split) {
+  return split > 1 ? (long)split * ((long)N * K + N) : 0;
+}
+CFM_EXPORT long cfm_wgrad_group_red_blocks(int N, int K, int split) {
+  if (split <= 1) return 0;
+  const long a = cdiv((long)N * K, 1024), b = cdiv(N, 256);
+  return a > b ? a : b;
+}
+CFM_EXPORT int cfm_wgrad_group_fill_split(void* host_tab, int i, const void* dy, const void* x, float* dw, float* db,
+                                          int M, int N, int K, int split, float* ws, long red0) {
+  const int rc = cfm_wgrad_group_fill(host_tab, i, dy, x, dw, db, M, N, K, 0);
+  if (rc != CFM_OK) return rc;
+  CFM_REQUIRE(split >= 1 && split <= 15, CFM_ERR_ARG, "split in 1..15");
+  WgTask& t = reinterpret_cast<WgTask*>(host_tab)[i];
+  t.red0 = red0;
+  t.dw = dw;
+  t.db = db;
+  if (split > 1) {
+    CFM_REQUIRE(ws && (uintptr_t)ws % 16 == 0, CFM_ERR_ALIGN, "16-B aligned workspace");
+    CFM_REQUIRE((long)split * N * K < (1L << 31), CFM_ERR_SHAPE, "split slabs too large");
+    t.p.split_k = split;
+    t.p.k_per_split = ((M + split - 1) / split + 31) / 32 * 32;
+    t.p.slab = ws;
+    t.p.acs_slab = db ? ws + (long)split * N * K : nullptr;
+    t.red_blocks = (int)cfm_wgrad_group_red_blocks(N, K, split);
+  }
+  return CFM_OK;
+}
+
+// Plan a grouped launch of ntasks GEMMs of task_tiles[i] output tiles each (cfm_wgrad_group_tiles) on nxcd XCDs
+// of `cus` CUs (one workgroup per CU: the kernel holds a 128-KiB ring):
+//  * tasks (cut into pieces of at most `cus` tiles) are packed first-fit-decreasing into bins of `cus` tiles;
+//  * each XCD x gets R = (full bins) / nxcd full bins -- workgroup ids x, x + nxcd, ... in bin order, so a bin's
+//    tiles start together on one XCD and every dY / X slice a bin reads is streamed into that XCD's L2 once;
+//  * the tiles of the remaining bins (the ragged last round) are split over S = min(8, nxcd * cus / tail) K slices
+//    (task_split[i] = S for their tasks, 1 otherwise) and dealt to the XCDs slice by slice, so the last round
+//    fills the chip instead of running a few tiles alone; with S < 2 (or a task cut across main and tail bins)
+//    they run unsplit as extra bins.
+// Writes grid words to sched (capacity cap; WG_SCHED_EMPTY pads the shorter XCD lists) and returns the grid size,
+// or a negative error code.
+CFM_EXPORT long cfm_wgrad_group_plan(const long* task_tiles, int ntasks, int nxcd, int cus, unsigned* sched,
+                                     long cap, int* task_split) {
+  if (!task_tiles || !sched || !task_split || ntasks <= 0 || ntasks > 4095 || nxcd <= 0 || cus <= 0)
+    return cfm::fail(CFM_ERR_ARG, "cfm_wgrad_group_plan: bad arguments");
+  struct Piece { int task, off, n; };
+  std::vector<Piece> pieces;
+  for (int i = 0; i < ntasks; ++i) {
+    if (task_tiles[i] <= 0 || task_tiles[i] > 65535)
+      return cfm::fail(CFM_ERR_SHAPE, "cfm_wgrad_group_plan: tiles per task in 1..65535");
+    for (int o = 0; o < task_tiles[i]; o += cus) pieces.push_back({i, o, (int)std::min<long>(cus, task_tiles[i] - o)});
+    task_split[i] = 1;
+  }
+  std::stable_sort(pieces.begin(), pieces.end(), [](const Piece& a, const Piece& b) { return a.n > b.n; });
+  std::vector<std::vector<Piece>> bins;
+  std::vector<int> fill;
+  for (const Piece& pc : pieces) {
+    size_t k = 0;
+    while (k < bins.size() && fill[k] + pc.n > cus) ++k;
+    if (k == bins.size()) { bins.emplace_back(); fill.push_back(0); }
+    bins[k].push_back(pc);
+    fill[k] += pc.n;
+  }
+  std::vector<int> full, rest;
+  for (size_t k = 0; k < bins.size(); ++k) (fill[k] == cus ? full : rest).push_back((int)k);
+  const int R = (int)full.size() / nxcd;
+  for (size_t k = (size_t)R * nxcd; k < full.size(); ++k) rest.push_back(full[k]);
+  full.resize((size_t)R * nxcd);
+  std::vector<std::vector<unsigned>> lists(nxcd);
+  auto emit_bin = [&](std::vector<unsigned>& l, int k, int ks) {
+    for (const Piece& pc : bins[k])
+      for (int t = 0; t < pc.n; ++t) l.push_back(wg_sched_word(pc.task, ks, pc.off + t));
+  };
+  for (int x = 0; x < nxcd; ++x)
+    for (int r = 0; r < R; ++r) emit_bin(lists[x], full[(size_t)x * R + r], 0);
+  long tail = 0;
+  std::vector<char> in_main(ntasks, 0), in_tail(ntasks, 0);
+  for (int k : full) for (const Piece& pc : bins[k]) in_main[pc.task] = 1;
+  for (int k : rest) for (const Piece& pc : bins[k]) { in_tail[pc.task] = 1; tail += pc.n; }
+  bool cut = false;
+  for (int i = 0; i < ntasks; ++i) cut |= in_main[i] && in_tail[i];
+  const int S = tail > 0 && !cut ? (int)std::min<long>(8, (long)nxcd * cus / tail) : 1;
+  if (S >= 2) {
+    std::vector<unsigned> parts;   // slice-major: XCD x gets a contiguous run (one slice per XCD when S == nxcd)
+    for (int ks = 0; ks < S; ++ks)
+      for (int k : rest) emit_bin(parts, k, ks);
+    const long np = (long)parts.size();
+    for (long q = 0; q < np; ++q) lists[(int)(q * nxcd / np)].push_back(parts[q]);
+    for (int i = 0; i < ntasks; ++i) if (in_tail[i]) task_split[i] = S;
+  } else {
+    for (size_t j = 0; j < rest.size(); ++j) emit_bin(lists[j % nxcd], rest[j], 0);
+  }
+  size_t len = 0;
+  for (auto& l : lists) len = std::max(len, l.size());
+  const long grid = (long)len * nxcd;
+  if (grid > cap) return cfm::fail(CFM_ERR_ARG, "cfm_wgrad_group_plan: schedule capacity too small");
+  for (size_t j = 0; j < len; ++j)
+    for (int x = 0; x < nxcd; ++x) sched[j * nxcd + x] = j < lists[x].size() ? lists[x][j] : WG_SCHED_EMPTY;
+  return grid;
+}
+
+// planned launch: dev_sched (grid words from cfm_wgrad_group_plan, on the device) over the table of
+// cfm_wgrad_group_fill_split tasks, then the reduce pass over the split tasks' slabs (red_blocks = the sum of the
+// tasks' cfm_wgrad_group_red_blocks; 0: no split task)
+CFM_EXPORT int cfm_wgrad_group_sched(const void* dev_tab, int ntasks, const unsigned* dev_sched, long grid,
+                                     long red_blocks, unsigned long long* probe, void* stream) {
+  CFM_REQUIRE(dev_tab && dev_sched && ntasks > 0 && grid > 0 && grid < (1L << 31) && red_blocks >= 0 &&
+              red_blocks < (1L << 31), CFM_ERR_ARG, "bad plan");
+  GemmP gp{};
+  gp.probe = probe;
+  GatherA ga{};
+  ga.group_tab = dev_tab;
+  ga.group_n = ntasks;
+  ga.group_sched = dev_sched;
+  hipStream_t s = cfm::as_stream(stream);
+  hipLaunchKernelGGL((gemm_pipe_kernel<256, 32, 4, 1, false, false, 8, 2, false, true, false, WG_BN>),
+                     dim3((unsigned)grid), dim3(512), 0, s, gp, PipeOp{}, PipeOp{}, ga);
+  if (red_blocks > 0)
+    hipLaunchKernelGGL(wgrad_split_reduce_kernel, dim3((unsigned)red_blocks), dim3(256), 0, s,
+                       reinterpret_cast<const WgTask*>(dev_tab), ntasks);
+  return cfm::check_launch("cfm_wgrad_group_sched");
 }
 
 CFM_EXPORT int cfm_wgrad_group_probed(const void* dev_tab, int ntasks, long total_tiles, unsigned long long* probe,

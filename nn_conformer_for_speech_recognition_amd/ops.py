@@ -21,9 +21,10 @@ def _gemm_desc(**kw):
 def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, alpha=1.0,
          bias=None, act=ACT_NONE, act_grad=False, pre=None, drop_p=0.0, seed=0, offset=0, out_scale=1.0,
          residual=None, ldr=None, split_k=1, batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None,
-         a_colsum=None, rowdot=None, alpha_a=None, alpha_b=None, allow_overlap=False):
+         a_colsum=None, rowdot=None, alpha_a=None, alpha_b=None, allow_overlap=False, mx_a=None, mx_b=None):
     """C = epilogue(alpha * A·Bᵀ) — see cfm_gemm_desc in include/cfm.h.  fp8 (e4m3fn) A and B: alpha_a /
-    alpha_b are their device dequantisation scalars (quant_fp8)."""
+    alpha_b are their device dequantisation scalars (quant_fp8), or mx_a / mx_b their e8m0 block scales
+    (quant_mx)."""
     if A.dtype != B.dtype:
         raise L.CfmError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
     d = _gemm_desc(
@@ -39,7 +40,7 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         split_k=int(split_k), workspace=L.ptr(workspace), a_colsum=L.ptr(a_colsum),
         rowdot_with=L.ptr(rowdot[0]) if rowdot else None, rowdot_out=L.ptr(rowdot[1]) if rowdot else None,
         rowdot_T=int(rowdot[2]) if rowdot else 0, alpha_a_dev=L.ptr(alpha_a), alpha_b_dev=L.ptr(alpha_b),
-        allow_overlap=int(bool(allow_overlap)))
+        allow_overlap=int(bool(allow_overlap)), mx_a=L.ptr(mx_a), mx_b=L.ptr(mx_b))
     if PROBE is not None:
         PROBE("gemm", (M, N, K), d, lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
     else:
@@ -48,19 +49,23 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
 
 
 PROBE = None   # optional timing hook (bench.py KernelProbe): PROBE(kind, shape, desc, launch)
+# grouped weight gradients on the XCD-aware plan (cfm_wgrad_group_plan); CFM_WGRAD_PLAN=0 keeps the unplanned
+# launch (tiles in task order, XCD-contiguous ids) for A/B
+WGRAD_PLAN = os.environ.get("CFM_WGRAD_PLAN", "1") != "0"
 
 
 def linear(x, w, bias=None, out_dtype=None, act=ACT_NONE, pre=None, drop_p=0.0, seed=0, offset=0,
-           out_scale=1.0, residual=None, out=None, x_scale=None, w_scale=None):
-    """y = x·wᵀ (+bias, epilogue) for x (M, K), w (N, K).  fp8 operands (quant_fp8 outputs) pass their
-    dequantisation scalars as x_scale / w_scale; the output then defaults to bf16."""
+           out_scale=1.0, residual=None, out=None, x_scale=None, w_scale=None, x_mx=None, w_mx=None):
+    """y = x·wᵀ (+bias, epilogue) for x (M, K), w (N, K).  fp8 operands pass their dequantisation: per-tensor
+    scalars x_scale / w_scale (quant_fp8) or MX block scales x_mx / w_mx (quant_mx); the output then defaults to
+    bf16."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
         od = out_dtype or (torch.bfloat16 if x.dtype == torch.float8_e4m3fn else x.dtype)
         out = torch.empty(M, N, device=x.device, dtype=od)
     return gemm(x, w, out, M, N, K, bias=bias, act=act, pre=pre, drop_p=drop_p, seed=seed, offset=offset,
-                out_scale=out_scale, residual=residual, alpha_a=x_scale, alpha_b=w_scale)
+                out_scale=out_scale, residual=residual, alpha_a=x_scale, alpha_b=w_scale, mx_a=x_mx, mx_b=w_mx)
 
 
 def quant_fp8(x, out=None, inv_scale=None):
@@ -73,6 +78,26 @@ def quant_fp8(x, out=None, inv_scale=None):
     ws = workspace(L.size_call("cfm_quant_fp8_ws_bytes"), x.device)
     L.call("cfm_quant_fp8", L.ptr(x), L.dt(x), x.numel(), L.ptr(y), L.ptr(sc), L.ptr(ws), L.stream())
     return y, sc
+
+
+def quant_mx(x, out=None, scales=None):
+    """MX e4m3 quantisation on the device (cfm_quant_mx): x (rows, K), K % 32 == 0 -> (y float8_e4m3fn (rows, K),
+    s uint8 (rows, K/32) e8m0 block scales): y = e4m3(x * 2^k) per 32-element block, k the largest with
+    amax(block) * 2^k <= 448, s = 127 - k."""
+    if x.dim() != 2 or not x.is_contiguous():
+        raise L.CfmError("quant_mx: contiguous 2-D input required")
+    rows, K = x.shape
+    y = out if out is not None else torch.empty(rows, K, device=x.device, dtype=torch.float8_e4m3fn)
+    s = scales if scales is not None else torch.empty(rows, K // 32, device=x.device, dtype=torch.uint8)
+    L.call("cfm_quant_mx", L.ptr(x), L.dt(x), rows, K, K, L.ptr(y), L.ptr(s), L.stream())
+    return y, s
+
+
+def dequant_mx(y, s):
+    """float32 view of an MX tensor: e4m3(y) * 2^(s - 127) per 32-element block (tests)."""
+    out = torch.empty(y.shape, device=y.device, dtype=torch.float32)
+    L.call("cfm_dequant_mx", L.ptr(y), L.ptr(s), y.numel(), L.ptr(out), L.stream())
+    return out
 
 
 def linear_dgrad(dy, w, out_dtype=None, pre=None, act_grad=False, drop_p=0.0, seed=0, offset=0, out=None,
@@ -212,6 +237,21 @@ class WgradGroup:
         self._stream = torch.cuda.current_stream(dy.device)
         return dw.view(N, K), db.view(N)
 
+    def _plan(self, dev, lib):
+        """cfm_wgrad_group_plan over the queued tasks: (schedule words (grid,), per-task split factors)."""
+        import numpy as np
+        n = len(self.tasks)
+        tiles = np.array([lib.cfm_wgrad_group_tiles(t[0].shape[1], t[1].shape[1]) for t in self.tasks], dtype=np.int64)
+        nxcd = 8                                       # MI355X: 8 XCDs (placement is a speed hint only)
+        cus = max(1, torch.cuda.get_device_properties(dev).multi_processor_count // nxcd)
+        cap = int(tiles.sum()) * 16 + 64 * nxcd
+        sched = np.empty(cap, dtype=np.uint32)
+        split = np.ones(n, dtype=np.int32)
+        grid = lib.cfm_wgrad_group_plan(tiles.ctypes.data, n, nxcd, cus, sched.ctypes.data, cap, split.ctypes.data)
+        if grid <= 0:
+            raise L.CfmError("cfm_wgrad_group_plan failed: " + lib.cfm_get_last_error().decode(errors="replace"))
+        return sched[:grid].copy(), split
+
     def flush(self):
         if not self.tasks:
             return
@@ -219,22 +259,40 @@ class WgradGroup:
         dev = self.tasks[0][0].device
         # (the tile width of the launch variant is part of the table: cfm_wgrad_group_tiles(256, 256) is 1 or 2)
         key = tuple((t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), t[0].shape[0],
-                     t[0].shape[1], t[1].shape[1]) for t in self.tasks) + (L.load().cfm_wgrad_group_tiles(256, 256),)
+                     t[0].shape[1], t[1].shape[1]) for t in self.tasks) + (L.load().cfm_wgrad_group_tiles(256, 256),
+                                                                           WGRAD_PLAN)
         hit = self._cache.get(key)
         if hit is None:
             lib = L.load()
             tb = L.size_call("cfm_wgrad_group_task_bytes")
             host = np.zeros(tb * len(self.tasks), dtype=np.uint8)
-            tile0 = 0
-            for i, (dy, x, dw, db) in enumerate(self.tasks):
-                M, N = dy.shape
-                K = x.shape[1]
-                L.call("cfm_wgrad_group_fill", host.ctypes.data, i, L.ptr(dy), L.ptr(x), L.ptr(dw), L.ptr(db), M, N,
-                       K, tile0)
-                tile0 += lib.cfm_wgrad_group_tiles(N, K)
             captured = torch.cuda.is_current_stream_capturing()
-            table = self._stage(host)
-            hit = (captured, table, tile0)
+            if WGRAD_PLAN:
+                sched, split = self._plan(dev, lib)
+                shapes = [(t[0].shape[1], t[1].shape[1]) for t in self.tasks]
+                wsf = [lib.cfm_wgrad_group_ws_floats(N, K, int(s)) for (N, K), s in zip(shapes, split)]
+                ws = torch.empty(max(1, sum(wsf)), dtype=torch.float32, device=dev) if sum(wsf) else None
+                off = red0 = 0
+                for i, (dy, x, dw, db) in enumerate(self.tasks):
+                    M, N = dy.shape
+                    K = x.shape[1]
+                    wp = ws.data_ptr() + 4 * off if wsf[i] else None
+                    L.call("cfm_wgrad_group_fill_split", host.ctypes.data, i, L.ptr(dy), L.ptr(x), L.ptr(dw),
+                           L.ptr(db), M, N, K, int(split[i]), wp, red0)
+                    off += wsf[i]
+                    red0 += lib.cfm_wgrad_group_red_blocks(N, K, int(split[i]))
+                table = self._stage(host)
+                hit = (captured, table, len(sched), self._stage(sched.view(np.uint8)), red0, ws)
+            else:
+                tile0 = 0
+                for i, (dy, x, dw, db) in enumerate(self.tasks):
+                    M, N = dy.shape
+                    K = x.shape[1]
+                    L.call("cfm_wgrad_group_fill", host.ctypes.data, i, L.ptr(dy), L.ptr(x), L.ptr(dw), L.ptr(db), M,
+                           N, K, tile0)
+                    tile0 += lib.cfm_wgrad_group_tiles(N, K)
+                table = self._stage(host)
+                hit = (captured, table, tile0)
             if len(self._cache) > 8:
                 # a captured graph's kernel node holds the device table's address: keep those entries
                 self._cache = {k: v for k, v in self._cache.items() if v[0]}
@@ -243,6 +301,10 @@ class WgradGroup:
         n = len(self.tasks)
 
         def launch():
+            if len(hit) > 3:
+                L.call("cfm_wgrad_group_sched", L.ptr(hit[1]), n, L.ptr(hit[3]), hit[2], hit[4], desc.probe,
+                       L.stream())
+                return
             L.call("cfm_wgrad_group_probed", L.ptr(hit[1]), n, hit[2], desc.probe, L.stream())
         if PROBE is not None:
             PROBE("wgroup", (n, hit[2]), desc, launch)
@@ -433,6 +495,41 @@ class Quant8Batch:
     def refresh(self):
         L.call("cfm_quant_fp8_batch", L.ptr(self.table), len(self.outs), self.nblocks, self.dtx, L.ptr(self.part),
                L.stream())
+        return self.outs
+
+
+class QuantMXBatch:
+    """Per-step MX e4m3 copies of a fixed list of 2-D tensors (rows, K) in ONE launch (cfm_quant_mx_batch): the
+    same bytes and block scales as quant_mx per tensor.  outs[i] = (y float8_e4m3fn (rows, K), s uint8 (rows, K/32)),
+    persistent across refresh() calls (graph-capturable: the table is built once)."""
+
+    def __init__(self, srcs):
+        import numpy as np
+        if not srcs:
+            raise L.CfmError("QuantMXBatch: empty list")
+        dts = {L.dt(t) for t in srcs}
+        if len(dts) != 1 or dts & {L.F32, L.BF16} != dts:
+            raise L.CfmError("QuantMXBatch: one fp32 or bf16 source dtype per batch")
+        self.dtx = dts.pop()
+        dev = srcs[0].device
+        self.outs = []
+        rec = np.zeros((len(srcs), 6), dtype=np.int64)   # cfm_mx_task: x, y, s, rows, (K | pad), blk0
+        blk = 0
+        for i, x in enumerate(srcs):
+            if x.dim() != 2 or not x.is_contiguous() or L.ptr(x) % 16 or x.shape[1] % 32:
+                raise L.CfmError("QuantMXBatch: contiguous 16-B aligned (rows, K) sources, K % 32 == 0")
+            rows, K = x.shape
+            y = torch.empty(rows, K, device=dev, dtype=torch.float8_e4m3fn)
+            s = torch.empty(rows, K // 32, device=dev, dtype=torch.uint8)
+            self.outs.append((y, s))
+            rec[i] = (L.ptr(x), L.ptr(y), L.ptr(s), rows, K, blk)
+            blk += L.load().cfm_quant_mx_batch_blocks(rows, K)
+        self.nblocks = blk
+        self.table = torch.from_numpy(rec.view(np.uint8).reshape(-1).copy()).to(dev)
+        self._keep = list(srcs)
+
+    def refresh(self):
+        L.call("cfm_quant_mx_batch", L.ptr(self.table), len(self.outs), self.nblocks, self.dtx, L.stream())
         return self.outs
 
 

@@ -126,3 +126,103 @@ def test_quant_fp8_batch_matches_per_tensor(dt):
         y_ref, sc_ref = ops.quant_fp8(x)
         assert torch.equal(sc, sc_ref), (x.shape, sc.item(), sc_ref.item())
         assert torch.equal(y.view(torch.uint8), y_ref.view(torch.uint8)), x.shape
+
+
+# ------------------------------------------------------------------------------------------- MX block scaling
+def _mx_ref(x):
+    """numpy/torch restatement of cfm_quant_mx: per 32-element block of a row, k = the largest integer with
+    amax * 2^k <= 448 (0 for an all-zero block, clamped to [-126, 126]), y = e4m3(x * 2^k), s = 127 - k."""
+    xf = x.float().cpu()
+    rows, K = xf.shape
+    blk = xf.view(rows, K // 32, 32)
+    amax = blk.abs().amax(-1).double()
+    m, e = torch.frexp(amax)                       # amax = m * 2^e, m in [0.5, 1)
+    k = torch.where(2 * m <= 1.75, 8 - (e - 1), 7 - (e - 1)).clamp(-126, 126)
+    k = torch.where(amax > 0, k, torch.zeros_like(k))
+    y = (blk.double() * torch.pow(2.0, k.double())[..., None]).float().view(rows, K).to(torch.float8_e4m3fn)
+    return y, (127 - k).to(torch.uint8)
+
+
+def _mx_deq(y, s):
+    yf = y.cpu().float().view(y.shape[0], -1, 32).double()
+    return (yf * torch.pow(2.0, s.cpu().double() - 127)[..., None]).view(y.shape[0], -1)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_quant_mx_bit_exact(dt):
+    """cfm_quant_mx (one pass, e8m0 scale per 32 elements) bit-exact against torch's float8_e4m3fn conversion of
+    x * 2^k per block; rows with very different magnitudes, an all-zero block, and the dequantised view."""
+    g = torch.Generator().manual_seed(2)
+    x = (torch.randn(1000, 512, generator=g) * torch.logspace(-6, 6, 1000)[:, None]).to(dt)
+    x[5, 32:64] = 0
+    x[7, 3] = -17.25
+    y, s = ops.quant_mx(x.to(DEV))
+    yr, sr = _mx_ref(x)
+    assert torch.equal(s.cpu(), sr)
+    assert torch.equal(y.cpu().view(torch.uint8), yr.view(torch.uint8))
+    deq = ops.dequant_mx(y, s)
+    assert torch.equal(deq.cpu().double(), _mx_deq(y, s))
+    assert _rel(deq, x.float()) < 6e-2
+
+
+def test_quant_mx_batch_matches_per_tensor():
+    g = torch.Generator().manual_seed(12)
+    shapes = [(2048, 512), (512, 2048), (1536, 512), (7, 64), (1, 32)]
+    srcs = [(torch.randn(*s, generator=g) * (10.0 ** (i - 2))).to(DEV).contiguous() for i, s in enumerate(shapes)]
+    qb = ops.QuantMXBatch(srcs)
+    for _ in range(2):
+        outs = qb.refresh()
+    for x, (y, s) in zip(srcs, outs):
+        yr, sr = ops.quant_mx(x)
+        assert torch.equal(s, sr) and torch.equal(y.view(torch.uint8), yr.view(torch.uint8)), x.shape
+
+
+@pytest.mark.parametrize("M,N,K", [(11936, 2048, 512), (11936, 512, 2048), (1000, 1536, 512), (77, 512, 128),
+                                   (300, 2048, 1024), (11984, 512, 512)])
+def test_mx_gemm_vs_fp64_of_dequantised(M, N, K):
+    """The MX GEMM (block scales inside v_mfma_scale_f32_32x32x64_f8f6f4) against an fp64 product of the SAME
+    dequantised operands (rows of very different magnitudes, so the per-block scales matter): relative L2 5e-5 with
+    fp32 output, 8e-3 with bf16; against the unquantised fp32 product 6e-2."""
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    x = (torch.randn(M, K, generator=g) * torch.logspace(-2, 2, K)[None, :]).to(DEV, torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g)).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    xq, sx = ops.quant_mx(x)
+    wq, sw = ops.quant_mx(w)
+    ref = _mx_deq(xq, sx) @ _mx_deq(wq, sw).t() + b.cpu().double()
+    y32 = ops.linear(xq, wq, b, out_dtype=torch.float32, x_mx=sx, w_mx=sw)
+    assert _rel(y32, ref) < 5e-5
+    y16 = ops.linear(xq, wq, b, x_mx=sx, w_mx=sw)
+    assert y16.dtype == torch.bfloat16 and _rel(y16.float(), ref) < 8e-3
+    full = x.double().cpu() @ w.double().cpu().t() + b.cpu().double()
+    assert _rel(y32, full) < 6e-2
+
+
+def test_mx_gemm_epilogues():
+    """The encoder's fp8 epilogues on MX operands (fast epilogue kinds): FFN up (bias + SiLU + dropout + saved
+    pre-activation, bf16) and FFN down / out-projection (bias + dropout + 0.5 scale + fp32 residual) against the
+    bf16-operand GEMM of the same dequantised values (identical dropout masks)."""
+    g = torch.Generator().manual_seed(4)
+    M = 3000
+    for N, K, kind in ((2048, 512, "up"), (512, 2048, "down")):
+        x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+        w = (0.05 * torch.randn(N, K, generator=g)).to(DEV)
+        b = torch.randn(N, generator=g).to(DEV)
+        xq, sx = ops.quant_mx(x)
+        wq, sw = ops.quant_mx(w)
+        xd = ops.dequant_mx(xq, sx)
+        wd = ops.dequant_mx(wq, sw)
+        if kind == "up":
+            pre8 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            y8 = ops.linear(xq, wq, b, act=ops.ACT_SILU, pre=pre8, drop_p=0.1, seed=5, x_mx=sx, w_mx=sw)
+            pre32 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            y32 = ops.linear(xd, wd, b, act=ops.ACT_SILU, pre=pre32, drop_p=0.1, seed=5, out_dtype=torch.bfloat16)
+            assert _rel(pre8.float(), pre32.float()) < 8e-3
+            assert torch.equal(y8 == 0, y32 == 0)
+            assert _rel(y8.float(), y32.float()) < 1e-2
+        else:
+            res = torch.randn(M, N, generator=g).to(DEV)
+            y8 = ops.linear(xq, wq, b, out_dtype=torch.float32, drop_p=0.1, seed=6, out_scale=0.5, residual=res,
+                            x_mx=sx, w_mx=sw)
+            y32 = ops.linear(xd, wd, b, out_dtype=torch.float32, drop_p=0.1, seed=6, out_scale=0.5, residual=res)
+            assert _rel(y8, y32) < 1e-5

@@ -11,7 +11,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-from nn_conformer_for_speech_recognition_amd import ops  # noqa: E402
+from nn_conformer_for_speech_recognition_amd import _lib, ops  # noqa: E402
 
 DEV = "cuda"
 
@@ -373,6 +373,42 @@ def test_wgrad_group_matches_per_gemm():
     for (dw, db), (rw, rb) in zip(outs, refs):
         assert _rel(dw, rw) < 1e-5
         assert _rel(db, rb) < 1e-5
+
+
+def test_wgrad_group_planned_l15_matches_unplanned():
+    """The planned grouped launch (cfm_wgrad_group_plan: whole-task rounds per XCD, the ragged last round's 28
+    tiles split over 8 K slices + the slab reduction) at the L15 backward's exact task list (17 layers x 8 GEMMs,
+    M 11,936) against the unplanned launch: unsplit tasks bit-identical (same tiles, same k order), split tasks
+    within fp32 summation-order noise; the split tasks against fp32 references too."""
+    M, d, F = 32 * 373, 512, 2048
+    g = torch.Generator(device=DEV).manual_seed(3)
+    shapes = [(d, F), (F, d), (d, d), (2 * d, d), (d, d), (3 * d, d), (d, F), (F, d)]   # backward order, per layer
+    pairs = [(torch.randn(M, n, device=DEV, generator=g).to(torch.bfloat16),
+              torch.randn(M, k, device=DEV, generator=g).to(torch.bfloat16)) for _ in range(17) for n, k in shapes]
+    res = {}
+    try:
+        for plan in (False, True):
+            ops.WGRAD_PLAN = plan
+            grp = ops.WgradGroup()
+            res[plan] = [grp.add(dy, x) for dy, x in pairs]
+            grp.flush()
+            torch.cuda.synchronize()
+    finally:
+        ops.WGRAD_PLAN = True
+    lib = _lib.load()
+    tiles = np.array([lib.cfm_wgrad_group_tiles(dy.shape[1], x.shape[1]) for dy, x in pairs], dtype=np.int64)
+    cap = int(tiles.sum()) * 16 + 512
+    sched, split = np.empty(cap, dtype=np.uint32), np.zeros(len(pairs), dtype=np.int32)
+    assert lib.cfm_wgrad_group_plan(tiles.ctypes.data, len(pairs), 8, 32, sched.ctypes.data, cap, split.ctypes.data) > 0
+    assert (split > 1).sum() == 7
+    for i, ((w0, b0), (w1, b1)) in enumerate(zip(res[False], res[True])):
+        if split[i] == 1:
+            assert torch.equal(w0, w1) and torch.equal(b0, b1), i
+        else:
+            assert _rel(w1, w0) < 1e-6 and _rel(b1, b0) < 1e-6, i
+            dy, x = pairs[i]
+            assert _rel(w1, dy.float().T @ x.float()) < 1e-5
+            assert _rel(b1, dy.float().sum(0)) < 1e-5
 
 
 @pytest.mark.parametrize("M", [1000, 11936, 37])

@@ -127,3 +127,60 @@ def test_hparams_surface():
     hp.set_max_len(40)
     hp.set_blank_index(0)
     assert (hp.input_rows, hp.input_cols, hp.max_len, hp.blank_idx) == (40, 40, 40, 0)
+
+
+def _plan(tiles, nxcd=8, cus=32):
+    from nn_conformer_for_speech_recognition_amd import _lib
+    lib = _lib.load()
+    t = np.array(tiles, dtype=np.int64)
+    cap = int(t.sum()) * 16 + 64 * nxcd
+    sched = np.empty(cap, dtype=np.uint32)
+    split = np.zeros(len(tiles), dtype=np.int32)
+    grid = lib.cfm_wgrad_group_plan(t.ctypes.data, len(tiles), nxcd, cus, sched.ctypes.data, cap, split.ctypes.data)
+    assert grid > 0
+    return sched[:grid], split
+
+
+def _check_plan(tiles, sched, split, nxcd):
+    """every (task, tile) covered exactly once per K slice of its task; padding only at the end of an XCD list"""
+    EMPTY = 0xFFFFFFFF
+    seen = {}
+    for w in sched.tolist():
+        if w == EMPTY:
+            continue
+        task, ks, tile = w >> 20, (w >> 16) & 15, w & 0xFFFF
+        assert tile < tiles[task] and ks < split[task]
+        seen[(task, tile, ks)] = seen.get((task, tile, ks), 0) + 1
+    want = {(i, t, s) for i, n in enumerate(tiles) for t in range(n) for s in range(split[i])}
+    assert set(seen) == want and all(v == 1 for v in seen.values())
+    lists = sched.reshape(-1, nxcd).T                  # XCD x: workgroups x, x + nxcd, ...
+    for l in lists:
+        nz = np.nonzero(l != EMPTY)[0]
+        assert len(nz) == 0 or nz[-1] == len(nz) - 1      # no padding before real work
+
+
+def test_wgrad_plan_l15_layout():
+    """The L15 backward (17 layers x [FFN2 down/up, pw2, pw1, out, QKV, FFN1 down/up] = 16,16,4,8,4,12,16,16 tiles):
+    6 full rounds of 32 tiles per XCD made of whole tasks, and the 28 leftover tiles (seven 4-tile tasks) split
+    over 8 K slices, one slice per XCD."""
+    layer = [16, 16, 4, 8, 4, 12, 16, 16]
+    tiles = layer * 17
+    sched, split = _plan(tiles)
+    _check_plan(tiles, sched, split, 8)
+    assert sorted(set(split.tolist())) == [1, 8] and sum(tiles[i] for i in range(len(tiles)) if split[i] > 1) == 28
+    assert len(sched) == 8 * (6 * 32 + 28)
+    lists = sched.reshape(-1, 8).T
+    for x, l in enumerate(lists):
+        rounds = l[: 6 * 32].reshape(6, 32)
+        for r in rounds:                                  # each round: whole tasks only
+            tasks = r >> 20
+            for t in set(tasks.tolist()):
+                assert (tasks == t).sum() == tiles[t]
+        assert set(((l[6 * 32:] >> 16) & 15).tolist()) == {x}   # the tail: K slice x on XCD x
+
+
+@pytest.mark.parametrize("tiles,nxcd,cus", [([3, 70, 1, 5], 8, 32), ([40] * 9, 8, 32), ([1], 8, 32),
+                                            ([7, 9, 33, 2, 64, 5], 2, 4), ([32] * 16, 8, 32)])
+def test_wgrad_plan_covers_every_tile(tiles, nxcd, cus):
+    sched, split = _plan(tiles, nxcd, cus)
+    _check_plan(tiles, sched, split, nxcd)
