@@ -17,6 +17,7 @@ run() {   # name limit cmd...
   if [ $rc -ge 124 ]; then echo "ABORT: $name rc=$rc"; exit $rc; fi
   return 0
 }
+NC=0
 for s in "$@"; do
   case $s in
     fulldepth) run fulldepth 900 "$PYT -s tests/test_gpu_fulldepth.py" ;;
@@ -36,7 +37,7 @@ for s in "$@"; do
     trace|trace:*)   # rocprofv3 kernel trace of a bench.py run -> profiles/summarize_trace.py family figures
       cfg=${s#trace}; cfg=${cfg#:}; cfg=${cfg:-L15}
       run trace_$cfg 600 "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$cfg -o run -- python3 $R/bench.py --config $cfg --steps 10 --warmup 3 --no-cpu-baseline > $OUT/trace_bench_$cfg.json && python3 $R/profiles/summarize_trace.py \$(find $OUT/trace_$cfg -name '*kernel_trace.csv' | head -1) $OUT/trace_$cfg.json --config $cfg --warmup 3 --steps 10 --lib $R/nn_conformer_for_speech_recognition_amd/libcfm.so > $OUT/trace_summary_$cfg.txt && python3 $R/profiles/summarize.py \$(find $OUT/trace_$cfg -name '*kernel_stats.csv' | head -1) auto 45 > $OUT/kernel_summary_$cfg.txt" ;;
-    *) run custom 900 "$s" ;;
+    *) NC=$((NC + 1)); run custom$NC 900 "$s" ;;
   esac
 done
 echo "=== session done"

@@ -180,6 +180,11 @@ typedef struct cfm_gemm_desc {
      applies them per 32-element run (alpha_*_dev must be NULL).  K % 128 == 0, K <= 2048. */
   const uint8_t* mx_a;
   const uint8_t* mx_b;
+  /* optional second output (MX fp8 launches with the FFN-up epilogue -- bias + SiLU + bf16 pre + dropout, bf16 C,
+     ldc == N, N % 32 == 0): the MX e4m3 copy of the bf16 C, exactly cfm_quant_mx of it -- mx_out (M x N e4m3),
+     mx_out_scales (M x N/32 e8m0) -- the next fp8 GEMM's operand, written by the same epilogue.  NULL: off. */
+  void* mx_out;
+  uint8_t* mx_out_scales;
 } cfm_gemm_desc;
 int cfm_gemm(const cfm_gemm_desc* d, void* stream);
 /* Per-tensor fp8 (e4m3fn) quantisation for the fp8 GEMM path (configs[4]; no reference counterpart -- the
@@ -293,6 +298,11 @@ int cfm_colsum(const void* x, int dtype_x, long M, int N, long ld, float* out, i
  * dgamma/dbeta accumulate (+=) over rows.  ws: >= 8*D*nblk bytes, see cfm_layernorm_ws_bytes. */
 int cfm_layernorm_fwd(const void* x, int dtype_x, const float* gamma, const float* beta, void* y,
                       int dtype_y, float* mean, float* rstd, long M, int D, float eps, void* stream);
+/* The same forward (fp32 x, bf16 y) with a second output: y's MX e4m3 copy -- y8 (M x D e4m3) and s8
+   (M x D/32 e8m0), exactly cfm_quant_mx of the bf16 y -- for the fp8 forward GEMM that consumes it
+   (configs[4]); D in {256, 512, 1024}. */
+int cfm_layernorm_fwd_mx(const float* x, const float* gamma, const float* beta, void* y, void* y8, uint8_t* s8,
+                         float* mean, float* rstd, long M, int D, float eps, void* stream);
 size_t cfm_layernorm_ws_bytes(long M, int D);
 int cfm_layernorm_bwd(const void* dy, int dtype_dy, const void* x, int dtype_x, const float* gamma,
                       const float* mean, const float* rstd, const void* dres, int dtype_dres,

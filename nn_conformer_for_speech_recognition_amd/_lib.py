@@ -45,6 +45,7 @@ class GemmDesc(ctypes.Structure):
         ("alpha_a_dev", c_void_p), ("alpha_b_dev", c_void_p),
         ("allow_overlap", c_int),
         ("mx_a", c_void_p), ("mx_b", c_void_p),
+        ("mx_out", c_void_p), ("mx_out_scales", c_void_p),
     ]
 
 
@@ -76,6 +77,7 @@ _SIGS = {
     "cfm_quant_fp8_batch_blocks": (c_long, [c_long]),
     "cfm_quant_fp8_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_void_p]),
     "cfm_dequant_fp8": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
+    "cfm_layernorm_fwd_mx": (c_int, [c_void_p] * 8 + [c_long, c_int, c_float, c_void_p]),
     "cfm_quant_mx": (c_int, [c_void_p, c_int, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p]),
     "cfm_quant_mx_batch_blocks": (c_long, [c_long, c_int]),
     "cfm_quant_mx_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p]),

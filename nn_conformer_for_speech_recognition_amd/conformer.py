@@ -185,30 +185,50 @@ def _wt(cfg, i):
     return cfg.shadow_t.get(i) if cfg.shadow_t else None
 
 
-def _fp8_linear(x, cfg, i, **kw):
+def _fp8_on(cfg, i, K):
+    return bool(cfg.shadow8) and i in cfg.shadow8 and K % 128 == 0
+
+
+def _ln_fwd(x, P, i, cfg, fp8_w=None):
+    """the module-input LayerNorm; when the consumer GEMM (weight fp8_w) runs on MX fp8, the same kernel also
+    writes the MX copy of its bf16 output (cfm_layernorm_fwd_mx): -> (xn, (xn8, s8) or None, mu, rs)"""
+    if fp8_w is not None and FP8_MX and cfg.cd == torch.bfloat16 and _fp8_on(cfg, fp8_w, x.shape[1]):
+        xn, q, mu, rs = ops.layernorm_fwd_mx(x, P[i], P[i + 1], _EPS)
+        return xn, q, mu, rs
+    xn, mu, rs = ops.layernorm_fwd(x, P[i], P[i + 1], _EPS, out_dtype=cfg.cd)
+    return xn, None, mu, rs
+
+
+def _fp8_linear(x, cfg, i, xq=None, **kw):
     """Forward GEMM with fp8 (e4m3fn) operands when the layer runs the fp8 path (BASELINE.json configs[4]):
     x quantised on the device -- MX block scales (one e8m0 per 32 K-elements, one pass, applied inside the
     block-scaled MFMA), or per tensor with CFM_FP8_SCALING=tensor (A/B) -- weight i from the per-step fp8 shadow;
     else None.  The backward keeps the bf16 operands (x, the bf16 weight shadow)."""
-    if not cfg.shadow8 or i not in cfg.shadow8 or x.shape[1] % 128:
+    if not _fp8_on(cfg, i, x.shape[1]):
         return None
     wq, sw = cfg.shadow8[i]
     if FP8_MX:
-        xq, sx = ops.quant_mx(x)
-        return ops.linear(xq, wq, x_mx=sx, w_mx=sw, **kw)
+        x8, sx = xq if xq is not None else ops.quant_mx(x)
+        return ops.linear(x8, wq, x_mx=sx, w_mx=sw, **kw)
     xq, sx = ops.quant_fp8(x)
     return ops.linear(xq, wq, x_scale=sx, w_scale=sw, **kw)
 
 
 def _ffn_fwd(x, P, o, cfg, seed):
     cd = cfg.cd
-    xn, mu, rs = ops.layernorm_fwd(x, P[o], P[o + 1], _EPS, out_dtype=cd)
+    xn, xq, mu, rs = _ln_fwd(x, P, o, cfg, o + 2)
     w1, w2 = _w(P[o + 2], cd), _w(P[o + 4], cd)
     pre = torch.empty(x.shape[0], cfg.ffn, device=x.device, dtype=cd)
-    h = _fp8_linear(xn, cfg, o + 2, bias=P[o + 3], act=ACT_SILU, pre=pre, drop_p=cfg.p, seed=seed)
+    # MX fp8 for both FFN GEMMs: the up-projection's epilogue also writes the MX copy of h (the down GEMM's operand)
+    hq = None
+    if FP8_MX and _fp8_on(cfg, o + 2, xn.shape[1]) and _fp8_on(cfg, o + 4, cfg.ffn) and cfg.ffn % 32 == 0:
+        hq = (torch.empty(x.shape[0], cfg.ffn, device=x.device, dtype=torch.float8_e4m3fn),
+              torch.empty(x.shape[0], cfg.ffn // 32, device=x.device, dtype=torch.uint8))
+    h = _fp8_linear(xn, cfg, o + 2, xq=xq, bias=P[o + 3], act=ACT_SILU, pre=pre, drop_p=cfg.p, seed=seed,
+                    **({"mx_out": hq} if hq is not None else {}))
     if h is None:
         h = ops.linear(xn, w1, P[o + 3], act=ACT_SILU, pre=pre, drop_p=cfg.p, seed=seed)
-    y = _fp8_linear(h, cfg, o + 4, bias=P[o + 5], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1,
+    y = _fp8_linear(h, cfg, o + 4, xq=hq, bias=P[o + 5], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1,
                     out_scale=0.5, residual=x)
     if y is None:
         y = ops.linear(h, w2, P[o + 5], out_dtype=torch.float32, drop_p=cfg.p, seed=seed + 1, out_scale=0.5,
@@ -257,9 +277,9 @@ def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads, side, g2=None, nxt=None):
 def _mha_fwd(x, P, R, cfg, seed, lens):
     cd = cfg.cd
     B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
-    xn, mu, rs = ops.layernorm_fwd(x, P[6], P[7], _EPS, out_dtype=cd)
+    xn, xq, mu, rs = _ln_fwd(x, P, 6, cfg, 8)
     win, wout = _w(P[8], cd), _w(P[10], cd)
-    qkv = _fp8_linear(xn, cfg, 8, bias=P[9])
+    qkv = _fp8_linear(xn, cfg, 8, xq=xq, bias=P[9])
     if qkv is None:
         qkv = ops.linear(xn, win, P[9])
     pos = pu = pv = None

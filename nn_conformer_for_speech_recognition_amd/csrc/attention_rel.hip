@@ -63,11 +63,6 @@ __device__ __forceinline__ void load_q_uv(const AttnM& p, const RelP& rp, int b,
   }
 }
 
-// s_waitcnt vmcnt(0) as a real instruction the compiler's wait insertion accounts for (inline asm is opaque to
-// it): issued once after a kernel's prologue loads (q fragments, K/V of the head) so that their first use inside
-// the tile loop does not make the compiler wait for everything outstanding -- the prefetch just issued included --
-// on every iteration.  gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15.
-__device__ __forceinline__ void wait_prologue_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 // 16-B chunk `v` (0..511) of a 64-row chunk of the band: row v>>3, columns (v&7)*8.  VEC: relative rows
 // outside [0, 2T-1) clamp to the nearest valid row instead of reading zero (branch-free prefetch, ld8c):

@@ -254,6 +254,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const bf16* base, lo
 }
 
 // piece `pc` (rows 8 pc .. 8 pc + 7) of the image at `img`: lane l's 16 B from row 8 pc + l / 8
+// (m0 is declared clobbered -- the asm does overwrite it -- which clang reports as a reserved register; silenced here)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void head_dma_piece(__amdgpu_buffer_rsrc_t r, char* img, int pc, long ld, int nrows,
                                                int lane) {
   const int row = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
@@ -263,6 +266,13 @@ __device__ __forceinline__ void head_dma_piece(__amdgpu_buffer_rsrc_t r, char* i
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                :: "s"(l), "v"(voff), "s"(r) : "memory", "m0");
 }
+#pragma clang diagnostic pop
+
+// s_waitcnt vmcnt(0) as a real instruction the compiler's wait insertion accounts for (inline asm is opaque to
+// it): issued once after a kernel's prologue loads (q fragments, K/V of the head) so that their first use inside
+// the tile loop does not make the compiler wait for everything outstanding -- the prefetch just issued included --
+// on every iteration.  gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15.
+__device__ __forceinline__ void wait_prologue_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n
 __device__ __forceinline__ void wait_vm_n(int n) {

@@ -206,4 +206,4 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -53,6 +53,8 @@ struct GemmP {
   const uint8_t* mxa;          // MX fp8 operands (cfm_gemm_desc.mx_a / mx_b): e8m0 block scales [rows][mxk]
   const uint8_t* mxb;
   int mxk;                     // blocks of 32 fp8 per row (K / 32)
+  uint8_t* mxo8;               // EF_BF16_SILU_MX: the MX e4m3 copy of the bf16 C (cfm_gemm_desc.mx_out)
+  uint8_t* mxos;               //   and its e8m0 block scales [M][N/32]
 };
 
 // salt the dropout seed and hoist the per-launch constants (hash key of the low 2^33 index range,
@@ -527,6 +529,8 @@ template <bool M16> __device__ __forceinline__ int accc(int r, int lane) {
 //   EF_BF16_RD   bf16 C; rowdot with rd_with (attention out-projection data gradient)
 //   EF_F32       f32 C; alpha, bias, SiLU (+ pre), dropout, out_scale as run-time options
 //   EF_F32_RES   f32 C; bias, dropout, out_scale, f32 residual (the d-wide residual-stream outputs)
+//   EF_BF16_SILU_MX  EF_BF16_SILU + the MX e4m3 copy of the bf16 C (fp8 FFN-up forward: the FFN-down GEMM's
+//                operand; the 4 threads of a 32-column block exchange maxima by two xor shuffles)
 // Every option a kind does not list is absent by construction (epi_fast_kind checks): a run-time test on a
 // uniform kernel argument is flattened by the compiler into per-lane selects with BOTH sides computed (the SiLU
 // of the bias-only QKV rows, the alpha and out_scale products), so the encoder's kinds carry no such tests.
@@ -537,7 +541,16 @@ template <bool M16> __device__ __forceinline__ int accc(int r, int lane) {
 // epilogue without the main loop: 49 MB in 21.9 us = 2.2 TB/s).  Arithmetic and its order are epilogue_store8's
 // (bit-identical outputs).
 enum { EF_GENERIC = 0, EF_BF16 = 1, EF_BF16_BIAS = 2, EF_BF16_SILU = 3, EF_BF16_ACTG = 4, EF_BF16_RD = 5, EF_F32 = 6,
-       EF_F32_RES = 7 };
+       EF_F32_RES = 7, EF_BF16_SILU_MX = 8 };
+
+// e8m0 block exponent of an MX block (fp8.hip mx_k): the largest k with amax * 2^k <= 448
+__device__ __forceinline__ int epi_mx_k(float a) {
+  if (!(a > 0.f) || !(a < INFINITY)) return 0;
+  int e;
+  const float m = 2.f * frexpf(a, &e);
+  const int k = (m <= 1.75f ? 8 : 7) - (e - 1);
+  return k < 126 ? (k > -126 ? k : -126) : 126;
+}
 
 __device__ __forceinline__ void epi_bias8(const GemmP& p, int n, float (&b)[8]) {
 #pragma unroll
@@ -604,11 +617,12 @@ __device__ __forceinline__ void epi_load_all(const GemmP& p, int z, int mbase, i
 template <int EK, int IT, int NTt, int CPW, int EPS, bool PRE = false>
 __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, int z, int mbase, int n0, int tid,
                                               const float (&b)[8], EpiIn<EK, IT>& in) {
-  static_assert(EK > EF_GENERIC && EK <= EF_F32_RES, "fast epilogue kind");
+  static_assert(EK > EF_GENERIC && EK <= EF_BF16_SILU_MX, "fast epilogue kind");
   constexpr bool CF32 = EK == EF_F32 || EK == EF_F32_RES, ACTG = EK == EF_BF16_ACTG, RD = EK == EF_BF16_RD;
   constexpr bool RES = EK == EF_F32_RES, GEN = EK == EF_F32;   // GEN: the run-time options of EF_F32
-  constexpr bool BIAS = EK == EF_BF16_BIAS || EK == EF_BF16_SILU || RES, SILU = EK == EF_BF16_SILU;
-  constexpr bool DROP = EK == EF_BF16_SILU || ACTG || RES || GEN;
+  constexpr bool MXO = EK == EF_BF16_SILU_MX;
+  constexpr bool SILU = EK == EF_BF16_SILU || MXO, BIAS = EK == EF_BF16_BIAS || SILU || RES;
+  constexpr bool DROP = SILU || ACTG || RES || GEN;
   constexpr int NW = epi_nw<EK>();
   constexpr int RPI = NTt / CPW;                       // rows per pass
   const int c8 = (tid % CPW) * 8, n = n0 + c8, r0 = tid / CPW;
@@ -692,6 +706,22 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
 #pragma unroll
         for (int e = 0; e < 8; ++e) q[e] = (bf16)v[e];
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.C) + cidx) = __builtin_bit_cast(uint4, q);
+        if constexpr (MXO) {   // (N % 32 == 0: a block's 4 threads share the row, so all four are here)
+          float mx = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf((float)q[e]));
+          mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+          mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+          const int k = epi_mx_k(mx);
+          const float sc = ldexpf(1.f, k);
+          int lo = 0, hi = 0;
+          lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)q[0] * sc, (float)q[1] * sc, lo, false);
+          lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)q[2] * sc, (float)q[3] * sc, lo, true);
+          hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)q[4] * sc, (float)q[5] * sc, hi, false);
+          hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)q[6] * sc, (float)q[7] * sc, hi, true);
+          *reinterpret_cast<uint2*>(p.mxo8 + (long)m * p.N + n) = make_uint2((unsigned)lo, (unsigned)hi);
+          if ((tid & 3) == 0) p.mxos[(long)m * (p.N / 32) + n / 32] = (uint8_t)(127 - k);
+        }
       }
     }
     if constexpr (RD) {   // 8-lane group = 64 columns (as tile_epilogue_g's generic rows)
@@ -964,9 +994,9 @@ __device__ __forceinline__ bool group_task(const GatherA& ga, GemmP& p, PipeOp& 
 
 // F8: A and B are fp8 e4m3 (OCP), K-major, viewed as bf16 PAIRS by everything up to the LDS image (K, ld and
 // the tile geometry in 2-byte units, so DMA, swizzle and ring are byte-identical to the bf16 kernel); each
-// 64-fp8 k-step (4 16-B chunks of a row) feeds one v_mfma_scale_f32_32x32x64_f8f6f4: lane (r, h) holds the
-// 32 bytes k = 32h .. 32h+31 (chunks 2h, 2h+1).  Unit block scales; the per-tensor dequantisation
-// (alpha_a * alpha_b) is applied in the epilogue.
+// 64-fp8 k-step (4 16-B chunks of a row) feeds one v_mfma_scale_f32_32x32x64_f8f6f4: lane (r, h) holds chunks h
+// and h + 2 (the instruction's k order, see frag8).  Per-tensor fp8: unit block scales, the dequantisation
+// (alpha_a * alpha_b) applied in the epilogue; MX: the e8m0 block scales below.
 // M16: the main loop on v_mfma_f32_16x16x32_bf16 (each 32x32 block of a wave's tile as four 16x16 blocks; same
 // LDS images, fragments per k and accumulator registers) -- K-major plain operands only.  On random data the
 // chip holds a higher clock under the 16x16 shape than under 32x32x16 (MI355X_MICROARCH.md, DVFS item 7).
@@ -1125,10 +1155,14 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
           sB[j] = BKt == 64 ? *reinterpret_cast<const unsigned*>(b) : *reinterpret_cast<const unsigned short*>(b);
         }
       }
+      // v_mfma_scale_f32_32x32x64_f8f6f4's k order (measured, benchmarks/mx_probe.hip): lane (r, h) bytes 0-15 hold
+      // k = 16h .. 16h+15 and bytes 16-31 k = 32+16h .. 32+16h+15 of the 64-step; the scale of lane r covers k 0..31
+      // (bytes 0-15 of both halves), that of lane r+32 k 32..63 -- so lane (r, h) loads 16-B chunks h and h + 2 of
+      // the step, and MX block 2q + h's scale sits in lane (r, h)
       auto frag8 = [&](const char* img, int row0, int q) {
-        const int r = row0 + (lane & 31), c = 4 * q + 2 * (lane >> 5);
+        const int r = row0 + (lane & 31), c = 4 * q + (lane >> 5);
         const uint4 lo = *reinterpret_cast<const uint4*>(img + r * S::RB + 16 * S::slot(r, c));
-        const uint4 hi = *reinterpret_cast<const uint4*>(img + r * S::RB + 16 * S::slot(r, c + 1));
+        const uint4 hi = *reinterpret_cast<const uint4*>(img + r * S::RB + 16 * S::slot(r, c + 2));
         i32x8 v;
         v[0] = (int)lo.x; v[1] = (int)lo.y; v[2] = (int)lo.z; v[3] = (int)lo.w;
         v[4] = (int)hi.x; v[5] = (int)hi.y; v[6] = (int)hi.z; v[7] = (int)hi.w;
@@ -1753,6 +1787,7 @@ void ek_dispatch(int ek, F&& f) {
       case EF_BF16_RD: f(std::integral_constant<int, EF_BF16_RD>{}); return;
       case EF_F32: f(std::integral_constant<int, EF_F32>{}); return;
       case EF_F32_RES: f(std::integral_constant<int, EF_F32_RES>{}); return;
+      case EF_BF16_SILU_MX: f(std::integral_constant<int, EF_BF16_SILU_MX>{}); return;
       default: break;
     }
   }
@@ -1854,7 +1889,8 @@ int epi_fast_kind(const GemmP& p, int batch) {
   if (p.rd_out)
     return bf && !p.bias && a1 && s1 && !silu && p.drop_p <= 0.f ? EF_BF16_RD : EF_GENERIC;
   if (f32) return silu && p.pre && p.dtpre != CFM_BF16 ? EF_GENERIC : EF_F32;
-  if (silu) return p.pre && p.dtpre == CFM_BF16 && p.bias && a1 && s1 ? EF_BF16_SILU : EF_GENERIC;
+  if (silu) return p.pre && p.dtpre == CFM_BF16 && p.bias && a1 && s1 ? (p.mxo8 ? EF_BF16_SILU_MX : EF_BF16_SILU)
+                                                                        : EF_GENERIC;
   if (p.drop_p > 0.f || !a1 || !s1) return EF_GENERIC;
   return p.bias ? EF_BF16_BIAS : EF_BF16;
 }
@@ -1894,7 +1930,12 @@ int launch_fp8(const cfm_gemm_desc& d, GemmP p, hipStream_t s) {
     p.mxa = d.mx_a;
     p.mxb = d.mx_b;
     p.mxk = d.K / 32;
+    p.mxo8 = (uint8_t*)d.mx_out;
+    p.mxos = d.mx_out_scales;
     p.efast = epi_fast_kind(p, 1);
+    if (p.mxo8 && p.efast != EF_BF16_SILU_MX)
+      return cfm::fail(CFM_ERR_UNSUPPORTED, "cfm_gemm: mx_out needs the FFN-up epilogue (bias + SiLU + bf16 pre, "
+                                            "bf16 C, ldc == N, N % 32 == 0)");
     if (p.N <= 512 || d.K > 512) {
       // d-wide outputs, and any K > 512 (the 2048-deep scale rows -- 20 KiB -- do not fit beside a two-per-CU ring)
       const dim3 g(cdiv(p.N, BN), cdiv(p.M, 192), 1);
@@ -1958,6 +1999,7 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
   p.out_scale = d->out_scale; p.res = d->residual; p.ldr = d->ldr; p.dtr = d->dtype_r;
   p.split_k = split;
   p.probe = d->probe;
+  CFM_REQUIRE(!d->mx_out || d->dtype_ab == CFM_FP8, CFM_ERR_UNSUPPORTED, "mx_out: fp8 MX launches only");
   if (d->dtype_ab == CFM_FP8) {
     CFM_REQUIRE(d->a_kmajor && d->b_kmajor && d->K % 128 == 0 && d->lda % 16 == 0 && d->ldb % 16 == 0 &&
                     (uintptr_t)d->A % 16 == 0 && (uintptr_t)d->B % 16 == 0 && split == 1 && d->batch == 1 &&
@@ -1966,6 +2008,9 @@ CFM_EXPORT int cfm_gemm(const cfm_gemm_desc* d, void* stream) {
                 CFM_ERR_UNSUPPORTED, "fp8: K-major A and B, K % 128 == 0, 16-B aligned rows, no split-K / batch");
     CFM_REQUIRE(!d->mx_a == !d->mx_b && (!d->mx_a || (d->K <= 2048 && !d->alpha_a_dev && !d->alpha_b_dev)),
                 CFM_ERR_ARG, "fp8 MX: both scale tensors, K <= 2048, no per-tensor alpha");
+    CFM_REQUIRE(!d->mx_out || (d->mx_a && d->mx_out_scales && d->dtype_c == CFM_BF16 && d->ldc == d->N &&
+                               d->N % 32 == 0 && (uintptr_t)d->mx_out % 8 == 0),
+                CFM_ERR_UNSUPPORTED, "mx_out: MX operands, bf16 C with ldc == N, N % 32 == 0");
     return launch_fp8(*d, p, cfm::as_stream(stream));
   }
   const bool bf = d->dtype_ab == CFM_BF16;

@@ -76,11 +76,49 @@ template <int V> __device__ __forceinline__ void stv(bf16* p, const float (&v)[V
 // LN_FWD_ROWS rows per wave: every row's load is issued before the first reduction, so a wave keeps
 // that many 2-KB row reads in flight (one row per wave left the kernel latency-bound at ~50 % of HBM)
 constexpr int LN_FWD_ROWS = 2;
-template <int V, typename TY>
+// MX: a second output of the bf16 y -- its MX e4m3 copy (cfm_quant_mx's bytes and block scales of the bf16 values,
+// for the fp8 forward GEMM that consumes it): the 32 / V lanes of a 32-feature block exchange their maxima by xor
+// shuffles, so the copy costs its 1.03 bytes per element of stores instead of a separate 3-byte pass.
+struct LnMx {
+  uint8_t* y8;    // M x D e4m3
+  uint8_t* s8;    // M x D/32 e8m0
+};
+__device__ __forceinline__ int ln_mx_k(float a) {   // = fp8.hip mx_k
+  if (!(a > 0.f) || !(a < INFINITY)) return 0;
+  int e;
+  const float m = 2.f * frexpf(a, &e);
+  const int k = (m <= 1.75f ? 8 : 7) - (e - 1);
+  return k < 126 ? (k > -126 ? k : -126) : 126;
+}
+template <int V>
+__device__ __forceinline__ void ln_store_mx(const LnMx& mx, long row, int D, int lane, const float (&v)[V]) {
+  constexpr int LPB = 32 / V;       // lanes per 32-feature block
+  float q[V], m = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    q[i] = (float)(bf16)v[i];       // the bf16 value the GEMM would otherwise read
+    m = fmaxf(m, fabsf(q[i]));
+  }
+#pragma unroll
+  for (int o = 1; o < LPB; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const int k = ln_mx_k(m);
+  const float sc = ldexpf(1.f, k);
+  uint8_t* yp = mx.y8 + row * D + lane * V;
+#pragma unroll
+  for (int i = 0; i < V; i += 4) {
+    int w = 0;
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(q[i] * sc, q[i + 1] * sc, w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(q[i + 2] * sc, q[i + 3] * sc, w, true);
+    *reinterpret_cast<int*>(yp + i) = w;
+  }
+  if (lane % LPB == 0) mx.s8[row * (D / 32) + lane / LPB] = (uint8_t)(127 - k);
+}
+
+template <int V, typename TY, bool MX = false>
 __global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, TY* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
-                                                  float eps) {
+                                                  float eps, LnMx mx = {}) {
   constexpr int D = 64 * V, R = LN_FWD_ROWS;
   const int lane = threadIdx.x & 63;
   const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
@@ -114,6 +152,7 @@ __global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, c
 #pragma unroll
       for (int i = 0; i < V; ++i) v[r][i] = v[r][i] * rstd * g[i] + b[i];
       stv<V>(y + (row0 + r) * D + lane * V, v[r]);
+      if constexpr (MX) ln_store_mx<V>(mx, row0 + r, D, lane, v[r]);
       if (lane == 0) {
         mean_out[row0 + r] = mean;
         rstd_out[row0 + r] = rstd;
@@ -300,10 +339,19 @@ bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0;
 
 template <int V>
 bool ln_fwd_fast(const void* x, int dtx, const float* gamma, const float* beta, void* y, int dty, float* mean,
-                 float* rstd, long M, int D, float eps, hipStream_t s) {
+                 float* rstd, long M, int D, float eps, hipStream_t s, LnMx mx = {}) {
   if (D != 64 * V || dtx != CFM_F32 || !aligned16(x) || !aligned16(y) || !aligned16(gamma) || !aligned16(beta))
     return false;
   dim3 g((unsigned)((M + 4 * LN_FWD_ROWS - 1) / (4 * LN_FWD_ROWS)));
+  if (mx.y8) {
+    if constexpr (V >= 4) {
+      if (dty != CFM_BF16) return false;
+      hipLaunchKernelGGL((ln_fwd_vec<V, bf16, true>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (bf16*)y, mean,
+                         rstd, M, eps, mx);
+      return true;
+    }
+    return false;
+  }
   if (dty == CFM_BF16)
     hipLaunchKernelGGL((ln_fwd_vec<V, bf16>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (bf16*)y, mean, rstd, M,
                        eps);
@@ -344,6 +392,21 @@ CFM_EXPORT int cfm_layernorm_fwd(const void* x, int dtx, const float* gamma, con
     hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, dtx, gamma, beta, y, dty,
                        mean, rstd, M, D, eps);
   return cfm::check_launch("cfm_layernorm_fwd");
+}
+
+CFM_EXPORT int cfm_layernorm_fwd_mx(const float* x, const float* gamma, const float* beta, void* y, void* y8,
+                                    uint8_t* s8, float* mean, float* rstd, long M, int D, float eps, void* stream) {
+  CFM_REQUIRE(x && gamma && beta && y && y8 && s8 && mean && rstd, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE((D == 256 || D == 512 || D == 1024) && M >= 0, CFM_ERR_SHAPE, "D in {256, 512, 1024}");
+  CFM_REQUIRE((uintptr_t)y8 % 8 == 0, CFM_ERR_ALIGN, "8-B aligned y8");
+  if (M == 0) return CFM_OK;
+  hipStream_t s = cfm::as_stream(stream);
+  const LnMx mx{(uint8_t*)y8, s8};
+  const bool ok = ln_fwd_fast<4>(x, CFM_F32, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx) ||
+                  ln_fwd_fast<8>(x, CFM_F32, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx) ||
+                  ln_fwd_fast<16>(x, CFM_F32, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx);
+  CFM_REQUIRE(ok, CFM_ERR_ALIGN, "16-B aligned x / y / gamma / beta");
+  return cfm::check_launch("cfm_layernorm_fwd_mx");
 }
 
 CFM_EXPORT size_t cfm_layernorm_ws_bytes(long M, int D) {

@@ -21,10 +21,11 @@ def _gemm_desc(**kw):
 def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None, alpha=1.0,
          bias=None, act=ACT_NONE, act_grad=False, pre=None, drop_p=0.0, seed=0, offset=0, out_scale=1.0,
          residual=None, ldr=None, split_k=1, batch=1, stride_a=0, stride_b=0, stride_c=0, workspace=None,
-         a_colsum=None, rowdot=None, alpha_a=None, alpha_b=None, allow_overlap=False, mx_a=None, mx_b=None):
+         a_colsum=None, rowdot=None, alpha_a=None, alpha_b=None, allow_overlap=False, mx_a=None, mx_b=None,
+         mx_out=None):
     """C = epilogue(alpha * A·Bᵀ) — see cfm_gemm_desc in include/cfm.h.  fp8 (e4m3fn) A and B: alpha_a /
     alpha_b are their device dequantisation scalars (quant_fp8), or mx_a / mx_b their e8m0 block scales
-    (quant_mx)."""
+    (quant_mx); mx_out = (y8, s8): the MX copy of a bf16 C written by the same epilogue (fp8 FFN-up)."""
     if A.dtype != B.dtype:
         raise L.CfmError(f"gemm operands differ in dtype: {A.dtype} vs {B.dtype}")
     d = _gemm_desc(
@@ -40,7 +41,8 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
         split_k=int(split_k), workspace=L.ptr(workspace), a_colsum=L.ptr(a_colsum),
         rowdot_with=L.ptr(rowdot[0]) if rowdot else None, rowdot_out=L.ptr(rowdot[1]) if rowdot else None,
         rowdot_T=int(rowdot[2]) if rowdot else 0, alpha_a_dev=L.ptr(alpha_a), alpha_b_dev=L.ptr(alpha_b),
-        allow_overlap=int(bool(allow_overlap)), mx_a=L.ptr(mx_a), mx_b=L.ptr(mx_b))
+        allow_overlap=int(bool(allow_overlap)), mx_a=L.ptr(mx_a), mx_b=L.ptr(mx_b),
+        mx_out=L.ptr(mx_out[0]) if mx_out else None, mx_out_scales=L.ptr(mx_out[1]) if mx_out else None)
     if PROBE is not None:
         PROBE("gemm", (M, N, K), d, lambda: L.call("cfm_gemm", L.ctypes.byref(d), L.stream()))
     else:
@@ -55,7 +57,7 @@ WGRAD_PLAN = os.environ.get("CFM_WGRAD_PLAN", "1") != "0"
 
 
 def linear(x, w, bias=None, out_dtype=None, act=ACT_NONE, pre=None, drop_p=0.0, seed=0, offset=0,
-           out_scale=1.0, residual=None, out=None, x_scale=None, w_scale=None, x_mx=None, w_mx=None):
+           out_scale=1.0, residual=None, out=None, x_scale=None, w_scale=None, x_mx=None, w_mx=None, mx_out=None):
     """y = x·wᵀ (+bias, epilogue) for x (M, K), w (N, K).  fp8 operands pass their dequantisation: per-tensor
     scalars x_scale / w_scale (quant_fp8) or MX block scales x_mx / w_mx (quant_mx); the output then defaults to
     bf16."""
@@ -65,7 +67,8 @@ def linear(x, w, bias=None, out_dtype=None, act=ACT_NONE, pre=None, drop_p=0.0, 
         od = out_dtype or (torch.bfloat16 if x.dtype == torch.float8_e4m3fn else x.dtype)
         out = torch.empty(M, N, device=x.device, dtype=od)
     return gemm(x, w, out, M, N, K, bias=bias, act=act, pre=pre, drop_p=drop_p, seed=seed, offset=offset,
-                out_scale=out_scale, residual=residual, alpha_a=x_scale, alpha_b=w_scale, mx_a=x_mx, mx_b=w_mx)
+                out_scale=out_scale, residual=residual, alpha_a=x_scale, alpha_b=w_scale, mx_a=x_mx, mx_b=w_mx,
+                mx_out=mx_out)
 
 
 def quant_fp8(x, out=None, inv_scale=None):
@@ -546,6 +549,20 @@ def layernorm_fwd(x, gamma, beta, eps=1e-5, out_dtype=None):
     L.call("cfm_layernorm_fwd", L.ptr(x), L.dt(x), L.ptr(gamma), L.ptr(beta), L.ptr(y), L.dt(y), L.ptr(mean),
            L.ptr(rstd), M, D, float(eps), L.stream())
     return y, mean, rstd
+
+
+def layernorm_fwd_mx(x, gamma, beta, eps=1e-5):
+    """layernorm_fwd with a bf16 y AND its MX e4m3 copy from the same kernel: (y, (y8, s8), mean, rstd), y8 / s8
+    exactly quant_mx(y) (cfm_layernorm_fwd_mx)."""
+    M, D = x.shape
+    y = torch.empty(M, D, device=x.device, dtype=torch.bfloat16)
+    y8 = torch.empty(M, D, device=x.device, dtype=torch.float8_e4m3fn)
+    s8 = torch.empty(M, D // 32, device=x.device, dtype=torch.uint8)
+    mean = torch.empty(M, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(M, device=x.device, dtype=torch.float32)
+    L.call("cfm_layernorm_fwd_mx", L.ptr(x), L.ptr(gamma), L.ptr(beta), L.ptr(y), L.ptr(y8), L.ptr(s8), L.ptr(mean),
+           L.ptr(rstd), M, D, float(eps), L.stream())
+    return y, (y8, s8), mean, rstd
 
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, dres=None, dx_dtype=torch.float32, side=None, drop=None):
