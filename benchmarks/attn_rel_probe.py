@@ -14,7 +14,11 @@ ap.add_argument("n", type=int, nargs="?", default=5)
 ap.add_argument("--none", action="store_true", help="no relative positions (tiled kernels)")
 ap.add_argument("--l15", action="store_true", help="the L15 shape (B 32, T 373: whole-head kernels when --none)")
 ap.add_argument("--p", type=float, default=0.1, help="attention dropout")
+ap.add_argument("--mode", type=int, default=0, help="cfm_attn_set_mode value (A/B)")
 a = ap.parse_args()
+if a.mode:
+    from nn_conformer_for_speech_recognition_amd import _lib  # noqa: E402
+    _lib.call("cfm_attn_set_mode", a.mode)
 B, T, H, dk = (32, 373, 8, 64) if a.l15 else (8, 1498, 8, 64)
 g = torch.Generator().manual_seed(0)
 qkv = torch.randn(B * T, 3 * H * dk, generator=g).to("cuda", torch.bfloat16)

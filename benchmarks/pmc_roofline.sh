@@ -24,6 +24,8 @@ run ffn_mfma "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACT
 run wg_fetch FETCH_SIZE $BE
 run wg_write WRITE_SIZE $BE
 run wg_mfma "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" $BE
-python3 $R/benchmarks/pmc_to_json.py "$OUT" ffn "gemm_pipe_kernel" "gemm_ffn_up_pmc.json" "$GP"
-python3 $R/benchmarks/pmc_to_json.py "$OUT" wg "false, true, false, " "wgrad_group_pmc.json" "$BE"
+# algorithmic bytes per launch (bench.py's gemm_desc_bytes at L15): FFN up A + B + y + pre-activation; wgrad the
+# sum over the 136 GEMMs of dY + X read once + dW / db written once
+python3 $R/benchmarks/pmc_to_json.py "$OUT" ffn "gemm_pipe_kernel" "gemm_ffn_up_pmc.json" "$GP" 112549888
+python3 $R/benchmarks/pmc_to_json.py "$OUT" wg "false, true, false, " "wgrad_group_pmc.json" "$BE" 6851823616
 rm -f "$OUT"/*.csv

@@ -4,7 +4,7 @@ entries read (matched on shape_key and the kernel name recorded here).
 
 HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> B): on gfx950 FETCH_SIZE counts half the bytes
 of 16-B-per-lane streaming reads, WRITE_SIZE is exact for 16-B stores (MI355X_MICROARCH.md §HBM).
-usage: python pmc_to_json.py DIR PREFIX KERNEL_FILTER OUT_NAME COMMAND"""
+usage: python pmc_to_json.py DIR PREFIX KERNEL_FILTER OUT_NAME COMMAND [ALGORITHMIC_BYTES_PER_LAUNCH]"""
 import csv
 import json
 import os
@@ -12,6 +12,7 @@ import statistics
 import sys
 
 d, pre, filt, out_name, cmd = sys.argv[1:6]
+alg = float(sys.argv[6]) if len(sys.argv) > 6 else None
 
 
 def medians(tag):
@@ -38,6 +39,9 @@ rec = {
     "hbm_bytes_per_launch": 2 * 1024 * fetch.get("FETCH_SIZE", 0) + 1024 * write.get("WRITE_SIZE", 0),
     "command": f"rocprofv3 --pmc <FETCH_SIZE | WRITE_SIZE | SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES "
                f"GRBM_GUI_ACTIVE> (three separate passes) -- {cmd}",
+    "algorithmic_bytes_per_launch": alg,
+    "traffic_over_algorithmic": None if not alg else round(
+        (2 * 1024 * fetch.get("FETCH_SIZE", 0) + 1024 * write.get("WRITE_SIZE", 0)) / alg, 3),
     "correction": "fetch_bytes = 2 * FETCH_SIZE * 1024 (gfx950 counts half of 16-B/lane streaming reads); "
                   "write_bytes = WRITE_SIZE * 1024",
 }

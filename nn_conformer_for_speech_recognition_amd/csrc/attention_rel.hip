@@ -769,7 +769,8 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
       sstore(cur ^ 1);
       ring_chunk_store(sring + ((qt + 3) & (RING - 1)) * TILE * KS, rr, tid);
     }
-    __syncthreads();
+    if (p.dbg & 256) __syncthreads();   // A/B (cfm_attn_set_mode bit 8): the round-4 fenced barrier
+    else lds_barrier();     // (not __syncthreads: its fence would wait for this tile's dS stores every tile)
   }
   float* stage = sst + wv * 32 * SS2;    // 32 x 68 >= 32 x 65 floats
   const int nvalid = min(32, p.T - k0w);
@@ -912,6 +913,178 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp
   }
 }
 
+// dpos, round 5 (dk = 64 operands): 128 relative rows x 64 d per workgroup, the (b, h) pairs dealt to XCDs.
+// The round-4 kernel above read 802 MB of HBM for 287 MB of dS at L60 (profiles/r05/rel_l60_pmc.txt: L2 hit rate
+// 0.19) -- the r-tiles of one (b, h) sat on eight XCDs, so the cache lines two neighbouring r-tiles share (a band row
+// segment is not line-aligned) and the (q+v) rows every r-tile of the pair re-reads were fetched once per XCD -- and
+// spent ~300 VALU per wave per tile building the skewed dS chunks from two aligned 16-B loads with data-dependent
+// selects.  Here:
+//  * 1-D grid, workgroup L runs on XCD L % 8 (round-robin placement: a speed hint, never correctness); XCD x takes
+//    the pairs x, x + 8, ... one after another, all r-tiles of a pair consecutively, so the pair's dS lines and
+//    (q+v) rows are shared through that XCD's L2;
+//  * a thread's 8 band elements dS[i][j0 .. j0+7] (j0 = i + r - (T-1)) come from three 8-B-aligned dword-pair loads,
+//    a one-dword select and four v_alignbit_b32 by 16 * (j0 & 1) -- j0 mod 4 is fixed per thread (rows
+//    I0 + 16q + tid/16, I0 and r0 multiples of 8), so the funnel is branch-free with loop-invariant selects; masks
+//    only on the edge tiles of the (i, r) parallelogram (a workgroup-uniform test per tile);
+//  * 128 r per workgroup halves the (q+v) tile traffic per output; 4 waves = (d half, r half of 64), 8 MFMAs per
+//    wave per 64-row i-tile.
+constexpr int DP_R = 128;              // relative rows per workgroup
+constexpr int DP_KS = DP_R + 72;       // sB row stride (elements): 400 B = 100 dwords == 36 mod 64, as KS's 144 B
+
+// trfrag_perm with an explicit row stride
+template <int S>
+__device__ __forceinline__ bf16x8 trfrag_perm_s(const bf16* tile, int r0, int c0, int lane) {
+  const int hh = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+  const bf16* base = tile + (r0 + 4 * hh + q) * S + c0 + 16 * g1 + 4 * p4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 8 * S));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+struct DposRegs {
+  uint4 q[2];         // raw q rows (q + v is formed at store time: converting at load time waits for the load)
+  uint2 w[4][3];      // raw dS: three 8-B-aligned dword pairs per band chunk (dwords (d0 & ~1) .. +5)
+};
+
+__global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP rp, const bf16* __restrict__ dsbuf,
+                                                                 int ldS, float* __restrict__ part, int nrt) {
+  __shared__ __attribute__((aligned(16))) bf16 sA[2][TILE * KS];     // (q+v)[ii][d]
+  __shared__ __attribute__((aligned(16))) bf16 sB[2][TILE * DP_KS];  // dS_band[ii][rr]
+  float* const sO = reinterpret_cast<float*>(&sB[0][0]);            // [DP_R][65] after the loop (33 KiB <= 50 KiB)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nbh = p.B * p.H;
+  const int xcd = blockIdx.x & 7, kx = blockIdx.x >> 3;
+  const int bh = xcd + 8 * (kx / nrt), rt = kx % nrt;
+  if (bh >= nbh) return;   // padding of the XCD deal (uniform over the workgroup)
+  const int b = bh / p.H, h = bh % p.H;
+  const int R0 = rt * DP_R;
+  const int dh = wv & 1, rq = wv >> 1;
+  const int T = p.T, nrel = 2 * T - 1;
+  const int len = min(p.len[b], T);
+  // i range with a key j = i + r - (T-1) in [0, len) for some r of the tile
+  const int ilo = max(0, T - 1 - (R0 + DP_R - 1));
+  const int ihi = min(T - 1, len - 1 + T - 1 - R0);
+  const uint32_t* dsw = reinterpret_cast<const uint32_t*>(dsbuf + ((long)b * p.H + h) * T * (long)ldS);
+  const int ldw = ldS >> 1;            // dwords per dS row (ldS is a multiple of 8)
+  const bf16* qbase = p.qkv + (long)b * T * p.D3 + h * p.dk;
+  const int c8 = (tid & 7) * 8;        // (q+v) chunk column
+  float pv8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) pv8[e] = rp.pv[h * p.dk + c8 + e];
+  const int cr = (tid & 15) * 8;       // band chunk column (relative row offset within the tile)
+  const int brow = tid >> 4;           // band chunk rows brow + 16 q
+  auto interior = [&](int I0) {
+    return I0 + TILE - 1 < T && I0 + R0 - (T - 1) >= 0 && I0 + TILE - 1 + R0 + DP_R - 1 - (T - 1) < len &&
+           R0 + DP_R - 1 < nrel;
+  };
+  auto load = [&](int I0, DposRegs& g) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) g.q[k] = ld8c(qbase, p.D3, I0 + ((tid + 256 * k) >> 3), T, c8);
+    // branch-free (a branch here makes the compiler wait for the loads at its join, and the prefetch two tiles
+    // ahead becomes a stall): row and dword indices clamped into the pair's dS rows.  On interior tiles the clamps
+    // change nothing that is used -- the fifth dword only feeds element j0 + 7 < len <= ldS when j0 is odd, i.e.
+    // d0 + 4 <= ldw - 1 -- and on edge tiles the clamped elements are masked in store()
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int i = I0 + brow + 16 * q4;
+      const int j0 = i + R0 + cr - (T - 1);
+      const int p0 = j0 >> 2;          // dword pair holding dword floor(j0 / 2) (j0 may be negative on edge tiles)
+      const uint2* s = reinterpret_cast<const uint2*>(dsw + (long)min(i, T - 1) * ldw);
+#pragma unroll
+      for (int u = 0; u < 3; ++u) g.w[q4][u] = s[min(max(p0 + u, 0), (ldw >> 1) - 1)];
+    }
+  };
+  auto store = [&](int buf, int I0, const DposRegs& g) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = I0 + ((tid + 256 * k) >> 3);
+      const bf16x8 q = __builtin_bit_cast(bf16x8, g.q[k]);
+      bf16x8 qv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qv[e] = (bf16)(i < T ? (float)q[e] + pv8[e] : 0.f);
+      *reinterpret_cast<uint4*>(sA[buf] + ((tid + 256 * k) >> 3) * KS + c8) = __builtin_bit_cast(uint4, qv);
+    }
+    const bool in = interior(I0);
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int row = brow + 16 * q4, i = I0 + row;
+      const int j0 = i + R0 + cr - (T - 1);
+      const unsigned sh = (unsigned)(j0 & 1) * 16u;
+      // dwords floor(j0/2) .. +4 from the six loaded: a one-dword shift when floor(j0/2) is odd (per-thread constant)
+      // (a bit-mask blend, not `odd ? r6[u + 1] : r6[u]`, which the compiler turned into a scratch-indexed load)
+      const uint32_t om = 0u - (uint32_t)((j0 >> 1) & 1);
+      const uint32_t r6[6] = {g.w[q4][0].x, g.w[q4][0].y, g.w[q4][1].x, g.w[q4][1].y, g.w[q4][2].x, g.w[q4][2].y};
+      uint32_t w5[5];
+#pragma unroll
+      for (int u = 0; u < 5; ++u) w5[u] = r6[u] ^ ((r6[u] ^ r6[u + 1]) & om);
+      uint32_t o[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = __builtin_amdgcn_alignbit(w5[u + 1], w5[u], sh);
+      if (!in) {   // elements e with i < T, 0 <= j0 + e < len, R0 + cr + e < nrel
+        const int lo = max(0, -j0), hi = i < T ? min(8, min(len - j0, nrel - R0 - cr)) : 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          o[u] &= ((2 * u >= lo && 2 * u < hi) ? 0xFFFFu : 0u) | ((2 * u + 1 >= lo && 2 * u + 1 < hi) ? 0xFFFF0000u : 0u);
+      }
+      *reinterpret_cast<uint4*>(sB[buf] + row * DP_KS + cr) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  };
+  f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
+  const int it0 = ilo & ~(TILE - 1);
+  const int nit = (len > 0 && ihi >= ilo) ? (ihi - it0) / TILE + 1 : 0;
+  // four register stages ahead of the LDS double buffer: step it issues tile it+3's loads, computes tile it from
+  // LDS and stores tile it+1 (loaded two steps earlier) into the other buffer.  Every load and store is issued
+  // unconditionally (tile indices clamped to the last tile; the surplus steps of the 4-step unroll only skip their
+  // MFMAs, a branch with no memory operation in it), so the compiler's vmcnt waits stay counted -- a conditional
+  // load makes the wait at its join a vmcnt(0) that also waits for the prefetch.
+  auto tile_of = [&](int it) { return it0 + min(it, nit - 1) * TILE; };
+  auto step = [&](int it, DposRegs& gl, const DposRegs& gs) {
+    load(tile_of(it + 3), gl);
+    if (it < nit) {
+      const int cur = it & 1;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 a = trfrag_perm(sA[cur], 16 * s, 32 * dh, lane);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, trfrag_perm_s<DP_KS>(sB[cur], 16 * s, 64 * rq, lane),
+                                                       acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, trfrag_perm_s<DP_KS>(sB[cur], 16 * s, 64 * rq + 32, lane),
+                                                       acc1, 0, 0, 0);
+      }
+    }
+    store((it + 1) & 1, tile_of(it + 1), gs);
+    lds_barrier();
+  };
+  if (nit > 0) {
+    DposRegs g0, g1, g2, g3;
+    load(tile_of(0), g0);
+    load(tile_of(1), g1);
+    load(tile_of(2), g2);
+    store(0, tile_of(0), g0);
+    lds_barrier();
+    for (int it = 0; it < nit; it += 4) {
+      step(it, g3, g1);
+      step(it + 1, g0, g2);
+      step(it + 2, g1, g3);
+      step(it + 3, g2, g0);
+    }
+  }
+  // acc0/acc1: rows d (32 dh + acc_row), lanes rr (64 rq + 32 j + lane&31) -> sO[rr][d] -> the partial rows
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    sO[(64 * rq + (lane & 31)) * 65 + 32 * dh + acc_row(r, hh)] = acc0[r] * p.scale;
+    sO[(64 * rq + 32 + (lane & 31)) * 65 + 32 * dh + acc_row(r, hh)] = acc1[r] * p.scale;
+  }
+  __syncthreads();
+  float* dst = part + (long)b * nrel * p.HD;
+  for (int idx = tid; idx < DP_R * 64; idx += 256) {
+    const int rr = idx >> 6, d = idx & 63;
+    if (R0 + rr < nrel) dst[(long)(R0 + rr) * p.HD + h * p.dk + d] = sO[rr * 65 + d];
+  }
+}
+
 }  // namespace
 
 namespace cfm {
@@ -960,7 +1133,8 @@ int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len
 int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, const int32_t* len, const void* pos,
                         const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
                         int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s) {
-  const AttnM p = make_attnm(qkv, dout, len, B, T, H, dk, drop_p, seed);
+  AttnM p = make_attnm(qkv, dout, len, B, T, H, dk, drop_p, seed);
+  p.dbg = g_rel_mode & 256;
   const RelP rp = make_relp(pos, pu, pv, p.dk);
   const size_t d_bytes = ((size_t)p.B * p.H * p.T * sizeof(float) + 255) & ~(size_t)255;
   float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + d_bytes);
@@ -981,7 +1155,11 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
   }
   const size_t ds_bytes = ((size_t)p.B * p.H * p.T * ldS * sizeof(bf16) + 255) & ~(size_t)255;
   float* dpos_part = reinterpret_cast<float*>(reinterpret_cast<char*>(dsbuf) + ds_bytes);
-  if (rel_vec(p, rp))
+  if (rel_vec(p, rp) && !(g_rel_mode & 128)) {
+    const int nrt = cdiv(2 * p.T - 1, DP_R);
+    hipLaunchKernelGGL(attn_rel_bwd_dpos3_kernel, dim3(8 * cdiv(p.B * p.H, 8) * nrt), dim3(256), 0, s, p, rp,
+                       (const bf16*)dsbuf, ldS, dpos_part, nrt);
+  } else if (rel_vec(p, rp))
     hipLaunchKernelGGL(attn_rel_bwd_dpos_kernel<true>, dim3(cdiv(2 * p.T - 1, TILE), p.H, p.B), dim3(256), 0, s, p, rp,
                        (const bf16*)dsbuf, ldS, dpos_part);
   else

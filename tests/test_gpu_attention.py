@@ -169,6 +169,24 @@ def test_rel_attention_mfma_matches_simt_under_dropout(attn_mode):
             assert _rel(a, b) < 3e-2
 
 
+@pytest.mark.parametrize("B,T,H,lens", [(2, 1498, 3, [1498, 1001]), (3, 373, 2, [373, 300, 41]), (2, 64, 1, [64, 1]),
+                                        (9, 130, 2, [130] * 8 + [77])])
+def test_rel_dpos_xcd_kernel_matches_round4(attn_mode, B, T, H, lens):
+    """The round-5 dpos kernel (128 relative rows per workgroup, (b, h) pairs dealt to XCDs, dword-funnel band
+    loads, masks on edge tiles only) == the round-4 kernel (cfm_attn_set_mode bit 7) bit for bit: the same MFMA
+    k-steps over the same i order, the extra leading rows contribute exact zeros.  B*H = 18 pads the XCD deal."""
+    dk = 64
+    qkv, pos, pu, pv, do, ln = _rel_case(B, T, H, dk, lens, 5)
+    outs = []
+    for mode in (0, 128):
+        attn_mode(mode)
+        o, lse = ops.attn_fwd(qkv, ln, B, T, H, dk, pos, pu, pv, drop_p=0.1, seed=11)
+        outs.append(ops.attn_bwd(qkv, o, do, lse, ln, B, T, H, dk, pos, pu, pv, drop_p=0.1, seed=11)[1])
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
+
+
 # ------------------------------------------------------------------------------------ dropout masks, read back
 def _keep(B, T, H, p, seed):
     """numpy restatement of the attention-dropout keep mask (cfm_common.h attn_mix / drop_key, attn_common.h
