@@ -21,11 +21,29 @@ constexpr int CHUNK = 4096;      // elements per block in the elementwise passes
 constexpr int RB = 32;           // rows per column-partial task (wide factored tensors)
 constexpr int KMAX = 40;         // 64-column groups a lane keeps in registers: wide means 64 <= C <= 2560
 
+// unsigned 32-bit division by an invariant divisor d >= 1 (Granlund-Montgomery): with l = ceil(log2 d) and
+// m = floor(2^32 (2^l - d) / d) + 1, n / d = (t + ((n - t) >> 1)) >> (l - 1) for t = mulhi(m, n) (d >= 2);
+// d == 1: m = 0, sh = 0 and the formula is replaced by n.  Exact for every 32-bit n.
+struct UDiv { uint32_t m, sh, one; };
+static inline UDiv udiv_make(uint32_t d) {
+  if (d <= 1) return UDiv{0u, 0u, 1u};
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return UDiv{(uint32_t)m, l - 1, 0u};
+}
+__device__ __forceinline__ uint32_t udiv(uint32_t n, const UDiv& v) {
+  if (v.one) return n;
+  const uint32_t t = __umulhi(v.m, n);
+  return (t + ((n - t) >> 1)) >> v.sh;
+}
+
 struct AdaP {
   float* p; const float* g; float* m; float* row; float* col;   // col == nullptr: unfactored (row = v)
   long numel; int nb, R, C, factored;
   long row_toff, col_off, blk_off, rm_off, rm_toff;              // prefix offsets (tasks / elements)
   long cp_toff, part_off;                                        // column-partial tasks / partial floats
+  UDiv div_rc, div_c;                                            // element index -> (matrix, row, column)
 };
 
 __host__ __device__ __forceinline__ bool is_wide(int C) { return C >= 64 && C <= 64 * KMAX; }
@@ -274,9 +292,11 @@ __device__ __forceinline__ void ada_u(const AdaP& q, const float* rowmean, unsig
     }
     return;
   }
+  // (the two divisions by the tensor's R*C and C as multiply-high sequences: as plain 32-bit divisions they were
+  // ~40 VALU per element group in two HBM-bound passes)
   const unsigned rc = (unsigned)q.R * (unsigned)q.C;
-  const unsigned b = i / rc, w = i - b * rc;
-  const unsigned r = w / (unsigned)q.C, c = w - r * (unsigned)q.C;
+  const unsigned b = udiv(i, q.div_rc), w = i - b * rc;
+  const unsigned r = udiv(w, q.div_c), c = w - r * (unsigned)q.C;
   const float rf = rsqrtf(q.row[(long)b * q.R + r] / rowmean[q.rm_off + b]);
   const float* cp = q.col + (long)b * q.C + c;
 #pragma unroll
@@ -398,6 +418,8 @@ CFM_EXPORT int cfm_adafactor_fill_table(void* host_table, int i, float* p, const
   AdaP* t = reinterpret_cast<AdaP*>(host_table) + i;
   t->p = p; t->g = g; t->m = m; t->row = row; t->col = col;
   t->numel = numel; t->nb = nb; t->R = R; t->C = C; t->factored = col != nullptr;
+  t->div_rc = udiv_make((uint32_t)R * (uint32_t)C);
+  t->div_c = udiv_make((uint32_t)C);
   t->row_toff = row_toff; t->col_off = col_off; t->blk_off = blk_off; t->rm_off = rm_off; t->rm_toff = rm_toff;
   t->cp_toff = cp_toff; t->part_off = part_off;
   return CFM_OK;
