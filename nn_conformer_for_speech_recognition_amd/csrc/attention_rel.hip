@@ -922,14 +922,18 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp
 //  * 1-D grid, workgroup L runs on XCD L % 8 (round-robin placement: a speed hint, never correctness); XCD x takes
 //    the pairs x, x + 8, ... one after another, all r-tiles of a pair consecutively, so the pair's dS lines and
 //    (q+v) rows are shared through that XCD's L2;
-//  * a thread's 8 band elements dS[i][j0 .. j0+7] (j0 = i + r - (T-1)) come from three 8-B-aligned dword-pair loads,
-//    a one-dword select and four v_alignbit_b32 by 16 * (j0 & 1) -- j0 mod 4 is fixed per thread (rows
-//    I0 + 16q + tid/16, I0 and r0 multiples of 8), so the funnel is branch-free with loop-invariant selects; masks
-//    only on the edge tiles of the (i, r) parallelogram (a workgroup-uniform test per tile);
+//  * the band skew moves to the LDS store: each row's needed dS run (128 elements from j = i + r0 - (T-1)) is read as
+//    17 ALIGNED 16-B chunks (one buffer load each; a (b, h) slab's buffer range turns every out-of-slab read into
+//    zeros, so no clamps) and each element is stored with ds_write_b16 at its band column r' = j - i - r0 + (T-1) of
+//    a padded [row][8 + 136] image -- the round-4 / first round-5 forms spent ~300 VALU per wave per tile on funnel
+//    shifts and clamps in registers; masks only on the edge tiles of the (i, r) parallelogram (a workgroup-uniform
+//    test per tile);
 //  * 128 r per workgroup halves the (q+v) tile traffic per output; 4 waves = (d half, r half of 64), 8 MFMAs per
 //    wave per 64-row i-tile.
 constexpr int DP_R = 128;              // relative rows per workgroup
 constexpr int DP_KS = DP_R + 72;       // sB row stride (elements): 400 B = 100 dwords == 36 mod 64, as KS's 144 B
+constexpr int DP_PADL = 8;             // band image column of r' = 0 (r' = -7 .. 135 are written, 0 .. 127 read)
+constexpr int DP_CH = DP_R / 8 + 1;    // aligned 8-element dS chunks per row (17)
 
 // trfrag_perm with an explicit row stride
 template <int S>
@@ -945,7 +949,7 @@ __device__ __forceinline__ bf16x8 trfrag_perm_s(const bf16* tile, int r0, int c0
 
 struct DposRegs {
   uint4 q[2];         // raw q rows (q + v is formed at store time: converting at load time waits for the load)
-  uint2 w[4][3];      // raw dS: three 8-B-aligned dword pairs per band chunk (dwords (d0 & ~1) .. +5)
+  uint4 w[5];         // raw dS: five aligned 8-element chunks (the fifth a real one for tid < 64 only)
 };
 
 __global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP rp, const bf16* __restrict__ dsbuf,
@@ -966,15 +970,27 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP r
   // i range with a key j = i + r - (T-1) in [0, len) for some r of the tile
   const int ilo = max(0, T - 1 - (R0 + DP_R - 1));
   const int ihi = min(T - 1, len - 1 + T - 1 - R0);
-  const uint32_t* dsw = reinterpret_cast<const uint32_t*>(dsbuf + ((long)b * p.H + h) * T * (long)ldS);
-  const int ldw = ldS >> 1;            // dwords per dS row (ldS is a multiple of 8)
+  // the pair's dS slab as a buffer resource: reads outside it (j < 0 on row 0, rows >= T) return zeros
+  const __amdgpu_buffer_rsrc_t rs = head_rsrc(dsbuf + ((long)b * p.H + h) * T * (long)ldS, (long)T * ldS * 2);
   const bf16* qbase = p.qkv + (long)b * T * p.D3 + h * p.dk;
   const int c8 = (tid & 7) * 8;        // (q+v) chunk column
   float pv8[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) pv8[e] = rp.pv[h * p.dk + c8 + e];
-  const int cr = (tid & 15) * 8;       // band chunk column (relative row offset within the tile)
-  const int brow = tid >> 4;           // band chunk rows brow + 16 q
+  // this thread's band chunks: q = tid + 256 k of the tile's 64 x 17; row, chunk column, the row's skew
+  // s = (row + r0 - (T-1)) & 7 (row i's run starts s elements into its first aligned chunk; I0 is a multiple of 64)
+  // and the chunk's element offset in the slab for tile I0: I0 * (ldS + 1) + base
+  int crow[5], ccol[5], csk[5], cbase[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    int q = tid + 256 * k;
+    if (q >= TILE * DP_CH) q = tid;    // (k = 4, tid >= 64: re-loads its first chunk, not stored)
+    crow[k] = q / DP_CH;
+    ccol[k] = q % DP_CH;
+    const int j0 = crow[k] + R0 - (T - 1);
+    csk[k] = j0 & 7;
+    cbase[k] = crow[k] * ldS + (j0 - csk[k]) + 8 * ccol[k];
+  }
   auto interior = [&](int I0) {
     return I0 + TILE - 1 < T && I0 + R0 - (T - 1) >= 0 && I0 + TILE - 1 + R0 + DP_R - 1 - (T - 1) < len &&
            R0 + DP_R - 1 < nrel;
@@ -982,19 +998,12 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP r
   auto load = [&](int I0, DposRegs& g) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) g.q[k] = ld8c(qbase, p.D3, I0 + ((tid + 256 * k) >> 3), T, c8);
-    // branch-free (a branch here makes the compiler wait for the loads at its join, and the prefetch two tiles
-    // ahead becomes a stall): row and dword indices clamped into the pair's dS rows.  On interior tiles the clamps
-    // change nothing that is used -- the fifth dword only feeds element j0 + 7 < len <= ldS when j0 is odd, i.e.
-    // d0 + 4 <= ldw - 1 -- and on edge tiles the clamped elements are masked in store()
+    // one aligned 16-B buffer load per chunk, no branch and no clamp (a branch here makes the compiler wait for the
+    // loads at its join, and the prefetch ahead becomes a stall); negative offsets wrap past the range: zeros
+    const int off0 = I0 * (ldS + 1);
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      const int i = I0 + brow + 16 * q4;
-      const int j0 = i + R0 + cr - (T - 1);
-      const int p0 = j0 >> 2;          // dword pair holding dword floor(j0 / 2) (j0 may be negative on edge tiles)
-      const uint2* s = reinterpret_cast<const uint2*>(dsw + (long)min(i, T - 1) * ldw);
-#pragma unroll
-      for (int u = 0; u < 3; ++u) g.w[q4][u] = s[min(max(p0 + u, 0), (ldw >> 1) - 1)];
-    }
+    for (int k = 0; k < 5; ++k)
+      g.w[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, 2 * (off0 + cbase[k]), 0, 0));
   };
   auto store = [&](int buf, int I0, const DposRegs& g) {
 #pragma unroll
@@ -1008,27 +1017,28 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP r
     }
     const bool in = interior(I0);
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      const int row = brow + 16 * q4, i = I0 + row;
-      const int j0 = i + R0 + cr - (T - 1);
-      const unsigned sh = (unsigned)(j0 & 1) * 16u;
-      // dwords floor(j0/2) .. +4 from the six loaded: a one-dword shift when floor(j0/2) is odd (per-thread constant)
-      // (a bit-mask blend, not `odd ? r6[u + 1] : r6[u]`, which the compiler turned into a scratch-indexed load)
-      const uint32_t om = 0u - (uint32_t)((j0 >> 1) & 1);
-      const uint32_t r6[6] = {g.w[q4][0].x, g.w[q4][0].y, g.w[q4][1].x, g.w[q4][1].y, g.w[q4][2].x, g.w[q4][2].y};
-      uint32_t w5[5];
-#pragma unroll
-      for (int u = 0; u < 5; ++u) w5[u] = r6[u] ^ ((r6[u] ^ r6[u + 1]) & om);
-      uint32_t o[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) o[u] = __builtin_amdgcn_alignbit(w5[u + 1], w5[u], sh);
-      if (!in) {   // elements e with i < T, 0 <= j0 + e < len, R0 + cr + e < nrel
-        const int lo = max(0, -j0), hi = i < T ? min(8, min(len - j0, nrel - R0 - cr)) : 0;
+    for (int k = 0; k < 5; ++k) {
+      if (k == 4 && tid >= TILE * DP_CH - 1024) break;
+      uint32_t o[4] = {g.w[k].x, g.w[k].y, g.w[k].z, g.w[k].w};
+      const int row = crow[k], i = I0 + row;
+      // element e: j = I0 + row + r0 - (T-1) - sk + 8c + e, band column r' = 8c + e - sk
+      const int rp0 = 8 * ccol[k] - csk[k];
+      if (!in) {   // valid: i < T, 0 <= j < len, r0 + r' < nrel
+        const int j0 = i + R0 - (T - 1) + rp0;
+        const int lo = max(0, -j0), hi = i < T ? min(8, min(len - j0, nrel - R0 - rp0)) : 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           o[u] &= ((2 * u >= lo && 2 * u < hi) ? 0xFFFFu : 0u) | ((2 * u + 1 >= lo && 2 * u + 1 < hi) ? 0xFFFF0000u : 0u);
       }
-      *reinterpret_cast<uint4*>(sB[buf] + row * DP_KS + cr) = make_uint4(o[0], o[1], o[2], o[3]);
+      // (volatile: 2-byte stores at 2-byte-aligned addresses; merged, they became misaligned ds_write_b128)
+      typedef volatile __attribute__((address_space(3))) unsigned short lds_u16;
+      lds_u16* d = reinterpret_cast<lds_u16*>((__attribute__((address_space(3))) bf16*)sB[buf]) + row * DP_KS + DP_PADL +
+                   rp0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        d[2 * u] = (unsigned short)(o[u] & 0xFFFFu);
+        d[2 * u + 1] = (unsigned short)(o[u] >> 16);
+      }
     }
   };
   f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
@@ -1047,10 +1057,10 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP r
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const bf16x8 a = trfrag_perm(sA[cur], 16 * s, 32 * dh, lane);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, trfrag_perm_s<DP_KS>(sB[cur], 16 * s, 64 * rq, lane),
-                                                       acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, trfrag_perm_s<DP_KS>(sB[cur], 16 * s, 64 * rq + 32, lane),
-                                                       acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            a, trfrag_perm_s<DP_KS>(sB[cur], 16 * s, DP_PADL + 64 * rq, lane), acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            a, trfrag_perm_s<DP_KS>(sB[cur], 16 * s, DP_PADL + 64 * rq + 32, lane), acc1, 0, 0, 0);
       }
     }
     store((it + 1) & 1, tile_of(it + 1), gs);
