@@ -596,6 +596,23 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_vec_kernel(const float* __
       zf[p] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(bn.dz) + ((long)b * T + t) * C + cqc);
     }
   }
+  // per-element BN + SiLU backward and GLU on packed FP32 pairs (v_pk_fma / v_pk_mul / v_pk_add: the transcendental
+  // exp / rcp stay scalar); the gate sigmoid of the tile's own rows is kept for the da stores (sg4: computed once --
+  // the stores recomputed it); same operations per element as the scalar form, up to FMA contraction
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 gi2[2], nmi2[2], bg2[2], bbt2[2], bk1_2[2], bk2_2[2];
+  if constexpr (BN) {
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      gi2[h2] = f2{bg[2 * h2] * bis[2 * h2], bg[2 * h2 + 1] * bis[2 * h2 + 1]};
+      nmi2[h2] = f2{-bmu[2 * h2] * bis[2 * h2], -bmu[2 * h2 + 1] * bis[2 * h2 + 1]};
+      bg2[h2] = f2{bg[2 * h2], bg[2 * h2 + 1]};
+      bbt2[h2] = f2{bbt[2 * h2], bbt[2 * h2 + 1]};
+      bk1_2[h2] = f2{bk1[2 * h2], bk1[2 * h2 + 1]};
+      bk2_2[h2] = f2{bk2[2 * h2], bk2[2 * h2 + 1]};
+    }
+  }
+  f32x4 sg4[NP];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const int r = rs + 16 * p, t = t0 - PAD + r;
@@ -603,20 +620,31 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_vec_kernel(const float* __
       const bool ok = cok && t >= 0 && t < T;
       f32x4 d, g;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float dv;
+      for (int h2 = 0; h2 < 2; ++h2) {
+        f2 dv;
         if constexpr (BN) {
-          const float yh = (v4[p][j] - bmu[j]) * bis[j];
-          float dzv;
-          if constexpr (DZ16) dzv = (float)z4[p][j];
-          else dzv = zf[p][j];
-          const float du = dzv * silu_grad_f(yh * bg[j] + bbt[j]);
-          dv = bg[j] * bis[j] * (du - bk1[j] - yh * bk2[j]);
+          const f2 v = {v4[p][2 * h2], v4[p][2 * h2 + 1]};
+          const f2 yh = __builtin_elementwise_fma(v, f2{bis[2 * h2], bis[2 * h2 + 1]}, nmi2[h2]);
+          const f2 pre = __builtin_elementwise_fma(yh, bg2[h2], bbt2[h2]);
+          const f2 sgm = {sigmoid_f(pre.x), sigmoid_f(pre.y)};
+          // silu'(x) = s (1 + x (1 - s))
+          const f2 sgr = __builtin_elementwise_fma(sgm, pre * (f2{1.f, 1.f} - sgm), sgm);
+          f2 dz;
+          if constexpr (DZ16) dz = f2{(float)z4[p][2 * h2], (float)z4[p][2 * h2 + 1]};
+          else dz = f2{zf[p][2 * h2], zf[p][2 * h2 + 1]};
+          const f2 du = dz * sgr;
+          dv = gi2[h2] * (__builtin_elementwise_fma(-yh, bk2_2[h2], du) - bk1_2[h2]);
         } else {
-          dv = v4[p][j];
+          dv = f2{v4[p][2 * h2], v4[p][2 * h2 + 1]};
         }
-        d[j] = ok ? dv : 0.f;
-        g[j] = ok ? (float)x4[p][j] * sigmoid_f((float)g4[p][j]) : 0.f;
+        const f2 sgg = {sigmoid_f((float)g4[p][2 * h2]), sigmoid_f((float)g4[p][2 * h2 + 1])};
+        const f2 gv = f2{(float)x4[p][2 * h2], (float)x4[p][2 * h2 + 1]} * sgg;
+        sg4[p][2 * h2] = sgg.x;
+        sg4[p][2 * h2 + 1] = sgg.y;
+        d[2 * h2] = ok ? dv.x : 0.f;
+        d[2 * h2 + 1] = ok ? dv.y : 0.f;
+        g[2 * h2] = ok ? gv.x : 0.f;
+        g[2 * h2 + 1] = ok ? gv.y : 0.f;
       }
       *reinterpret_cast<f32x4*>(sdy + r * CT + 4 * q) = d;
       *reinterpret_cast<f32x4*>(sg + r * CT + 4 * q) = g;
@@ -681,7 +709,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_bwd_vec_kernel(const float* __
       bf16x4 o1, o2;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float sg1 = sigmoid_f((float)g4[p][j]);
+        const float sg1 = sg4[p][j];
         o1[j] = (bf16)(d[j] * sg1);
         o2[j] = (bf16)(d[j] * (float)x4[p][j] * sg1 * (1.f - sg1));
       }
