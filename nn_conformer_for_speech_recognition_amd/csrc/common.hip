@@ -307,8 +307,15 @@ __global__ __launch_bounds__(1024) void colreduce2_kernel(const float* __restric
   const long n = (long)blockIdx.x * 64 + lane;
   float s = 0.f;
   if (n < N) {
-#pragma unroll 4
-    for (int p = wv; p < nparts; p += 16) s += part[(long)p * N + n];
+    // 16 of the wave's parts loaded before any is added (the round-4 `unroll 4` paid 3 memory round trips for the
+    // 12 parts a wave holds at 192 partial rows); same order of additions: bit-identical
+    for (int p0 = wv; p0 < nparts; p0 += 16 * 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = p0 + 16 * u < nparts ? part[(long)(p0 + 16 * u) * N + n] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
   }
   red[wv][lane] = s;
   __syncthreads();

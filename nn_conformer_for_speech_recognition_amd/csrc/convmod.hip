@@ -208,6 +208,54 @@ __global__ __launch_bounds__(256) void glu_dwconv_fwd_vec_kernel(const bf16* __r
   }
 }
 
+// the column sums of the (sum, sumsq) partial rows and the batch stats + running-stat update in one launch
+// (round 4: cfm::colreduce_pair then bn_finalize_kernel, two ~5 us launches per BatchNorm forward): per 64
+// channels, 16 waves sum parts wv, wv + 16, ... of both arrays in the colreduce2 order, wave 0 adds the 16 wave
+// sums in order and finalises -- bit-identical to the two-launch form
+__global__ __launch_bounds__(1024) void bn_stats_kernel(const float* __restrict__ partA, const float* __restrict__ partB,
+                                                        int nparts, long M, int C, float* __restrict__ mean,
+                                                        float* __restrict__ invstd, float* __restrict__ rmean,
+                                                        float* __restrict__ rvar, float momentum, float eps) {
+  __shared__ float red[2][16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float sa = 0.f, sb = 0.f;
+  if (c < C) {
+    for (int p0 = wv; p0 < nparts; p0 += 16 * 8) {
+      float va[8], vb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool ok = p0 + 16 * u < nparts;
+        va[u] = ok ? partA[(long)(p0 + 16 * u) * C + c] : 0.f;
+        vb[u] = ok ? partB[(long)(p0 + 16 * u) * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        sa += va[u];
+        sb += vb[u];
+      }
+    }
+  }
+  red[0][wv][lane] = sa;
+  red[1][wv][lane] = sb;
+  __syncthreads();
+  if (wv != 0 || c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    s1 += red[0][q][lane];
+    s2 += red[1][q][lane];
+  }
+  const double mu = (double)s1 / (double)M;
+  double var = (double)s2 / (double)M - mu * mu;
+  if (var < 0.0) var = 0.0;
+  mean[c] = (float)mu;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
+  if (rvar)
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(M > 1 ? var * (double)M / (double)(M - 1) : var);
+}
+
 // batch stats from column sums s1 (sum) and s2 (sum of squares) + running-stat update.
 __global__ void bn_finalize_kernel(const float* __restrict__ s1, const float* __restrict__ s2, long M, int C,
                                    float* __restrict__ mean, float* __restrict__ invstd,
@@ -765,10 +813,8 @@ long conv_nparts(int B, int T) { return (long)B * ((T + TT - 1) / TT); }
 // fwd stats from [2][nparts][C] partials at ws; scratch (2C) right after them
 void bn_stats_finalize(const float* ws, int nparts, long M, int C, float* mean, float* invstd, float* rm, float* rv,
                        float mom, float eps, hipStream_t s) {
-  float* sums = const_cast<float*>(ws) + 2L * nparts * C;
-  cfm::colreduce_pair(ws, ws + (long)nparts * C, nparts, C, sums, sums + C, s);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, sums + C, M, C, mean, invstd,
-                     rm, rv, mom, eps);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, s, ws, ws + (long)nparts * C, nparts, M, C,
+                     mean, invstd, rm, rv, mom, eps);
 }
 
 int bn_bwd_impl(const void* dz, int dtdz, const float* y, const float* gamma, const float* beta, const float* mean,
