@@ -274,12 +274,6 @@ __device__ __forceinline__ void head_dma_piece(__amdgpu_buffer_rsrc_t r, char* i
 // on every iteration.  gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15.
 __device__ __forceinline__ void wait_prologue_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
-// workgroup barrier for LDS hand-offs only: this wave's LDS operations complete, then s_barrier.  __syncthreads()
-// is also a workgroup release fence, which makes every wave wait for ALL its outstanding vector-memory operations
-// (s_waitcnt vmcnt(0)) -- global stores included, whose acknowledgements a loop that streams results out (the
-// rel-pos dK/dV kernel's dS rows) then pays once per tile.  Only for barriers whose consumers read LDS, never for
-// global data written before the barrier and read after it by another wave.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n
 __device__ __forceinline__ void wait_vm_n(int n) {

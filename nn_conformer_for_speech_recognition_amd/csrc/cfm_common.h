@@ -61,6 +61,14 @@ __device__ __forceinline__ void st_dyn(void* p, int dtype, long idx, float v) {
 
 // sigmoid via the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division (~10 VALU ops):
 // these run per element in GEMM epilogues.  exp(-x) = inf gives rcp = 0 (silu(-inf side) = -0).
+// workgroup barrier for LDS hand-offs only: this wave's LDS operations complete, then s_barrier.  __syncthreads()
+// is also a workgroup release fence, which makes every wave wait for ALL its outstanding vector-memory operations
+// (s_waitcnt vmcnt(0)) -- global stores included, whose acknowledgements a loop that streams results out (the
+// rel-pos dK/dV kernel's dS rows, the CTC recursion's alpha / beta rows) then pays once per tile or frame, and
+// loads issued ahead as a prefetch, which it turns into a stall.  Only for barriers whose consumers read LDS, never for
+// global data written before the barrier and read after it by another wave.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
 __device__ __forceinline__ float silu_grad_f(float x) {

@@ -177,7 +177,9 @@ __global__ __launch_bounds__(AB_THREADS) void ctc_alphabeta(CtcP p) {
         wr[s] = v;
         out[(long)t * p.S + s] = v;
       }
-      __syncthreads();
+      // LDS hand-off only: __syncthreads() also waited, every frame, for the frame's alpha / beta stores and for the
+      // lpe prefetch 16 frames ahead (read by ctc_grad / this loop later; kernel boundary / counted waits order them)
+      lds_barrier();
     }
 #pragma unroll
     for (int q = 0; q < PF; ++q)
