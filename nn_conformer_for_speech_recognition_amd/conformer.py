@@ -96,10 +96,15 @@ _PNAMES = [
 _REL_PNAMES = ["self_attn.linear_pos.weight", "self_attn.pos_bias_u", "self_attn.pos_bias_v"]
 
 
+# rel-pos: all layers' projected tables from one batched GEMM, dW_pos in the grouped weight-gradient launch
+# (CFM_REL_BATCH=0: the per-layer projection and weight-gradient GEMMs, A/B)
+REL_BATCH = os.environ.get("CFM_REL_BATCH", "1") != "0"
+
+
 class _Cfg:
     __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
                  "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t", "group_wgrad", "layer_index",
-                 "grad_dest", "flush_here", "on_flushed", "on_routed", "sync_bn", "shadow8")
+                 "grad_dest", "flush_here", "on_flushed", "on_routed", "sync_bn", "shadow8", "pos_pre")
 
 
 # the 2-D (and pointwise-conv) weight matrices of _PNAMES: cast to the compute dtype once per step
@@ -284,8 +289,10 @@ def _mha_fwd(x, P, R, cfg, seed, lens):
         qkv = ops.linear(xn, win, P[9])
     pos = pu = pv = None
     if cfg.rel:
-        wpos = _w(R[0], cd)
-        pos = ops.linear(_w(cfg.pe, cd), wpos)          # (2T-1, d) projected table (no bias)
+        if cfg.pos_pre is not None:     # this layer's slice of Conformer._rel_tables' one batched projection
+            pos = cfg.pos_pre
+        else:
+            pos = ops.linear(_w(cfg.pe, cd), _w(R[0], cd))      # (2T-1, d) projected table (no bias)
         pu = R[1].reshape(-1).float().contiguous()
         pv = R[2].reshape(-1).float().contiguous()
     o, lse = ops.attn_fwd(qkv, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
@@ -313,7 +320,13 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
     dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed,
                                         D=Dh)
     if cfg.rel:
-        rgrads[0] = ops.linear_wgrad(_w(dpos, cd), _w(cfg.pe, cd))
+        dpc, pec = _w(dpos, cd), _w(cfg.pe, cd)
+        if REL_BATCH and side.group is not None and ops.wgrad_group_ok(dpc, pec):
+            # dW_pos = dposᵀ·pe as one more task of the grouped weight-gradient launch (M = 2T-1 rows; its bias
+            # sums are not used) -- alone it ran on 16 workgroups (L60: 30 us per layer)
+            rgrads[0], _ = side.group.add(dpc, pec)
+        else:
+            rgrads[0] = ops.linear_wgrad(dpc, pec)
         rgrads[1] = dpu.view(H, d // H)
         rgrads[2] = dpv.view(H, d // H)
     grads[8], grads[9] = _wgrad_bias(side, dqkv, xn, 8)
@@ -499,7 +512,7 @@ class ConformerLayer(nn.Module):
 
     def forward_tokens(self, x, lens_i32, B, T, compute_dtype, seed, pe=None, shadow=None, layer_index=0,
                        group_wgrad=False, grad_dest=None, flush_here=False, on_flushed=None, sync_bn=None,
-                       count_batches=True, on_routed=None):
+                       count_batches=True, on_routed=None, pos_pre=None):
         """x: (B*T, d) fp32 token-major; lens_i32: (B,) int32 on the device; shadow: optional
         ({param index: compute-dtype copy}, {param index: its transposed K-major copy}) of this
         layer's weight matrices (see Conformer._shadows)."""
@@ -516,6 +529,7 @@ class ConformerLayer(nn.Module):
         cfg.bn_rm, cfg.bn_rv = bn.running_mean, bn.running_var
         cfg.bn_mom = bn.momentum if bn.momentum is not None else 0.1
         cfg.pe = pe
+        cfg.pos_pre = pos_pre
         cfg.layer_index = layer_index
         cfg.group_wgrad = bool(group_wgrad) and "wgroup" not in ops.DISABLED
         cfg.grad_dest, cfg.flush_here, cfg.on_flushed, cfg.on_routed = grad_dest, flush_here, on_flushed, on_routed
@@ -553,6 +567,7 @@ class Conformer(nn.Module):
         # fp8 (e4m3fn) forward GEMMs (FFN up/down, QKV, out-projection; K % 128 == 0): BASELINE configs[4]
         self.fp8 = bool(fp8)
         self._pe_cache = {}
+        self._rel_cache = {}
         self._step = 0
         self._shadow = None
         self._q8 = None         # (key, ops.Quant8Batch) of the fp8 forward weights
@@ -569,6 +584,33 @@ class Conformer(nn.Module):
         if key not in self._pe_cache:
             self._pe_cache[key] = rel_pos_table(T, self.input_dim, device)
         return self._pe_cache[key]
+
+    def _rel_tables(self, T, device):
+        """rel-pos: the compute-dtype positional table (cached: it is constant) and every layer's projected table
+        pos_l = pe · W_pos,lᵀ from ONE batched GEMM (pe shared, batch = layers) over a per-step stacked compute-dtype
+        copy of the linear_pos weights (one cast launch) -- per layer this was a cast of pe, a cast of W_pos and a
+        48-workgroup GEMM (L60: ~24 us per layer).  -> (pe in the compute dtype, (L, 2T-1, d) tables)"""
+        cd, d, nl = self.compute_dtype, self.input_dim, len(self.conformer_layers)
+        ws = [ly.self_attn.linear_pos.weight for ly in self.conformer_layers]
+        key = (T, str(device), cd)
+        ptrs = tuple(w.data_ptr() for w in ws)
+        ent = self._rel_cache.get(key)
+        if ent is None or ent[0] != ptrs:
+            pe = self._pe(T, device)
+            pe_cd = pe if pe.dtype == cd else ops.cast(pe, cd)
+            wstack = torch.empty(nl, d, d, device=device, dtype=cd)
+            cb = None if cd == torch.float32 else ops.CastBatch([w.detach() for w in ws], [wstack[i] for i in range(nl)])
+            ent = (ptrs, pe_cd, wstack, cb, torch.empty(nl, 2 * T - 1, d, device=device, dtype=cd))
+            self._rel_cache[key] = ent
+        _, pe_cd, wstack, cb, pos_all = ent
+        if cb is not None:
+            cb.refresh()
+        else:
+            for i, w in enumerate(ws):
+                wstack[i].copy_(w.detach())
+        ops.gemm(pe_cd, wstack, pos_all, 2 * T - 1, d, d, batch=nl, stride_a=0, stride_b=d * d,
+                 stride_c=(2 * T - 1) * d)
+        return pe_cd, pos_all
 
     def _shadows(self, device):
         """Compute-dtype copies of every layer's weight matrices and their transposes, refreshed by
@@ -622,7 +664,12 @@ class Conformer(nn.Module):
         if seed is None:
             seed = (self._step * 1000003 + 12345) & 0x7FFFFFFF
             self._step += 1
-        pe = self._pe(T, x.device) if self.pos_enc == "rel" else None
+        pe = pos_all = None
+        if self.pos_enc == "rel":
+            if REL_BATCH:
+                pe, pos_all = self._rel_tables(T, x.device)
+            else:
+                pe = self._pe(T, x.device)
         shadows = self._shadows(x.device)
         # grouped weight gradients need layer 0 to run backward last (it flushes the group): true for the
         # sequential encoder; deferral is per layer and falls back when a .grad accumulates
@@ -632,7 +679,8 @@ class Conformer(nn.Module):
                                      layer_index=i, group_wgrad=group,
                                      grad_dest=self.grad_dest[i] if self.grad_dest else None,
                                      flush_here=i in self.flush_layers, on_flushed=self.on_flushed,
-                                     sync_bn=self.sync_bn, count_batches=False, on_routed=self.on_routed)
+                                     sync_bn=self.sync_bn, count_batches=False, on_routed=self.on_routed,
+                                     pos_pre=None if pos_all is None else pos_all[i])
         # every layer's BatchNorm num_batches_tracked += 1 in one multi-tensor launch (not one per layer)
         counters = [ly.conv_module.sequential[3].num_batches_tracked for ly in self.conformer_layers
                     if self.training and ly.conv_module.sequential[3].track_running_stats]

@@ -116,8 +116,10 @@ __global__ __launch_bounds__(256) void ctc_prep(CtcP p) {
 // ---------------------------------------------------------------------------------- alpha / beta
 // blockIdx.x = utterance, blockIdx.y = 0 (alpha, forward in time) / 1 (beta, backward in time).
 // Thread `tid` owns states tid + 256 j, j < SPT.
-template <int SPT>
-__global__ __launch_bounds__(AB_THREADS) void ctc_alphabeta(CtcP p) {
+// NT threads (one state each when S <= NT): the L60 targets (749 states) ran at SPT 4 on 256 threads, one
+// state chain after another on one wave per SIMD (0.67 us per frame); NT 1024 puts four waves on each SIMD
+template <int SPT, int NT = AB_THREADS>
+__global__ __launch_bounds__(NT) void ctc_alphabeta(CtcP p) {
   extern __shared__ float sh[];        // [2][S]
   const int b = blockIdx.x, dir = blockIdx.y, tid = threadIdx.x;
   const int Tb = in_len_of(p, b), L = tgt_len_of(p, b), Sb = 2 * L + 1;
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(AB_THREADS) void ctc_alphabeta(CtcP p) {
   int sidx[SPT];
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
-    const int s = tid + AB_THREADS * j;
+    const int s = tid + NT * j;
     sidx[j] = s;
     if (dir == 0) skip[j] = s < Sb && s >= 2 && (s & 1) && ext_label(p, tg, s) != ext_label(p, tg, s - 2);
     else skip[j] = s + 2 < Sb && (s & 1) && ext_label(p, tg, s) != ext_label(p, tg, s + 2);
@@ -363,10 +365,10 @@ CFM_EXPORT int cfm_ctc_loss_fwd(const float* logits, long sb, long st, const int
   const size_t sh = 2 * S * sizeof(float);
   if (S <= AB_THREADS)
     hipLaunchKernelGGL(ctc_alphabeta<1>, dim3(B, 2), dim3(AB_THREADS), sh, s, p);
-  else if (S <= 2 * AB_THREADS)
-    hipLaunchKernelGGL(ctc_alphabeta<2>, dim3(B, 2), dim3(AB_THREADS), sh, s, p);
+  else if (S <= 512)
+    hipLaunchKernelGGL((ctc_alphabeta<1, 512>), dim3(B, 2), dim3(512), sh, s, p);
   else
-    hipLaunchKernelGGL(ctc_alphabeta<4>, dim3(B, 2), dim3(AB_THREADS), sh, s, p);
+    hipLaunchKernelGGL((ctc_alphabeta<1, 1024>), dim3(B, 2), dim3(1024), sh, s, p);
   hipLaunchKernelGGL(ctc_finish, dim3(cdiv(B, 256)), dim3(256), 0, s, p.nll_raw, B, zero_infinity, nll);
   return cfm::check_launch("cfm_ctc_loss_fwd");
 }
