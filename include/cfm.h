@@ -410,7 +410,8 @@ int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, const float* 
                  void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H,
                  int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream);
 /* The same with D = rowsum(dO * O) already in ws (cfm_gemm_desc.rowdot_* of the GEMM that produced dout):
-   the D kernel is skipped.  bf16 MFMA path only (no rel-pos, dk <= 64); others behave as cfm_attn_bwd. */
+   the D kernel is skipped.  bf16 MFMA path only (dk <= 64); rel-pos: ws is the full cfm_attn_bwd_ws_bytes
+   workspace with D in its first B*H*T floats. */
 int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* dout, const float* lse,
                         const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                         void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H,

@@ -310,15 +310,20 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
     g4 = _g2(g, g2, "mha", cfg, seed)
     grads[10], grads[11] = _wgrad_bias(side, g4, o, 10)
     wt = _wt(cfg, 10)
-    if wt is not None and not cfg.rel and d // H == 64 and cd == torch.bfloat16 and "rowdot" not in ops.DISABLED:
-        # D = rowsum(dO * O) per head from the epilogue of the GEMM producing dO (no separate pass)
-        Dh = torch.empty(B * H * T, device=g4.device, dtype=torch.float32)
+    aws = None
+    if wt is not None and d // H == 64 and cd == torch.bfloat16 and "rowdot" not in ops.DISABLED:
+        # D = rowsum(dO * O) per head from the epilogue of the GEMM producing dO (no separate pass); rel-pos: written
+        # into the head of the attention backward's workspace
+        if cfg.rel:
+            aws, Dh = ops.attn_ws(B, T, H, d // H, True, g4.device)
+        else:
+            Dh = torch.empty(B * H * T, device=g4.device, dtype=torch.float32)
         do = ops.linear_dgrad(g4, wout, wt=wt, rowdot=(o, Dh, T))
     else:
         Dh = None
         do = ops.linear_dgrad(g4, wout, wt=wt)
     dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed,
-                                        D=Dh)
+                                        D=Dh, ws=aws)
     if cfg.rel:
         dpc, pec = _w(dpos, cd), _w(cfg.pe, cd)
         if REL_BATCH and side.group is not None and ops.wgrad_group_ok(dpc, pec):

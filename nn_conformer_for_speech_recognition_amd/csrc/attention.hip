@@ -822,8 +822,7 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
   CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0, CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(!pos || (pos_u && pos_v && dpos && dpos_u && dpos_v), CFM_ERR_ARG, "rel-pos grads need buffers");
   hipStream_t s = cfm::as_stream(stream);
-  CFM_REQUIRE(!d_ready || (use_mfma(dtype, pos, dk) && !pos), CFM_ERR_UNSUPPORTED,
-              "precomputed D: bf16 MFMA path without rel-pos only");
+  CFM_REQUIRE(!d_ready || use_mfma(dtype, pos, dk), CFM_ERR_UNSUPPORTED, "precomputed D: bf16 MFMA path only");
   if (!use_mfma(dtype, pos, dk))
     return cfm::attn_simt_bwd_launch(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B,
                                      T, H, dk, dtype, drop_p, seed, ws, s);

@@ -771,12 +771,24 @@ def attn_fwd(qkv, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, dr
     return o, lse
 
 
+def attn_ws(B, T, H, dk, rel, device, dtype=torch.bfloat16):
+    """A backward workspace (cfm_attn_bwd_ws_bytes) whose first B*H*T floats are the D slot: (ws, D view)."""
+    ws = workspace(L.size_call("cfm_attn_bwd_ws_bytes", B, T, H, dk, int(rel), L.dt(torch.empty(0, dtype=dtype))),
+                   device)
+    return ws, ws[: B * H * T]
+
+
 def attn_bwd(qkv, o, dout, lse, lengths_i32, B, T, H, dk, pos=None, pos_u=None, pos_v=None, drop_p=0.0, seed=0,
-             D=None):
+             D=None, ws=None):
     """D: optional (B*H*T,) fp32 rowsum(dO * O) per head, precomputed by the GEMM that produced dout
-    (linear_dgrad(rowdot=...)); bf16 MFMA path only."""
+    (linear_dgrad(rowdot=...)); bf16 MFMA path only.  Rel-pos: D must be the head of ws (attn_ws)."""
     rel = pos is not None
-    if D is not None:
+    if D is not None and ws is not None:
+        if D.data_ptr() != ws.data_ptr():
+            raise L.CfmError("attn_bwd: D must be the first B*H*T floats of ws")
+    elif D is not None:
+        if rel:
+            raise L.CfmError("attn_bwd: rel-pos with a precomputed D needs its workspace (attn_ws)")
         ws = D
     else:
         ws = workspace(L.size_call("cfm_attn_bwd_ws_bytes", B, T, H, dk, int(rel), L.dt(qkv)), qkv.device)
