@@ -1177,8 +1177,7 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
                        rp, (const bf16*)dsbuf, ldS, dpos_part);
   colreduce(dpos_part, p.B, (long)(2 * p.T - 1) * p.HD, dpos, 0, s);
   const int nrows = p.B * 4 * cdiv(p.T, 128);
-  colreduce(part, nrows, (long)p.HD, dpu, 0, s, 2L * p.HD);
-  colreduce(part + p.HD, nrows, (long)p.HD, dpv, 0, s, 2L * p.HD);
+  colreduce_pair(part, part + p.HD, nrows, (long)p.HD, dpu, dpv, s, 2L * p.HD);   // du, dv: one launch
   return check_launch("cfm_attn_bwd(rel)");
 }
 

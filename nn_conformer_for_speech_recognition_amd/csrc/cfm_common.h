@@ -27,9 +27,10 @@ int fail(int code, const std::string& msg);
 int check_launch(const char* what);
 // out[n] (+)= sum_p part[p*ldp + n]  (deterministic, block = 16 waves x 64 columns; ldp 0 -> N)
 void colreduce(const float* part, int nparts, long N, float* out, int accumulate, hipStream_t s, long ldp = 0);
-// out{A,B}[n] = sum_p part{A,B}[p * N + n]: two reductions, one launch (bit-identical to two colreduce calls)
+// out{A,B}[n] = sum_p part{A,B}[p * ldp + n]: two reductions, one launch (bit-identical to two colreduce calls;
+// ldp 0 -> N)
 void colreduce_pair(const float* partA, const float* partB, int nparts, long N, float* outA, float* outB,
-                    hipStream_t s);
+                    hipStream_t s, long ldp = 0);
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // device step counter bound by cfm_rng_bind (nullptr: seeds are used as passed); read by every
 // dropout kernel at run time so one captured HIP graph replays with fresh masks each step

@@ -298,7 +298,7 @@ __global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict
 // two independent column reductions in one launch (blockIdx.y selects): BatchNorm's (sum, sumsq) /
 // (dbeta, dgamma) partial pairs
 __global__ __launch_bounds__(1024) void colreduce2_kernel(const float* __restrict__ partA, const float* __restrict__ partB,
-                                                          int nparts, long N, float* __restrict__ outA,
+                                                          int nparts, long N, long ldp, float* __restrict__ outA,
                                                           float* __restrict__ outB) {
   __shared__ float red[16][64];
   const float* part = blockIdx.y ? partB : partA;
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(1024) void colreduce2_kernel(const float* __restric
     for (int p0 = wv; p0 < nparts; p0 += 16 * 16) {
       float v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = p0 + 16 * u < nparts ? part[(long)(p0 + 16 * u) * N + n] : 0.f;
+      for (int u = 0; u < 16; ++u) v[u] = p0 + 16 * u < nparts ? part[(long)(p0 + 16 * u) * ldp + n] : 0.f;
 #pragma unroll
       for (int u = 0; u < 16; ++u) s += v[u];
     }
@@ -351,9 +351,9 @@ __global__ __launch_bounds__(256) void colreduce_few_kernel(const float* __restr
 
 namespace cfm {
 void colreduce_pair(const float* partA, const float* partB, int nparts, long N, float* outA, float* outB,
-                    hipStream_t s) {
+                    hipStream_t s, long ldp) {
   hipLaunchKernelGGL(colreduce2_kernel, dim3((unsigned)((N + 63) / 64), 2), dim3(1024), 0, s, partA, partB, nparts, N,
-                     outA, outB);
+                     ldp > 0 ? ldp : N, outA, outB);
 }
 void colreduce(const float* part, int nparts, long N, float* out, int accumulate, hipStream_t s, long ldp) {
   const long lp = ldp > 0 ? ldp : N;

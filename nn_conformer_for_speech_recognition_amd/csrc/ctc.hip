@@ -210,23 +210,41 @@ __global__ void ctc_finish(const float* nll_raw, int B, int zero_inf, float* nll
 // chain -- O(L) per frame instead of the O(L^2) first-occurrence scans it did per frame (global label loads
 // per comparison: 0.8 ms per step at L60's ~500-label utterances)
 __global__ __launch_bounds__(256) void ctc_group(CtcP p) {
-  const int b = blockIdx.x, L = tgt_len_of(p, b);
+  const int b = blockIdx.x, L = tgt_len_of(p, b), Lp = (L + 15) & ~15;
   const int32_t* tg = tgt_of(p, b);
-  extern __shared__ int lab[];            // [Smax] clamped labels of the utterance
-  for (int u = threadIdx.x; u < L; u += 256) lab[u] = label_of(p, tg, u);
+  extern __shared__ int4 lab4[];          // [Smax rounded up to 16] clamped labels of the utterance, -1 past L
+  int* lab = reinterpret_cast<int*>(lab4);
+  for (int u = threadIdx.x; u < Lp; u += 256) lab[u] = u < L ? label_of(p, tg, u) : -1;
   __syncthreads();
   int32_t* head = p.grp + (long)b * 2 * p.Smax;
   int32_t* nxt = head + p.Smax;
+  // both scans read 16 labels (four ds_read_b128) per step: the loops are LDS-latency bound, and a rare class
+  // walks the whole utterance (one label per read: 65 us at L60's ~500-label utterances)
   for (int u = threadIdx.x; u < L; u += 256) {
     const int c = lab[u];
     bool first = true;
-    for (int w = 0; w < u && first; ++w) first = lab[w] != c;
-    int n = -1;
-    for (int w = u + 1; w < L; ++w)
-      if (lab[w] == c) {
-        n = w;
-        break;
+    for (int w0 = 0; w0 < u && first; w0 += 16) {
+      int v[16];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int4 q = lab4[w0 / 4 + k];
+        v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
       }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) first = first && !(w0 + j < u && v[j] == c);
+    }
+    int n = -1;
+    for (int w0 = (u + 1) & ~15; w0 < L && n < 0; w0 += 16) {
+      int v[16];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int4 q = lab4[w0 / 4 + k];
+        v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
+      }
+#pragma unroll
+      for (int j = 15; j >= 0; --j)           // descending: the smallest match in the chunk wins
+        if (w0 + j > u && v[j] == c) n = w0 + j;
+    }
     head[u] = first ? 1 : 0;
     nxt[u] = n;
   }
@@ -386,7 +404,7 @@ CFM_EXPORT int cfm_ctc_loss_bwd(const float* logits, long sb, long st, const int
   CtcP p = make_p(logits, sb, st, targets, ldt, tgt_off, in_len, tgt_len, B, T, V, Smax, blank, const_cast<float*>(ws));
   const size_t sh = (size_t)V * sizeof(float);
   const dim3 grid((unsigned)((long)B * T));
-  if (Smax > 0) hipLaunchKernelGGL(ctc_group, dim3(B), dim3(256), (size_t)Smax * sizeof(int), s, p);
+  if (Smax > 0) hipLaunchKernelGGL(ctc_group, dim3(B), dim3(256), (size_t)((Smax + 15) & ~15) * sizeof(int), s, p);
   if (dtype_grad == CFM_BF16)
     hipLaunchKernelGGL(ctc_grad<bf16>, grid, dim3(256), sh, s, p, grad_out, grad_out_stride, reduction,
                        zero_infinity, (bf16*)grad_logits, gsb, gst);
