@@ -12,9 +12,9 @@
 // Kernels (B utterances, T frames, V classes, L_b target labels, S_b = 2 L_b + 1 states):
 //   ctc_prep     one wave per frame row: lse = logsumexp(logits row); lpe[b,t,s] = logit of the
 //                s-th extended label (blank, l1, blank, l2, ...) - lse          HBM: one row read
-//   ctc_alphabeta one workgroup per (utterance, direction); states across threads, the time loop
-//                sequential with one barrier per frame; lpe rows are prefetched 16 frames ahead
-//                into registers (coalesced, latency hidden behind the recursion)
+//   ctc_alphabeta one workgroup per (utterance, direction), one state per thread; the time loop sequential,
+//                the 16 waves pipelined a block of 16 frames apart through edge rings in LDS (no workgroup
+//                barrier per frame); lpe rows are prefetched 16 frames ahead into registers
 //   ctc_grad     one workgroup per frame row: grad[v] = (exp(logit - lse) - sum_{s: l'(s)=v}
 //                exp(alpha + beta + nll - lpe)) * scale; duplicate labels are summed in label order
 //                (deterministic, no atomics)
@@ -25,7 +25,6 @@
 namespace {
 
 constexpr float NEG_INF = -INFINITY;
-constexpr int AB_THREADS = 256;
 constexpr int PF = 16;   // frames of lpe prefetched per chunk
 
 __device__ __forceinline__ float lse2(float a, float b) {
@@ -114,85 +113,146 @@ __global__ __launch_bounds__(256) void ctc_prep(CtcP p) {
 }
 
 // ---------------------------------------------------------------------------------- alpha / beta
-// blockIdx.x = utterance, blockIdx.y = 0 (alpha, forward in time) / 1 (beta, backward in time).
-// Thread `tid` owns states tid + 256 j, j < SPT.
-// NT threads (one state each when S <= NT): the L60 targets (749 states) ran at SPT 4 on 256 threads, one
-// state chain after another on one wave per SIMD (0.67 us per frame); NT 1024 puts four waves on each SIMD
-template <int SPT, int NT = AB_THREADS>
-__global__ __launch_bounds__(NT) void ctc_alphabeta(CtcP p) {
-  extern __shared__ float sh[];        // [2][S]
-  const int b = blockIdx.x, dir = blockIdx.y, tid = threadIdx.x;
+// blockIdx.x = utterance, blockIdx.y = 0 (alpha, forward in time) / 1 (beta, backward in time); 1024 threads.
+// Wave-pipelined in blocks of PF frames: wave w owns states 64 w + lane and keeps its state's value of the previous
+// frame in a register; the in-wave neighbours s - 1, s - 2 (beta: s + 1, s + 2) arrive by DPP wave shifts, and only
+// the two states across a wave boundary come through LDS: every frame the edge lanes store their values into a
+// ring, and after each block of PF frames the wave publishes the block index.  Its successor waits for that once
+// per block, loads the block's PF edge pairs into lanes 0..PF-1 and reads them per frame with v_readlane, so it
+// runs one block behind with no synchronisation inside the block (the barrier form paid a workgroup barrier and
+// an LDS round trip on every frame: 0.35 us per frame at L60).  A wait gives up after AB_SPIN polls (the loss is
+// then NaN), so no wave can spin forever.  The per-state arithmetic and its argument order are the barrier
+// form's: the same sums bit for bit.
+constexpr int AB_NT = 1024;
+constexpr int AB_RB = 4;                  // ring depth in blocks
+constexpr int AB_RF = AB_RB * PF;         // ring depth in frames
+constexpr int AB_SPIN = 1 << 16;
+typedef float f32x2e __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) volatile int lds_int;
+typedef __attribute__((address_space(3))) volatile float lds_float;
+
+template <int DIR>
+__device__ __forceinline__ void ctc_alphabeta_dir(const CtcP& p, f32x2e* edge_mem, int* tag_mem, int* abort_mem,
+                                                  float* fin) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int Tb = in_len_of(p, b), L = tgt_len_of(p, b), Sb = 2 * L + 1;
   const int32_t* tg = tgt_of(p, b);
-  float* out = (dir == 0 ? p.alpha : p.beta) + (long)b * p.T * p.S;
+  float* out = (DIR == 0 ? p.alpha : p.beta) + (long)b * p.T * p.S;
   const float* lp = p.lpe + (long)b * p.T * p.S;
-  if (Tb <= 0) {
-    if (dir == 0 && tid == 0) p.nll_raw[b] = L == 0 ? 0.f : INFINITY;
-    return;
-  }
-  // per-state transition flags: alpha may skip from s-2 (beta: from s+2) when the labels differ
-  bool skip[SPT];
-  int sidx[SPT];
-#pragma unroll
-  for (int j = 0; j < SPT; ++j) {
-    const int s = tid + NT * j;
-    sidx[j] = s;
-    if (dir == 0) skip[j] = s < Sb && s >= 2 && (s & 1) && ext_label(p, tg, s) != ext_label(p, tg, s - 2);
-    else skip[j] = s + 2 < Sb && (s & 1) && ext_label(p, tg, s) != ext_label(p, tg, s + 2);
-  }
-  // frame order: step i handles t = i (alpha) or Tb-1-i (beta)
-  auto frame = [&](int i) { return dir == 0 ? i : Tb - 1 - i; };
-  float cur[SPT][PF], nxt[SPT][PF];
-  auto fetch = [&](float (&r)[SPT][PF], int i0) {
-#pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int i = i0 + q;
-#pragma unroll
-      for (int j = 0; j < SPT; ++j)
-        r[j][q] = (i < Tb && sidx[j] < Sb) ? lp[(long)frame(i) * p.S + sidx[j]] : NEG_INF;
+  lds_int* tags = (lds_int*)tag_mem;
+  lds_int* abort_flag = (lds_int*)abort_mem;
+  lds_float* edge = (lds_float*)edge_mem;   // [wave][frame % AB_RF][2]
+  const int nw = (Sb + 63) >> 6;
+  const int s = 64 * w + lane, sc = min(s, Sb - 1);
+  const bool valid = s < Sb;
+  bool skip;   // alpha may skip from s-2 (beta: from s+2) when the labels differ
+  if (DIR == 0) skip = valid && s >= 2 && (s & 1) && ext_label(p, tg, s) != ext_label(p, tg, s - 2);
+  else skip = s + 2 < Sb && (s & 1) && ext_label(p, tg, s) != ext_label(p, tg, s + 2);
+  const bool has_pred = DIR == 0 ? (w > 0) : (w + 1 < nw);     // the wave whose edge states this one reads
+  const bool has_succ = DIR == 0 ? (w + 1 < nw) : (w > 0);     // the wave that reads this one's
+  const int pw = DIR == 0 ? w - 1 : w + 1, sw = DIR == 0 ? w + 1 : w - 1;
+  const int le0 = DIR == 0 ? 63 : 0, le1 = DIR == 0 ? 62 : 1;   // this wave's edge lanes (nearest first)
+  auto frame = [&](int i) { return DIR == 0 ? i : Tb - 1 - i; };
+  auto wait_tag = [&](int ww, int want) {   // wave-uniform spin until wave ww has published block `want`
+    for (int spin = 0;; ++spin) {
+      if (__builtin_amdgcn_readfirstlane(tags[ww]) >= want) return;
+      if (spin >= AB_SPIN || __builtin_amdgcn_readfirstlane(*abort_flag)) {
+        *abort_flag = 1;
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
     }
   };
-  fetch(cur, 0);
-  for (int i0 = 0; i0 < Tb; i0 += PF) {
-    if (i0 + PF < Tb) fetch(nxt, i0 + PF);
+  // lpe of this state, PF frames per block prefetched one block ahead (unconditional clamped loads)
+  float cur[PF], nxt[PF];
+  auto fetch = [&](float (&r)[PF], int i0) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) r[q] = lp[(long)frame(min(i0 + q, Tb - 1)) * p.S + sc];
+  };
+  const int nsteps = w < nw ? Tb : 0;
+  float prev = NEG_INF;
+  if (nsteps) fetch(cur, 0);
+  for (int i0 = 0; i0 < nsteps; i0 += PF) {
+    const int kb = i0 / PF;
+    fetch(nxt, min(i0 + PF, Tb - 1));
+    // the predecessor's edge pairs of frames i0 - 1 .. i0 + PF - 2, frame i0 - 1 + j in lane j
+    float ex = NEG_INF, ey = NEG_INF;
+    if (has_pred) {
+      wait_tag(pw, kb);
+      const int f = (max(i0 - 1 + lane, 0) & (AB_RF - 1)) + pw * AB_RF;
+      ex = edge[2 * f];
+      ey = edge[2 * f + 1];
+    }
+    // ring reuse: this block overwrites block kb - RB, whose last frame the successor loads when it starts block
+    // kb - RB + 1 (after which it publishes kb - RB + 1)
+    if (has_succ && kb >= AB_RB) wait_tag(sw, kb - AB_RB + 1);
+    // branch-free body (the DPP / readlane are convergent: a data-dependent exit keeps the loop from unrolling);
+    // steps past the utterance in the last block change nothing
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
       const int i = i0 + q;
-      if (i >= Tb) break;
-      const int t = frame(i);
-      float* wr = sh + (i & 1) * p.S;
-      const float* rd = sh + ((i + 1) & 1) * p.S;
-#pragma unroll
-      for (int j = 0; j < SPT; ++j) {
-        const int s = sidx[j];
-        if (s >= Sb) continue;
-        float v;
-        if (i == 0) {
-          v = dir == 0 ? (s <= 1 ? cur[j][q] : NEG_INF) : (s >= Sb - 2 ? cur[j][q] : NEG_INF);
-        } else if (dir == 0) {
-          const float a0 = rd[s], a1 = s >= 1 ? rd[s - 1] : NEG_INF, a2 = skip[j] ? rd[s - 2] : NEG_INF;
-          v = lse3(a0, a1, a2) + cur[j][q];
-        } else {
-          const float a0 = rd[s], a1 = s + 1 < Sb ? rd[s + 1] : NEG_INF, a2 = skip[j] ? rd[s + 2] : NEG_INF;
-          v = lse3(a0, a1, a2) + cur[j][q];
-        }
-        wr[s] = v;
-        out[(long)t * p.S + s] = v;
+      const bool live = i < nsteps;
+      // previous frame's neighbours: alpha lane l <- lane l - 1 (wave_shr), beta lane l <- lane l + 1 (wave_shl);
+      // the edge lanes get -inf, then the predecessor's pair
+      constexpr int SH = DIR == 0 ? 0x138 : 0x130;
+      const int ninf = __float_as_int(NEG_INF);
+      float n1 = __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(prev), SH, 0xF, 0xF, false));
+      float n2 = __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(n1), SH, 0xF, 0xF, false));
+      if (has_pred) {
+        const float e0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ex), q));
+        const float e1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ey), q));
+        const int l0 = DIR == 0 ? 0 : 63, l1 = DIR == 0 ? 1 : 62;
+        if (lane == l0) { n1 = e0; n2 = e1; }
+        if (lane == l1) n2 = e0;
       }
-      // LDS hand-off only: __syncthreads() also waited, every frame, for the frame's alpha / beta stores and for the
-      // lpe prefetch 16 frames ahead (read by ctc_grad / this loop later; kernel boundary / counted waits order them)
-      lds_barrier();
+      float a1, a2;
+      if (DIR == 0) { a1 = s >= 1 ? n1 : NEG_INF; a2 = skip ? n2 : NEG_INF; }
+      else { a1 = s + 1 < Sb ? n1 : NEG_INF; a2 = skip ? n2 : NEG_INF; }
+      float v = lse3(prev, a1, a2) + cur[q];
+      if (i == 0) v = DIR == 0 ? (s <= 1 ? cur[q] : NEG_INF) : (s >= Sb - 2 ? cur[q] : NEG_INF);
+      if (!valid) v = NEG_INF;
+      if (live) {
+        if (valid) out[(long)frame(i) * p.S + s] = v;
+        prev = v;
+        const int f = (i & (AB_RF - 1)) + w * AB_RF;
+        if (lane == le0) edge[2 * f] = v;
+        if (lane == le1) edge[2 * f + 1] = v;
+      }
     }
+    // the block's edge stores land before its index (every wave publishes: the index is also the progress its
+    // predecessor's ring reuse waits on)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) tags[w] = kb;
 #pragma unroll
-    for (int q = 0; q < PF; ++q)
-#pragma unroll
-      for (int j = 0; j < SPT; ++j) cur[j][q] = nxt[j][q];
+    for (int q = 0; q < PF; ++q) cur[q] = nxt[q];
   }
-  if (dir == 0 && tid == 0) {
-    const float* last = sh + ((Tb - 1) & 1) * p.S;
-    const float l1 = last[Sb - 1], l2 = Sb >= 2 ? last[Sb - 2] : NEG_INF;
-    p.nll_raw[b] = -lse2(l1, l2);
+  if (DIR == 0) {
+    if (s == Sb - 1) fin[0] = prev;
+    if (s == Sb - 2) fin[1] = prev;
   }
+}
+
+__global__ __launch_bounds__(AB_NT) void ctc_alphabeta(CtcP p) {
+  __shared__ f32x2e edge[(AB_NT / 64) * AB_RF];
+  __shared__ int tags[AB_NT / 64];
+  __shared__ int abort_flag;
+  __shared__ float fin[2];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int Tb = in_len_of(p, b), L = tgt_len_of(p, b);
+  if (Tb <= 0) {   // uniform over the workgroup
+    if (blockIdx.y == 0 && tid == 0) p.nll_raw[b] = L == 0 ? 0.f : INFINITY;
+    return;
+  }
+  if (tid < AB_NT / 64) tags[tid] = -1;
+  if (tid == 0) {
+    abort_flag = 0;
+    fin[0] = fin[1] = NEG_INF;
+  }
+  __syncthreads();
+  if (blockIdx.y == 0) ctc_alphabeta_dir<0>(p, edge, tags, &abort_flag, fin);
+  else ctc_alphabeta_dir<1>(p, edge, tags, &abort_flag, fin);
+  __syncthreads();
+  if (blockIdx.y == 0 && tid == 0) p.nll_raw[b] = abort_flag ? NAN : -lse2(fin[0], fin[1]);
 }
 
 // nll (B): -log p, or 0 where infinite and zero_infinity
@@ -375,18 +435,11 @@ CFM_EXPORT int cfm_ctc_loss_fwd(const float* logits, long sb, long st, const int
   CFM_REQUIRE(B > 0 && T > 0 && V > 0 && Smax >= 0 && (tgt_off || ldt >= Smax), CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(blank >= 0 && blank < V, CFM_ERR_ARG, "blank out of range");
   const int S = 2 * Smax + 1;
-  CFM_REQUIRE(S <= 4 * AB_THREADS, CFM_ERR_UNSUPPORTED, "target length must be <= 511");
-  CFM_REQUIRE(2L * S * sizeof(float) <= 64 * 1024, CFM_ERR_UNSUPPORTED, "state count");
+  CFM_REQUIRE(S <= AB_NT, CFM_ERR_UNSUPPORTED, "target length must be <= 511");
   hipStream_t s = cfm::as_stream(stream);
   CtcP p = make_p(logits, sb, st, targets, ldt, tgt_off, in_len, tgt_len, B, T, V, Smax, blank, ws);
   hipLaunchKernelGGL(ctc_prep, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s, p);
-  const size_t sh = 2 * S * sizeof(float);
-  if (S <= AB_THREADS)
-    hipLaunchKernelGGL(ctc_alphabeta<1>, dim3(B, 2), dim3(AB_THREADS), sh, s, p);
-  else if (S <= 512)
-    hipLaunchKernelGGL((ctc_alphabeta<1, 512>), dim3(B, 2), dim3(512), sh, s, p);
-  else
-    hipLaunchKernelGGL((ctc_alphabeta<1, 1024>), dim3(B, 2), dim3(1024), sh, s, p);
+  hipLaunchKernelGGL(ctc_alphabeta, dim3(B, 2), dim3(AB_NT), 0, s, p);
   hipLaunchKernelGGL(ctc_finish, dim3(cdiv(B, 256)), dim3(256), 0, s, p.nll_raw, B, zero_infinity, nll);
   return cfm::check_launch("cfm_ctc_loss_fwd");
 }
