@@ -35,6 +35,15 @@ __device__ __forceinline__ float lse2(float a, float b) {
 // the alpha / beta recursion's 3-way log-sum-exp on the hardware exp2 / log2 (v_exp_f32 / v_log_f32: the
 // arguments are <= 0 and the sum is in [1, 3], where both are accurate to about an ulp): the libm expf / logf
 // range reductions made this the recursion's critical path (one barrier-separated frame per ~0.9 us at L60)
+// the recursion's form: the largest of the three contributes exactly 1, so only the other two need an exponential
+// (max3 / med3 / min3 are single instructions; the recursion is VALU-issue bound with 16 waves on 4 SIMDs)
+__device__ __forceinline__ float lse3r(float a, float b, float c) {
+  constexpr float L2E = 1.4426950408889634f, LN2F = 0.6931471805599453f;
+  const float m = fmaxf(fmaxf(a, b), c), md = __builtin_amdgcn_fmed3f(a, b, c), lo = fminf(fminf(a, b), c);
+  if (m == NEG_INF) return NEG_INF;
+  const float s = 1.f + (__builtin_amdgcn_exp2f((md - m) * L2E) + __builtin_amdgcn_exp2f((lo - m) * L2E));
+  return m + __builtin_amdgcn_logf(s) * LN2F;
+}
 __device__ __forceinline__ float lse3(float a, float b, float c) {
   constexpr float L2E = 1.4426950408889634f, LN2F = 0.6931471805599453f;
   const float m = fmaxf(fmaxf(a, b), c);
@@ -116,23 +125,22 @@ __global__ __launch_bounds__(256) void ctc_prep(CtcP p) {
 // blockIdx.x = utterance, blockIdx.y = 0 (alpha, forward in time) / 1 (beta, backward in time); 1024 threads.
 // Wave-pipelined in blocks of PF frames: wave w owns states 64 w + lane and keeps its state's value of the previous
 // frame in a register; the in-wave neighbours s - 1, s - 2 (beta: s + 1, s + 2) arrive by DPP wave shifts, and only
-// the two states across a wave boundary come through LDS: every frame the edge lanes store their values into a
-// ring, and after each block of PF frames the wave publishes the block index.  Its successor waits for that once
-// per block, loads the block's PF edge pairs into lanes 0..PF-1 and reads them per frame with v_readlane, so it
+// the two states across a wave boundary come through LDS: the edge lanes store the block's PF values into a ring
+// (four 16-B stores each), and the wave then publishes the block index.  Its successor waits for that once per
+// block, loads the block's PF edge pairs into lanes 0..PF-1 and reads them per frame with v_readlane, so it
 // runs one block behind with no synchronisation inside the block (the barrier form paid a workgroup barrier and
 // an LDS round trip on every frame: 0.35 us per frame at L60).  A wait gives up after AB_SPIN polls (the loss is
-// then NaN), so no wave can spin forever.  The per-state arithmetic and its argument order are the barrier
-// form's: the same sums bit for bit.
+// then NaN), so no wave can spin forever.
 constexpr int AB_NT = 1024;
 constexpr int AB_RB = 4;                  // ring depth in blocks
 constexpr int AB_RF = AB_RB * PF;         // ring depth in frames
 constexpr int AB_SPIN = 1 << 16;
-typedef float f32x2e __attribute__((ext_vector_type(2)));
+typedef float f32x4e __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) volatile int lds_int;
 typedef __attribute__((address_space(3))) volatile float lds_float;
 
 template <int DIR>
-__device__ __forceinline__ void ctc_alphabeta_dir(const CtcP& p, f32x2e* edge_mem, int* tag_mem, int* abort_mem,
+__device__ __forceinline__ void ctc_alphabeta_dir(const CtcP& p, float* edge_mem, int* tag_mem, int* abort_mem,
                                                   float* fin) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int Tb = in_len_of(p, b), L = tgt_len_of(p, b), Sb = 2 * L + 1;
@@ -141,7 +149,7 @@ __device__ __forceinline__ void ctc_alphabeta_dir(const CtcP& p, f32x2e* edge_me
   const float* lp = p.lpe + (long)b * p.T * p.S;
   lds_int* tags = (lds_int*)tag_mem;
   lds_int* abort_flag = (lds_int*)abort_mem;
-  lds_float* edge = (lds_float*)edge_mem;   // [wave][frame % AB_RF][2]
+  lds_float* edge = (lds_float*)edge_mem;   // [2: nearest / second edge state][wave][frame % AB_RF]
   const int nw = (Sb + 63) >> 6;
   const int s = 64 * w + lane, sc = min(s, Sb - 1);
   const bool valid = s < Sb;
@@ -176,12 +184,12 @@ __device__ __forceinline__ void ctc_alphabeta_dir(const CtcP& p, f32x2e* edge_me
     const int kb = i0 / PF;
     fetch(nxt, min(i0 + PF, Tb - 1));
     // the predecessor's edge pairs of frames i0 - 1 .. i0 + PF - 2, frame i0 - 1 + j in lane j
-    float ex = NEG_INF, ey = NEG_INF;
+    float ex = NEG_INF, ey = NEG_INF, ev[PF];
     if (has_pred) {
       wait_tag(pw, kb);
       const int f = (max(i0 - 1 + lane, 0) & (AB_RF - 1)) + pw * AB_RF;
-      ex = edge[2 * f];
-      ey = edge[2 * f + 1];
+      ex = edge[f];
+      ey = edge[AB_NT / 64 * AB_RF + f];
     }
     // ring reuse: this block overwrites block kb - RB, whose last frame the successor loads when it starts block
     // kb - RB + 1 (after which it publishes kb - RB + 1)
@@ -205,18 +213,24 @@ __device__ __forceinline__ void ctc_alphabeta_dir(const CtcP& p, f32x2e* edge_me
         if (lane == l0) { n1 = e0; n2 = e1; }
         if (lane == l1) n2 = e0;
       }
-      float a1, a2;
-      if (DIR == 0) { a1 = s >= 1 ? n1 : NEG_INF; a2 = skip ? n2 : NEG_INF; }
-      else { a1 = s + 1 < Sb ? n1 : NEG_INF; a2 = skip ? n2 : NEG_INF; }
-      float v = lse3(prev, a1, a2) + cur[q];
-      if (i == 0) v = DIR == 0 ? (s <= 1 ? cur[q] : NEG_INF) : (s >= Sb - 2 ? cur[q] : NEG_INF);
+      // alpha: s - 1 < 0 only for lane 0 of wave 0, whose n1 is the DPP's -inf; beta: s + 1 >= Sb reads an invalid
+      // lane (kept at -inf) or the DPP's -inf
+      const float a2 = skip ? n2 : NEG_INF;
+      float v = lse3r(prev, n1, a2) + cur[q];
+      if (q == 0 && i0 == 0) v = DIR == 0 ? (s <= 1 ? cur[q] : NEG_INF) : (s >= Sb - 2 ? cur[q] : NEG_INF);
       if (!valid) v = NEG_INF;
       if (live) {
         if (valid) out[(long)frame(i) * p.S + s] = v;
         prev = v;
-        const int f = (i & (AB_RF - 1)) + w * AB_RF;
-        if (lane == le0) edge[2 * f] = v;
-        if (lane == le1) edge[2 * f + 1] = v;
+      }
+      ev[q] = v;   // the edge lanes' values of the block, stored once per block below
+    }
+    if (has_succ) {   // lanes le0 / le1: the block's PF values as four 16-B stores each
+      if (lane == le0 || lane == le1) {
+        lds_float* dst = edge + (lane == le0 ? 0 : AB_NT / 64 * AB_RF) + w * AB_RF + (i0 & (AB_RF - 1));
+#pragma unroll
+        for (int q = 0; q < PF; q += 4)
+          *(__attribute__((address_space(3))) volatile f32x4e*)(dst + q) = (f32x4e){ev[q], ev[q + 1], ev[q + 2], ev[q + 3]};
       }
     }
     // the block's edge stores land before its index (every wave publishes: the index is also the progress its
@@ -233,7 +247,7 @@ __device__ __forceinline__ void ctc_alphabeta_dir(const CtcP& p, f32x2e* edge_me
 }
 
 __global__ __launch_bounds__(AB_NT) void ctc_alphabeta(CtcP p) {
-  __shared__ f32x2e edge[(AB_NT / 64) * AB_RF];
+  __shared__ __attribute__((aligned(16))) float edge[2 * (AB_NT / 64) * AB_RF];
   __shared__ int tags[AB_NT / 64];
   __shared__ int abort_flag;
   __shared__ float fin[2];
