@@ -399,7 +399,8 @@ int cfm_glu_dwconv_bwd_bn(const void* dz, int dtype_dz, const float* y, const fl
    whole-head ones (T <= 384: one workgroup per (b, h) with K/V staged once in LDS); bits 1-2 timing
    experiments of the whole-head forward (value 2: staging only, 4: no output stores -- outputs invalid);
    bit 4 runs bf16 relative-position attention on the SIMT kernels (parity cross-check); bit 6 keeps the
-   rel-pos kernels' zero-filling (non-clamped) tile loads. */
+   rel-pos kernels' zero-filling (non-clamped) tile loads; bit 7 runs the round-4 rel-pos dpos kernel (one
+   workgroup per (utterance, head, 64 relative rows); the round-5 kernel is checked against it). */
 int cfm_attn_set_mode(int mode);
 int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t* lengths, const void* pos,
                  const float* pos_u, const float* pos_v, int B, int T, int H, int dk, int dtype,

@@ -769,8 +769,7 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dkdv_kernel(AttnM p, RelP rp
       sstore(cur ^ 1);
       ring_chunk_store(sring + ((qt + 3) & (RING - 1)) * TILE * KS, rr, tid);
     }
-    if (p.dbg & 256) __syncthreads();   // A/B (cfm_attn_set_mode bit 8): the round-4 fenced barrier
-    else lds_barrier();     // (not __syncthreads: its fence would wait for this tile's dS stores every tile)
+    lds_barrier();     // (not __syncthreads: its fence would wait for this tile's dS stores every tile)
   }
   float* stage = sst + wv * 32 * SS2;    // 32 x 68 >= 32 x 65 floats
   const int nvalid = min(32, p.T - k0w);
@@ -1144,7 +1143,6 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
                         const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
                         int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s) {
   AttnM p = make_attnm(qkv, dout, len, B, T, H, dk, drop_p, seed);
-  p.dbg = g_rel_mode & 256;
   const RelP rp = make_relp(pos, pu, pv, p.dk);
   const size_t d_bytes = ((size_t)p.B * p.H * p.T * sizeof(float) + 255) & ~(size_t)255;
   float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + d_bytes);
