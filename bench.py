@@ -32,7 +32,7 @@ from nn_conformer_for_speech_recognition_amd import _lib  # noqa: E402
 from nn_conformer_for_speech_recognition_amd import dist as cdist  # noqa: E402
 from nn_conformer_for_speech_recognition_amd import ops  # noqa: E402
 from nn_conformer_for_speech_recognition_amd import specaugment  # noqa: E402
-from nn_conformer_for_speech_recognition_amd.ctc import ctc_head_loss  # noqa: E402
+from nn_conformer_for_speech_recognition_amd.ctc import ctc_head_loss, set_nonfinite_counter  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.conformer import Conformer  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.frontend import frame_frontend, linear  # noqa: E402
 from nn_conformer_for_speech_recognition_amd.lib.convsubsampling import ConvSubSampling  # noqa: E402
@@ -519,6 +519,8 @@ class Harness:
         self.tlen_i32 = torch.full((B,), U, dtype=torch.int32, device=dev)
         self.seed0 = 17 * rank + 1
         self.bad = torch.zeros(1, dtype=torch.int32, device=dev)     # steps whose loss was not finite
+        self.one = torch.ones((), device=dev)                          # the loss gradient (no fill per step)
+        set_nonfinite_counter(self.bad)     # the CTC mean's own launch counts non-finite losses (cfm_ctc_mean)
         self.steps_run = 0
         # SpecAugment (configs[2]): the global batch's draws on the host in the reference's order
         # (specaugment.draw, python random seeded as speechcommands.py:18), this rank's slice packed into
@@ -547,8 +549,7 @@ class Harness:
         self.rng.add_(1)
         loss, _ = self.model(self.x, self.lens_i32, self.tgt_i32, self.tlen_i32, seed=self.seed0,
                              specaug_params=self.sa_params)
-        loss.backward()
-        self.bad.add_((~torch.isfinite(loss.detach())).to(torch.int32))
+        loss.backward(self.one)
         return loss
 
     def post(self):
@@ -644,6 +645,7 @@ class Harness:
         """Unbind the device dropout counter (libcfm keeps its address; it dies with this harness)."""
         torch.cuda.synchronize()
         _lib.call("cfm_rng_bind", None)
+        set_nonfinite_counter(None)
 
     def params_finite(self):
         """All parameters finite (one pass over the weights; after the timed region)."""

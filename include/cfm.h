@@ -541,6 +541,13 @@ int cfm_ctc_loss_bwd(const float* logits, long sb, long st, const int32_t* targe
                      const float* grad_out, int grad_out_stride, int reduction, void* grad_logits,
                      int dtype_grad, long gsb, long gst, void* stream);
 
+/* reduction='mean' of the forward's nll (torch.nn.CTCLoss: mean over b of nll[b] / max(tgt_len[b], 1)) as
+ * ONE launch: *loss (fp32 scalar).  nonfinite (nullable): incremented by 1 when the mean is not finite (a
+ * device step counter of bad steps, read once after a run).  Replaces the four element-wise passes of the
+ * reduction and the host-side finiteness check's seven. */
+int cfm_ctc_mean(const float* nll, const int32_t* tgt_len, int B, float* loss, int32_t* nonfinite,
+                 void* stream);
+
 /* Greedy decode: ASRNN.predict (asrnn.py:48-58, torch.argmax over classes: first maximum,
  * NaN wins) -> ids (B, T) int64; optionally (out, out_len != NULL) the Vocab.decode id filter
  * (myvocab.py:211-231): frames t < lens[b] (lens NULL: all T), ids equal to `blank` or `pad`

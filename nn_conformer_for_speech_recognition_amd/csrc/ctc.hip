@@ -278,6 +278,23 @@ __global__ void ctc_finish(const float* nll_raw, int B, int zero_inf, float* nll
   }
 }
 
+// reduction 'mean' (torch: mean_b(nll_b / max(L_b, 1))) in one workgroup, sums in a fixed order; a non-finite
+// result increments *bad (nullable)
+__global__ __launch_bounds__(256) void ctc_mean_kernel(const float* __restrict__ nll, const int32_t* __restrict__ tl,
+                                                       int B, float* __restrict__ loss, int32_t* __restrict__ bad) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int b = threadIdx.x; b < B; b += 256) s += nll[b] / (float)max(tl[b], 1);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = (red[0] + red[1] + red[2] + red[3]) / (float)B;
+    *loss = m;
+    if (bad && !isfinite(m)) atomicAdd(bad, 1);
+  }
+}
+
 // ---------------------------------------------------------------------------------- label classes
 // once per utterance (one workgroup): for every label position u, whether it is the first occurrence of its
 // class and the next position of the same class.  ctc_grad then sums a class's occurrences by walking that
@@ -481,6 +498,13 @@ CFM_EXPORT int cfm_ctc_loss_bwd(const float* logits, long sb, long st, const int
   else
     return cfm::fail(CFM_ERR_DTYPE, "cfm_ctc_loss_bwd: grad dtype");
   return cfm::check_launch("cfm_ctc_loss_bwd");
+}
+
+CFM_EXPORT int cfm_ctc_mean(const float* nll, const int32_t* tgt_len, int B, float* loss, int32_t* nonfinite,
+                            void* stream) {
+  CFM_REQUIRE(nll && tgt_len && loss && B > 0, CFM_ERR_ARG, "bad args");
+  hipLaunchKernelGGL(ctc_mean_kernel, dim3(1), dim3(256), 0, cfm::as_stream(stream), nll, tgt_len, B, loss, nonfinite);
+  return cfm::check_launch("cfm_ctc_mean");
 }
 
 CFM_EXPORT int cfm_ctc_greedy_decode(const float* logits, long sb, long st, const int32_t* lens, int B, int T, int V,

@@ -61,12 +61,25 @@ def _prep_targets(targets, tgt_len, B, device):
     raise ValueError("targets must be (B, S) padded or 1-D concatenated")
 
 
+_NONFINITE = None
+
+
+def set_nonfinite_counter(counter):
+    """Bind a (1,) int32 device counter that every reduction='mean' CTC loss increments when its value is not
+    finite (no host sync; e.g. a training loop's bad-step count, read once after the run).  None unbinds."""
+    global _NONFINITE
+    if counter is not None and (counter.dtype != torch.int32 or counter.numel() != 1 or not counter.is_cuda):
+        raise ValueError("nonfinite counter: a (1,) int32 CUDA tensor")
+    _NONFINITE = counter
+
+
 def _reduce(nll, tl, reduction):
     if reduction == "none":
         return nll
     if reduction == "sum":
         return nll.sum()
-    return (nll / tl.clamp(min=1).float()).mean()
+    # mean_b(nll_b / max(L_b, 1)) as one launch (cfm_ctc_mean; was clamp + cast + divide + mean)
+    return ops.ctc_mean(nll, tl, _NONFINITE)
 
 
 class _CTCFn(torch.autograd.Function):
@@ -134,6 +147,7 @@ class _CTCHeadFn(torch.autograd.Function):
         ctx.save_for_backward(logits, yc, wc, tg, off if off is not None else tg, il, tl, ws)
         ctx.cfg = (ldt, off is not None, smax, blank, zero_infinity, reduction, cd, y.dtype, b is not None)
         ctx.mark_non_differentiable(logits)
+        ctx.set_materialize_grads(False)     # no (B, T, V) zero gradient for the logits output
         return _reduce(nll, tl, reduction), logits
 
     @staticmethod

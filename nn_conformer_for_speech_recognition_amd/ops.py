@@ -910,6 +910,14 @@ def ctc_loss_fwd(x, targets_i32, ldt, tgt_off, in_len_i32, tgt_len_i32, smax, bl
     return nll, ws
 
 
+def ctc_mean(nll, tgt_len_i32, nonfinite=None):
+    """torch.nn.CTCLoss reduction='mean' of nll (B,) as one launch -> 0-d fp32; nonfinite: optional (1,) int32
+    device counter incremented when the result is not finite."""
+    out = torch.empty((), device=nll.device, dtype=torch.float32)
+    L.call("cfm_ctc_mean", L.ptr(nll), L.ptr(tgt_len_i32), nll.numel(), L.ptr(out), L.ptr(nonfinite), L.stream())
+    return out
+
+
 def ctc_loss_bwd(x, targets_i32, ldt, tgt_off, in_len_i32, tgt_len_i32, smax, blank, zero_infinity, batch_first, ws,
                  grad_out, reduction, grad_dtype=torch.float32):
     """d loss / d logits (softmax - posterior, scaled) in x's layout, dtype grad_dtype."""
