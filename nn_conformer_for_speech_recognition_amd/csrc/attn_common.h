@@ -37,6 +37,13 @@ __device__ __forceinline__ void dropout_pair(uint32_t thr, float keep, uint32_t 
   m1 = (h >> 16) >= thr ? keep : 0.f;
 }
 
+// v_max3_f32 (IEEE maxNum of three, as two fmaxf)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // 2^x for softmax arguments <= 0: the bare v_exp_f32 (results below 2^-126 flush to 0)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -181,9 +188,15 @@ __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16&
       s1[r] = (k0 + 32 < len) ? s1[r] : -INFINITY;
     }
   }
-  float mloc = fmaxf(s0[0], s1[0]);
+  // the tile maximum as two chains of v_max3_f32 (fmaxf chains compile to v_max_f32 with a canonicalising
+  // v_max per MFMA output in IEEE mode: ~57 instructions per tile, here 17; max is exact either way)
+  float ma = max3f(s0[0], s0[1], s0[2]), mb = max3f(s1[0], s1[1], s1[2]);
 #pragma unroll
-  for (int r = 1; r < 16; ++r) mloc = fmaxf(mloc, fmaxf(s0[r], s1[r]));
+  for (int r = 3; r < 15; r += 2) {
+    ma = max3f(ma, s0[r], s0[r + 1]);
+    mb = max3f(mb, s1[r], s1[r + 1]);
+  }
+  float mloc = max3f(ma, mb, fmaxf(s0[15], s1[15]));
   mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
   const float mn = fmaxf(m, mloc * c);
   const float alpha = fast_exp2(m - mn);
