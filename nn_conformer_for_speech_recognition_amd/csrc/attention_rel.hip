@@ -464,9 +464,10 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
       for (int s = 0; s < 4; ++s)
         dd = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag(sV, 32 * t, 16 * s, lane), gf[s], dd, 0, 0, 0);
       if (p.drop_p > 0.f) {
+        const uint32_t hb = rowj + dkey + 2u * (uint32_t)hh;   // + a compile-time constant per pair (one add)
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const uint32_t hs = attn_mix(rowj + ((acc_row(r, hh) + 32 * t) >> 1) + dkey);
+          const uint32_t hs = attn_mix(hb + (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2) + 16 * t));
           dd[r] = (hs & 0xFFFFu) >= dthr ? dd[r] : 0.f;
           dd[r + 1] = (hs >> 16) >= dthr ? dd[r + 1] : 0.f;
         }

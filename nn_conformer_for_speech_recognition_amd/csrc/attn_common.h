@@ -229,11 +229,15 @@ __device__ __forceinline__ void softmax_tile(const AttnM& p, f32x16& s0, f32x16&
   }
   if (p.drop_p > 0.f) {
     const uint32_t rowj = (uint32_t)(didx(p, b, h, qi, kbase) >> 1);   // even: 32-bit pair indices
+    // pair index + key = hb + a compile-time constant per register pair (k0 / 2 = ((r & 3) >> 1) + 4 (r >> 2) + 2 hh):
+    // one add per hash instead of two (the same 32-bit sums)
+    const uint32_t hb = rowj + dkey + 2u * (uint32_t)hh;
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {     // registers r, r+1 = keys k, k+1 with k even: one hash
       const int k0 = acc_row(r, hh);
       if constexpr (LATE) {
-        const uint32_t h0 = attn_mix(rowj + (k0 >> 1) + dkey), h1 = attn_mix(rowj + (k0 >> 1) + 16 + dkey);
+        const uint32_t cr = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2));
+        const uint32_t h0 = attn_mix(hb + cr), h1 = attn_mix(hb + cr + 16u);
         s0[r] = (h0 & 0xFFFFu) >= dthr ? s0[r] : 0.f;
         s0[r + 1] = (h0 >> 16) >= dthr ? s0[r + 1] : 0.f;
         s1[r] = (h1 & 0xFFFFu) >= dthr ? s1[r] : 0.f;
