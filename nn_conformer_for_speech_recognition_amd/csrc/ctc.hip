@@ -40,9 +40,9 @@ __device__ __forceinline__ float lse2(float a, float b) {
 __device__ __forceinline__ float lse3r(float a, float b, float c) {
   constexpr float L2E = 1.4426950408889634f, LN2F = 0.6931471805599453f;
   const float m = fmaxf(fmaxf(a, b), c), md = __builtin_amdgcn_fmed3f(a, b, c), lo = fminf(fminf(a, b), c);
-  if (m == NEG_INF) return NEG_INF;
   const float s = 1.f + (__builtin_amdgcn_exp2f((md - m) * L2E) + __builtin_amdgcn_exp2f((lo - m) * L2E));
-  return m + __builtin_amdgcn_logf(s) * LN2F;
+  const float r = m + __builtin_amdgcn_logf(s) * LN2F;
+  return m == NEG_INF ? NEG_INF : r;   // a select, not a branch (all -inf: the NaN of -inf - -inf is discarded)
 }
 __device__ __forceinline__ float lse3(float a, float b, float c) {
   constexpr float L2E = 1.4426950408889634f, LN2F = 0.6931471805599453f;
@@ -219,10 +219,8 @@ __device__ __forceinline__ void ctc_alphabeta_dir(const CtcP& p, float* edge_mem
       float v = lse3r(prev, n1, a2) + cur[q];
       if (q == 0 && i0 == 0) v = DIR == 0 ? (s <= 1 ? cur[q] : NEG_INF) : (s >= Sb - 2 ? cur[q] : NEG_INF);
       if (!valid) v = NEG_INF;
-      if (live) {
-        if (valid) out[(long)frame(i) * p.S + s] = v;
-        prev = v;
-      }
+      if (live && valid) out[(long)frame(i) * p.S + s] = v;
+      prev = live ? v : prev;
       ev[q] = v;   // the edge lanes' values of the block, stored once per block below
     }
     if (has_succ) {   // lanes le0 / le1: the block's PF values as four 16-B stores each
