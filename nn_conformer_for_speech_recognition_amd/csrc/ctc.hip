@@ -202,17 +202,16 @@ __device__ __forceinline__ void ctc_alphabeta_dir(const CtcP& p, float* edge_mem
       const bool live = i < nsteps;
       // previous frame's neighbours: alpha lane l <- lane l - 1 (wave_shr), beta lane l <- lane l + 1 (wave_shl);
       // the edge lanes get -inf, then the predecessor's pair
+      // (the shifts write 0 into the edge lanes, which the predecessor's pair then replaces -- -inf for the first
+      // wave, whose ex / ey stay -inf: no old-value moves and no branch on has_pred)
       constexpr int SH = DIR == 0 ? 0x138 : 0x130;
-      const int ninf = __float_as_int(NEG_INF);
-      float n1 = __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(prev), SH, 0xF, 0xF, false));
-      float n2 = __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(n1), SH, 0xF, 0xF, false));
-      if (has_pred) {
-        const float e0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ex), q));
-        const float e1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ey), q));
-        const int l0 = DIR == 0 ? 0 : 63, l1 = DIR == 0 ? 1 : 62;
-        if (lane == l0) { n1 = e0; n2 = e1; }
-        if (lane == l1) n2 = e0;
-      }
+      constexpr int l0 = DIR == 0 ? 0 : 63, l1 = DIR == 0 ? 1 : 62;
+      float n1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(prev), SH, 0xF, 0xF, true));
+      float n2 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(n1), SH, 0xF, 0xF, true));
+      const float e0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ex), q));
+      const float e1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ey), q));
+      n1 = lane == l0 ? e0 : n1;
+      n2 = lane == l0 ? e1 : (lane == l1 ? e0 : n2);
       // alpha: s - 1 < 0 only for lane 0 of wave 0, whose n1 is the DPP's -inf; beta: s + 1 >= Sb reads an invalid
       // lane (kept at -inf) or the DPP's -inf
       const float a2 = skip ? n2 : NEG_INF;
