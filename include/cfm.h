@@ -417,6 +417,14 @@ int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* dout, const 
                         const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                         void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H,
                         int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream);
+/* cfm_attn_bwd (d_ready 0) / cfm_attn_bwd_with_d (d_ready 1) with the projected-table gradient dpos written in
+   dtype_dpos: CFM_F32, or CFM_BF16 on the rel-pos MFMA path (each fp32 column sum rounded as cfm_cast rounds
+   it -- the compute-dtype copy the dW_pos GEMM reads, without an fp32 dpos and a cast pass). */
+int cfm_attn_bwd_ex(const void* qkv, const void* o, const void* dout, const float* lse,
+                    const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
+                    void* dqkv, void* dpos, int dtype_dpos, float* dpos_u, float* dpos_v, int B, int T,
+                    int H, int dk, int dtype, float drop_p, uint64_t seed, int d_ready, float* ws,
+                    void* stream);
 
 /* ---------------------------------------------------------------- ConvSubSampling
  * lib/convsubsampling.py:16-45: Conv2d(1->C1, 7x7, s2) -> Conv2d(C1->C2, 3x3, s2), no padding.

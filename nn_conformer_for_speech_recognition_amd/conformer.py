@@ -322,8 +322,10 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
     else:
         Dh = None
         do = ops.linear_dgrad(g4, wout, wt=wt)
+    # rel-pos in bf16: dpos comes back in the compute dtype (the dW_pos GEMM operand; no fp32 copy + cast)
+    dpos_dt = torch.bfloat16 if (cfg.rel and cd == torch.bfloat16) else torch.float32
     dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed,
-                                        D=Dh, ws=aws)
+                                        D=Dh, ws=aws, dpos_dtype=dpos_dt)
     if cfg.rel:
         dpc, pec = _w(dpos, cd), _w(cfg.pe, cd)
         if REL_BATCH and side.group is not None and ops.wgrad_group_ok(dpc, pec):

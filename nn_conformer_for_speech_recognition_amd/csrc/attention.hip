@@ -27,8 +27,8 @@ extern int g_rel_mode;   // attention_rel.hip: cfm_attn_set_mode's bits for the 
 int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len, const void* pos, const float* pu,
                         const float* pv, int B, int T, int H, int dk, float drop_p, uint64_t seed, hipStream_t s);
 int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, const int32_t* len, const void* pos,
-                        const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
-                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s);
+                        const float* pu, const float* pv, void* dqkv, void* dpos, int dpos_dt, float* dpu, float* dpv,
+                        int B, int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s);
 int attn_simt_bwd_launch(const void*, const void*, const void*, const float*, const int32_t*, const void*,
                          const float*, const float*, void*, float*, float*, float*, int, int, int, int, int, float,
                          uint64_t, float*, hipStream_t);
@@ -816,16 +816,18 @@ CFM_EXPORT size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel, in
 
 static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const float* lse,
                          const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
-                         void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
-                         int dtype, float drop_p, uint64_t seed, float* ws, void* stream, bool d_ready) {
+                         void* dqkv, void* dpos, int dpos_dt, float* dpos_u, float* dpos_v, int B, int T, int H,
+                         int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream, bool d_ready) {
   CFM_REQUIRE(qkv && o && dout && lse && lengths && dqkv && ws, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0, CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(!pos || (pos_u && pos_v && dpos && dpos_u && dpos_v), CFM_ERR_ARG, "rel-pos grads need buffers");
   hipStream_t s = cfm::as_stream(stream);
   CFM_REQUIRE(!d_ready || use_mfma(dtype, pos, dk), CFM_ERR_UNSUPPORTED, "precomputed D: bf16 MFMA path only");
+  CFM_REQUIRE(dpos_dt == CFM_F32 || (dpos_dt == CFM_BF16 && pos && use_mfma(dtype, pos, dk)), CFM_ERR_DTYPE,
+              "dpos: fp32, or bf16 on the rel-pos MFMA path");
   if (!use_mfma(dtype, pos, dk))
-    return cfm::attn_simt_bwd_launch(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B,
-                                     T, H, dk, dtype, drop_p, seed, ws, s);
+    return cfm::attn_simt_bwd_launch(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, (float*)dpos, dpos_u,
+                                     dpos_v, B, T, H, dk, dtype, drop_p, seed, ws, s);
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0),
           g_attn_mode & 6, cfm::g_rng_salt};
@@ -836,8 +838,8 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
     hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s,
                        (const bf16*)dout, (const bf16*)o, ws, B, T, H, dk);
   if (pos)
-    return cfm::attn_rel_bwd_launch(qkv, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H,
-                                    dk, drop_p, seed, ws, s);
+    return cfm::attn_rel_bwd_launch(qkv, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_dt, dpos_u, dpos_v, B,
+                                    T, H, dk, drop_p, seed, ws, s);
   if (use_head(T))
     hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), dkdv_wave_lds_bytes(T), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);
@@ -857,16 +859,25 @@ CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, co
                             const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                             void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
                             int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
-  return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H, dk, dtype,
-                       drop_p, seed, ws, stream, false);
+  return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, CFM_F32, dpos_u, dpos_v, B, T, H, dk,
+                       dtype, drop_p, seed, ws, stream, false);
 }
 
 CFM_EXPORT int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* dout, const float* lse,
                                    const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                                    void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
                                    int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
-  return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_u, dpos_v, B, T, H, dk, dtype,
-                       drop_p, seed, ws, stream, true);
+  return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, CFM_F32, dpos_u, dpos_v, B, T, H, dk,
+                       dtype, drop_p, seed, ws, stream, true);
+}
+
+CFM_EXPORT int cfm_attn_bwd_ex(const void* qkv, const void* o, const void* dout, const float* lse,
+                               const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
+                               void* dqkv, void* dpos, int dtype_dpos, float* dpos_u, float* dpos_v, int B, int T,
+                               int H, int dk, int dtype, float drop_p, uint64_t seed, int d_ready, float* ws,
+                               void* stream) {
+  return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dtype_dpos, dpos_u, dpos_v, B, T, H,
+                       dk, dtype, drop_p, seed, ws, stream, d_ready != 0);
 }
 
 CFM_EXPORT int cfm_attn_set_mode(int mode) {

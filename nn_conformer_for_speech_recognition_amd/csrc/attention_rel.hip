@@ -1141,8 +1141,8 @@ int attn_rel_fwd_launch(const void* qkv, void* o, float* lse, const int32_t* len
 
 // D (rowsum dO*O per head) must already be in ws[0 .. B*H*T)
 int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, const int32_t* len, const void* pos,
-                        const float* pu, const float* pv, void* dqkv, float* dpos, float* dpu, float* dpv, int B,
-                        int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s) {
+                        const float* pu, const float* pv, void* dqkv, void* dpos, int dpos_dt, float* dpu, float* dpv,
+                        int B, int T, int H, int dk, float drop_p, uint64_t seed, float* ws, hipStream_t s) {
   AttnM p = make_attnm(qkv, dout, len, B, T, H, dk, drop_p, seed);
   const RelP rp = make_relp(pos, pu, pv, p.dk);
   const size_t d_bytes = ((size_t)p.B * p.H * p.T * sizeof(float) + 255) & ~(size_t)255;
@@ -1174,7 +1174,10 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
   else
     hipLaunchKernelGGL(attn_rel_bwd_dpos_kernel<false>, dim3(cdiv(2 * p.T - 1, TILE), p.H, p.B), dim3(256), 0, s, p,
                        rp, (const bf16*)dsbuf, ldS, dpos_part);
-  colreduce(dpos_part, p.B, (long)(2 * p.T - 1) * p.HD, dpos, 0, s);
+  if (dpos_dt == CFM_BF16)   // the compute-dtype copy the dW_pos GEMM reads: no fp32 dpos + cast pass
+    colreduce_bf16(dpos_part, p.B, (long)(2 * p.T - 1) * p.HD, (bf16*)dpos, s);
+  else
+    colreduce(dpos_part, p.B, (long)(2 * p.T - 1) * p.HD, (float*)dpos, 0, s);
   const int nrows = p.B * 4 * cdiv(p.T, 128);
   colreduce_pair(part, part + p.HD, nrows, (long)p.HD, dpu, dpv, s, 2L * p.HD);   // du, dv: one launch
   return check_launch("cfm_attn_bwd(rel)");

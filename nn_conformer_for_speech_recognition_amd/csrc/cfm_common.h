@@ -27,6 +27,8 @@ int fail(int code, const std::string& msg);
 int check_launch(const char* what);
 // out[n] (+)= sum_p part[p*ldp + n]  (deterministic, block = 16 waves x 64 columns; ldp 0 -> N)
 void colreduce(const float* part, int nparts, long N, float* out, int accumulate, hipStream_t s, long ldp = 0);
+// the same sums written as bf16 (rounded as cfm_cast; may use part's first row as scratch)
+void colreduce_bf16(float* part, int nparts, long N, bf16* out, hipStream_t s, long ldp = 0);
 // out{A,B}[n] = sum_p part{A,B}[p * ldp + n]: two reductions, one launch (bit-identical to two colreduce calls;
 // ldp 0 -> N)
 void colreduce_pair(const float* partA, const float* partB, int nparts, long N, float* outA, float* outB,

@@ -347,9 +347,37 @@ __global__ __launch_bounds__(256) void colreduce_few_kernel(const float* __restr
     *o = t;
   }
 }
+// the same writing bf16 (each column's fp32 sum rounded as cfm_cast rounds it; out 8-B aligned)
+__global__ __launch_bounds__(256) void colreduce_few_bf16_kernel(const float* __restrict__ part, int nparts, long N,
+                                                                 long ldp, bf16* __restrict__ out) {
+  const long n4 = N / 4;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = 0; p < nparts; ++p) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (long)p * ldp + 4 * i);
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    bf16x4 o = {from_f32<bf16>(t.x), from_f32<bf16>(t.y), from_f32<bf16>(t.z), from_f32<bf16>(t.w)};
+    *reinterpret_cast<bf16x4*>(out + 4 * i) = o;
+  }
+}
 }  // namespace
 
 namespace cfm {
+// out (bf16) = sum_p part[p * ldp + n]: the few-rows kernel when it applies, else the fp32 reduction into part's
+// row 0 (in place: every column's parts are read before its sum is written) and a cast
+void colreduce_bf16(float* part, int nparts, long N, bf16* out, hipStream_t s, long ldp) {
+  const long lp = ldp > 0 ? ldp : N;
+  if (nparts <= 16 && N % 4 == 0 && lp % 4 == 0 && (uintptr_t)part % 16 == 0 && (uintptr_t)out % 8 == 0 &&
+      N >= 65536) {
+    const long blocks = (N / 4 + 255) / 256;
+    hipLaunchKernelGGL(colreduce_few_bf16_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, s,
+                       part, nparts, N, lp, out);
+    return;
+  }
+  colreduce(part, nparts, N, part, 0, s, lp);
+  cfm_cast(part, CFM_F32, out, CFM_BF16, N, s);
+}
 void colreduce_pair(const float* partA, const float* partB, int nparts, long N, float* outA, float* outB,
                     hipStream_t s, long ldp) {
   hipLaunchKernelGGL(colreduce2_kernel, dim3((unsigned)((N + 63) / 64), 2), dim3(1024), 0, s, partA, partB, nparts, N,

@@ -229,3 +229,19 @@ def test_dropout_masks_read_back(attn_mode, mode, T, seed):
     val = o.float().view(B, T, H, dk)[..., :T][torch.from_numpy(ref).permute(0, 2, 1, 3).to(DEV)]
     assert torch.allclose(val, torch.full_like(val, 1.0 / ((1 - p) * T)), rtol=1e-2)
     assert 0.85 < ref.mean() < 0.95
+
+
+def test_rel_dpos_bf16_output_is_the_cast():
+    """cfm_attn_bwd_ex with dtype_dpos bf16: dpos written in the compute dtype by the column reduction equals the
+    fp32 dpos cast to bf16 (the same fp32 sums, rounded as cfm_cast), at the L60 width and at a width below the
+    few-rows kernel's range (the reduce-in-place + cast fallback); every other output unchanged."""
+    for (B, T, H, lens) in [(2, 1498, 2, [1498, 1001]), (2, 97, 4, [97, 60])]:
+        qkv, pos, pu, pv, do, ln = _rel_case(B, T, H, 64, lens, 13)
+        o, lse = ops.attn_fwd(qkv, ln, B, T, H, 64, pos, pu, pv, drop_p=0.1, seed=3)
+        ref = ops.attn_bwd(qkv, o, do, lse, ln, B, T, H, 64, pos, pu, pv, drop_p=0.1, seed=3)
+        got = ops.attn_bwd(qkv, o, do, lse, ln, B, T, H, 64, pos, pu, pv, drop_p=0.1, seed=3, dpos_dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+        assert got[1].dtype == torch.bfloat16
+        assert torch.equal(got[1], ops.cast(ref[1], torch.bfloat16))
+        for a, b in zip((got[0], got[2], got[3]), (ref[0], ref[2], ref[3])):
+            assert torch.equal(a, b)
