@@ -15,6 +15,7 @@ ap.add_argument("--none", action="store_true", help="no relative positions (tile
 ap.add_argument("--l15", action="store_true", help="the L15 shape (B 32, T 373: whole-head kernels when --none)")
 ap.add_argument("--p", type=float, default=0.1, help="attention dropout")
 ap.add_argument("--mode", type=int, default=0, help="cfm_attn_set_mode value (A/B)")
+ap.add_argument("--dpos-f32", action="store_true", help="fp32 dpos (the step writes bf16 dpos for bf16 rel-pos)")
 a = ap.parse_args()
 if a.mode:
     from nn_conformer_for_speech_recognition_amd import _lib  # noqa: E402
@@ -33,7 +34,8 @@ for i in range(a.n + 1):
         torch.cuda.synchronize()
         s.record()
     o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, pos, pu, pv, drop_p=a.p, seed=3)
-    ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, pos, pu, pv, drop_p=a.p, seed=3)
+    ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, pos, pu, pv, drop_p=a.p, seed=3,
+                 dpos_dtype=torch.float32 if (a.dpos_f32 or a.none) else torch.bfloat16)
 e.record()
 torch.cuda.synchronize()
 print(f"fwd+bwd {s.elapsed_time(e) / max(a.n, 1) * 1e3:.1f} us per call")
