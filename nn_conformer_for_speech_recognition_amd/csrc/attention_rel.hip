@@ -931,7 +931,11 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos_kernel(AttnM p, RelP rp
 //  * 128 r per workgroup halves the (q+v) tile traffic per output; 4 waves = (d half, r half of 64), 8 MFMAs per
 //    wave per 64-row i-tile.
 constexpr int DP_R = 128;              // relative rows per workgroup
-constexpr int DP_KS = DP_R + 72;       // sB row stride (elements): 400 B = 100 dwords == 36 mod 64, as KS's 144 B
+// sB row stride (elements): 320 B = 80 dwords.  With the chunk-to-lane deal below (each 32-lane half of a store:
+// rows r, r+2, r+4, r+6 x 8 consecutive chunks) every ds_write_b16 of the band image and every transposed
+// fragment read is bank-conflict free (the 400-B stride with the row-major deal: ~740 extra LDS cycles per tile,
+// 20.6 M in profiles/r05/rel_l60_pmc_final.txt -- the stores, whose lanes met on banks 4 and more ways)
+constexpr int DP_KS = 160;
 constexpr int DP_PADL = 8;             // band image column of r' = 0 (r' = -7 .. 135 are written, 0 .. 127 read)
 constexpr int DP_CH = DP_R / 8 + 1;    // aligned 8-element dS chunks per row (17)
 
@@ -956,7 +960,8 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP r
                                                                  int ldS, float* __restrict__ part, int nrt) {
   __shared__ __attribute__((aligned(16))) bf16 sA[2][TILE * KS];     // (q+v)[ii][d]
   __shared__ __attribute__((aligned(16))) bf16 sB[2][TILE * DP_KS];  // dS_band[ii][rr]
-  float* const sO = reinterpret_cast<float*>(&sB[0][0]);            // [DP_R][65] after the loop (33 KiB <= 50 KiB)
+  float* const sO = reinterpret_cast<float*>(&sB[0][0]);            // [DP_R][65] after the loop (33 KiB <= 40 KiB)
+  static_assert(DP_R * 65 * 4 <= 2 * TILE * DP_KS * 2, "the output stage fits in sB");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nbh = p.B * p.H;
   const int xcd = blockIdx.x & 7, kx = blockIdx.x >> 3;
@@ -977,16 +982,22 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP r
   float pv8[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) pv8[e] = rp.pv[h * p.dk + c8 + e];
-  // this thread's band chunks: q = tid + 256 k of the tile's 64 x 17; row, chunk column, the row's skew
-  // s = (row + r0 - (T-1)) & 7 (row i's run starts s elements into its first aligned chunk; I0 is a multiple of 64)
-  // and the chunk's element offset in the slab for tile I0: I0 * (ldS + 1) + base
+  // this thread's band chunks of the tile's 64 x 17: k < 4 -- 32-lane group G = 8k + 2 wv + (lane >> 5) takes rows
+  // 8m + par + {0, 2, 4, 6} (G >> 1 = 2m + par) x chunks 8 (G & 1) .. +7 (conflict-free stores, see DP_KS; a wave
+  // loads 4 rows x 16 whole chunks); k = 4 -- chunk 16 of row `lane` (wave 0; the other waves re-load their first
+  // chunk, not stored).  Per chunk: row, chunk column, the row's skew s = (row + r0 - (T-1)) & 7 (row i's run starts
+  // s elements into its first aligned chunk; I0 is a multiple of 64) and its element offset in the slab for tile
+  // I0: I0 * (ldS + 1) + base
   int crow[5], ccol[5], csk[5], cbase[5];
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    int q = tid + 256 * k;
-    if (q >= TILE * DP_CH) q = tid;    // (k = 4, tid >= 64: re-loads its first chunk, not stored)
-    crow[k] = q / DP_CH;
-    ccol[k] = q % DP_CH;
+    const int G = 8 * (k < 4 ? k : 0) + 2 * wv + (lane >> 5), rs = G >> 1;
+    crow[k] = 8 * (rs >> 1) + (rs & 1) + 2 * ((lane & 31) >> 3);
+    ccol[k] = 8 * (G & 1) + (lane & 7);
+    if (k == 4 && wv == 0) {
+      crow[k] = lane;
+      ccol[k] = 16;
+    }
     const int j0 = crow[k] + R0 - (T - 1);
     csk[k] = j0 & 7;
     cbase[k] = crow[k] * ldS + (j0 - csk[k]) + 8 * ccol[k];
