@@ -1,7 +1,9 @@
 """Throughput benchmark: mel-frames/s of the Conformer-L encoder training step on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config L15]
-    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+    (N > 1: either under python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N, or plain
+    `python bench.py --gpus N`, which starts that launcher itself as a child process; --gpus must equal the
+    launcher's WORLD_SIZE, else the run exits 2)
 
 One step = one utterance batch through the hot path, forward + backward:
 ConvSubSampling -> frame projection -> 17 Conformer-L layers -> fused CTC head (Linear d->V +
@@ -173,6 +175,8 @@ def run_nst(args, model, x, lens_i32, dev, cfg, rank, world):
                       "seq_len": T_in, "enc_frames": model.T2, "parallelism": f"dp{world} (sharded utterances)",
                       "launch": "hip-graph (fwd + decode)"},
            "per_gpu_value": round(value / world, 1),
+           "dist_backend": torch.distributed.get_backend() if torch.distributed.is_initialized() else None,
+           "world_size_reported": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
            "step_algorithmic_tflops": round(fwd_pf * B * T_in / (ms * 1e-3) / 1e12, 1),
            "labels_nonempty": int((out[2] > 0).sum().item())}
     if rank == 0:
@@ -655,9 +659,56 @@ class Harness:
         return bool(ok.item())
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` run WITHOUT a torchrun environment: start N ranks of this same command under
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) as a CHILD process and exit with its code.
+    The parent never touches the GPU (nothing before this point loads libcfm or calls HIP), so no process that
+    initialised the device is replaced.  stdout lines that are JSON objects (rank 0's one result line) pass through
+    to stdout; everything else the launcher prints goes to stderr."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    print("bench: launching", n, "ranks:", " ".join(cmd), file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in proc.stdout:
+        s = line.strip()
+        is_json = s.startswith("{") and s.endswith("}")
+        print(s if is_json else line.rstrip("\n"), file=sys.stdout if is_json else sys.stderr, flush=True)
+    return proc.wait()
+
+
+def check_launch(args, rank, world):
+    """--check-launch: the process-group plumbing alone (no model, no kernels): every rank contributes 1 to one
+    all-reduce; rank 0 prints the world the launcher built and the count the collective saw."""
+    import torch.distributed as tdist
+    backend = tdist.get_backend() if tdist.is_initialized() else None
+    seen = 1
+    if world > 1:
+        dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        t = torch.ones(1, device=dev)
+        tdist.all_reduce(t)
+        seen = int(t.item())
+    if rank == 0:
+        print(json.dumps({"check": "launch", "n_gpus": world, "gpus_requested": args.gpus, "dist_backend": backend,
+                          "world_size_reported": tdist.get_world_size() if tdist.is_initialized() else 1,
+                          "ranks_in_allreduce": seen}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); N > 1 without a torchrun env spawns torch.distributed.run itself")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="only build the process group and run one all-reduce (launcher test; no GPU work)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="L15", choices=sorted(CONFIGS))
@@ -694,6 +745,17 @@ def main():
     ap.add_argument("--poison", action="store_true",
                     help="debug: NaN-fill every torch.empty (deterministic algorithms + fill_uninitialized_memory)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks", file=sys.stderr)
+        sys.exit(2)
+    if args.check_launch:
+        rank, world, _ = cdist.init_from_env()
+        return check_launch(args, rank, world)
     if args.poison:
         torch.use_deterministic_algorithms(True, warn_only=True)
         torch.utils.deterministic.fill_uninitialized_memory = True
@@ -885,6 +947,8 @@ def main():
                    "grad_reduce_dtype": "bf16" if h.reducer.grad_dtype == torch.bfloat16 else "fp32",
                    **({"dp_chunk_layers": args.dp_chunk_layers} if h.seg is not None else {})},
         "per_gpu_value": round(value / world, 1),
+        "dist_backend": torch.distributed.get_backend() if torch.distributed.is_initialized() else None,
+        "world_size_reported": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
         # FLOPs the step executes (encoder + the folded front-end GEMMs; CTC head excluded), and the reference
         # composition's count (conv1 + conv2 + projection as the reference computes them) beside it
         "step_executed_tflops": round(step_tflops, 1),
