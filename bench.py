@@ -525,6 +525,8 @@ class Harness:
         self.bad = torch.zeros(1, dtype=torch.int32, device=dev)     # steps whose loss was not finite
         self.one = torch.ones((), device=dev)                          # the loss gradient (no fill per step)
         set_nonfinite_counter(self.bad)     # the CTC mean's own launch counts non-finite losses (cfm_ctc_mean)
+        self.ctc_aborts = torch.zeros(1, dtype=torch.int32, device=dev)   # recursion waits given up (cfm.h)
+        _lib.call("cfm_ctc_bind_abort_counter", _lib.ptr(self.ctc_aborts))
         self.steps_run = 0
         # SpecAugment (configs[2]): the global batch's draws on the host in the reference's order
         # (specaugment.draw, python random seeded as speechcommands.py:18), this rank's slice packed into
@@ -649,6 +651,7 @@ class Harness:
         """Unbind the device dropout counter (libcfm keeps its address; it dies with this harness)."""
         torch.cuda.synchronize()
         _lib.call("cfm_rng_bind", None)
+        _lib.call("cfm_ctc_bind_abort_counter", None)
         set_nonfinite_counter(None)
 
     def params_finite(self):
@@ -963,6 +966,7 @@ def main():
                                "replayed 20x after the timed region (HIP events); it runs inside the timed step"},
         "loss": loss_val,
         "steps_checked": h.steps_run, "nonfinite_steps": nonfinite, "nonfinite_before_timing": bad_before,
+        "ctc_recursion_aborts": int(h.ctc_aborts.item()),
         "params_finite": params_ok, "valid": valid,
         # the dominant kernel family: d-wide-output GEMMs (mean FLOP / mean launch; bytes per launch from its
         # descriptor (gemm_desc_bytes): A + B read, C written in its dtype -- bf16 data gradients, fp32

@@ -556,6 +556,15 @@ int cfm_ctc_loss_bwd(const float* logits, long sb, long st, const int32_t* targe
 int cfm_ctc_mean(const float* nll, const int32_t* tgt_len, int B, float* loss, int32_t* nonfinite,
                  void* stream);
 
+/* Alpha / beta recursion health (no reference counterpart: the device recursion's own guard).  Each of the
+ * recursion's inter-wave waits is bounded; a wait that gives up marks its direction aborted and the forward then
+ * makes that utterance's nll NaN (so the loss and the logits gradient are NaN, never silently wrong).
+ * cfm_ctc_bind_abort_counter(counter): int32 device counter (NULL unbinds) incremented once per aborted
+ * utterance by every later cfm_ctc_loss_fwd -- told apart from genuine non-finite losses.
+ * cfm_ctc_set_debug(mask): test hook, forces the abort path of the alpha (bit 0) / beta (bit 1) recursion. */
+int cfm_ctc_bind_abort_counter(int32_t* counter);
+int cfm_ctc_set_debug(int force_abort_mask);
+
 /* Greedy decode: ASRNN.predict (asrnn.py:48-58, torch.argmax over classes: first maximum,
  * NaN wins) -> ids (B, T) int64; optionally (out, out_len != NULL) the Vocab.decode id filter
  * (myvocab.py:211-231): frames t < lens[b] (lens NULL: all T), ids equal to `blank` or `pad`

@@ -177,6 +177,8 @@ _SIGS = {
                                         c_void_p, c_void_p]),
     "cfm_ctc_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
     "cfm_ctc_mean": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "cfm_ctc_bind_abort_counter": (c_int, [c_void_p]),
+    "cfm_ctc_set_debug": (c_int, [c_int]),
     "cfm_ctc_loss_fwd": (c_int, [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                  c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "cfm_ctc_loss_bwd": (c_int, [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,

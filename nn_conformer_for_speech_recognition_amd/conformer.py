@@ -573,8 +573,9 @@ class Conformer(nn.Module):
             raise ValueError("fp8=True needs compute_dtype=torch.bfloat16 (the backward runs in bf16)")
         # fp8 (e4m3fn) forward GEMMs (FFN up/down, QKV, out-projection; K % 128 == 0): BASELINE configs[4]
         self.fp8 = bool(fp8)
-        self._pe_cache = {}
-        self._rel_cache = {}
+        self._pe_cache = {}       # (device, dtype) -> (longest T, its (2T-1, d) table): _pe slices it
+        self._pe_retired = []     # superseded tables (a captured graph may still read one)
+        self._rel_cache = None    # (device, dtype, weight storage) -> linear_pos weight stack + its cast batch
         self._step = 0
         self._shadow = None
         self._q8 = None         # (key, ops.Quant8Batch) of the fp8 forward weights
@@ -586,35 +587,50 @@ class Conformer(nn.Module):
         self.on_routed = None
         self.sync_bn = None     # (reduce_sums(t) in-place all-reduce, world) -> cross-replica BatchNorm
 
-    def _pe(self, T, device):
-        key = (T, str(device))
-        if key not in self._pe_cache:
-            self._pe_cache[key] = rel_pos_table(T, self.input_dim, device)
-        return self._pe_cache[key]
+    def _pe(self, T, device, dtype=torch.float32):
+        """The (2T-1, d) positional table of length T in `dtype`, as the middle rows of ONE table built for the
+        longest length seen: row r of the Tcap table is relative position (Tcap-1)-r and its values depend on the
+        position alone, so rows Tcap-T .. Tcap+T-2 ARE the length-T table, bit for bit.  Variable-length batches
+        therefore share one table per (device, dtype) instead of one per distinct T.  It grows geometrically; a
+        superseded table is kept referenced (a captured graph may still read it), so the memory stays below about
+        twice the longest table."""
+        key = (str(device), dtype)
+        ent = self._pe_cache.get(key)
+        if ent is None or ent[0] < T:
+            tcap = max(T, 2 * ent[0]) if ent is not None else T
+            full = rel_pos_table(tcap, self.input_dim, device)
+            if dtype != torch.float32:
+                full = ops.cast(full, dtype)
+            if ent is not None:
+                self._pe_retired.append(ent[1])
+            ent = (tcap, full)
+            self._pe_cache[key] = ent
+        tcap, full = ent
+        return full[tcap - T:tcap + T - 1]
 
     def _rel_tables(self, T, device):
-        """rel-pos: the compute-dtype positional table (cached: it is constant) and every layer's projected table
-        pos_l = pe · W_pos,lᵀ from ONE batched GEMM (pe shared, batch = layers) over a per-step stacked compute-dtype
-        copy of the linear_pos weights (one cast launch) -- per layer this was a cast of pe, a cast of W_pos and a
-        48-workgroup GEMM (L60: ~24 us per layer).  -> (pe in the compute dtype, (L, 2T-1, d) tables)"""
+        """rel-pos: the compute-dtype positional table (a slice of the shared table, _pe) and every layer's
+        projected table pos_l = pe · W_pos,lᵀ from ONE batched GEMM (pe shared, batch = layers) over a per-step
+        stacked compute-dtype copy of the linear_pos weights (one cast launch) -- per layer this was a cast of pe, a
+        cast of W_pos and a 48-workgroup GEMM (L60: ~24 us per layer).  The weight stack does not depend on T (one
+        entry, keyed on the weights' storage); the projected tables are allocated per forward (the backward saves
+        them; under graph capture they come from the graph's pool), so no per-length buffers accumulate.
+        -> (pe in the compute dtype, (L, 2T-1, d) tables)"""
         cd, d, nl = self.compute_dtype, self.input_dim, len(self.conformer_layers)
         ws = [ly.self_attn.linear_pos.weight for ly in self.conformer_layers]
-        key = (T, str(device), cd)
-        ptrs = tuple(w.data_ptr() for w in ws)
-        ent = self._rel_cache.get(key)
-        if ent is None or ent[0] != ptrs:
-            pe = self._pe(T, device)
-            pe_cd = pe if pe.dtype == cd else ops.cast(pe, cd)
+        key = (str(device), cd, tuple(w.data_ptr() for w in ws))
+        if self._rel_cache is None or self._rel_cache[0] != key:
             wstack = torch.empty(nl, d, d, device=device, dtype=cd)
             cb = None if cd == torch.float32 else ops.CastBatch([w.detach() for w in ws], [wstack[i] for i in range(nl)])
-            ent = (ptrs, pe_cd, wstack, cb, torch.empty(nl, 2 * T - 1, d, device=device, dtype=cd))
-            self._rel_cache[key] = ent
-        _, pe_cd, wstack, cb, pos_all = ent
+            self._rel_cache = (key, wstack, cb)
+        _, wstack, cb = self._rel_cache
         if cb is not None:
             cb.refresh()
         else:
             for i, w in enumerate(ws):
                 wstack[i].copy_(w.detach())
+        pe_cd = self._pe(T, device, cd)
+        pos_all = torch.empty(nl, 2 * T - 1, d, device=device, dtype=cd)
         ops.gemm(pe_cd, wstack, pos_all, 2 * T - 1, d, d, batch=nl, stride_a=0, stride_b=d * d,
                  stride_c=(2 * T - 1) * d)
         return pe_cd, pos_all

@@ -145,6 +145,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnM p, bf16* __restrict
 // ceil(T/128)*B*H workgroups that each re-stream K/V tile by tile behind a barrier per tile.
 constexpr int HEAD_TMAX = 384;      // 12 waves of 32 queries; K+V images 2 * 384 * 144 B = 108 KiB
 
+// the whole-head kernels' work split: when B*H workgroups would leave CUs idle (Conformer-S / M: 4 heads, B*H = 128
+// on 256 CUs) each (b, h) runs as p.qs workgroups, each staging the whole head and sweeping its own contiguous range
+// of 32-row blocks (queries: fwd / dQ; keys: dK/dV).  -> (b, h, first block of this workgroup)
+struct HeadPart { int b, h, blk0; };
+__device__ __forceinline__ HeadPart head_part(const AttnM& p) {
+  const int qs = p.qs > 1 ? p.qs : 1;
+  const int bh = blockIdx.x / qs, part = blockIdx.x - bh * qs;
+  return {bh / p.H, bh % p.H, part * (int)(blockDim.x >> 6)};
+}
+
 
 // stage rows [0, nrows) of two head slices (dk <= 64 columns at base0 / base1, row stride ld) into
 // LDS images [nrows][KS]; rows >= T read as zero
@@ -179,7 +189,8 @@ __device__ __forceinline__ void head_stage(const AttnM& p, const bf16* base0, co
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * nthreads + tid;
       const int which = i >= nch, j = i - which * nch;
-      r[u] = i < 2 * nch ? ld8(which ? base1 : base0, which ? ld1 : ld0, j >> 3, p.T, (j & 7) * 8, p.dk, p.vec)
+      r[u] = i < 2 * nch ? ld8(which ? base1 : base0, which ? ld1 : ld0, j >> 3, p.T, (j & 7) * 8, p.dk, p.vec,
+                               p.vec4)
                          : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -201,7 +212,8 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
   const float dkeep = drop_keep_scale(dthr);
   extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const HeadPart hp = head_part(p);
+  const int b = hp.b, h = hp.h;
   const int len = p.len[b];
   const int nkt = (len + TILE - 1) / TILE, Tp = nkt * TILE;
   bf16* sKall = hsm;
@@ -209,7 +221,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_fwd_head_kernel(Attn
   const bf16* kvbase = p.qkv + (long)b * p.T * p.D3;
   head_stage(p, kvbase + p.HD + h * p.dk, kvbase + 2 * p.HD + h * p.dk, p.D3, p.D3, Tp, sKall, sVall, tid,
              blockDim.x);
-  const int q0 = wv * 32;
+  const int q0 = (hp.blk0 + wv) * 32;
   bf16x8 qf[4];
   load_bfrags(p, kvbase + h * p.dk, p.D3, q0 + (lane & 31), p.T, qf, lane);
   __syncthreads();
@@ -281,7 +293,8 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
   const float dkeep = drop_keep_scale(dthr);
   extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const HeadPart hp = head_part(p);
+  const int b = hp.b, h = hp.h;
   const int len = p.len[b];
   const int nkt = (len + TILE - 1) / TILE, Tp = nkt * TILE;
   bf16* sKall = hsm;
@@ -289,7 +302,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dq_head_kernel(A
   const bf16* kvbase = p.qkv + (long)b * p.T * p.D3;
   head_stage(p, kvbase + p.HD + h * p.dk, kvbase + 2 * p.HD + h * p.dk, p.D3, p.D3, Tp, sKall, sVall, tid,
              blockDim.x);
-  const int q0 = wv * 32;
+  const int q0 = (hp.blk0 + wv) * 32;
   const int qi = q0 + (lane & 31);
   bf16x8 qf[4], gf[4];
   load_bfrags(p, kvbase + h * p.dk, p.D3, qi, p.T, qf, lane);
@@ -404,7 +417,8 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
   const float dkeep = drop_keep_scale(dthr);
   extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5;
-  const int b = blockIdx.x / p.H, h = blockIdx.x % p.H;
+  const HeadPart hp = head_part(p);
+  const int b = hp.b, h = hp.h;
   const int len = p.len[b];
   const int nq = (p.T + 31) / 32, Tq = nq * 32;
   bf16* sQall = hsm;
@@ -418,7 +432,7 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
     sL[i] = i < p.T ? lse[((long)b * p.H + h) * p.T + i] * LOG2E : INFINITY;
     sD[i] = i < p.T ? Dg[((long)b * p.H + h) * p.T + i] : 0.f;
   }
-  const int k0w = wv * 32;
+  const int k0w = (hp.blk0 + wv) * 32;
   const int kj = k0w + (lane & 31);
   const bool kvalid = kj < len;
   bf16x8 kf[4], vf[4];
@@ -540,9 +554,9 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
   }
 }
 
-size_t dkdv_wave_lds_bytes(int T) {
+size_t dkdv_wave_lds_bytes(int T, int waves) {
   const size_t nq = (size_t)cdiv(T, 32), rows = nq * 32;
-  return 2 * rows * KS * sizeof(bf16) + 2 * rows * sizeof(float) + nq * nq * 64 * sizeof(unsigned short);
+  return 2 * rows * KS * sizeof(bf16) + 2 * rows * sizeof(float) + (size_t)waves * nq * 64 * sizeof(unsigned short);
 }
 
 // ------------------------------------------------------------------------------------ D = rowsum(dO*O)
@@ -772,11 +786,32 @@ bool use_mfma(int dtype, const void* pos, int dk) {
 
 // whole-head kernels: T <= HEAD_TMAX; cfm_attn_set_mode bit 0 forces the tiled kernels (A/B, parity)
 bool use_head(int T) { return T <= HEAD_TMAX && (g_attn_mode & 1) == 0; }
-size_t head_lds_bytes(int T) {
+size_t head_lds_bytes(int T, int waves) {
   const size_t rows = (size_t)cdiv(T, TILE) * TILE;
   const size_t img = 2 * rows * KS * sizeof(bf16);
-  const size_t stage = (size_t)cdiv(T, 32) * 32 * 65 * sizeof(float);
+  const size_t stage = (size_t)waves * 32 * 65 * sizeof(float);
   return img > stage ? img : stage;
+}
+
+int attn_num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// workgroups per (b, h) of the whole-head kernels: enough to give every CU one (B*H*qs <= CUs), at most 4 and at most
+// one 32-row block each (cfm_attn_set_mode bit 6: always one, A/B)
+int head_split(int B, int H, int T) {
+  if (g_attn_mode & 64) return 1;
+  const int nb = cdiv(T, 32), bh = B * H, cus = attn_num_cus();
+  int qs = 1;
+  while (qs < 4 && qs < nb && (long)bh * (qs + 1) <= cus) ++qs;
+  return qs;
 }
 
 }  // namespace
@@ -798,10 +833,13 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0), g_attn_mode & 6,
           cfm::g_rng_salt};
+  p.vec4 = ((uintptr_t)qkv % 8 == 0) && (dk % 4 == 0) && ((3 * H * dk) % 4 == 0);
   if (use_head(T)) {
     // LDS sized for the full padded length (lengths are device data; len <= T)
-    hipLaunchKernelGGL(attn_fwd_head_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), head_lds_bytes(T), s, p, (bf16*)o,
-                       lse);
+    p.qs = head_split(B, H, T);
+    const int waves = cdiv(cdiv(T, 32), p.qs);
+    hipLaunchKernelGGL(attn_fwd_head_kernel, dim3(B * H * p.qs), dim3(64 * waves), head_lds_bytes(T, waves), s, p,
+                       (bf16*)o, lse);
     return cfm::check_launch("cfm_attn_fwd");
   }
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (bf16*)o, lse);
@@ -831,6 +869,7 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
   AttnM p{(const bf16*)qkv, B, T, H, dk, 3 * H * dk, H * dk, lengths, 1.f / sqrtf((float)dk), drop_p, seed,
           ((uintptr_t)qkv % 16 == 0) && ((uintptr_t)dout % 16 == 0) && (dk % 8 == 0) && ((3 * H * dk) % 8 == 0),
           g_attn_mode & 6, cfm::g_rng_salt};
+  p.vec4 = ((uintptr_t)qkv % 8 == 0) && ((uintptr_t)dout % 8 == 0) && (dk % 4 == 0) && ((3 * H * dk) % 4 == 0);
   const long nrow = (long)B * H * T;
   (void)nrow;
   CFM_REQUIRE(H * dk <= 1024, CFM_ERR_UNSUPPORTED, "H*dk must be <= 1024");
@@ -840,14 +879,16 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
   if (pos)
     return cfm::attn_rel_bwd_launch(qkv, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dpos_dt, dpos_u, dpos_v, B,
                                     T, H, dk, drop_p, seed, ws, s);
+  p.qs = use_head(T) ? head_split(B, H, T) : 1;
+  const int hwaves = cdiv(cdiv(T, 32), p.qs);
   if (use_head(T))
-    hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), dkdv_wave_lds_bytes(T), s, p,
-                       (const bf16*)dout, lse, ws, (bf16*)dqkv);
+    hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H * p.qs), dim3(64 * hwaves), dkdv_wave_lds_bytes(T, hwaves),
+                       s, p, (const bf16*)dout, lse, ws, (bf16*)dqkv);
   else
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse,
                        ws, (bf16*)dqkv);
   if (use_head(T))
-    hipLaunchKernelGGL(attn_bwd_dq_head_kernel, dim3(B * H), dim3(64 * cdiv(T, 32)), head_lds_bytes(T), s, p,
+    hipLaunchKernelGGL(attn_bwd_dq_head_kernel, dim3(B * H * p.qs), dim3(64 * hwaves), head_lds_bytes(T, hwaves), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);
   else
     hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse, ws,

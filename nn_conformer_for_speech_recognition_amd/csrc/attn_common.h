@@ -21,6 +21,8 @@ struct AttnM {
   bool vec;    // 16-B vector loads legal
   int dbg;     // timing experiments (cfm_attn_set_mode bits 1-2)
   const uint64_t* salt;   // bound dropout step counter or nullptr
+  bool vec4;   // 8-B vector loads legal (dk % 4 == 0, 8-B aligned rows: Conformer-S's dk 36)
+  int qs;      // whole-head kernels: workgroups per (b, h), each a contiguous range of 32-row blocks (<= 1: one)
 };
 
 // attention-dropout element index: rows of an EVEN stride (T rounded up to even), so the keys 2m and
@@ -56,11 +58,18 @@ __device__ __forceinline__ void dropout_pair32(uint32_t thr, float keep, uint32_
 }
 
 // 8 consecutive head-dim elements c..c+7 of row `row` of matrix base (row stride ld), zero-padded
-__device__ __forceinline__ uint4 ld8(const bf16* base, long ld, int row, int nrows, int c, int dk, bool vec) {
+// (vec: one 16-B load; vec4: two 8-B loads, the upper one zero past dk -- dk 36 rows start 8-B aligned only)
+__device__ __forceinline__ uint4 ld8(const bf16* base, long ld, int row, int nrows, int c, int dk, bool vec,
+                                     bool vec4 = false) {
   uint4 r = make_uint4(0, 0, 0, 0);
   if (row >= nrows || c >= dk) return r;
   const bf16* p = base + (long)row * ld + c;
   if (vec && c + 8 <= dk) return *reinterpret_cast<const uint4*>(p);
+  if (vec4) {
+    const uint2 lo = *reinterpret_cast<const uint2*>(p);
+    const uint2 hi = c + 8 <= dk ? *reinterpret_cast<const uint2*>(p + 4) : make_uint2(0, 0);
+    return make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
   unsigned short t[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) t[e] = (c + e < dk) ? reinterpret_cast<const unsigned short*>(p)[e] : 0;
@@ -130,7 +139,7 @@ __device__ __forceinline__ void load_bfrags(const AttnM& p, const bf16* base, lo
                                             bf16x8 (&f)[4], int lane) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    uint4 u = ld8(base, ld, row, nrows, 16 * s + 8 * (lane >> 5), p.dk, p.vec);
+    uint4 u = ld8(base, ld, row, nrows, 16 * s + 8 * (lane >> 5), p.dk, p.vec, p.vec4);
     f[s] = __builtin_bit_cast(bf16x8, u);
   }
 }

@@ -70,6 +70,8 @@ struct CtcP {
   float* nll_raw;                     // (B) -log p, may be +inf
   int32_t* grp;                       // (B, 2, Smax): per label position u: [0] head flag (first occurrence of
                                       // its class), [1] next position of the same class (-1: none)
+  int32_t* ab_abort;                  // (2, B): 1 where the alpha (row 0) / beta (row 1) recursion gave up a wait
+  int dbg_abort;                      // debug (cfm_ctc_set_debug): bit d forces direction d's abort path
 };
 
 __device__ __forceinline__ const int32_t* tgt_of(const CtcP& p, int b) {
@@ -129,12 +131,15 @@ __global__ __launch_bounds__(256) void ctc_prep(CtcP p) {
 // (four 16-B stores each), and the wave then publishes the block index.  Its successor waits for that once per
 // block, loads the block's PF edge pairs into lanes 0..PF-1 and reads them per frame with v_readlane, so it
 // runs one block behind with no synchronisation inside the block (the barrier form paid a workgroup barrier and
-// an LDS round trip on every frame: 0.35 us per frame at L60).  A wait gives up after AB_SPIN polls (the loss is
-// then NaN), so no wave can spin forever.
+// an LDS round trip on every frame: 0.35 us per frame at L60).  A wait gives up after AB_SPIN polls, so no wave
+// can spin forever: either direction's abort is recorded in ab_abort, and ctc_finish turns the utterance's loss
+// (nll and the nll_raw ctc_grad reads) into NaN and counts it in the bound abort counter (cfm_ctc_bind_abort_counter),
+// apart from genuine non-finite losses.  AB_SPIN polls of s_sleep 1 are ~0.1 s: a delayed co-resident wave
+// (a side-stream kernel sharing the CU) slows the step, it does not abort it.
 constexpr int AB_NT = 1024;
 constexpr int AB_RB = 4;                  // ring depth in blocks
 constexpr int AB_RF = AB_RB * PF;         // ring depth in frames
-constexpr int AB_SPIN = 1 << 16;
+constexpr int AB_SPIN = 1 << 22;
 typedef float f32x4e __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) volatile int lds_int;
 typedef __attribute__((address_space(3))) volatile float lds_float;
@@ -252,25 +257,36 @@ __global__ __launch_bounds__(AB_NT) void ctc_alphabeta(CtcP p) {
   const int Tb = in_len_of(p, b), L = tgt_len_of(p, b);
   if (Tb <= 0) {   // uniform over the workgroup
     if (blockIdx.y == 0 && tid == 0) p.nll_raw[b] = L == 0 ? 0.f : INFINITY;
+    if (tid == 0) p.ab_abort[blockIdx.y * p.B + b] = 0;
     return;
   }
   if (tid < AB_NT / 64) tags[tid] = -1;
   if (tid == 0) {
-    abort_flag = 0;
+    abort_flag = (p.dbg_abort >> blockIdx.y) & 1;
     fin[0] = fin[1] = NEG_INF;
   }
   __syncthreads();
   if (blockIdx.y == 0) ctc_alphabeta_dir<0>(p, edge, tags, &abort_flag, fin);
   else ctc_alphabeta_dir<1>(p, edge, tags, &abort_flag, fin);
   __syncthreads();
-  if (blockIdx.y == 0 && tid == 0) p.nll_raw[b] = abort_flag ? NAN : -lse2(fin[0], fin[1]);
+  if (tid == 0) {
+    if (blockIdx.y == 0) p.nll_raw[b] = abort_flag ? NAN : -lse2(fin[0], fin[1]);
+    p.ab_abort[blockIdx.y * p.B + b] = abort_flag;
+  }
 }
 
-// nll (B): -log p, or 0 where infinite and zero_infinity
-__global__ void ctc_finish(const float* nll_raw, int B, int zero_inf, float* nll) {
+// nll (B): -log p, or 0 where infinite and zero_infinity; NaN (nll and nll_raw, which ctc_grad reads) where either
+// recursion aborted, each such utterance counted in *aborts (nullable)
+__global__ void ctc_finish(float* nll_raw, const int32_t* ab_abort, int B, int zero_inf, float* nll,
+                           int32_t* aborts) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) {
-    const float v = nll_raw[b];
+    float v = nll_raw[b];
+    if (ab_abort[b] | ab_abort[B + b]) {
+      v = NAN;
+      nll_raw[b] = v;
+      if (aborts) atomicAdd(aborts, 1);
+    }
     nll[b] = (zero_inf && isinf(v)) ? 0.f : v;
   }
 }
@@ -446,14 +462,31 @@ CtcP make_p(const float* logits, long sb, long st, const int32_t* targets, int l
   p.beta = p.alpha + bts;
   p.nll_raw = p.beta + bts;
   p.grp = reinterpret_cast<int32_t*>(p.nll_raw + B);
+  p.ab_abort = p.grp + 2L * B * Smax;
+  p.dbg_abort = 0;
   return p;
 }
+
+int g_ctc_dbg_abort = 0;          // cfm_ctc_set_debug
+int32_t* g_ctc_aborts = nullptr;  // cfm_ctc_bind_abort_counter
 
 }  // namespace
 
 CFM_EXPORT size_t cfm_ctc_ws_bytes(int B, int T, int Smax) {
   const long bt = (long)B * T;
-  return sizeof(float) * (size_t)(bt + 3 * bt * (2L * Smax + 1) + B) + sizeof(int32_t) * 2 * (size_t)B * Smax;
+  return sizeof(float) * (size_t)(bt + 3 * bt * (2L * Smax + 1) + B) + sizeof(int32_t) * 2 * (size_t)B * Smax +
+         sizeof(int32_t) * 2 * (size_t)B;
+}
+
+CFM_EXPORT int cfm_ctc_set_debug(int force_abort_mask) {
+  CFM_REQUIRE(force_abort_mask >= 0 && force_abort_mask <= 3, CFM_ERR_ARG, "mask: bit 0 alpha, bit 1 beta");
+  g_ctc_dbg_abort = force_abort_mask;
+  return CFM_OK;
+}
+
+CFM_EXPORT int cfm_ctc_bind_abort_counter(int32_t* counter) {
+  g_ctc_aborts = counter;
+  return CFM_OK;
 }
 
 CFM_EXPORT int cfm_ctc_loss_fwd(const float* logits, long sb, long st, const int32_t* targets, int ldt,
@@ -466,9 +499,11 @@ CFM_EXPORT int cfm_ctc_loss_fwd(const float* logits, long sb, long st, const int
   CFM_REQUIRE(S <= AB_NT, CFM_ERR_UNSUPPORTED, "target length must be <= 511");
   hipStream_t s = cfm::as_stream(stream);
   CtcP p = make_p(logits, sb, st, targets, ldt, tgt_off, in_len, tgt_len, B, T, V, Smax, blank, ws);
+  p.dbg_abort = g_ctc_dbg_abort;
   hipLaunchKernelGGL(ctc_prep, dim3((unsigned)(((long)B * T + 3) / 4)), dim3(256), 0, s, p);
   hipLaunchKernelGGL(ctc_alphabeta, dim3(B, 2), dim3(AB_NT), 0, s, p);
-  hipLaunchKernelGGL(ctc_finish, dim3(cdiv(B, 256)), dim3(256), 0, s, p.nll_raw, B, zero_infinity, nll);
+  hipLaunchKernelGGL(ctc_finish, dim3(cdiv(B, 256)), dim3(256), 0, s, p.nll_raw, p.ab_abort, B, zero_infinity, nll,
+                     g_ctc_aborts);
   return cfm::check_launch("cfm_ctc_loss_fwd");
 }
 

@@ -863,7 +863,7 @@ struct PipeGeo {
   static constexpr int NTt = NWV * 64, NW = NWV;
   static constexpr int ABYTES = BMt * BKt * 2, BBYTES = BNt * BKt * 2;
   static constexpr int STAGE = ABYTES + BBYTES;
-  static constexpr int RING = NST * STAGE, EPI = 128 * (BNt + 4) * 4;
+  static constexpr int RING = NST * STAGE, EPI = (BMt < 128 ? BMt : 128) * (BNt + 4) * 4;
   static constexpr int LDS = RING > EPI ? RING : EPI;
   // 1-KiB DMA pieces per stage, spread over the waves: wave w issues pieces w, w + NW, ... (AI / BI rounds;
   // when a count is not a multiple of NW the first waves issue one more piece, and their counted waits say so)
@@ -943,6 +943,14 @@ __device__ __forceinline__ unsigned pipe_src(const PipeOp& o, int lc, int row0, 
     const int col = row0 + 8 * c < o.lim - 8 ? row0 + 8 * c : o.lim - 8;
     return (unsigned)(((long)(k0 + k) * o.ld + col) * 2);
   }
+}
+
+// k offset (elements, within the BKt-deep tile) of the 16-B chunk that lands in K-major LDS slot `lc`
+template <int BKt>
+__device__ __forceinline__ int pipe_kchunk(int lc) {
+  typedef KmSw<BKt> S;
+  const int r = lc / S::CPR;
+  return 8 * S::slot(r, lc % S::CPR);
 }
 
 // one 32x32x16 operand fragment from a swizzled stage image
@@ -1065,6 +1073,15 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
 #pragma unroll
   for (int i = 0; i < G::BI; ++i)
     offb[i] = pipe_src<BKM, BNt, BKt>(ob, ((i * G::NW + wid) % G::BP) * 64 + lane, n0, kbeg);
+  // K tail (K-major operands, K % BKt != 0, K % 8 == 0): the last stage's chunks at k >= kend read zero through an
+  // out-of-range offset (a K-major row's tail would otherwise read the next row's head); MN-major operands already
+  // read zero past K (their extent ends at row K - 1).  kca / kcb: the k offset of each piece's chunk in its tile
+  const bool ktail = ((kend - kbeg) % BKt) != 0;
+  int kca[G::AI], kcb[G::BI];
+#pragma unroll
+  for (int i = 0; i < G::AI; ++i) kca[i] = AK ? pipe_kchunk<BKt>(((i * G::NW + wid) % G::AP) * 64 + lane) : 0;
+#pragma unroll
+  for (int i = 0; i < G::BI; ++i) kcb[i] = BKM ? pipe_kchunk<BKt>(((i * G::NW + wid) % G::BP) * 64 + lane) : 0;
   // this wave's DMA pieces per stage (all waves alike unless the piece counts do not divide evenly)
   const int per_w = G::EVEN ? G::AI + G::BI
                             : (G::AP / G::NW + (wid < G::AP % G::NW)) + (G::BP / G::NW + (wid < G::BP % G::NW));
@@ -1096,6 +1113,17 @@ void gemm_pipe_kernel(GemmP p, PipeOp oa, PipeOp ob, GatherA ga) {
         const bool ok = ii >= 0 && jj >= 0 && ii < ga.Ilim && jj < ga.Jlim;
         dma16(ra, sa + (i * G::NW + wid) * 1024, ok ? offa[i] + shift : 0xFFFFFF00u);
       }
+    } else if (ktail && kt == nk - 1) {   // wave-uniform: the last, partial K tile
+      const int lim = kend - kbeg - kt * BKt;
+#pragma unroll
+      for (int i = 0; i < G::AI; ++i)
+        if (G::EVEN || i * G::NW + wid < G::AP)
+          dma16(ra, sa + (i * G::NW + wid) * 1024, !AK || kca[i] < lim ? offa[i] + kt * stepa : 0xFFFFFF00u);
+#pragma unroll
+      for (int i = 0; i < G::BI; ++i)
+        if (G::EVEN || i * G::NW + wid < G::BP)
+          dma16(rb, sb + (i * G::NW + wid) * 1024, !BKM || kcb[i] < lim ? offb[i] + kt * stepb : 0xFFFFFF00u);
+      return;
     } else {
 #pragma unroll
       for (int i = 0; i < G::AI; ++i)
@@ -1312,7 +1340,7 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
   xcd_tile3(tm, tn, zz);
   const int m0 = tm * BMt, n0 = tn * BNt;
   const int z = zz;                       // split_k == 1: the batch index
-  const int nk = (p.dbg & 4) ? 0 : p.K / BKt;   // (dbg 4: epilogue only)
+  const int nk = (p.dbg & 4) ? 0 : (p.K + BKt - 1) / BKt;   // (dbg 4: epilogue only; a partial last tile: below)
   // the epilogue rows' global inputs (f32 residual / bf16 rd_with / pre-activation), issued before the main loop
   // so their latency hides under it (the loaders' counted stage waits see them as older, completed first)
   constexpr int EIT = BMt * CPW / NTt;
@@ -1328,7 +1356,7 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
     const int lw = wid - NC;
     const __amdgpu_buffer_rsrc_t ra = pipe_rsrc(oa, z), rb = pipe_rsrc(ob, z);
     unsigned off[PW];
-    int ldo[PW];
+    int ldo[PW], kc[PW];
     bool isa[PW];
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
@@ -1338,8 +1366,17 @@ __global__ __launch_bounds__((WM * WN + NL) * 64) void gemm_ws_kernel(GemmP p, P
       off[i] = isa[i] ? pipe_src<true, BMt, BKt>(oa, qq * 64 + lane, m0, 0)
                       : pipe_src<true, BNt, BKt>(ob, qq * 64 + lane, n0, 0);
       ldo[i] = (isa[i] ? 0 : ABYTES) + qq * 1024;
+      kc[i] = pipe_kchunk<BKt>(qq * 64 + lane);
     }
+    // K % BKt != 0 (K % 8 == 0): the last tile's chunks at k >= K read zero (out-of-range offset), not the next row
+    const int klast = p.K - (nk - 1) * BKt;
     auto issue = [&](int kt) {
+      if (kt == nk - 1 && klast < BKt) {   // wave-uniform
+#pragma unroll
+        for (int i = 0; i < PW; ++i)
+          dma16(isa[i] ? ra : rb, lds + (kt % NST) * STAGE + ldo[i], kc[i] < klast ? off[i] + kt * (BKt * 2) : 0xFFFFFF00u);
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < PW; ++i)
         dma16(isa[i] ? ra : rb, lds + (kt % NST) * STAGE + ldo[i], off[i] + kt * (BKt * 2));
@@ -1758,8 +1795,11 @@ bool pipe_ok(const cfm_gemm_desc& d, const GemmP& p, bool va, bool vb) {
   auto fits = [](long bytes) { return bytes > 0 && bytes < (1L << 31); };
   const long ea = pipe_extent(d.a_kmajor, d.M, d.K, d.lda), eb = pipe_extent(d.b_kmajor, d.N, d.K, d.ldb);
   if (!fits(ea * 2) || !fits(eb * 2)) return false;
-  if (d.a_kmajor ? d.K % BK16 != 0 : d.M % 8 != 0) return false;
-  if (d.b_kmajor ? d.K % BK16 != 0 : d.N % 8 != 0) return false;
+  // K-major: whole 16-B chunks along K; a partial last K tile reads zero past K (the kernels' tail stage), so K need
+  // not be a multiple of the tile depth -- Conformer-S's K = 144 / 432 / 288 (d 144) take the pipeline too
+  const int kq = p.split_k == 1 ? 8 : BK16;
+  if (d.a_kmajor ? d.K % kq != 0 : d.M % 8 != 0) return false;
+  if (d.b_kmajor ? d.K % kq != 0 : d.N % 8 != 0) return false;
   return true;
 }
 
@@ -1800,6 +1840,21 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
   const int sel = (g_gemm_mode >> 4) & 7;
   const dim3 g256(cdiv(p.N, BN), cdiv(p.M, 256), batch * p.split_k);
   int v = sel;
+  if constexpr (AK && BKM) {
+    // auto: 129..160-column outputs (Conformer-S's d = 144) on 64 x 160 tiles, five waves of 64 x 32, BK 64 in a
+    // 4-deep ring (84 KiB in flight: one workgroup per CU, 187 of them, each bound by its DMA latency): ONE column tile (the 128-wide tiles took two, the second 16 columns wide -- 126 workgroups for
+    // 256 CUs with 44 % of the MFMA work padding); these K <= 576 GEMMs are bandwidth-bound, so the tile's 187 row
+    // blocks each stream their A rows once.  cfm_gemm_set_mode bit 22 keeps the 128-wide tiles (A/B)
+    if (v == 0 && p.N > 128 && p.N <= 160 && p.split_k == 1 && !(g_gemm_mode & 4194304)) {
+      const dim3 g64(1, cdiv(p.M, 64), batch);
+      ek_dispatch<true>(p.efast, [&](auto ek) {
+        hipLaunchKernelGGL((gemm_pipe_kernel<64, 64, 4, 1, true, true, 5, 5, false, false, false, 160, M16,
+                                             decltype(ek)::value>),
+                           g64, dim3(320), 0, s, p, oa, ob, GatherA{});
+      });
+      return;
+    }
+  }
   if constexpr (AK) {
     // auto: outputs <= 512 columns (the encoder's d-wide outputs) take the 192-row tiles: 63 x 4 = 252
     // tiles fill 256 CUs in one round where 256-row tiles leave 68 CUs idle (A/B: 9-18 % faster)
@@ -1830,8 +1885,10 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
     // 1024- / 1536-wide K-major x K-major outputs (QKV, pointwise-conv-1 forward) on the warp-specialised kernel:
     // QKV 32.41 -> 30.97 us, pw1 22.53 -> 21.41 us same box, bit-identical (gpurun_out r04y; the 2048-wide ones
     // stay on the two-per-CU 256-row tiles: 45.5 vs 57.3 us).  cfm_gemm_set_mode bit 21 keeps the 192-row pipeline.
+    // (short reductions, K <= 256 -- Conformer-S's FFN up / down-gradient at K 144: three K tiles -- keep the two-per-CU
+    // pipeline: S15 step 8.27 -> 8.07 ms same box, gpurun_out r06c)
     if constexpr (BKM) {
-      if (v == 7 && sel == 0 && !(g_gemm_mode & 2097152)) {
+      if (v == 7 && sel == 0 && !(g_gemm_mode & 2097152) && p.k_per_split > 256) {
         const dim3 g192(cdiv(p.N, BN), cdiv(p.M, 192), batch * p.split_k);
         ek_dispatch<true>(p.efast, [&](auto ek) {
           hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 4, 4, 4, decltype(ek)::value>), g192, dim3(768), 0, s, p, oa, ob);

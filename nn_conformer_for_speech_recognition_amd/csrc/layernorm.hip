@@ -233,6 +233,157 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TDY* __restrict__ dy, co
     ws[(long)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
+// ---------------------------------------------------------------- lane-group kernels (D % 8 == 0, D <= 8 G)
+// Widths that are not 64 * V (Conformer-S: D = 144) on 16-B vectors: a group of G lanes owns one row, 8 contiguous
+// features per lane (lanes 8 j >= D idle), 64 / G rows per wave, the row sums over the group by xor shuffles inside
+// it.  (The strided generic kernels below moved 4-B elements with per-element dtype branches: 20 us per D-144
+// backward where the bytes take ~5.)
+template <int G> __device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int G, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_grp(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, TY* __restrict__ y,
+                                                  float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
+                                                  int D, float eps) {
+  constexpr int RPW = 64 / G, R = LN_FWD_ROWS;
+  const int lane = threadIdx.x & 63, j = lane % G, c = 8 * j;
+  const bool act = c < D;
+  const long row0 = (((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / G) * R;
+  float v[R][8], g[8], b[8];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (act && row0 + r < M) {
+      ldv<8>(x + (row0 + r) * D + c, v[r]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[r][i] = 0.f;
+    }
+  }
+  if (act) {
+    ldv<8>(gamma + c, g);
+    ldv<8>(beta + c, b);
+  }
+  const float invd = 1.f / (float)D;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[r][i];
+    const float mean = group_sum<G>(s) * invd;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      v[r][i] = act ? v[r][i] - mean : 0.f;
+      q += v[r][i] * v[r][i];
+    }
+    const float rstd = rsqrtf(group_sum<G>(q) * invd + eps);
+    if (row0 + r < M) {
+      if (act) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[r][i] = v[r][i] * rstd * g[i] + b[i];
+        stv<8>(y + (row0 + r) * D + c, v[r]);
+      }
+      if (j == 0) {
+        mean_out[row0 + r] = mean;
+        rstd_out[row0 + r] = rstd;
+      }
+    }
+  }
+}
+
+template <int G, typename TDY>
+__global__ __launch_bounds__(256) void ln_bwd_grp(const TDY* __restrict__ dy, const float* __restrict__ x,
+                                                  const float* __restrict__ gamma, const float* __restrict__ mean_in,
+                                                  const float* __restrict__ rstd_in, const float* __restrict__ dres,
+                                                  float* __restrict__ dx, float* __restrict__ ws, long M, int D,
+                                                  LnDrop dr) {
+  if (dr.g2 && dr.p > 0.f) dr.seed = salted_seed(dr.seed, dr.salt);
+  constexpr int RPW = 64 / G;
+  __shared__ float red[4][2 * 8 * G];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, j = lane % G, c = 8 * j;
+  const bool act = c < D;
+  const long slot = ((long)blockIdx.x * 4 + wv) * RPW + lane / G;
+  const long nslots = (long)gridDim.x * 4 * RPW;
+  float gm[8], pg[8], pb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) gm[i] = pg[i] = pb[i] = 0.f;
+  if (act) ldv<8>(gamma + c, gm);
+  const float invd = 1.f / (float)D;
+  // every group of the wave runs the same trip count (the shuffles span the wave); rows past M are masked
+  const long nrow_iter = (M + nslots - 1) / nslots;
+  for (long it = 0; it < nrow_iter; ++it) {
+    const long row = slot + it * nslots;
+    const bool live = act && row < M;
+    const float mean = row < M ? mean_in[row] : 0.f, rstd = row < M ? rstd_in[row] : 0.f;
+    float d[8], xh[8], g[8];
+    if (live) {
+      ldv<8>(dy + row * D + c, d);
+      ldv<8>(x + row * D + c, xh);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = xh[i] = 0.f;
+    }
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      xh[i] = live ? (xh[i] - mean) * rstd : 0.f;
+      g[i] = d[i] * gm[i];
+      pg[i] += d[i] * xh[i];
+      pb[i] += d[i];
+      sg += g[i];
+      sgx += g[i] * xh[i];
+    }
+    sg = group_sum<G>(sg) * invd;
+    sgx = group_sum<G>(sgx) * invd;
+    if (live) {
+      float o[8];
+      if (dres) ldv<8>(dres + row * D + c, o);
+      else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] += rstd * (g[i] - sg - xh[i] * sgx);
+      stv<8>(dx + row * D + c, o);
+      if (dr.g2) {   // the next module's input gradient: bf16(dx * scale * dropout mask), as cfm_scale_dropout
+        float sc[8];
+        if (dr.p > 0.f) dropout_scale8(dr.p, dr.seed, (uint64_t)(row * D + c), sc);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sc[i] = dr.p > 0.f ? dr.scale * sc[i] : dr.scale;
+        float q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = o[i] * sc[i];
+        st8_dyn(dr.g2, CFM_BF16, row * D + c, q);
+      }
+    }
+  }
+  // the groups of a wave hold the same columns: fold them (xor over the group index bits), then group 0 writes
+#pragma unroll
+  for (int o = G; o < 64; o <<= 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pg[i] += __shfl_xor(pg[i], o, 64);
+      pb[i] += __shfl_xor(pb[i], o, 64);
+    }
+  }
+  if (lane < G) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[wv][c + i] = pg[i];
+      red[wv][8 * G + c + i] = pb[i];
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < 2 * D; q += 256) {
+    const int k = q < D ? q : 8 * G + (q - D);
+    ws[(long)blockIdx.x * 2 * D + q] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  }
+}
+
 // ---------------------------------------------------------------- generic kernels (any D <= 1024)
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int dtx,
                                                      const float* __restrict__ gamma,
@@ -376,6 +527,58 @@ bool ln_bwd_fast(const void* dy, int dtdy, const void* x, int dtx, const float* 
                        mean, rstd, (const float*)dres, (float*)dx, ws, M, dr);
   return true;
 }
+// D % 8 == 0 widths below 512 that are not 64 * V: the lane-group kernels (G = next power of two >= D / 8)
+int ln_group(int D) {
+  if (D % 8 || D > 512) return 0;
+  const int n = D / 8;
+  return n <= 16 ? 16 : n <= 32 ? 32 : 64;
+}
+
+bool ln_fwd_grouped(const void* x, int dtx, const float* gamma, const float* beta, void* y, int dty, float* mean,
+                    float* rstd, long M, int D, float eps, hipStream_t s) {
+  const int G = ln_group(D);
+  if (!G || dtx != CFM_F32 || (dty != CFM_F32 && dty != CFM_BF16) || !aligned16(x) || !aligned16(y) ||
+      !aligned16(gamma) || !aligned16(beta))
+    return false;
+  const long rows_per_block = 4L * (64 / G) * LN_FWD_ROWS;
+  const dim3 g((unsigned)((M + rows_per_block - 1) / rows_per_block));
+  auto go = [&](auto gt) {
+    constexpr int GG = decltype(gt)::value;
+    if (dty == CFM_BF16)
+      hipLaunchKernelGGL((ln_fwd_grp<GG, bf16>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (bf16*)y, mean,
+                         rstd, M, D, eps);
+    else
+      hipLaunchKernelGGL((ln_fwd_grp<GG, float>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (float*)y, mean,
+                         rstd, M, D, eps);
+  };
+  if (G == 16) go(std::integral_constant<int, 16>{});
+  else if (G == 32) go(std::integral_constant<int, 32>{});
+  else go(std::integral_constant<int, 64>{});
+  return true;
+}
+
+bool ln_bwd_grouped(const void* dy, int dtdy, const void* x, int dtx, const float* gamma, const float* mean,
+                    const float* rstd, const void* dres, int dtres, void* dx, int dtdx, float* ws, long M, int D,
+                    int nb, hipStream_t s, LnDrop dr) {
+  const int G = ln_group(D);
+  if (!G || dtx != CFM_F32 || dtdx != CFM_F32 || (dres && dtres != CFM_F32)) return false;
+  if (dtdy != CFM_BF16 && dtdy != CFM_F32) return false;
+  if (!aligned16(dy) || !aligned16(x) || !aligned16(dres) || !aligned16(dx) || !aligned16(gamma)) return false;
+  if (dr.g2 && !aligned16(dr.g2)) return false;
+  auto go = [&](auto gt) {
+    constexpr int GG = decltype(gt)::value;
+    if (dtdy == CFM_BF16)
+      hipLaunchKernelGGL((ln_bwd_grp<GG, bf16>), dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const float*)x, gamma,
+                         mean, rstd, (const float*)dres, (float*)dx, ws, M, D, dr);
+    else
+      hipLaunchKernelGGL((ln_bwd_grp<GG, float>), dim3(nb), dim3(256), 0, s, (const float*)dy, (const float*)x, gamma,
+                         mean, rstd, (const float*)dres, (float*)dx, ws, M, D, dr);
+  };
+  if (G == 16) go(std::integral_constant<int, 16>{});
+  else if (G == 32) go(std::integral_constant<int, 32>{});
+  else go(std::integral_constant<int, 64>{});
+  return true;
+}
 }  // namespace
 
 CFM_EXPORT int cfm_layernorm_fwd(const void* x, int dtx, const float* gamma, const float* beta, void* y, int dty,
@@ -387,7 +590,8 @@ CFM_EXPORT int cfm_layernorm_fwd(const void* x, int dtx, const float* gamma, con
   const bool fast = ln_fwd_fast<2>(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s) ||
                     ln_fwd_fast<4>(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s) ||
                     ln_fwd_fast<8>(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s) ||
-                    ln_fwd_fast<16>(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s);
+                    ln_fwd_fast<16>(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s) ||
+                    ln_fwd_grouped(x, dtx, gamma, beta, y, dty, mean, rstd, M, D, eps, s);
   if (!fast)
     hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, dtx, gamma, beta, y, dty,
                        mean, rstd, M, D, eps);
@@ -428,14 +632,16 @@ CFM_EXPORT int cfm_layernorm_bwd_drop(const void* dy, int dtdy, const void* x, i
   bool fast = ln_bwd_fast<2>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr) ||
               ln_bwd_fast<4>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr) ||
               ln_bwd_fast<8>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr) ||
-              ln_bwd_fast<16>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr);
+              ln_bwd_fast<16>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr) ||
+              ln_bwd_grouped(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, dr);
   bool g2_done = fast && g2 != nullptr;
   if (!fast && g2) {   // no fused path for this shape: the vectorised kernel without g2, then a separate pass
     const LnDrop none{nullptr, 0.f, 0.f, 0, nullptr};
     fast = ln_bwd_fast<2>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none) ||
            ln_bwd_fast<4>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none) ||
            ln_bwd_fast<8>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none) ||
-           ln_bwd_fast<16>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none);
+           ln_bwd_fast<16>(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none) ||
+           ln_bwd_grouped(dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres, dx, dtdx, ws, M, D, nb, s, none);
   }
   if (!fast)
     hipLaunchKernelGGL(ln_bwd_kernel, dim3(nb), dim3(256), 0, s, dy, dtdy, x, dtx, gamma, mean, rstd, dres, dtres,

@@ -86,9 +86,10 @@ class _FrameFoldFn(torch.autograd.Function):
         B, T2, T2p, D = g.B, g.T2, g.T2p, g.D
         dh = dh.contiguous()
         gr = ops.scale_dropout(dh, 1.0, drop_p, seed, 0, out_dtype=cd) if drop_p > 0 else _cd(dh, cd)
-        # zero rows past T2 (the view's padding): a persistent buffer whose padding rows are zeroed once; only the
-        # T2 rows of each utterance are rewritten per step (under graph replay the buffer's address is fixed)
-        gpad = _gpad_buffer(B, T2p, D, dh.device, cd)
+        # the gradient in the view's slot layout: T2 rows per utterance, the padding rows past T2 zero (a fresh
+        # buffer per backward: no state shared between models, streams or shapes)
+        gpad = torch.empty(B, T2p, D, device=dh.device, dtype=cd)
+        gpad[:, T2:].zero_()
         gpad[:, :T2].copy_(gr.view(B, T2, D))
         K = B * T2p
         H = torch.empty(D, g.Kp, device=dh.device, dtype=torch.float32)
@@ -105,18 +106,6 @@ class _FrameFoldFn(torch.autograd.Function):
             S = ops.colsum(gpad.view(K, D))
         dw1, db1, dw2, db2, dwp = ops.ffold_bwd_weights(H, S, w1, b1, w2, wp, ws, g)
         return None, dw1, db1, dw2, db2, dwp, S, None, None, None, None, None, None
-
-
-_GPAD = {}
-
-
-def _gpad_buffer(B, T2p, D, device, dtype):
-    key = (B, T2p, D, str(device), dtype)     # made by the first (eager) step: a capture then records no fill
-    buf = _GPAD.get(key)
-    if buf is None:
-        buf = torch.zeros(B, T2p, D, device=device, dtype=dtype)
-        _GPAD[key] = buf
-    return buf
 
 
 def frame_frontend(convsub, proj, x, cd, drop_p=0.0, seed=0, hilo=True):

@@ -192,3 +192,62 @@ def test_ctc_mean_and_nonfinite_counter():
     tb = torch.randint(0, 40, (700,), dtype=torch.int32, device=DEV)
     ref = (big.double().cpu() / tb.clamp(min=1).double().cpu()).mean().item()
     assert abs(ops.ctc_mean(big, tb).item() - ref) <= 1e-5 * abs(ref)
+
+
+def test_ctc_long_targets_vs_torch():
+    """The wave-pipelined recursion at its limits: S = 2 Smax + 1 up to 1021 states (16 waves, the LDS edge rings
+    wrapping over hundreds of frames), mixed target lengths so utterances run different wave counts (1 .. 16), both
+    directions (loss and logits gradient) against torch fp64 -- as test_ctc_bench_shape_vs_torch, held to 2x the
+    distance of torch's own fp32 CTC from fp64."""
+    g = torch.Generator().manual_seed(21)
+    B, T, V, U = 6, 1200, 64, 510
+    x = torch.randn(B, T, V, generator=g)
+    tgt = torch.randint(1, V, (B, U), generator=g)
+    tgt[1, 10:20] = 5                    # repeats: states that cannot skip
+    il = torch.tensor([T, T, 1100, 700, 300, T])
+    tl = torch.tensor([U, 500, 260, 31, 100, 1])
+    xr = x.double().clone().requires_grad_()
+    ref = F.ctc_loss(F.log_softmax(xr, -1).transpose(0, 1), tgt, il, tl, reduction="sum", zero_infinity=True)
+    ref.backward()
+    x32 = x.clone().requires_grad_()
+    F.ctc_loss(F.log_softmax(x32, -1).transpose(0, 1), tgt, il, tl, reduction="sum", zero_infinity=True).backward()
+    xd = x.to(DEV).requires_grad_()
+    loss = ctc.ctc_loss(xd, tgt.to(DEV), il.to(DEV), tl.to(DEV), reduction="none", zero_infinity=True,
+                        batch_first=True)
+    loss.sum().backward()
+    ref_none = F.ctc_loss(F.log_softmax(x.double(), -1).transpose(0, 1), tgt, il, tl, reduction="none",
+                          zero_infinity=True)
+    np.testing.assert_allclose(loss.detach().cpu().double().numpy(), ref_none.numpy(), rtol=2e-5)
+    err_ref32 = (x32.grad.double() - xr.grad).abs().max().item()
+    err = (xd.grad.cpu().double() - xr.grad).abs().max().item()
+    assert err <= 2 * err_ref32 + 1e-6, (err, err_ref32)
+
+
+@pytest.mark.parametrize("mask", [1, 2, 3])
+def test_ctc_recursion_abort_is_visible(mask):
+    """A recursion that gives up a wait (forced here per direction) must not leave a finite loss with a wrong
+    gradient: the aborted utterances' nll and logits gradient are NaN, the others untouched, and the abort counter
+    counts them (the beta workgroup's abort used to reach nothing)."""
+    from nn_conformer_for_speech_recognition_amd import _lib
+    x, tgt, il, tl = _case(3)
+    cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+    _lib.call("cfm_ctc_bind_abort_counter", _lib.ptr(cnt))
+    _lib.call("cfm_ctc_set_debug", mask)
+    try:
+        xd = x.to(DEV).requires_grad_()
+        loss = ctc.ctc_loss(xd, tgt.to(DEV), il.to(DEV), tl.to(DEV), reduction="none", zero_infinity=True,
+                            batch_first=True)
+        loss.sum().backward()
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("cfm_ctc_set_debug", 0)
+        _lib.call("cfm_ctc_bind_abort_counter", None)
+    B = x.shape[0]
+    assert torch.isnan(loss).all().item(), loss           # every utterance forced (Tb > 0 for all)
+    assert torch.isnan(xd.grad[0]).any().item()
+    assert int(cnt.item()) == B
+    # the debug mask off again: finite
+    xd2 = x.to(DEV).requires_grad_()
+    l2 = ctc.ctc_loss(xd2, tgt.to(DEV), il.to(DEV), tl.to(DEV), reduction="none", zero_infinity=True,
+                      batch_first=True)
+    assert torch.isfinite(l2).all().item()

@@ -76,6 +76,9 @@ CASES = [   # (stack, pos_enc, T_enc, lengths): every benchmarked stack at T 94 
     # relative positions (L60's arithmetic) at T 94 and at L60's own length T 1498 (B 1, 60 s); the L15 length 373
     ("L17", "none", 94, [94, 71]), ("M16", "none", 94, [94, 71]), ("S16", "none", 94, [94, 71]),
     ("L17", "rel", 94, [94, 71]), ("L17", "none", 373, [373, 301]), ("L17", "rel", 1498, [1498]),
+    # round 6: Conformer-S / -M at the S15 / M15 length T 373 (dk 36 / 64 on the split whole-head attention kernels,
+    # d 144 on the 64 x 160 GEMM tiles, the K-tail pipeline and the lane-group LayerNorm)
+    ("S16", "none", 373, [373, 301]), ("M16", "none", 373, [373, 301]),
 ]
 
 

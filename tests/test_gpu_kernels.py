@@ -188,9 +188,11 @@ def test_gemm_dropout_deterministic():
     assert torch.allclose(o1[kept], ref[kept] / 0.75, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("D", [144, 256, 512, 100])
+@pytest.mark.parametrize("D", [144, 256, 512, 100, 64, 200, 384])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_layernorm(D, dtype):
+    """64 * V widths on the one-row-per-wave kernels, other multiples of 8 (Conformer-S 144, 64, 200, 384) on the
+    lane-group kernels, the rest (100) on the generic strided kernels."""
     g = torch.Generator().manual_seed(D)
     M = 777
     x = torch.randn(M, D, generator=g) * 2 + 0.3
@@ -321,10 +323,10 @@ def test_conv2_fwd_pipeline(gemm_mode, B, F1, T1, C1, C2):
     assert _rel(fast, slow) < 1e-5
 
 
-@pytest.mark.parametrize("D", [512, 144])
+@pytest.mark.parametrize("D", [512, 144, 200, 100])
 def test_layernorm_bwd_fused_dropout_output(D):
-    """cfm_layernorm_bwd_drop's g2 is bit-identical to cfm_scale_dropout(dx) (fused for D = 512, the
-    separate pass otherwise), dx unchanged."""
+    """cfm_layernorm_bwd_drop's g2 is bit-identical to cfm_scale_dropout(dx) (fused for D = 512 and the lane-group
+    widths 144 / 200, the separate pass for 100), dx unchanged."""
     g = torch.Generator().manual_seed(D)
     M = 1000
     x = torch.randn(M, D, generator=g).to(DEV)
@@ -620,3 +622,34 @@ def test_bn_folded_dwconv_bwd(training, sync, B, T, C, K, dt):
     assert _rel(da.float(), da2.float()) < 1e-5
     assert _rel(dw, dw2) < 1e-5 and (db - db2).norm() < 1e-5 * dw.norm()
     assert torch.equal(dg, dg2) and torch.equal(dbt, dbt2)
+
+@pytest.mark.parametrize("M,N,K", [(11936, 144, 144), (11936, 576, 144), (11936, 432, 144), (11936, 144, 432),
+                                   (11936, 144, 288), (1000, 512, 8), (777, 2048, 72), (500, 144, 576),
+                                   (3000, 1024, 200)])
+def test_gemm_k_tail_pipeline(gemm_mode, M, N, K):
+    """K-major GEMMs whose K is a multiple of 8 but not of the 64-deep tile (Conformer-S: K 144 / 288 / 432) on the
+    LDS-DMA pipeline and the warp-specialised kernel: the last K tile's chunks past K read zero (out-of-range DMA
+    offsets) instead of the next row's head.  fp32 output and the fp32 residual-stream epilogue against fp64 of the
+    bf16 operands, and against the register-staged kernel (cfm_gemm_set_mode 1)."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV)
+    ref = x.double() @ w.double().T
+    outs = {}
+    for mode in (3, 1):
+        gemm_mode(mode)
+        y = torch.empty(M, N, device=DEV, dtype=torch.float32)
+        ops.gemm(x, w, y, M, N, K)
+        yr = torch.empty(M, N, device=DEV, dtype=torch.float32)
+        ops.linear(x, w, b, out=yr, out_scale=0.5, residual=res)
+        yb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.gemm(x, w, yb, M, N, K)
+        torch.cuda.synchronize()
+        outs[mode] = (y, yr, yb)
+    for mode, (y, yr, yb) in outs.items():
+        assert _rel(y, ref) < 1e-5, mode
+        assert _rel(yr, res.double() + 0.5 * (ref + b.double())) < 1e-5, mode
+        assert _rel(yb.float(), ref) < 5e-3, mode
+    assert _rel(outs[3][0], outs[1][0]) < 1e-5
