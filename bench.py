@@ -52,6 +52,7 @@ CONFIGS = {
     "L60": ("Conformer-L", 17, 512, 8, 2048, 31, 8, 60, "rel"),
 }
 PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
+PEAK_FP8_TFLOPS = 5000.0      # MI355X_MICROARCH.md:44: ~5 PF dense fp8 (block-scaled e4m3 MFMA: 2x the bf16 rate)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
@@ -800,7 +801,9 @@ def main():
     # (the FFN down-projection's data-gradient GEMM has the same (M, N, K): match the forward's
     # bias + SiLU epilogue on K-major operands, not the shape alone)
     probe = KernelProbe(lambda kind, shape, dsc: kind == "gemm" and shape == (M_ffn, ffn, d) and dsc.act == 1
-                        and not dsc.act_grad and dsc.a_kmajor and dsc.b_kmajor, dev)
+                        and not dsc.act_grad and dsc.a_kmajor and dsc.b_kmajor and dsc.dtype_ab == _lib.BF16, dev)
+    # --fp8: every fp8 (MX e4m3) forward GEMM -- FFN up / down, QKV, out-projection -- as one family against the fp8 peak
+    fprobe = KernelProbe(lambda kind, shape, dsc: kind == "gemm" and dsc.dtype_ab == _lib.FP8, dev)
     # second probed family: the grouped weight-gradient launch (one per step)
     wprobe = KernelProbe(lambda kind, shape, dsc: kind == "wgroup", dev)
     # the dominant kernel family (round-3 kernel trace): every bf16 GEMM with a d-wide output over the step's
@@ -809,18 +812,17 @@ def main():
     dprobe = KernelProbe(lambda kind, shape, dsc: kind == "gemm" and shape[1] == d and shape[0] * dsc.batch == M_ffn
                          and dsc.dtype_ab == _lib.BF16 and dsc.split_k <= 1 and dsc.a_kmajor and dsc.b_kmajor, dev)
     ops.PROBE = lambda kind, shape, dsc, launch: probe(kind, shape, dsc, lambda: wprobe(
-        kind, shape, dsc, lambda: dprobe(kind, shape, dsc, launch)))
-    h.setup(args.warmup, probes=(probe, wprobe, dprobe))
-    probe.reset()
-    wprobe.reset()
-    dprobe.reset()
+        kind, shape, dsc, lambda: dprobe(kind, shape, dsc, lambda: fprobe(kind, shape, dsc, launch))))
+    h.setup(args.warmup, probes=(probe, wprobe, dprobe, fprobe))
+    for pr in (probe, wprobe, dprobe, fprobe):
+        pr.reset()
     bad_before = h.nonfinite_steps()
 
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     if h.graph is None:
-        probe.active = wprobe.active = dprobe.active = True
+        probe.active = wprobe.active = dprobe.active = fprobe.active = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = h.step()
@@ -828,7 +830,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
-    probe.active = wprobe.active = dprobe.active = False
+    probe.active = wprobe.active = dprobe.active = fprobe.active = False
     elapsed = t1 - t0
     if world > 1:
         tt = torch.tensor([elapsed], device=dev)
@@ -879,7 +881,7 @@ def main():
     cfg_key = args.config + ("+fp8" if args.fp8 else "") + ("+specaug" if args.specaug else "") + (
         f"+pos_{args.pos_enc}" if args.pos_enc else "") + (f"+L{args.layers}" if args.layers else "")
 
-    def roofline_entry(kernel, flops, nbytes, pr, pmc_file, family):
+    def roofline_entry(kernel, flops, nbytes, pr, pmc_file, family, peak_tflops=PEAK_BF16_TFLOPS):
         """bound from the kernel's arithmetic intensity against the machine balance (peak FLOP/s over peak
         HBM B/s); `achieved`/`peak`/`frac` in that bound's unit, both fractions reported.  Duration per launch, three
         ways: live probes (dispatch-inclusive and busy, KernelProbe) and the rocprofv3 kernel-trace mean of the same
@@ -888,19 +890,24 @@ def main():
         live dispatch-inclusive mean."""
         ms_live, n_launch = pr.mean_ms(incl=True)
         ms_busy, _ = pr.mean_ms()
-        tr = trace_family_ms(f"profiles/r05/trace_{cfg_key}.json", cfg_key, family)
+        tr = None
+        for rnd in ("r06", "r05"):      # this round's committed trace summary of the config, else the last round's
+            tr = trace_family_ms(f"profiles/{rnd}/trace_{cfg_key}.json", cfg_key, family)
+            if tr is not None:
+                break
         use_trace = tr is not None and tr[3]
         ms = tr[0] if use_trace else ms_live
         intensity = flops / nbytes
-        balance = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+        balance = peak_tflops * 1e12 / (PEAK_HBM_GBS * 1e9)
         tflops = flops / (ms * 1e-3) / 1e12
         gbs = nbytes / (ms * 1e-3) / 1e9
         hbm = intensity < balance
         e = {"kernel": kernel, "bound": "hbm" if hbm else "mfma",
-             "achieved": round(gbs if hbm else tflops, 1), "peak": PEAK_HBM_GBS if hbm else PEAK_BF16_TFLOPS,
+             "achieved": round(gbs if hbm else tflops, 1), "peak": PEAK_HBM_GBS if hbm else peak_tflops,
              "unit": "GB/s" if hbm else "TFLOP/s",
-             "frac": round(gbs / PEAK_HBM_GBS if hbm else tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
-             "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+             "frac": round(gbs / PEAK_HBM_GBS if hbm else tflops / peak_tflops, 4), "traffic": None,
+             "mfma_frac": round(tflops / peak_tflops, 4), "mfma_peak_tflops": peak_tflops,
+             "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
              "intensity_flop_per_byte": round(intensity, 1), "machine_balance_flop_per_byte": round(balance, 1),
              "avg_launch_ms": round(ms, 4),
              "duration_basis": "rocprofv3 kernel trace of this build (avg_launch_ms_trace)" if use_trace else
@@ -982,6 +989,15 @@ def main():
                                          f"M={M_ffn} tokens", wg_flops, wg_bytes, wprobe, "wgrad_group_pmc.json",
                                          "wgrad"),
     }
+    if probe.mean_ms()[1] == 0:      # --fp8: the FFN up-projection runs on fp8 (roofline_fp8 below)
+        del result["roofline_ffn_up"]
+    if fprobe.mean_ms()[1] > 0:
+        # the MX fp8 forward GEMM family (FFN up / down, QKV, out-projection; mean FLOP and descriptor bytes per
+        # launch) against the ~5 PF dense fp8 peak
+        result["roofline_fp8"] = roofline_entry(
+            f"MX e4m3 forward GEMMs (v_mfma_scale_f32_32x32x64_f8f6f4, gemm_pipe F8): FFN up / down, QKV, out-projection, "
+            f"{fprobe.mean_ms()[1] // max(1, args.steps)} launches per step", fprobe.mean_flops(), fprobe.mean_bytes(),
+            fprobe, "gemm_fp8_pmc.json", "fp8", peak_tflops=PEAK_FP8_TFLOPS)
     if args.poison:
         result["poison"] = True
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

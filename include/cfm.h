@@ -303,6 +303,9 @@ int cfm_layernorm_fwd(const void* x, int dtype_x, const float* gamma, const floa
    (configs[4]); D in {256, 512, 1024}. */
 int cfm_layernorm_fwd_mx(const float* x, const float* gamma, const float* beta, void* y, void* y8, uint8_t* s8,
                          float* mean, float* rstd, long M, int D, float eps, void* stream);
+/* The same with x of dtype_x (CFM_F32 or CFM_BF16: the bf16 mode's bf16 residual stream). */
+int cfm_layernorm_fwd_mx_ex(const void* x, int dtype_x, const float* gamma, const float* beta, void* y, void* y8,
+                            uint8_t* s8, float* mean, float* rstd, long M, int D, float eps, void* stream);
 size_t cfm_layernorm_ws_bytes(long M, int D);
 int cfm_layernorm_bwd(const void* dy, int dtype_dy, const void* x, int dtype_x, const float* gamma,
                       const float* mean, const float* rstd, const void* dres, int dtype_dres,

@@ -540,8 +540,11 @@ template <bool M16> __device__ __forceinline__ int accc(int r, int lane) {
 // between the previous row's stores, waited for every previous row's write acknowledgements (bias-only FFN-up
 // epilogue without the main loop: 49 MB in 21.9 us = 2.2 TB/s).  Arithmetic and its order are epilogue_store8's
 // (bit-identical outputs).
+// residual-stream kinds: EF_F32_RES (fp32 residual in, fp32 out: the parity mode), EF_BF16_RES (bf16 in, bf16 out: the
+// bf16 mode's bf16 residual stream), EF_F32R_BF16 (fp32 in, bf16 out: a layer's first residual add, whose input is the
+// previous layer's fp32 LayerNorm output)
 enum { EF_GENERIC = 0, EF_BF16 = 1, EF_BF16_BIAS = 2, EF_BF16_SILU = 3, EF_BF16_ACTG = 4, EF_BF16_RD = 5, EF_F32 = 6,
-       EF_F32_RES = 7, EF_BF16_SILU_MX = 8 };
+       EF_F32_RES = 7, EF_BF16_SILU_MX = 8, EF_BF16_RES = 9, EF_F32R_BF16 = 10 };
 
 // e8m0 block exponent of an MX block (fp8.hip mx_k): the largest k with amax * 2^k <= 448
 __device__ __forceinline__ int epi_mx_k(float a) {
@@ -580,7 +583,8 @@ __device__ __forceinline__ void drop8_fast(float (&v)[8], uint32_t j0, const Gem
 
 // per-row global inputs of a fast epilogue kind: dwords per row, and the holder (IT rows of one thread)
 template <int EK> constexpr int epi_nw() {
-  return EK == EF_F32_RES ? 8 : (EK == EF_BF16_ACTG || EK == EF_BF16_RD) ? 4 : 0;
+  return (EK == EF_F32_RES || EK == EF_F32R_BF16) ? 8 : (EK == EF_BF16_ACTG || EK == EF_BF16_RD || EK == EF_BF16_RES) ? 4
+                                                                                                                     : 0;
 }
 template <int EK, int IT> struct EpiIn { uint4 v[IT][epi_nw<EK>() == 8 ? 2 : 1]; };
 
@@ -589,11 +593,14 @@ __device__ __forceinline__ void epi_load_row(const GemmP& p, int z, int mbase, i
                                              EpiIn<EK, IT>& in) {
   const int n = n0 + (tid % CPW) * 8, m = mbase + it * (NTt / CPW) + tid / CPW;
   if (m < p.M && n < p.N) {
-    if constexpr (EK == EF_F32_RES) {
+    if constexpr (EK == EF_F32_RES || EK == EF_F32R_BF16) {
       const uint4* s = reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(p.res) + (long)z * p.sc +
                                                       (long)m * p.ldr + n);
       in.v[it][0] = s[0];
       in.v[it][1] = s[1];
+    } else if constexpr (EK == EF_BF16_RES) {
+      in.v[it][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.res) + (long)z * p.sc +
+                                                    (long)m * p.ldr + n);
     } else if constexpr (EK == EF_BF16_ACTG) {
       in.v[it][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.pre) + (long)z * p.sc +
                                                     (long)m * p.ldc + n);
@@ -617,9 +624,10 @@ __device__ __forceinline__ void epi_load_all(const GemmP& p, int z, int mbase, i
 template <int EK, int IT, int NTt, int CPW, int EPS, bool PRE = false>
 __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, int z, int mbase, int n0, int tid,
                                               const float (&b)[8], EpiIn<EK, IT>& in) {
-  static_assert(EK > EF_GENERIC && EK <= EF_BF16_SILU_MX, "fast epilogue kind");
+  static_assert(EK > EF_GENERIC && EK <= EF_F32R_BF16, "fast epilogue kind");
   constexpr bool CF32 = EK == EF_F32 || EK == EF_F32_RES, ACTG = EK == EF_BF16_ACTG, RD = EK == EF_BF16_RD;
-  constexpr bool RES = EK == EF_F32_RES, GEN = EK == EF_F32;   // GEN: the run-time options of EF_F32
+  constexpr bool RESB = EK == EF_BF16_RES;                      // bf16 residual operand
+  constexpr bool RES = EK == EF_F32_RES || RESB || EK == EF_F32R_BF16, GEN = EK == EF_F32;   // GEN: EF_F32's options
   constexpr bool MXO = EK == EF_BF16_SILU_MX;
   constexpr bool SILU = EK == EF_BF16_SILU || MXO, BIAS = EK == EF_BF16_BIAS || SILU || RES;
   constexpr bool DROP = SILU || ACTG || RES || GEN;
@@ -693,7 +701,11 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
           for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
         }
       }
-      if constexpr (RES) {
+      if constexpr (RESB) {
+        const bf16x8 r = __builtin_bit_cast(bf16x8, in.v[it][0]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
+      } else if constexpr (RES) {
         const float4 ra = __builtin_bit_cast(float4, in.v[it][0]), rb = __builtin_bit_cast(float4, in.v[it][1]);
         v[0] += ra.x; v[1] += ra.y; v[2] += ra.z; v[3] += ra.w; v[4] += rb.x; v[5] += rb.y; v[6] += rb.z; v[7] += rb.w;
       }
@@ -1827,6 +1839,8 @@ void ek_dispatch(int ek, F&& f) {
       case EF_BF16_RD: f(std::integral_constant<int, EF_BF16_RD>{}); return;
       case EF_F32: f(std::integral_constant<int, EF_F32>{}); return;
       case EF_F32_RES: f(std::integral_constant<int, EF_F32_RES>{}); return;
+      case EF_BF16_RES: f(std::integral_constant<int, EF_BF16_RES>{}); return;
+      case EF_F32R_BF16: f(std::integral_constant<int, EF_F32R_BF16>{}); return;
       case EF_BF16_SILU_MX: f(std::integral_constant<int, EF_BF16_SILU_MX>{}); return;
       default: break;
     }
@@ -1939,8 +1953,11 @@ int epi_fast_kind(const GemmP& p, int batch) {
   const bool f32 = p.dtc == CFM_F32, bf = p.dtc == CFM_BF16, silu = p.act == CFM_ACT_SILU;
   const bool a1 = p.alpha == 1.f, s1 = p.out_scale == 1.f;
   if (!f32 && !bf) return EF_GENERIC;
-  if (p.res)
-    return f32 && p.dtr == CFM_F32 && p.bias && a1 && !silu && !p.act_grad && !p.rd_out ? EF_F32_RES : EF_GENERIC;
+  if (p.res) {
+    if (!p.bias || !a1 || silu || p.act_grad || p.rd_out) return EF_GENERIC;
+    if (f32) return p.dtr == CFM_F32 ? EF_F32_RES : EF_GENERIC;
+    return p.dtr == CFM_BF16 ? EF_BF16_RES : p.dtr == CFM_F32 ? EF_F32R_BF16 : EF_GENERIC;
+  }
   if (p.act_grad)
     return bf && p.dtpre == CFM_BF16 && !p.bias && a1 && s1 && !silu && !p.rd_out ? EF_BF16_ACTG : EF_GENERIC;
   if (p.rd_out)

@@ -114,8 +114,8 @@ __device__ __forceinline__ void ln_store_mx(const LnMx& mx, long row, int D, int
   if (lane % LPB == 0) mx.s8[row * (D / 32) + lane / LPB] = (uint8_t)(127 - k);
 }
 
-template <int V, typename TY, bool MX = false>
-__global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, const float* __restrict__ gamma,
+template <int V, typename TY, bool MX = false, typename TX = float>
+__global__ __launch_bounds__(256) void ln_fwd_vec(const TX* __restrict__ x, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, TY* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
                                                   float eps, LnMx mx = {}) {
@@ -169,8 +169,8 @@ struct LnDrop {
   const uint64_t* salt;
 };
 
-template <int V, typename TDY>
-__global__ __launch_bounds__(256) void ln_bwd_vec(const TDY* __restrict__ dy, const float* __restrict__ x,
+template <int V, typename TDY, typename TX = float>
+__global__ __launch_bounds__(256) void ln_bwd_vec(const TDY* __restrict__ dy, const TX* __restrict__ x,
                                                   const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                   const float* __restrict__ rstd_in, const float* __restrict__ dres,
                                                   float* __restrict__ dx, float* __restrict__ ws, long M, LnDrop dr) {
@@ -244,8 +244,8 @@ template <int G> __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-template <int G, typename TY>
-__global__ __launch_bounds__(256) void ln_fwd_grp(const float* __restrict__ x, const float* __restrict__ gamma,
+template <int G, typename TY, typename TX = float>
+__global__ __launch_bounds__(256) void ln_fwd_grp(const TX* __restrict__ x, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, TY* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
                                                   int D, float eps) {
@@ -295,8 +295,8 @@ __global__ __launch_bounds__(256) void ln_fwd_grp(const float* __restrict__ x, c
   }
 }
 
-template <int G, typename TDY>
-__global__ __launch_bounds__(256) void ln_bwd_grp(const TDY* __restrict__ dy, const float* __restrict__ x,
+template <int G, typename TDY, typename TX = float>
+__global__ __launch_bounds__(256) void ln_bwd_grp(const TDY* __restrict__ dy, const TX* __restrict__ x,
                                                   const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                   const float* __restrict__ rstd_in, const float* __restrict__ dres,
                                                   float* __restrict__ dx, float* __restrict__ ws, long M, int D,
@@ -499,40 +499,52 @@ bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0;
 template <int V>
 bool ln_fwd_fast(const void* x, int dtx, const float* gamma, const float* beta, void* y, int dty, float* mean,
                  float* rstd, long M, int D, float eps, hipStream_t s, LnMx mx = {}) {
-  if (D != 64 * V || dtx != CFM_F32 || !aligned16(x) || !aligned16(y) || !aligned16(gamma) || !aligned16(beta))
+  // x: the fp32 residual stream, or bf16 (the bf16 mode's residual stream, conformer.py RES_BF16)
+  if (D != 64 * V || (dtx != CFM_F32 && dtx != CFM_BF16) || !aligned16(x) || !aligned16(y) || !aligned16(gamma) ||
+      !aligned16(beta))
     return false;
   dim3 g((unsigned)((M + 4 * LN_FWD_ROWS - 1) / (4 * LN_FWD_ROWS)));
-  if (mx.y8) {
-    if constexpr (V >= 4) {
-      if (dty != CFM_BF16) return false;
-      hipLaunchKernelGGL((ln_fwd_vec<V, bf16, true>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (bf16*)y, mean,
-                         rstd, M, eps, mx);
-      return true;
+  auto go = [&](auto xt) {
+    typedef decltype(xt) TX;
+    if (mx.y8) {
+      if constexpr (V >= 4) {
+        if (dty != CFM_BF16) return false;
+        hipLaunchKernelGGL((ln_fwd_vec<V, bf16, true, TX>), g, dim3(256), 0, s, (const TX*)x, gamma, beta, (bf16*)y,
+                           mean, rstd, M, eps, mx);
+        return true;
+      }
+      return false;
     }
-    return false;
-  }
-  if (dty == CFM_BF16)
-    hipLaunchKernelGGL((ln_fwd_vec<V, bf16>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (bf16*)y, mean, rstd, M,
-                       eps);
-  else
-    hipLaunchKernelGGL((ln_fwd_vec<V, float>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (float*)y, mean, rstd,
-                       M, eps);
-  return true;
+    if (dty == CFM_BF16)
+      hipLaunchKernelGGL((ln_fwd_vec<V, bf16, false, TX>), g, dim3(256), 0, s, (const TX*)x, gamma, beta, (bf16*)y, mean,
+                         rstd, M, eps, LnMx{});
+    else
+      hipLaunchKernelGGL((ln_fwd_vec<V, float, false, TX>), g, dim3(256), 0, s, (const TX*)x, gamma, beta, (float*)y,
+                         mean, rstd, M, eps, LnMx{});
+    return true;
+  };
+  return dtx == CFM_BF16 ? go(bf16{}) : go(float{});
 }
 
 template <int V>
 bool ln_bwd_fast(const void* dy, int dtdy, const void* x, int dtx, const float* gamma, const float* mean,
                  const float* rstd, const void* dres, int dtres, void* dx, int dtdx, float* ws, long M, int D, int nb,
                  hipStream_t s, LnDrop dr) {
-  if (D != 64 * V || dtx != CFM_F32 || dtdx != CFM_F32 || (dres && dtres != CFM_F32)) return false;
+  if (D != 64 * V || (dtx != CFM_F32 && dtx != CFM_BF16) || dtdx != CFM_F32 || (dres && dtres != CFM_F32))
+    return false;
   if (!aligned16(dy) || !aligned16(x) || !aligned16(dres) || !aligned16(dx) || !aligned16(gamma)) return false;
   if (dr.g2 && (V != 8 || !aligned16(dr.g2))) return false;
-  if (dtdy == CFM_BF16)
-    hipLaunchKernelGGL((ln_bwd_vec<V, bf16>), dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const float*)x, gamma, mean,
-                       rstd, (const float*)dres, (float*)dx, ws, M, dr);
-  else
-    hipLaunchKernelGGL((ln_bwd_vec<V, float>), dim3(nb), dim3(256), 0, s, (const float*)dy, (const float*)x, gamma,
-                       mean, rstd, (const float*)dres, (float*)dx, ws, M, dr);
+  auto go = [&](auto xt) {
+    typedef decltype(xt) TX;
+    if (dtdy == CFM_BF16)
+      hipLaunchKernelGGL((ln_bwd_vec<V, bf16, TX>), dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const TX*)x, gamma,
+                         mean, rstd, (const float*)dres, (float*)dx, ws, M, dr);
+    else
+      hipLaunchKernelGGL((ln_bwd_vec<V, float, TX>), dim3(nb), dim3(256), 0, s, (const float*)dy, (const TX*)x, gamma,
+                         mean, rstd, (const float*)dres, (float*)dx, ws, M, dr);
+  };
+  if (dtx == CFM_BF16) go(bf16{});
+  else go(float{});
   return true;
 }
 // D % 8 == 0 widths below 512 that are not 64 * V: the lane-group kernels (G = next power of two >= D / 8)
@@ -545,19 +557,24 @@ int ln_group(int D) {
 bool ln_fwd_grouped(const void* x, int dtx, const float* gamma, const float* beta, void* y, int dty, float* mean,
                     float* rstd, long M, int D, float eps, hipStream_t s) {
   const int G = ln_group(D);
-  if (!G || dtx != CFM_F32 || (dty != CFM_F32 && dty != CFM_BF16) || !aligned16(x) || !aligned16(y) ||
-      !aligned16(gamma) || !aligned16(beta))
+  if (!G || (dtx != CFM_F32 && dtx != CFM_BF16) || (dty != CFM_F32 && dty != CFM_BF16) || !aligned16(x) ||
+      !aligned16(y) || !aligned16(gamma) || !aligned16(beta))
     return false;
   const long rows_per_block = 4L * (64 / G) * LN_FWD_ROWS;
   const dim3 g((unsigned)((M + rows_per_block - 1) / rows_per_block));
   auto go = [&](auto gt) {
     constexpr int GG = decltype(gt)::value;
-    if (dty == CFM_BF16)
-      hipLaunchKernelGGL((ln_fwd_grp<GG, bf16>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (bf16*)y, mean,
-                         rstd, M, D, eps);
-    else
-      hipLaunchKernelGGL((ln_fwd_grp<GG, float>), g, dim3(256), 0, s, (const float*)x, gamma, beta, (float*)y, mean,
-                         rstd, M, D, eps);
+    auto go2 = [&](auto xt) {
+      typedef decltype(xt) TX;
+      if (dty == CFM_BF16)
+        hipLaunchKernelGGL((ln_fwd_grp<GG, bf16, TX>), g, dim3(256), 0, s, (const TX*)x, gamma, beta, (bf16*)y, mean,
+                           rstd, M, D, eps);
+      else
+        hipLaunchKernelGGL((ln_fwd_grp<GG, float, TX>), g, dim3(256), 0, s, (const TX*)x, gamma, beta, (float*)y,
+                           mean, rstd, M, D, eps);
+    };
+    if (dtx == CFM_BF16) go2(bf16{});
+    else go2(float{});
   };
   if (G == 16) go(std::integral_constant<int, 16>{});
   else if (G == 32) go(std::integral_constant<int, 32>{});
@@ -569,18 +586,23 @@ bool ln_bwd_grouped(const void* dy, int dtdy, const void* x, int dtx, const floa
                     const float* rstd, const void* dres, int dtres, void* dx, int dtdx, float* ws, long M, int D,
                     int nb, hipStream_t s, LnDrop dr) {
   const int G = ln_group(D);
-  if (!G || dtx != CFM_F32 || dtdx != CFM_F32 || (dres && dtres != CFM_F32)) return false;
+  if (!G || (dtx != CFM_F32 && dtx != CFM_BF16) || dtdx != CFM_F32 || (dres && dtres != CFM_F32)) return false;
   if (dtdy != CFM_BF16 && dtdy != CFM_F32) return false;
   if (!aligned16(dy) || !aligned16(x) || !aligned16(dres) || !aligned16(dx) || !aligned16(gamma)) return false;
   if (dr.g2 && !aligned16(dr.g2)) return false;
   auto go = [&](auto gt) {
     constexpr int GG = decltype(gt)::value;
-    if (dtdy == CFM_BF16)
-      hipLaunchKernelGGL((ln_bwd_grp<GG, bf16>), dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const float*)x, gamma,
-                         mean, rstd, (const float*)dres, (float*)dx, ws, M, D, dr);
-    else
-      hipLaunchKernelGGL((ln_bwd_grp<GG, float>), dim3(nb), dim3(256), 0, s, (const float*)dy, (const float*)x, gamma,
-                         mean, rstd, (const float*)dres, (float*)dx, ws, M, D, dr);
+    auto go2 = [&](auto xt) {
+      typedef decltype(xt) TX;
+      if (dtdy == CFM_BF16)
+        hipLaunchKernelGGL((ln_bwd_grp<GG, bf16, TX>), dim3(nb), dim3(256), 0, s, (const bf16*)dy, (const TX*)x, gamma,
+                           mean, rstd, (const float*)dres, (float*)dx, ws, M, D, dr);
+      else
+        hipLaunchKernelGGL((ln_bwd_grp<GG, float, TX>), dim3(nb), dim3(256), 0, s, (const float*)dy, (const TX*)x,
+                           gamma, mean, rstd, (const float*)dres, (float*)dx, ws, M, D, dr);
+    };
+    if (dtx == CFM_BF16) go2(bf16{});
+    else go2(float{});
   };
   if (G == 16) go(std::integral_constant<int, 16>{});
   else if (G == 32) go(std::integral_constant<int, 32>{});
@@ -606,19 +628,25 @@ CFM_EXPORT int cfm_layernorm_fwd(const void* x, int dtx, const float* gamma, con
   return cfm::check_launch("cfm_layernorm_fwd");
 }
 
-CFM_EXPORT int cfm_layernorm_fwd_mx(const float* x, const float* gamma, const float* beta, void* y, void* y8,
-                                    uint8_t* s8, float* mean, float* rstd, long M, int D, float eps, void* stream) {
+CFM_EXPORT int cfm_layernorm_fwd_mx_ex(const void* x, int dtx, const float* gamma, const float* beta, void* y, void* y8,
+                                       uint8_t* s8, float* mean, float* rstd, long M, int D, float eps, void* stream) {
   CFM_REQUIRE(x && gamma && beta && y && y8 && s8 && mean && rstd, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE(dtx == CFM_F32 || dtx == CFM_BF16, CFM_ERR_DTYPE, "x: f32 or bf16");
   CFM_REQUIRE((D == 256 || D == 512 || D == 1024) && M >= 0, CFM_ERR_SHAPE, "D in {256, 512, 1024}");
   CFM_REQUIRE((uintptr_t)y8 % 8 == 0, CFM_ERR_ALIGN, "8-B aligned y8");
   if (M == 0) return CFM_OK;
   hipStream_t s = cfm::as_stream(stream);
   const LnMx mx{(uint8_t*)y8, s8};
-  const bool ok = ln_fwd_fast<4>(x, CFM_F32, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx) ||
-                  ln_fwd_fast<8>(x, CFM_F32, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx) ||
-                  ln_fwd_fast<16>(x, CFM_F32, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx);
+  const bool ok = ln_fwd_fast<4>(x, dtx, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx) ||
+                  ln_fwd_fast<8>(x, dtx, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx) ||
+                  ln_fwd_fast<16>(x, dtx, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx);
   CFM_REQUIRE(ok, CFM_ERR_ALIGN, "16-B aligned x / y / gamma / beta");
   return cfm::check_launch("cfm_layernorm_fwd_mx");
+}
+
+CFM_EXPORT int cfm_layernorm_fwd_mx(const float* x, const float* gamma, const float* beta, void* y, void* y8,
+                                    uint8_t* s8, float* mean, float* rstd, long M, int D, float eps, void* stream) {
+  return cfm_layernorm_fwd_mx_ex(x, CFM_F32, gamma, beta, y, y8, s8, mean, rstd, M, D, eps, stream);
 }
 
 CFM_EXPORT size_t cfm_layernorm_ws_bytes(long M, int D) {

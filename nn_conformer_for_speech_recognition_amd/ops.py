@@ -560,8 +560,8 @@ def layernorm_fwd_mx(x, gamma, beta, eps=1e-5):
     s8 = torch.empty(M, D // 32, device=x.device, dtype=torch.uint8)
     mean = torch.empty(M, device=x.device, dtype=torch.float32)
     rstd = torch.empty(M, device=x.device, dtype=torch.float32)
-    L.call("cfm_layernorm_fwd_mx", L.ptr(x), L.ptr(gamma), L.ptr(beta), L.ptr(y), L.ptr(y8), L.ptr(s8), L.ptr(mean),
-           L.ptr(rstd), M, D, float(eps), L.stream())
+    L.call("cfm_layernorm_fwd_mx_ex", L.ptr(x), L.dt(x), L.ptr(gamma), L.ptr(beta), L.ptr(y), L.ptr(y8), L.ptr(s8),
+           L.ptr(mean), L.ptr(rstd), M, D, float(eps), L.stream())
     return y, (y8, s8), mean, rstd
 
 

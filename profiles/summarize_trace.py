@@ -10,6 +10,7 @@ per step).  Family figures are the mean durations (End - Start, the kernel trace
 UNBRACKETED dispatches in the K timed replays, i.e. in the timed graph that carries no probe kernels:
 * wgrad  -- the grouped weight-gradient launch (gemm_pipe_kernel<256, 32, 4, 1, ...> + its split-slab reduction);
 * ffn_up -- the FFN up-projection forward (gemm_pipe_kernel<256, 32, 3, 2, ...>, the bracketed signature only);
+* fp8    -- the fp8 (MX e4m3) forward GEMMs of a --fp8 run (gemm_pipe_kernel<..., F8 = true, ...>);
 * dwide  -- every other bracketed signature (the d-wide GEMM family of bench.py's `roofline`).
 Also written: every signature's launches per timed step and mean duration, and the timed steps' kernel time."""
 import argparse
@@ -67,10 +68,18 @@ while i < len(disp):
             d["bracketed"] = True
         groups.append(tuple(d["sig"] for d in disp[i + 1:j]))
     i = j + 1
-fam_groups = {"wgrad": set(), "ffn_up": set(), "dwide": set()}
+def is_f8(name):
+    """gemm_pipe_kernel's 11th template argument is F8 (fp8 e4m3 operands, the --fp8 forward GEMMs)."""
+    if "gemm_pipe_kernel<" not in name:
+        return False
+    args = name.split("gemm_pipe_kernel<", 1)[1].split(">", 1)[0].split(", ")
+    return len(args) > 10 and args[10] == "true"
+
+
+fam_groups = {"wgrad": set(), "ffn_up": set(), "dwide": set(), "fp8": set()}
 for g in groups:
     n = g[0][0]
-    fam_groups["wgrad" if WGRAD in n else "ffn_up" if FFNUP in n else "dwide"].add(g)
+    fam_groups["wgrad" if WGRAD in n else "fp8" if is_f8(n) else "ffn_up" if FFNUP in n else "dwide"].add(g)
 t0, t1 = a.warmup + 1, a.warmup + 1 + a.steps          # timed replays: steps [t0, t1)
 timed = [d for d in disp if t0 <= d["step"] < t1 and not d["bracketed"] and PROBE not in d["name"]]
 if not timed:

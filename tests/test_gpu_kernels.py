@@ -653,3 +653,58 @@ def test_gemm_k_tail_pipeline(gemm_mode, M, N, K):
         assert _rel(yr, res.double() + 0.5 * (ref + b.double())) < 1e-5, mode
         assert _rel(yb.float(), ref) < 5e-3, mode
     assert _rel(outs[3][0], outs[1][0]) < 1e-5
+
+
+@pytest.mark.parametrize("D", [512, 144, 256, 100])
+def test_layernorm_bf16_residual_input(D):
+    """LayerNorm forward / backward reading a bf16 x (the bf16 mode's residual stream inside a layer, conformer.py
+    RES_BF16): against torch on the same bf16 values in fp32; the MX forward (fp8 mode) bit-identical to quant_mx of
+    its bf16 y."""
+    g = torch.Generator().manual_seed(D + 3)
+    M = 555
+    x = (torch.randn(M, D, generator=g) * 2 + 0.3).to(torch.bfloat16)
+    gamma = torch.rand(D, generator=g) + 0.5
+    beta = torch.randn(D, generator=g)
+    y, mean, rstd = ops.layernorm_fwd(x.to(DEV), gamma.to(DEV), beta.to(DEV), out_dtype=torch.bfloat16)
+    xr = x.float().clone().requires_grad_()
+    gr, br = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+    yr = torch.nn.functional.layer_norm(xr, (D,), gr, br, 1e-5)
+    assert _rel(y, yr) < 5e-3
+    dy = torch.randn(M, D, generator=g).to(torch.bfloat16)
+    dres = torch.randn(M, D, generator=g)
+    yr.backward(dy.float())
+    dx, dgamma, dbeta = ops.layernorm_bwd(dy.to(DEV), x.to(DEV), gamma.to(DEV), mean, rstd, dres=dres.to(DEV))
+    assert dx.dtype == torch.float32
+    assert _rel(dx, xr.grad + dres) < 1e-5
+    assert _rel(dgamma, gr.grad) < 1e-5 and _rel(dbeta, br.grad) < 1e-5
+    if D in (256, 512):
+        y2, (y8, s8), _, _ = ops.layernorm_fwd_mx(x.to(DEV), gamma.to(DEV), beta.to(DEV))
+        q8, qs = ops.quant_mx(y2)
+        torch.cuda.synchronize()
+        assert torch.equal(y2, y) and torch.equal(y8.view(torch.uint8), q8.view(torch.uint8)) and torch.equal(s8, qs)
+
+
+@pytest.mark.parametrize("res_dt,out_dt", [(torch.bfloat16, torch.bfloat16), (torch.float32, torch.bfloat16),
+                                           (torch.float32, torch.float32)])
+@pytest.mark.parametrize("M,N,K", [(11936, 512, 2048), (11936, 512, 512), (3000, 144, 576), (777, 256, 1024)])
+def test_gemm_residual_epilogue_dtypes(gemm_mode, res_dt, out_dt, M, N, K):
+    """The residual-add epilogue kinds (EF_F32_RES, EF_BF16_RES, EF_F32R_BF16): out = residual + out_scale *
+    dropout(x·wᵀ + b), bit-identical to the generic epilogue rows (cfm_gemm_set_mode bit 14) on the same main loop,
+    and within rounding of fp64."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV, res_dt)
+    outs = []
+    for mode in (3, 3 | 16384):
+        gemm_mode(mode)
+        y = torch.empty(M, N, device=DEV, dtype=out_dt)
+        ops.linear(x, w, b, out=y, drop_p=0.1, seed=11, out_scale=0.5, residual=res)
+        outs.append(y.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    y0 = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ops.linear(x, w, b, out=y0, out_scale=0.5, residual=res.float())   # no dropout: the fp64 check
+    ref = res.double() + 0.5 * (x.double() @ w.double().T + b.double())
+    assert _rel(y0, ref) < 1e-5
