@@ -12,6 +12,8 @@ Ops (SURVEY.md §3.3 block; the reference reaches them through torchaudio.models
   cfm::linear_silu / _bwd         y = dropout(silu(x·wᵀ + b)), pre-activation returned for the backward
   cfm::layer_norm / _bwd          (y, mean, rstd) over the last dim
   cfm::attention / _bwd           key-padding-masked multi-head attention core on packed [q|k|v] rows
+  cfm::attention_rel / _bwd       the same with Transformer-XL relative positions (projected table pos, biases u / v:
+                                  transformers modeling_wav2vec2_conformer.py:528-565, the rel-pos MFMA kernels)
   cfm::conv_glu_dwconv_bn_silu / _bwd   GLU -> depthwise Conv1d -> BatchNorm1d -> SiLU of the ConvModule
   cfm::ctc_loss / _bwd            per-utterance CTC negative log-likelihood (log-probs, batch-first)
 
@@ -238,6 +240,71 @@ def _attn_backward(ctx, go, _glse):
 attention.register_autograd(_attn_backward, setup_context=_attn_setup)
 
 
+# ----------------------------------------------------------------------------- relative-position attention
+@torch.library.custom_op("cfm::attention_rel", mutates_args=(), device_types="cuda")
+def attention_rel(qkv: Tensor, pos: Tensor, pos_u: Tensor, pos_v: Tensor, lengths: Tensor, B: int, T: int, H: int,
+                  drop_p: float, seed: int) -> tuple[Tensor, Tensor]:
+    """(o, lse) of relative-position attention: scores scale * ((q+u)·k_j + (q+v)·pos[T-1-i+j]); pos (2T-1, H*dk)
+    in qkv's dtype (the projected table linear_pos(pe)), pos_u / pos_v (H*dk,) fp32."""
+    dk = qkv.shape[1] // (3 * H)
+    return ops.attn_fwd(qkv.contiguous(), lengths.to(torch.int32).contiguous(), B, T, H, dk, pos.contiguous(),
+                        pos_u.float().contiguous(), pos_v.float().contiguous(), drop_p=drop_p, seed=seed)
+
+
+@attention_rel.register_fake
+def _(qkv, pos, pos_u, pos_v, lengths, B, T, H, drop_p, seed):
+    return qkv.new_empty(qkv.shape[0], qkv.shape[1] // 3), qkv.new_empty(B * H * T, dtype=torch.float32)
+
+
+@torch.library.custom_op("cfm::attention_rel_bwd", mutates_args=(), device_types="cuda")
+def attention_rel_bwd(qkv: Tensor, o: Tensor, do: Tensor, lse: Tensor, pos: Tensor, pos_u: Tensor, pos_v: Tensor,
+                      lengths: Tensor, B: int, T: int, H: int, drop_p: float, seed: int
+                      ) -> tuple[Tensor, Tensor, Tensor, Tensor]:
+    """(dqkv, dpos in pos's dtype, dpos_u, dpos_v fp32)."""
+    dk = qkv.shape[1] // (3 * H)
+    dpos_dt = torch.bfloat16 if pos.dtype == torch.bfloat16 else torch.float32
+    dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv.contiguous(), o.contiguous(), do.contiguous(), lse,
+                                        lengths.to(torch.int32).contiguous(), B, T, H, dk, pos.contiguous(),
+                                        pos_u.float().contiguous(), pos_v.float().contiguous(), drop_p=drop_p,
+                                        seed=seed, dpos_dtype=dpos_dt)
+    return dqkv, dpos.to(pos.dtype), dpu, dpv
+
+
+@attention_rel_bwd.register_fake
+def _(qkv, o, do, lse, pos, pos_u, pos_v, lengths, B, T, H, drop_p, seed):
+    return (qkv.new_empty(qkv.shape), pos.new_empty(pos.shape), pos_u.new_empty(pos_u.shape, dtype=torch.float32),
+            pos_v.new_empty(pos_v.shape, dtype=torch.float32))
+
+
+def _attn_rel_setup(ctx, inputs, output):
+    qkv, pos, pos_u, pos_v, lengths, B, T, H, drop_p, seed = inputs
+    ctx.save_for_backward(qkv, pos, pos_u, pos_v, lengths, output[0], output[1])
+    ctx.cfg = (B, T, H, drop_p, seed)
+
+
+def _attn_rel_backward(ctx, go, _glse):
+    qkv, pos, pos_u, pos_v, lengths, o, lse = ctx.saved_tensors
+    B, T, H, drop_p, seed = ctx.cfg
+    dqkv, dpos, dpu, dpv = torch.ops.cfm.attention_rel_bwd(qkv, o, go.to(qkv.dtype), lse, pos, pos_u, pos_v, lengths,
+                                                           B, T, H, drop_p, seed)
+    return dqkv, dpos, dpu.to(pos_u.dtype), dpv.to(pos_v.dtype), None, None, None, None, None, None
+
+
+attention_rel.register_autograd(_attn_rel_backward, setup_context=_attn_rel_setup)
+
+
+def _rel_table(T, d, device, dtype):
+    """The (2T-1, d) sinusoid of conformer.rel_pos_table (the same host ops, so the same values), as traceable
+    torch ops, cast to the compute dtype."""
+    import math
+    pos = torch.arange(T - 1, -T, -1, dtype=torch.int64).float().unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2, dtype=torch.int64).float() * -(math.log(10000.0) / d))
+    pe = torch.zeros(2 * T - 1, d)
+    pe[:, 0::2] = torch.sin(pos * div)
+    pe[:, 1::2] = torch.cos(pos * div)
+    return pe.to(device=device, dtype=dtype)
+
+
 # ----------------------------------------------------------------------------- ConvModule middle
 @torch.library.custom_op("cfm::conv_glu_dwconv_bn_silu", mutates_args=(), device_types="cuda")
 def conv_glu_dwconv_bn_silu(a: Tensor, w_dw: Tensor, b_dw: Tensor, gamma: Tensor, beta: Tensor,
@@ -372,11 +439,11 @@ ctc_loss.register_autograd(_ctc_backward, setup_context=_ctc_setup)
 def layer_forward(layer, x, lens, B, T, cd, seed):
     """torchaudio ConformerLayer.forward on x (B*T, d) fp32 token-major, composed of
     torch.ops.cfm.* so FakeTensor / AOTAutograd / torch.compile(fullgraph=True) trace it.  Same kernels,
-    seeds and dropout placement as the fused node in conformer.py (rel-pos attention stays there)."""
-    if layer.pos_enc != "none":
-        raise NotImplementedError("the traced (torch.ops.cfm) layer covers pos_enc='none'; rel-pos runs eager")
+    seeds and dropout placement as the fused node in conformer.py; pos_enc='rel' projects the positional table per
+    layer (cfm::linear, dW_pos through its backward) and runs cfm::attention_rel."""
     cfm = torch.ops.cfm
     P = layer.params()
+    R = P[30:]            # rel-pos: linear_pos.weight, pos_bias_u, pos_bias_v (conformer._REL_PNAMES)
     p = float(layer.dropout) if layer.training else 0.0
     d, H, K = layer.d, layer.H, layer.K
     f32 = torch.float32
@@ -389,7 +456,11 @@ def layer_forward(layer, x, lens, B, T, cd, seed):
     def mha(x, s):
         xn, _, _ = cfm.layer_norm(x, P[6], P[7], _EPS, cd)
         qkv = cfm.linear(xn, P[8], P[9], None, 0.0, 0, 1.0, cd)
-        o, _ = cfm.attention(qkv, lens, B, T, H, p, s)
+        if layer.pos_enc == "rel":
+            pos = cfm.linear(_rel_table(T, d, x.device, cd), R[0], None, None, 0.0, 0, 1.0, cd)
+            o, _ = cfm.attention_rel(qkv, pos, R[1].reshape(-1), R[2].reshape(-1), lens, B, T, H, p, s)
+        else:
+            o, _ = cfm.attention(qkv, lens, B, T, H, p, s)
         return cfm.linear(o, P[10], P[11], x, p, s + 1, 1.0, f32)
 
     def conv(x, s):

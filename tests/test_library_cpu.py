@@ -8,8 +8,8 @@ import nn_conformer_for_speech_recognition_amd  # noqa: F401  (registers the ops
 from nn_conformer_for_speech_recognition_amd.conformer import Conformer
 
 OPS = ["gemm", "linear", "linear_bwd", "linear_silu", "linear_silu_bwd", "layer_norm", "layer_norm_bwd",
-       "attention", "attention_bwd", "conv_glu_dwconv_bn_silu", "conv_glu_dwconv_bn_silu_bwd", "ctc_loss",
-       "ctc_loss_bwd"]
+       "attention", "attention_bwd", "attention_rel", "attention_rel_bwd", "conv_glu_dwconv_bn_silu",
+       "conv_glu_dwconv_bn_silu_bwd", "ctc_loss", "ctc_loss_bwd"]
 M = "meta"
 
 
@@ -89,6 +89,34 @@ def test_encoder_compiles_fullgraph_on_meta(conv_first):
     assert x.grad is not None and all(p.grad is not None for p in model.parameters())
     for op in ("linear", "linear_silu", "layer_norm", "attention", "conv_glu_dwconv_bn_silu"):
         assert f"cfm.{op}.default" in seen and f"cfm.{op}_bwd.default" in seen, op
+
+
+def test_rel_encoder_compiles_fullgraph_on_meta():
+    """pos_enc='rel' (BASELINE configs[4]'s arithmetic) on the torch.ops route: the per-layer table projection
+    (cfm::linear) and cfm::attention_rel with its registered backward, traced fullgraph on meta tensors."""
+    seen = []
+
+    def backend(gm, example_inputs):
+        from functorch.compile import make_boxed_func
+        from torch._dynamo.backends.common import aot_autograd
+
+        def keep(g, _):
+            seen.extend(str(n.target) for n in g.graph.nodes if n.op == "call_function")
+            return make_boxed_func(g.forward)
+        return aot_autograd(fw_compiler=keep, bw_compiler=keep)(gm, example_inputs)
+
+    B, T, d = 2, 19, 64
+    with torch.device(M):
+        model = Conformer(d, 4, 128, 2, 31, dropout=0.1, pos_enc="rel")
+        x = torch.randn(B * T, d, requires_grad=True)
+        lens = torch.full((B,), T, dtype=torch.int32)
+    torch._dynamo.reset()
+    y = torch.compile(model.forward_tokens, fullgraph=True, backend=backend)(x, lens, B, T, 123)
+    y.sum().backward()
+    assert y.shape == (B * T, d)
+    assert all(p.grad is not None for p in model.parameters())
+    assert "cfm.attention_rel.default" in seen and "cfm.attention_rel_bwd.default" in seen
+    assert "cfm.attention.default" not in seen
 
 
 def test_compiled_route_refuses_repeated_dropout_masks():
