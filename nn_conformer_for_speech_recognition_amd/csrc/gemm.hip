@@ -782,6 +782,12 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
   // (one pass per band chunk; not unrolled -- the epilogue body is large and nothing in it is indexed by hf)
 #pragma nounroll
   for (int hf = 0; hf < WM / CHB; ++hf) {
+    // fast kinds with a per-row global input (pre-activation, residual, rowdot operand): every row of this pass is
+    // issued here, before the accumulators are staged -- the loads' latency hides under the staging and its barrier
+    // (issued two rows ahead of the stores instead, the FFN-down data gradient's pre-activation reads exposed ~4
+    // round trips per pass)
+    EpiIn<EK == EF_GENERIC ? EF_BF16 : EK, RC * CPW / NTt> ein;
+    if constexpr (EK != EF_GENERIC) epi_load_all<EK, RC * CPW / NTt, NTt, CPW>(p, z, m0 + RC * hf, n0, tid, ein);
     if (wm / CHB == hf) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -797,8 +803,7 @@ __device__ __forceinline__ void tile_epilogue_g(const GemmP& p, f32x16 (&acc)[FM
     __syncthreads();
     static_assert((RC * CPW) % NTt == 0 && NTt % CPW == 0, "whole rows per pass");
     if constexpr (EK != EF_GENERIC) {
-      EpiIn<EK, RC * CPW / NTt> ein;
-      epi_rows_fast<EK, RC * CPW / NTt, NTt, CPW, EPS>(p, st, z, m0 + RC * hf, n0, tid, bias8, ein);
+      epi_rows_fast<EK, RC * CPW / NTt, NTt, CPW, EPS, true>(p, st, z, m0 + RC * hf, n0, tid, bias8, ein);
       if (hf + 1 < WM / CHB) __syncthreads();
       continue;
     }
