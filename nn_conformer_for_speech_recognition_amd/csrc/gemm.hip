@@ -1883,6 +1883,15 @@ void launch_pipe_t(const GemmP& p, const PipeOp& oa, const PipeOp& ob, int batch
         // warp-specialised loading (cfm_gemm_set_mode bit 19 keeps the shared-DMA kernel below for A/B): d-wide
         // layer family 266.6 -> 240.2 us same box (gpurun_out r04b dgemm; 4 compute waves of 96 x 64: 244.4 us)
         if (!(g_gemm_mode & 524288) && p.split_k == 1) {
+          // outputs narrow enough that 192-row tiles leave most CUs idle (Conformer-M's d = 256: 63 x 2 = 126 tiles
+          // for 256 CUs) take 96-row tiles -- 125 x 2 = 250, one round (cfm_gemm_set_mode bit 23 keeps 192, A/B)
+          if ((long)g192.x * g192.y * g192.z * 5 <= (long)num_cus() * 3 && !(g_gemm_mode & 8388608)) {
+            const dim3 g96(cdiv(p.N, BN), cdiv(p.M, 96), batch * p.split_k);
+            ek_dispatch<true>(p.efast, [&](auto ek) {
+              hipLaunchKernelGGL((gemm_ws_kernel<96, 2, 4, 4, 4, decltype(ek)::value>), g96, dim3(768), 0, s, p, oa, ob);
+            });
+            return;
+          }
           ek_dispatch<true>(p.efast, [&](auto ek) {
             hipLaunchKernelGGL((gemm_ws_kernel<192, 2, 4, 4, 4, decltype(ek)::value>), g192, dim3(768), 0, s, p, oa, ob);
           });

@@ -708,3 +708,31 @@ def test_gemm_residual_epilogue_dtypes(gemm_mode, res_dt, out_dt, M, N, K):
     ops.linear(x, w, b, out=y0, out_scale=0.5, residual=res.float())   # no dropout: the fp64 check
     ref = res.double() + 0.5 * (x.double() @ w.double().T + b.double())
     assert _rel(y0, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,K", [(11936, 1024), (11936, 256), (1000, 768)])
+@pytest.mark.parametrize("res", [False, True])
+def test_gemm_ws96_narrow_outputs(gemm_mode, M, K, res):
+    """256-wide outputs (Conformer-M's d) on the 96-row warp-specialised tiles (250 tiles at M 11,936 where 192-row
+    tiles give 126) against the 192-row warp-specialised kernel (cfm_gemm_set_mode bit 23): the same 16x16x32 MFMAs
+    in the same k order and the same epilogue -> bit-identical, bf16 data-gradient and fp32 residual epilogues."""
+    N = 256
+    g = torch.Generator().manual_seed(M + K + res)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    r = torch.randn(M, N, generator=g).to(DEV)
+    outs = []
+    for mode in (3, 3 | 8388608):
+        gemm_mode(mode)
+        if res:
+            y = torch.empty(M, N, device=DEV, dtype=torch.float32)
+            ops.linear(x, w, b, out=y, drop_p=0.1, seed=5, out_scale=0.5, residual=r)
+        else:
+            y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(x, w, y, M, N, K)
+        outs.append(y.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    if not res:
+        assert _rel(outs[0].float(), x.double() @ w.double().T) < 5e-3
