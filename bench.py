@@ -199,6 +199,10 @@ def gemm_desc_bytes(desc):
     n = ea * (desc.M * desc.K * bt + desc.N * desc.K * b_batches) + ec * desc.M * desc.N * bt
     if desc.residual:
         n += _ELT[int(desc.dtype_r)] * desc.M * desc.N * bt
+    if desc.mx_a:      # MX fp8: the e8m0 block scales of A and B (one byte per 32 K-elements of a row)
+        n += (desc.M * bt + desc.N * b_batches) * (desc.K // 32)
+    if desc.mx_out:    # the FFN-up epilogue's MX e4m3 copy of its output (+ its block scales)
+        n += desc.M * desc.N * bt + desc.M * (desc.N // 32) * bt
     return float(n)
 
 
@@ -923,7 +927,7 @@ def main():
             e["live_over_trace"] = round(ms_live / tr[0], 4)
             e["trace_source"] = tr[2] + " (rocprofv3 --kernel-trace of a bench.py run of this config: the family's "\
                                         "mean dispatch duration over the timed graph replays)"
-        for rnd in ("r05", "r04", "r03", "r02"):
+        for rnd in ("r06", "r05", "r04", "r03", "r02"):
             path = os.path.join(REPO, "profiles", rnd, pmc_file)
             if not os.path.exists(path):
                 continue

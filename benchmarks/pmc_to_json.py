@@ -4,7 +4,9 @@ entries read (matched on shape_key and the kernel name recorded here).
 
 HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> B): on gfx950 FETCH_SIZE counts half the bytes
 of 16-B-per-lane streaming reads, WRITE_SIZE is exact for 16-B stores (MI355X_MICROARCH.md §HBM).
-usage: python pmc_to_json.py DIR PREFIX KERNEL_FILTER OUT_NAME COMMAND [ALGORITHMIC_BYTES_PER_LAUNCH]"""
+usage: python pmc_to_json.py DIR PREFIX KERNEL_FILTER OUT_NAME COMMAND [ALGORITHMIC_BYTES_PER_LAUNCH]
+env PMC_AGG=mean: per-dispatch MEANS instead of medians (a family of several shapes, whose algorithmic bytes are a
+mean per launch); env PMC_SHAPE="M,d,ffn,L": the bench config's shape key (default L15's)."""
 import csv
 import json
 import os
@@ -20,7 +22,8 @@ def medians(tag):
     by = {}
     for r in rows:
         by.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    return {k: statistics.median(v) for k, v in by.items()}, (rows[0]["Kernel_Name"] if rows else "?"), \
+    agg = statistics.mean if os.environ.get("PMC_AGG") == "mean" else statistics.median
+    return {k: agg(v) for k, v in by.items()}, (rows[0]["Kernel_Name"] if rows else "?"), \
         len({r.get("Dispatch_Id", i) for i, r in enumerate(rows)})
 
 
@@ -29,7 +32,9 @@ write, _, nw = medians("write")
 mfma, _, nm = medians("mfma")
 rec = {
     "kernel": kname,
-    "shape_key": [32 * 373, 512, 2048, 17],       # M tokens, d, ffn, layers (bench.py L15)
+    "shape_key": [int(v) for v in os.environ["PMC_SHAPE"].split(",")] if os.environ.get("PMC_SHAPE") else
+                 [32 * 373, 512, 2048, 17],       # M tokens, d, ffn, layers (bench.py L15)
+    "aggregate": os.environ.get("PMC_AGG", "median"),
     "FETCH_SIZE_KiB_median": fetch.get("FETCH_SIZE"), "WRITE_SIZE_KiB_median": write.get("WRITE_SIZE"),
     "dispatches": {"fetch": nf, "write": nw, "mfma": nm},
     "SQ_INSTS_MFMA_median": mfma.get("SQ_INSTS_MFMA"),

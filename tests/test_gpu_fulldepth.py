@@ -79,10 +79,12 @@ CASES = [   # (stack, pos_enc, T_enc, lengths): every benchmarked stack at T 94 
     # round 6: Conformer-S / -M at the S15 / M15 length T 373 (dk 36 / 64 on the split whole-head attention kernels,
     # d 144 on the 64 x 160 GEMM tiles, the K-tail pipeline and the lane-group LayerNorm)
     ("S16", "none", 373, [373, 301]), ("M16", "none", 373, [373, 301]),
+    # L60's batch shape at depth: two ragged 60 s utterances (B 2) with relative positions
+    ("L17", "rel", 1498, [1498, 1203]),
 ]
 
 
-@pytest.mark.parametrize("stack,pos,T,lens", CASES, ids=[f"{c[0]}-{c[1]}-T{c[2]}" for c in CASES])
+@pytest.mark.parametrize("stack,pos,T,lens", CASES, ids=[f"{c[0]}-{c[1]}-T{c[2]}-B{len(c[3])}" for c in CASES])
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
 def test_full_depth_encoder_vs_oracle(stack, pos, cd, T, lens):
     """Every layer of the benchmarked stack, fwd + bwd, ragged lengths.  The rel-pos biases' gradients (u, v: a sum
@@ -110,8 +112,14 @@ def test_full_depth_encoder_vs_oracle(stack, pos, cd, T, lens):
     eg = {n: e for n, e in eg.items() if "pos_bias" not in n}
     worst = max(eg, key=eg.get)
     eb = max(rel_err(b1, b2) for (n, b1), (_, b2) in zip(m.named_buffers(), ref.named_buffers()) if "running" in n)
-    _report(f"encoder {stack} {pos} {str(cd)[6:]} T{T}", y=ey, dx=ex, worst_grad=eg[worst], worst_param=worst,
-            median_grad=sorted(eg.values())[len(eg) // 2], bn_running=eb,
+    # the error's growth with depth: each layer's worst parameter gradient (layer 0 runs backward last)
+    per_layer = {}
+    for n, e in eg.items():
+        li = int(n.split(".")[1])
+        per_layer[li] = max(per_layer.get(li, 0.0), e)
+    _report(f"encoder {stack} {pos} {str(cd)[6:]} T{T} B{len(lens)}", y=ey, dx=ex, worst_grad=eg[worst],
+            worst_param=worst, median_grad=sorted(eg.values())[len(eg) // 2], bn_running=eb,
+            per_layer_worst_grad=[round(per_layer[i], 5) for i in sorted(per_layer)],
             **({"worst_pos_bias_grad": max(eu.values())} if eu else {}))
     ty, tx, tg = TOL[cd]
     assert ey < ty and ex < tx, (ey, ex)
