@@ -306,6 +306,15 @@ int cfm_layernorm_fwd_mx(const float* x, const float* gamma, const float* beta, 
 /* The same with x of dtype_x (CFM_F32 or CFM_BF16: the bf16 mode's bf16 residual stream). */
 int cfm_layernorm_fwd_mx_ex(const void* x, int dtype_x, const float* gamma, const float* beta, void* y, void* y8,
                             uint8_t* s8, float* mean, float* rstd, long M, int D, float eps, void* stream);
+/* The residual add of the module before a LayerNorm, done by the LayerNorm: xout = x + delta (fp32; delta of dtype_d,
+   CFM_BF16 -- the module's GEMM output with bias, dropout and out_scale, no residual -- or CFM_F32), then
+   y = LN(xout) as cfm_layernorm_fwd, and, with y8 / s8 non-null, y's MX copy as cfm_layernorm_fwd_mx.  Replaces the
+   residual-stream GEMM epilogue `x + out_scale * dropout(h W^T + b)` (torchaudio ConformerLayer, ffn / attention /
+   conv residual adds; asrnn.py:214) followed by the next module's LayerNorm.  xout must not alias x or
+   delta. */
+int cfm_layernorm_fwd_res(const float* x, const void* delta, int dtype_d, float* xout, const float* gamma,
+                          const float* beta, void* y, int dtype_y, void* y8, uint8_t* s8, float* mean, float* rstd,
+                          long M, int D, float eps, void* stream);
 size_t cfm_layernorm_ws_bytes(long M, int D);
 int cfm_layernorm_bwd(const void* dy, int dtype_dy, const void* x, int dtype_x, const float* gamma,
                       const float* mean, const float* rstd, const void* dres, int dtype_dres,

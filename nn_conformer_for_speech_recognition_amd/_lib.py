@@ -79,6 +79,8 @@ _SIGS = {
     "cfm_dequant_fp8": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     "cfm_layernorm_fwd_mx": (c_int, [c_void_p] * 8 + [c_long, c_int, c_float, c_void_p]),
     "cfm_layernorm_fwd_mx_ex": (c_int, [c_void_p, c_int] + [c_void_p] * 7 + [c_long, c_int, c_float, c_void_p]),
+    "cfm_layernorm_fwd_res": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_float, c_void_p]),
     "cfm_quant_mx": (c_int, [c_void_p, c_int, c_long, c_int, c_long, c_void_p, c_void_p, c_void_p]),
     "cfm_quant_mx_batch_blocks": (c_long, [c_long, c_int]),
     "cfm_quant_mx_batch": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p]),

@@ -106,12 +106,20 @@ REL_BATCH = os.environ.get("CFM_REL_BATCH", "1") != "0"
 # L60 31.68 -> 31.37 ms, while the 17-layer bf16 errors grow ~2.5x (y 0.6 -> 1.6 %, dx 0.9 -> 1.7 %, worst gradient
 # 1.6 -> 2.9 %; rel T 1498 unchanged at 3.6 %): below the 0.6 ms bar set for it, so the fp32 stream stays the default.
 RES_BF16 = os.environ.get("CFM_RES_BF16", "0") == "1"
+# CFM_RES_FUSE=1 (opt-in, bf16 compute, fp32 stream): each sub-module's residual GEMM writes its output without the
+# residual -- bf16 out_scale * dropout(h W^T + b), 2 B per element -- and the next LayerNorm forms x + delta (fp32, the
+# stream the backward reads) and normalises it in one pass (cfm_layernorm_fwd_res), instead of the fp32 residual
+# epilogue at the end of the GEMM.  Isolated, the GEMMs drop 6 / 5 us (K 2048 / 512) and the LayerNorm grows 2.8 us;
+# in the step (round 6, same box, profiles/r06/misc/res_fuse_ab.txt) the GEMMs drop only 28.9 -> 25.3 us while the
+# LayerNorms grow 8.4 -> 15.5 us: the unfused LayerNorm reads the stream the GEMM has just written from the Infinity
+# Cache, the fused one reads the older x.  L15 18.7 -> 19.0 ms, so the epilogue form stays the default.
+RES_FUSE = os.environ.get("CFM_RES_FUSE", "0") == "1"
 
 
 class _Cfg:
     __slots__ = ("B", "T", "d", "H", "ffn", "K", "p", "cd", "training", "conv_first", "rel", "seed",
                  "bn_rm", "bn_rv", "bn_mom", "pe", "shadow", "shadow_t", "group_wgrad", "layer_index",
-                 "grad_dest", "flush_here", "on_flushed", "on_routed", "sync_bn", "shadow8", "pos_pre", "rdt")
+                 "grad_dest", "flush_here", "on_flushed", "on_routed", "sync_bn", "shadow8", "pos_pre", "rdt", "rfuse")
 
 
 # the 2-D (and pointwise-conv) weight matrices of _PNAMES: cast to the compute dtype once per step
@@ -201,14 +209,27 @@ def _fp8_on(cfg, i, K):
     return bool(cfg.shadow8) and i in cfg.shadow8 and K % 128 == 0
 
 
-def _ln_fwd(x, P, i, cfg, fp8_w=None):
+def _ln_fwd(x, P, i, cfg, fp8_w=None, d=None):
     """the module-input LayerNorm; when the consumer GEMM (weight fp8_w) runs on MX fp8, the same kernel also
-    writes the MX copy of its bf16 output (cfm_layernorm_fwd_mx): -> (xn, (xn8, s8) or None, mu, rs)"""
-    if fp8_w is not None and FP8_MX and cfg.cd == torch.bfloat16 and _fp8_on(cfg, fp8_w, x.shape[1]):
+    writes the MX copy of its bf16 output (cfm_layernorm_fwd_mx).  d: the previous module's pending output (RES_FUSE)
+    -- the module input is then x + d, formed here.  -> (xn, (xn8, s8) or None, mu, rs, module input)"""
+    mx = fp8_w is not None and FP8_MX and cfg.cd == torch.bfloat16 and _fp8_on(cfg, fp8_w, x.shape[1])
+    if d is not None:
+        if mx:
+            x, xn, q, mu, rs = ops.layernorm_fwd_res(x, d, P[i], P[i + 1], _EPS, mx=True)
+            return xn, q, mu, rs, x
+        x, xn, mu, rs = ops.layernorm_fwd_res(x, d, P[i], P[i + 1], _EPS, out_dtype=cfg.cd)
+        return xn, None, mu, rs, x
+    if mx:
         xn, q, mu, rs = ops.layernorm_fwd_mx(x, P[i], P[i + 1], _EPS)
-        return xn, q, mu, rs
+        return xn, q, mu, rs, x
     xn, mu, rs = ops.layernorm_fwd(x, P[i], P[i + 1], _EPS, out_dtype=cfg.cd)
-    return xn, None, mu, rs
+    return xn, None, mu, rs, x
+
+
+def _res_kw(cfg, x):
+    """the residual GEMM's output arguments: the new stream (x + ...) or, under RES_FUSE, the bf16 module output"""
+    return {"out_dtype": torch.bfloat16} if cfg.rfuse else {"out_dtype": cfg.rdt, "residual": x}
 
 
 def _fp8_linear(x, cfg, i, xq=None, **kw):
@@ -226,9 +247,10 @@ def _fp8_linear(x, cfg, i, xq=None, **kw):
     return ops.linear(xq, wq, x_scale=sx, w_scale=sw, **kw)
 
 
-def _ffn_fwd(x, P, o, cfg, seed):
+def _ffn_fwd(x, P, o, cfg, seed, d=None):
+    """-> (the new stream, or the bf16 module output under RES_FUSE; saved tensors; the module input)"""
     cd = cfg.cd
-    xn, xq, mu, rs = _ln_fwd(x, P, o, cfg, o + 2)
+    xn, xq, mu, rs, x = _ln_fwd(x, P, o, cfg, o + 2, d)
     w1, w2 = _w(P[o + 2], cd), _w(P[o + 4], cd)
     pre = torch.empty(x.shape[0], cfg.ffn, device=x.device, dtype=cd)
     # MX fp8 for both FFN GEMMs: the up-projection's epilogue also writes the MX copy of h (the down GEMM's operand)
@@ -240,12 +262,12 @@ def _ffn_fwd(x, P, o, cfg, seed):
                     **({"mx_out": hq} if hq is not None else {}))
     if h is None:
         h = ops.linear(xn, w1, P[o + 3], act=ACT_SILU, pre=pre, drop_p=cfg.p, seed=seed)
-    y = _fp8_linear(h, cfg, o + 4, xq=hq, bias=P[o + 5], out_dtype=cfg.rdt, drop_p=cfg.p, seed=seed + 1,
-                    out_scale=0.5, residual=x)
+    y = _fp8_linear(h, cfg, o + 4, xq=hq, bias=P[o + 5], drop_p=cfg.p, seed=seed + 1, out_scale=0.5,
+                    **_res_kw(cfg, x))
     if y is None:
-        y = ops.linear(h, w2, P[o + 5], out_dtype=cfg.rdt, drop_p=cfg.p, seed=seed + 1, out_scale=0.5, residual=x)
+        y = ops.linear(h, w2, P[o + 5], drop_p=cfg.p, seed=seed + 1, out_scale=0.5, **_res_kw(cfg, x))
     _chk(f"ffn{o}_fwd", xn, mu, rs, pre, h, y)
-    return y, (xn, mu, rs, pre, h, w1, w2)
+    return y, (xn, mu, rs, pre, h, w1, w2), x
 
 
 def _in_drop(kind, cfg, seed):
@@ -285,10 +307,10 @@ def _ffn_bwd(g, x, sv, P, o, cfg, seed, grads, side, g2=None, nxt=None):
     return dx, g2n
 
 
-def _mha_fwd(x, P, R, cfg, seed, lens):
+def _mha_fwd(x, P, R, cfg, seed, lens, dprev=None):
     cd = cfg.cd
     B, T, d, H = cfg.B, cfg.T, cfg.d, cfg.H
-    xn, xq, mu, rs = _ln_fwd(x, P, 6, cfg, 8)
+    xn, xq, mu, rs, x = _ln_fwd(x, P, 6, cfg, 8, dprev)
     win, wout = _w(P[8], cd), _w(P[10], cd)
     qkv = _fp8_linear(xn, cfg, 8, xq=xq, bias=P[9])
     if qkv is None:
@@ -302,11 +324,11 @@ def _mha_fwd(x, P, R, cfg, seed, lens):
         pu = R[1].reshape(-1).float().contiguous()
         pv = R[2].reshape(-1).float().contiguous()
     o, lse = ops.attn_fwd(qkv, lens, B, T, H, d // H, pos, pu, pv, drop_p=cfg.p, seed=seed)
-    y = _fp8_linear(o, cfg, 10, bias=P[11], out_dtype=cfg.rdt, drop_p=cfg.p, seed=seed + 1, residual=x)
+    y = _fp8_linear(o, cfg, 10, bias=P[11], drop_p=cfg.p, seed=seed + 1, **_res_kw(cfg, x))
     if y is None:
-        y = ops.linear(o, wout, P[11], out_dtype=cfg.rdt, drop_p=cfg.p, seed=seed + 1, residual=x)
+        y = ops.linear(o, wout, P[11], drop_p=cfg.p, seed=seed + 1, **_res_kw(cfg, x))
     _chk("mha_fwd", xn, mu, rs, qkv, pos, o, lse, y)
-    return y, (xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv)
+    return y, (xn, mu, rs, qkv, o, lse, win, wout, pos, pu, pv), x
 
 
 def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=None):
@@ -349,10 +371,10 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
     return dx, g2n
 
 
-def _conv_fwd(x, P, cfg, seed):
+def _conv_fwd(x, P, cfg, seed, dprev=None):
     cd = cfg.cd
     B, T, d, K = cfg.B, cfg.T, cfg.d, cfg.K
-    xn, mu, rs = ops.layernorm_fwd(x, P[12], P[13], _EPS, out_dtype=cd)
+    xn, _, mu, rs, x = _ln_fwd(x, P, 12, cfg, None, dprev)
     wp1, wp2 = _w(P[14].view(2 * d, d), cd), _w(P[20].view(d, d), cd)
     wdw = P[16].view(d, K)
     a = ops.linear(xn, wp1, P[15])
@@ -364,9 +386,9 @@ def _conv_fwd(x, P, cfg, seed):
     else:
         z, bmean, binv = ops.bn_silu_fwd(yv, P[18], P[19], cfg.bn_rm, cfg.bn_rv, cfg.bn_mom, _EPS, cfg.training, B,
                                          T, d, ws, cd)
-    y = ops.linear(z, wp2, P[21], out_dtype=cfg.rdt, drop_p=cfg.p, seed=seed, residual=x)
+    y = ops.linear(z, wp2, P[21], drop_p=cfg.p, seed=seed, **_res_kw(cfg, x))
     _chk("conv_fwd", xn, mu, rs, a, yv, bmean, binv, z, y)
-    return y, (xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw)
+    return y, (xn, mu, rs, a, yv, z, bmean, binv, wp1, wp2, wdw), x
 
 
 def _conv_bwd(g, x, sv, P, cfg, seed, grads, side, g2=None, nxt=None):
@@ -416,19 +438,30 @@ class _ConformerLayerFn(torch.autograd.Function):
             cfg.shadow_t = cfg.shadow8 = None
         s = cfg.seed
         x0 = x
-        x1, sv1 = _ffn_fwd(x0, P, 0, cfg, s)
+        # each module returns its output (the new stream; under RES_FUSE the pending bf16 module output, added by the
+        # next LayerNorm) and its input, materialised by that LayerNorm -- the tensors the backward saves
+        y1, sv1, _ = _ffn_fwd(x0, P, 0, cfg, s)
+        step = (lambda xin, y: (xin, y)) if cfg.rfuse else (lambda xin, y: (y, None))
+        cur = step(x0, y1)
         if cfg.conv_first:
-            xc, svc = _conv_fwd(x1, P, cfg, s + 10)
-            xa, sva = _mha_fwd(xc, P, R, cfg, s + 20, lens)
+            yc, svc, x1 = _conv_fwd(cur[0], P, cfg, s + 10, cur[1])
+            cur = step(x1, yc)
+            ya, sva, xc = _mha_fwd(cur[0], P, R, cfg, s + 20, lens, cur[1])
+            cur = step(xc, ya)
             chain = (x1, xc)
-            x3 = xa
         else:
-            xa, sva = _mha_fwd(x1, P, R, cfg, s + 20, lens)
-            xc, svc = _conv_fwd(xa, P, cfg, s + 10)
+            ya, sva, x1 = _mha_fwd(cur[0], P, R, cfg, s + 20, lens, cur[1])
+            cur = step(x1, ya)
+            yc, svc, xa = _conv_fwd(cur[0], P, cfg, s + 10, cur[1])
+            cur = step(xa, yc)
             chain = (x1, xa)
-            x3 = xc
-        x4, sv4 = _ffn_fwd(x3, P, 22, cfg, s + 30)
-        out, mu5, rs5 = ops.layernorm_fwd(x4, P[28], P[29], _EPS, out_dtype=torch.float32)
+        y4, sv4, x3 = _ffn_fwd(cur[0], P, 22, cfg, s + 30, cur[1])
+        cur = step(x3, y4)
+        if cur[1] is not None:
+            x4, out, mu5, rs5 = ops.layernorm_fwd_res(cur[0], cur[1], P[28], P[29], _EPS, out_dtype=torch.float32)
+        else:
+            x4 = cur[0]
+            out, mu5, rs5 = ops.layernorm_fwd(x4, P[28], P[29], _EPS, out_dtype=torch.float32)
         _chk(f"layer{cfg.layer_index}_fwd_out", out, mu5, rs5)
         ctx.cfg = cfg
         ctx.sv = (sv1, sva, svc, sv4)
@@ -535,6 +568,7 @@ class ConformerLayer(nn.Module):
         cfg.p = float(self.dropout) if self.training else 0.0
         cfg.cd = compute_dtype
         cfg.rdt = torch.bfloat16 if (compute_dtype == torch.bfloat16 and RES_BF16) else torch.float32
+        cfg.rfuse = compute_dtype == torch.bfloat16 and RES_FUSE and not RES_BF16
         cfg.training = self.training
         cfg.conv_first = self.convolution_first
         cfg.rel = self.pos_enc == "rel"

@@ -542,9 +542,10 @@ template <bool M16> __device__ __forceinline__ int accc(int r, int lane) {
 // (bit-identical outputs).
 // residual-stream kinds: EF_F32_RES (fp32 residual in, fp32 out: the parity mode), EF_BF16_RES (bf16 in, bf16 out: the
 // bf16 mode's bf16 residual stream), EF_F32R_BF16 (fp32 in, bf16 out: a layer's first residual add, whose input is the
-// previous layer's fp32 LayerNorm output)
+// previous layer's fp32 LayerNorm output); EF_BF16_DELTA: a residual module's output without the residual (bias,
+// dropout, out_scale, bf16) -- the add happens in the next LayerNorm (cfm_layernorm_fwd_res)
 enum { EF_GENERIC = 0, EF_BF16 = 1, EF_BF16_BIAS = 2, EF_BF16_SILU = 3, EF_BF16_ACTG = 4, EF_BF16_RD = 5, EF_F32 = 6,
-       EF_F32_RES = 7, EF_BF16_SILU_MX = 8, EF_BF16_RES = 9, EF_F32R_BF16 = 10 };
+       EF_F32_RES = 7, EF_BF16_SILU_MX = 8, EF_BF16_RES = 9, EF_F32R_BF16 = 10, EF_BF16_DELTA = 11 };
 
 // e8m0 block exponent of an MX block (fp8.hip mx_k): the largest k with amax * 2^k <= 448
 __device__ __forceinline__ int epi_mx_k(float a) {
@@ -624,13 +625,13 @@ __device__ __forceinline__ void epi_load_all(const GemmP& p, int z, int mbase, i
 template <int EK, int IT, int NTt, int CPW, int EPS, bool PRE = false>
 __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, int z, int mbase, int n0, int tid,
                                               const float (&b)[8], EpiIn<EK, IT>& in) {
-  static_assert(EK > EF_GENERIC && EK <= EF_F32R_BF16, "fast epilogue kind");
+  static_assert(EK > EF_GENERIC && EK <= EF_BF16_DELTA, "fast epilogue kind");
   constexpr bool CF32 = EK == EF_F32 || EK == EF_F32_RES, ACTG = EK == EF_BF16_ACTG, RD = EK == EF_BF16_RD;
   constexpr bool RESB = EK == EF_BF16_RES;                      // bf16 residual operand
   constexpr bool RES = EK == EF_F32_RES || RESB || EK == EF_F32R_BF16, GEN = EK == EF_F32;   // GEN: EF_F32's options
-  constexpr bool MXO = EK == EF_BF16_SILU_MX;
-  constexpr bool SILU = EK == EF_BF16_SILU || MXO, BIAS = EK == EF_BF16_BIAS || SILU || RES;
-  constexpr bool DROP = SILU || ACTG || RES || GEN;
+  constexpr bool MXO = EK == EF_BF16_SILU_MX, DLT = EK == EF_BF16_DELTA;
+  constexpr bool SILU = EK == EF_BF16_SILU || MXO, BIAS = EK == EF_BF16_BIAS || SILU || RES || DLT;
+  constexpr bool DROP = SILU || ACTG || RES || GEN || DLT;
   constexpr int NW = epi_nw<EK>();
   constexpr int RPI = NTt / CPW;                       // rows per pass
   const int c8 = (tid % CPW) * 8, n = n0 + c8, r0 = tid / CPW;
@@ -692,7 +693,7 @@ __device__ __forceinline__ void epi_rows_fast(const GemmP& p, const float* st, i
           else drop8_fast<false>(v, j0, p);
         }
       }
-      if constexpr (RES) {   // (unconditional: x * 1.0f == x, and no per-lane select for the 1.0 launches)
+      if constexpr (RES || DLT) {   // (unconditional: x * 1.0f == x, and no per-lane select for the 1.0 launches)
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] *= p.out_scale;
       } else if constexpr (GEN) {
@@ -1846,6 +1847,7 @@ void ek_dispatch(int ek, F&& f) {
       case EF_F32_RES: f(std::integral_constant<int, EF_F32_RES>{}); return;
       case EF_BF16_RES: f(std::integral_constant<int, EF_BF16_RES>{}); return;
       case EF_F32R_BF16: f(std::integral_constant<int, EF_F32R_BF16>{}); return;
+      case EF_BF16_DELTA: f(std::integral_constant<int, EF_BF16_DELTA>{}); return;
       case EF_BF16_SILU_MX: f(std::integral_constant<int, EF_BF16_SILU_MX>{}); return;
       default: break;
     }
@@ -1979,7 +1981,9 @@ int epi_fast_kind(const GemmP& p, int batch) {
   if (f32) return silu && p.pre && p.dtpre != CFM_BF16 ? EF_GENERIC : EF_F32;
   if (silu) return p.pre && p.dtpre == CFM_BF16 && p.bias && a1 && s1 ? (p.mxo8 ? EF_BF16_SILU_MX : EF_BF16_SILU)
                                                                         : EF_GENERIC;
-  if (p.drop_p > 0.f || !a1 || !s1) return EF_GENERIC;
+  if (p.drop_p > 0.f || !s1)
+    return bf && p.bias && a1 && p.act == CFM_ACT_NONE && !p.pre ? EF_BF16_DELTA : EF_GENERIC;
+  if (!a1) return EF_GENERIC;
   return p.bias ? EF_BF16_BIAS : EF_BF16;
 }
 

@@ -114,23 +114,46 @@ __device__ __forceinline__ void ln_store_mx(const LnMx& mx, long row, int D, int
   if (lane % LPB == 0) mx.s8[row * (D / 32) + lane / LPB] = (uint8_t)(127 - k);
 }
 
-template <int V, typename TY, bool MX = false, typename TX = float>
+// RS: the residual add of the module before this LayerNorm moved in here (cfm_layernorm_fwd_res): the row is
+// x + delta (delta: that module's bf16 output -- bias, dropout and out_scale applied by its GEMM's epilogue), stored
+// to xo (the fp32 residual stream the backward reads) and normalised.  The GEMM then writes 2 B per element instead of
+// reading and writing the 4-B stream in an epilogue nothing overlaps; the bytes move into this streaming pass.
+struct LnRes {
+  const bf16* d;   // M x D delta
+  float* xo;       // M x D: x + delta
+};
+
+template <int V, typename TY, bool MX = false, typename TX = float, bool RS = false>
 __global__ __launch_bounds__(256) void ln_fwd_vec(const TX* __restrict__ x, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, TY* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
-                                                  float eps, LnMx mx = {}) {
+                                                  float eps, LnMx mx = {}, LnRes rs = {}) {
   constexpr int D = 64 * V, R = LN_FWD_ROWS;
   const int lane = threadIdx.x & 63;
   const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   if (row0 >= M) return;
   float v[R][V], g[V], b[V];
+  [[maybe_unused]] float dl[RS ? R : 1][RS ? V : 1];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (row0 + r < M) {
       ldv<V>(x + (row0 + r) * D + lane * V, v[r]);
+      if constexpr (RS) ldv<V>(rs.d + (row0 + r) * D + lane * V, dl[r]);
     } else {
 #pragma unroll
       for (int i = 0; i < V; ++i) v[r][i] = 0.f;
+      if constexpr (RS) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) dl[r][i] = 0.f;
+      }
+    }
+  }
+  if constexpr (RS) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) v[r][i] += dl[r][i];
+      if (row0 + r < M) stv<V>(rs.xo + (row0 + r) * D + lane * V, v[r]);
     }
   }
   ldv<V>(gamma + lane * V, g);
@@ -244,23 +267,37 @@ template <int G> __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-template <int G, typename TY, typename TX = float>
+template <int G, typename TY, typename TX = float, bool RS = false>
 __global__ __launch_bounds__(256) void ln_fwd_grp(const TX* __restrict__ x, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, TY* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out, long M,
-                                                  int D, float eps) {
+                                                  int D, float eps, LnRes rs = {}) {
   constexpr int RPW = 64 / G, R = LN_FWD_ROWS;
   const int lane = threadIdx.x & 63, j = lane % G, c = 8 * j;
   const bool act = c < D;
   const long row0 = (((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / G) * R;
   float v[R][8], g[8], b[8];
+  [[maybe_unused]] float dl[RS ? R : 1][8];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (act && row0 + r < M) {
       ldv<8>(x + (row0 + r) * D + c, v[r]);
+      if constexpr (RS) ldv<8>(rs.d + (row0 + r) * D + c, dl[r]);
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[r][i] = 0.f;
+      if constexpr (RS) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dl[r][i] = 0.f;
+      }
+    }
+  }
+  if constexpr (RS) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[r][i] += dl[r][i];
+      if (act && row0 + r < M) stv<8>(rs.xo + (row0 + r) * D + c, v[r]);
     }
   }
   if (act) {
@@ -397,7 +434,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, void* __restrict__ y,
                                                      int dty, float* __restrict__ mean_out,
-                                                     float* __restrict__ rstd_out, long M, int D, float eps) {
+                                                     float* __restrict__ rstd_out, long M, int D, float eps,
+                                                     const void* __restrict__ delta = nullptr, int dtd = 0,
+                                                     float* __restrict__ xo = nullptr) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -407,6 +446,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
   for (int j = 0; j < MAXJ; ++j) {
     const int c = lane + 64 * j;
     v[j] = c < D ? ld_dyn(x, dtx, row * D + c) : 0.f;
+    if (delta && c < D) {   // (cfm_layernorm_fwd_res: x + delta, stored to xo)
+      v[j] += ld_dyn(delta, dtd, row * D + c);
+      xo[row * D + c] = v[j];
+    }
     s += v[j];
   }
   const float mean = wave_sum(s) / D;
@@ -498,12 +541,32 @@ bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0;
 
 template <int V>
 bool ln_fwd_fast(const void* x, int dtx, const float* gamma, const float* beta, void* y, int dty, float* mean,
-                 float* rstd, long M, int D, float eps, hipStream_t s, LnMx mx = {}) {
+                 float* rstd, long M, int D, float eps, hipStream_t s, LnMx mx = {}, LnRes rs = {}) {
   // x: the fp32 residual stream, or bf16 (the bf16 mode's residual stream, conformer.py RES_BF16)
   if (D != 64 * V || (dtx != CFM_F32 && dtx != CFM_BF16) || !aligned16(x) || !aligned16(y) || !aligned16(gamma) ||
       !aligned16(beta))
     return false;
   dim3 g((unsigned)((M + 4 * LN_FWD_ROWS - 1) / (4 * LN_FWD_ROWS)));
+  if (rs.d) {   // fp32 x + bf16 delta (cfm_layernorm_fwd_res)
+    if (dtx != CFM_F32 || !aligned16(rs.d) || !aligned16(rs.xo) || (V < 4 && ((uintptr_t)rs.d & 15)))
+      return false;
+    if (mx.y8) {
+      if constexpr (V >= 4) {
+        if (dty != CFM_BF16) return false;
+        hipLaunchKernelGGL((ln_fwd_vec<V, bf16, true, float, true>), g, dim3(256), 0, s, (const float*)x, gamma, beta,
+                           (bf16*)y, mean, rstd, M, eps, mx, rs);
+        return true;
+      }
+      return false;
+    }
+    if (dty == CFM_BF16)
+      hipLaunchKernelGGL((ln_fwd_vec<V, bf16, false, float, true>), g, dim3(256), 0, s, (const float*)x, gamma, beta,
+                         (bf16*)y, mean, rstd, M, eps, LnMx{}, rs);
+    else
+      hipLaunchKernelGGL((ln_fwd_vec<V, float, false, float, true>), g, dim3(256), 0, s, (const float*)x, gamma, beta,
+                         (float*)y, mean, rstd, M, eps, LnMx{}, rs);
+    return true;
+  }
   auto go = [&](auto xt) {
     typedef decltype(xt) TX;
     if (mx.y8) {
@@ -555,15 +618,25 @@ int ln_group(int D) {
 }
 
 bool ln_fwd_grouped(const void* x, int dtx, const float* gamma, const float* beta, void* y, int dty, float* mean,
-                    float* rstd, long M, int D, float eps, hipStream_t s) {
+                    float* rstd, long M, int D, float eps, hipStream_t s, LnRes rs = {}) {
   const int G = ln_group(D);
   if (!G || (dtx != CFM_F32 && dtx != CFM_BF16) || (dty != CFM_F32 && dty != CFM_BF16) || !aligned16(x) ||
       !aligned16(y) || !aligned16(gamma) || !aligned16(beta))
     return false;
+  if (rs.d && (dtx != CFM_F32 || !aligned16(rs.d) || !aligned16(rs.xo))) return false;
   const long rows_per_block = 4L * (64 / G) * LN_FWD_ROWS;
   const dim3 g((unsigned)((M + rows_per_block - 1) / rows_per_block));
   auto go = [&](auto gt) {
     constexpr int GG = decltype(gt)::value;
+    if (rs.d) {
+      if (dty == CFM_BF16)
+        hipLaunchKernelGGL((ln_fwd_grp<GG, bf16, float, true>), g, dim3(256), 0, s, (const float*)x, gamma, beta,
+                           (bf16*)y, mean, rstd, M, D, eps, rs);
+      else
+        hipLaunchKernelGGL((ln_fwd_grp<GG, float, float, true>), g, dim3(256), 0, s, (const float*)x, gamma, beta,
+                           (float*)y, mean, rstd, M, D, eps, rs);
+      return;
+    }
     auto go2 = [&](auto xt) {
       typedef decltype(xt) TX;
       if (dty == CFM_BF16)
@@ -642,6 +715,37 @@ CFM_EXPORT int cfm_layernorm_fwd_mx_ex(const void* x, int dtx, const float* gamm
                   ln_fwd_fast<16>(x, dtx, gamma, beta, y, CFM_BF16, mean, rstd, M, D, eps, s, mx);
   CFM_REQUIRE(ok, CFM_ERR_ALIGN, "16-B aligned x / y / gamma / beta");
   return cfm::check_launch("cfm_layernorm_fwd_mx");
+}
+
+CFM_EXPORT int cfm_layernorm_fwd_res(const float* x, const void* delta, int dtd, float* xout, const float* gamma,
+                                     const float* beta, void* y, int dty, void* y8, uint8_t* s8, float* mean,
+                                     float* rstd, long M, int D, float eps, void* stream) {
+  CFM_REQUIRE(x && delta && xout && gamma && beta && y && mean && rstd, CFM_ERR_ARG, "null pointer");
+  CFM_REQUIRE((const void*)x != (const void*)xout && delta != (const void*)xout, CFM_ERR_ARG,
+              "xout must not alias x or delta");
+  CFM_REQUIRE(dtd == CFM_F32 || dtd == CFM_BF16, CFM_ERR_DTYPE, "delta: f32 or bf16");
+  CFM_REQUIRE(dty == CFM_F32 || dty == CFM_BF16, CFM_ERR_DTYPE, "y: f32 or bf16");
+  CFM_REQUIRE(D > 0 && D <= 64 * MAXJ && M >= 0, CFM_ERR_SHAPE, "D must be in (0, 1024]");
+  CFM_REQUIRE(!y8 || (s8 && dty == CFM_BF16 && (D == 256 || D == 512 || D == 1024) && (uintptr_t)y8 % 8 == 0),
+              CFM_ERR_SHAPE, "MX copy: bf16 y, D in {256, 512, 1024}, 8-B aligned y8, s8");
+  if (M == 0) return CFM_OK;
+  hipStream_t s = cfm::as_stream(stream);
+  const LnMx mx{(uint8_t*)y8, s8};
+  const LnRes rs{dtd == CFM_BF16 ? (const bf16*)delta : nullptr, xout};
+  bool fast = false;
+  if (rs.d) {
+    fast = ln_fwd_fast<2>(x, CFM_F32, gamma, beta, y, dty, mean, rstd, M, D, eps, s, mx, rs) ||
+           ln_fwd_fast<4>(x, CFM_F32, gamma, beta, y, dty, mean, rstd, M, D, eps, s, mx, rs) ||
+           ln_fwd_fast<8>(x, CFM_F32, gamma, beta, y, dty, mean, rstd, M, D, eps, s, mx, rs) ||
+           ln_fwd_fast<16>(x, CFM_F32, gamma, beta, y, dty, mean, rstd, M, D, eps, s, mx, rs) ||
+           (!y8 && ln_fwd_grouped(x, CFM_F32, gamma, beta, y, dty, mean, rstd, M, D, eps, s, rs));
+  }
+  if (!fast) {
+    CFM_REQUIRE(!y8, CFM_ERR_ALIGN, "MX copy: 16-B aligned x / delta / xout / y / gamma / beta");
+    hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, (const void*)x, (int)CFM_F32,
+                       gamma, beta, y, dty, mean, rstd, M, D, eps, delta, dtd, xout);
+  }
+  return cfm::check_launch("cfm_layernorm_fwd_res");
 }
 
 CFM_EXPORT int cfm_layernorm_fwd_mx(const float* x, const float* gamma, const float* beta, void* y, void* y8,

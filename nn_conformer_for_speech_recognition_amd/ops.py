@@ -565,6 +565,30 @@ def layernorm_fwd_mx(x, gamma, beta, eps=1e-5):
     return y, (y8, s8), mean, rstd
 
 
+def layernorm_fwd_res(x, delta, gamma, beta, eps=1e-5, out_dtype=None, mx=False):
+    """x' = x + delta (fp32, a new tensor) and LayerNorm(x') from one kernel (cfm_layernorm_fwd_res): the residual add
+    of the module before the LayerNorm, whose GEMM wrote delta (bf16) without the residual.
+    -> (x', y, mean, rstd), or with mx=True (bf16 y and its MX e4m3 copy) (x', y, (y8, s8), mean, rstd)."""
+    M, D = x.shape
+    if x.dtype != torch.float32 or delta.shape != x.shape:
+        raise L.CfmError("layernorm_fwd_res: fp32 x and a delta of x's shape")
+    x = x.contiguous()
+    delta = delta.contiguous()
+    xo = torch.empty_like(x)
+    yd = torch.bfloat16 if mx else (out_dtype or x.dtype)
+    y = torch.empty(M, D, device=x.device, dtype=yd)
+    y8 = torch.empty(M, D, device=x.device, dtype=torch.float8_e4m3fn) if mx else None
+    s8 = torch.empty(M, D // 32, device=x.device, dtype=torch.uint8) if mx else None
+    mean = torch.empty(M, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(M, device=x.device, dtype=torch.float32)
+    L.call("cfm_layernorm_fwd_res", L.ptr(x), L.ptr(delta), L.dt(delta), L.ptr(xo), L.ptr(gamma), L.ptr(beta),
+           L.ptr(y), L.dt(y), L.ptr(y8) if mx else None, L.ptr(s8) if mx else None, L.ptr(mean), L.ptr(rstd), M, D,
+           float(eps), L.stream())
+    if mx:
+        return xo, y, (y8, s8), mean, rstd
+    return xo, y, mean, rstd
+
+
 def layernorm_bwd(dy, x, gamma, mean, rstd, dres=None, dx_dtype=torch.float32, side=None, drop=None):
     """dx (+ dres) and (dgamma, dbeta).  side: optional object with run(fn, *keep) (conformer._Side):
     the dgamma|dbeta partial-row reduction is then launched there, off the data-gradient chain.

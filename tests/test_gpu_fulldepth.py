@@ -128,6 +128,16 @@ def test_full_depth_encoder_vs_oracle(stack, pos, cd, T, lens):
     assert eb < ty
 
 
+@pytest.mark.parametrize("stack,pos,T,lens", [("L17", "none", 94, [94, 71]), ("S16", "none", 373, [373, 301]),
+                                            ("L17", "rel", 94, [94, 71])])
+def test_full_depth_residual_add_in_layernorm(monkeypatch, stack, pos, T, lens):
+    """The opt-in CFM_RES_FUSE form (conformer.RES_FUSE: residual GEMMs write their bf16 output, the next LayerNorm
+    adds it to the stream -- cfm_layernorm_fwd_res) at depth, bf16, under the same tolerances."""
+    import nn_conformer_for_speech_recognition_amd.conformer as cm
+    monkeypatch.setattr(cm, "RES_FUSE", True)
+    test_full_depth_encoder_vs_oracle(stack, pos, torch.bfloat16, T, lens)
+
+
 def _encoder_ctc(cd, L=17, T_in=385, V=1024, seed=0):
     import bench
     torch.manual_seed(seed)

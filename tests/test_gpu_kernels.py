@@ -710,6 +710,64 @@ def test_gemm_residual_epilogue_dtypes(gemm_mode, res_dt, out_dt, M, N, K):
     assert _rel(y0, ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(11936, 512, 2048), (11936, 512, 512), (3000, 144, 576), (11936, 256, 1024),
+                                   (777, 2048, 512)])
+@pytest.mark.parametrize("drop_p,out_scale", [(0.1, 0.5), (0.1, 1.0), (0.0, 0.5)])
+def test_gemm_delta_epilogue(gemm_mode, M, N, K, drop_p, out_scale):
+    """The residual module's output without the residual (EF_BF16_DELTA: bf16 out_scale * dropout(x·wᵀ + b), the
+    RES_FUSE form whose add the next LayerNorm does): bit-identical to the generic epilogue rows (cfm_gemm_set_mode
+    bit 14) on the same main loop, and equal to the fp32 residual epilogue's output minus its residual up to the
+    bf16 rounding of the delta (same dropout mask)."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    outs = []
+    for mode in (3, 3 | 16384):
+        gemm_mode(mode)
+        y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.linear(x, w, b, out=y, drop_p=drop_p, seed=11, out_scale=out_scale)
+        outs.append(y.clone())
+    gemm_mode(3)
+    zero = torch.zeros(M, N, device=DEV)
+    yr = torch.empty(M, N, device=DEV)
+    ops.linear(x, w, b, out=yr, drop_p=drop_p, seed=11, out_scale=out_scale, residual=zero)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], yr.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("D", [512, 256, 144, 1024, 128, 100])
+@pytest.mark.parametrize("dd", [torch.bfloat16, torch.float32])
+def test_layernorm_fwd_residual_add(D, dd):
+    """cfm_layernorm_fwd_res: x' = x + delta (fp32, exactly the fp32 sum) and y = LN(x') -- bit-identical to
+    cfm_layernorm_fwd of x' (the same kernel family on the same values); with the MX copy (fp8 mode, D in 256 / 512 /
+    1024) bit-identical to layernorm_fwd_mx of x'; ragged M (555 rows, a partial last workgroup)."""
+    g = torch.Generator().manual_seed(D + 11)
+    M = 555
+    x = (torch.randn(M, D, generator=g) * 2 + 0.3).to(DEV)
+    delta = torch.randn(M, D, generator=g).to(DEV, dd)
+    gamma = (torch.rand(D, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(D, generator=g).to(DEV)
+    for od in (torch.bfloat16, torch.float32):
+        xo, y, mean, rstd = ops.layernorm_fwd_res(x, delta, gamma, beta, out_dtype=od)
+        xs = x + delta.float()
+        y2, mean2, rstd2 = ops.layernorm_fwd(xs, gamma, beta, out_dtype=od)
+        torch.cuda.synchronize()
+        assert torch.equal(xo, xs)
+        if (dd == torch.bfloat16 and D % 64 == 0) or D == 100:   # the vector kernels, the generic kernel
+            assert torch.equal(y, y2) and torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
+        else:   # an fp32 delta takes the generic kernel (another summation order than the vector kernels); the lane-
+            # group kernel (D 144) differs from its plain instantiation in the last bit of rstd (contraction choices)
+            assert _rel(y, y2) < (5e-3 if od == torch.bfloat16 else 1e-5) and _rel(rstd, rstd2) < 1e-6
+            assert _rel(mean, mean2) < 1e-6
+    if D in (256, 512, 1024) and dd == torch.bfloat16:
+        xo, y, (y8, s8), mean, rstd = ops.layernorm_fwd_res(x, delta, gamma, beta, mx=True)
+        ym, (q8, qs), _, _ = ops.layernorm_fwd_mx(x + delta.float(), gamma, beta)
+        torch.cuda.synchronize()
+        assert torch.equal(y, ym) and torch.equal(y8.view(torch.uint8), q8.view(torch.uint8)) and torch.equal(s8, qs)
+
+
 @pytest.mark.parametrize("M,K", [(11936, 1024), (11936, 256), (1000, 768)])
 @pytest.mark.parametrize("res", [False, True])
 def test_gemm_ws96_narrow_outputs(gemm_mode, M, K, res):
