@@ -14,7 +14,9 @@
 // the skewed b32 reads are both bank-conflict free).  ac and bd add in fp32 before the softmax.
 //
 // Backward (deterministic, no atomics):
-//   dQ kernel  (queries on the lanes, streams key tiles): recomputes S (same band), dP, dS;
+//   dQ kernel  (round 6 default, attn_rel_bwd_dqs_kernel): runs after dK/dV and reads the dS it stored --
+//              dq = scale * (sum_j dS k_j + sum_j dS p_{T-1-i+j}), the band sum as below; no recompute.
+//   dQ2 kernel (queries on the lanes, streams key tiles; cfm_attn_set_mode bit 9): recomputes S (same band), dP, dS;
 //              dq = scale * (sum_j dS k_j  +  sum_j dS p_{T-1-i+j}) -- the second sum is a plain
 //              MFMA over the band once dS^T is scattered into the stage in band coordinates;
 //              per-wave column sums of both terms -> du, dv partials (one reduction launch).
@@ -544,6 +546,206 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
                      p.dk, lane);
 }
 
+// ------------------------------------------------------------------------------------ dQ from the stored dS
+// (default since round 6; cfm_attn_set_mode bit 9 keeps the recomputing dQ2 kernel above, A/B).  The dK/dV kernel
+// already writes dS (bf16, unscaled, query-major) for the dpos pass; dQ is a plain product of it with K and, in band
+// coordinates, with the projected table:  dq_i = scale * (sum_j dS_ij k_j + sum_j dS_ij p_{T-1-i+j}).  No scores,
+// softmax, dropout hash or dO x V recompute: per 64-key tile a wave runs 8 + 12 MFMAs (dQ2: 48) and no exp.
+// grid (ceil(T/128), H, B), 4 waves x 32 queries; LDS: the K tile, a ring of 3 band chunks (as dQ2), and per wave
+// one region that holds in turn the tile's dS rows ([query][DSW] bf16, 16-B global loads) and the band-coordinate
+// image of dS^T ([query][SBQ] bf16, as dQ2); after the loop the K tile + ring bytes hold the waves' f32 stages of the
+// du / dv sums and the dq store.
+// dS entries of keys >= len are not defined in the buffer (the dK/dV kernel leaves them unmasked or unwritten):
+// they are replaced by zeros on the way into LDS.  part: as dQ2.
+// Row strides of the two bf16 images are an odd number of 8-B units (19 and 25: 76 / 100 elements): the
+// 8-B fragment reads of the 32 query rows then hit 32 distinct bank pairs (the 16-B aligned strides -- 144 / 208 B --
+// put rows i and i + 16 on one bank pair: 12 M conflict cycles per L60 launch); the images are written in 8-B pieces.
+// K tile and band ring of the dQ-from-dS kernel: read only through the transposed fragments (ds_read_b64_tr_b16:
+// 4 rows x 64 B per 32-lane half), so 192-B rows (48 dwords: an odd multiple of 16) put the four rows on disjoint
+// bank quarters -- the 144-B rows the score kernels need for their b128 row fragments leave these reads 2-way
+// conflicted
+constexpr int KSQ = 96;
+// trfrag_perm with an explicit row stride (also the dpos kernel's)
+template <int STR>
+__device__ __forceinline__ bf16x8 trfrag_perm_s(const bf16* tile, int r0, int c0, int lane) {
+  const int hh = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+  const bf16* base = tile + (r0 + 4 * hh + q) * STR + c0 + 16 * g1 + 4 * p4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 8 * STR));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+template <int STR>
+__device__ __forceinline__ void tile_store_s(bf16* t, const uint4 (&reg)[2], int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + 256 * i;
+    *reinterpret_cast<uint4*>(t + (v >> 3) * STR + (v & 7) * 8) = reg[i];
+  }
+}
+template <int STR>
+__device__ __forceinline__ void ring_chunk_store_s(bf16* slot, const uint4 (&reg)[2], int tid) { tile_store_s<STR>(slot, reg, tid); }
+constexpr int DSW = 76;                       // dS tile row stride (bf16 elements): 152 B
+constexpr int SBQ = 100;                      // band image row stride (bf16 elements): 200 B
+constexpr int DQS_WAVE = 32 * SBQ * 2;        // per-wave region (bytes): the band image, the larger of the two
+static_assert(32 * DSW * 2 <= DQS_WAVE, "per-wave region");
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void attn_rel_bwd_dqs_kernel(AttnM p, RelP rp, const bf16* __restrict__ dsbuf,
+                                                                  int ldS, bf16* __restrict__ dqkv,
+                                                                  float* __restrict__ part) {
+  // sk and sring adjacent: after the loop their 48 KiB hold the four 32 x 65 f32 stages (33 KiB)
+  __shared__ __attribute__((aligned(16))) bf16 skr[4 * TILE * KSQ];
+  __shared__ __attribute__((aligned(16))) char swv[4 * DQS_WAVE];
+  static_assert(4 * TILE * KSQ * 2 >= 4 * 32 * 65 * 4, "final stages fit the K tile + ring");
+  bf16* sk = skr;
+  bf16* sring = skr + TILE * KSQ;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, ii = lane & 31;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int Q0 = blockIdx.x * 128, q0 = Q0 + wv * 32;
+  const int len = p.len[b];
+  const int rbase = p.T - 1 - Q0 - 127;
+  const int nkt = (len + TILE - 1) / TILE;
+  const int kcol = p.HD + h * p.dk;
+  char* wreg = swv + wv * DQS_WAVE;
+  bf16* dimg = reinterpret_cast<bf16*>(wreg);      // [query][DSW] dS rows of the tile
+  bf16* bimg = reinterpret_cast<bf16*>(wreg);      // [query][SBQ] band image of dS^T (after the rows are read)
+  bf16* bcol = bimg + ii * SBQ;
+  bf16* bsk = bcol + 31 - ii;                       // band position of key k (0..63) of query ii: bsk[k]
+  const bf16* dsb = dsbuf + ((long)b * p.H + h) * p.T * (long)ldS;
+  // the wave's 32 dS rows of key tile kt: chunk idx = lane + 64 i -> row idx >> 3, keys 8 (idx & 7) .. +7; rows past
+  // T, chunks past the row's ldS, and (below, at the store) keys >= len read as zero.  Two tiles in flight (the
+  // register sets rdA / rdB alternate): one tile's MFMAs are far shorter than an HBM round trip
+  uint4 rdA[4], rdB[4];
+  auto dload = [&](uint4 (&rd)[4], int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = lane + 64 * i, row = q0 + (idx >> 3), k = kt * TILE + 8 * (idx & 7);
+      rd[i] = row < p.T && k < ldS ? *reinterpret_cast<const uint4*>(dsb + (long)row * ldS + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto dstore = [&](const uint4 (&rd)[4], int kt) {
+    const bool tail = kt * TILE + TILE > len;     // (uniform)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = lane + 64 * i, k = kt * TILE + 8 * (idx & 7);
+      uint4 v = rd[i];
+      if (tail) {
+        bf16x8 e = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) e[j] = k + j < len ? e[j] : (bf16)0.f;
+        v = __builtin_bit_cast(uint4, e);
+      }
+      uint2* d2 = reinterpret_cast<uint2*>(dimg + (idx >> 3) * DSW + 8 * (idx & 7));
+      d2[0] = make_uint2(v.x, v.y);
+      d2[1] = make_uint2(v.z, v.w);
+    }
+  };
+  f32x16 a0 = (f32x16){0}, a1 = (f32x16){0}, e0 = (f32x16){0}, e1 = (f32x16){0};   // K-term, band term
+  uint4 rk[2], rq[2];
+  if (nkt > 0) {
+    tile_load<VEC>(p, b, 0, kcol, rk, tid);
+    dload(rdB, 0);
+    if (nkt > 1) dload(rdA, 1);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + ch * TILE, tid + 256 * i);
+      ring_chunk_store_s<KSQ>(sring + ch * TILE * KSQ, rq, tid);
+    }
+    tile_store_s<KSQ>(sk, rk, tid);
+    dstore(rdB, 0);
+    if (nkt > 2) dload(rdB, 2);
+    __syncthreads();
+  }
+  // tile kt: rdA holds tile kt + 1 when kt is even, rdB when odd; each is refilled with tile kt + 3 once stored
+  auto step = [&](int kt, uint4 (&rnext)[4]) {
+    if (kt + 1 < nkt) {                           // the next K tile and band chunk in flight under this tile's MFMAs
+      tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rq[i] = ring_chunk_load<VEC>(p, rp, h, rbase + (kt + 3) * TILE, tid + 256 * i);
+    }
+    const bf16* blk[3];
+#pragma unroll
+    for (int mm = 0; mm < 3; ++mm) {
+      const int off = 32 * (3 - wv) + 32 * mm;
+      blk[mm] = sring + ((kt + (off >> 6)) % 3) * TILE * KSQ + (off & 63) * KSQ;
+    }
+    // B fragments of dS^T (k order of an accumulator used as the B operand: element j of k-step s of key half t is
+    // key 32 t + 16 s + 8 (j >> 2) + 4 hh + (j & 3)): two 8-B runs of query ii's row each
+    bf16x8 f[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16* rowp = dimg + ii * DSW + 32 * t + 16 * s2 + 4 * hh;
+        const uint2 lo = *reinterpret_cast<const uint2*>(rowp);
+        const uint2 hi = *reinterpret_cast<const uint2*>(rowp + 8);
+        f[t][s2] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+    // K-term: dQ^T[d][q] += sum_key K[key][d] dS^T[key][q]
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<KSQ>(sk, 32 * t + 16 * s2, 0, lane), f[t][s2], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<KSQ>(sk, 32 * t + 16 * s2, 32, lane), f[t][s2], a1, 0, 0,
+                                                     0);
+      }
+    // band term: dS^T in band coordinates, bf16 image [i][j - i + 31] (zero elsewhere; the region's dS rows are all
+    // read -- LDS operations of a wave complete in order), then dQ^T[d][q] += sum_r' P_band[r'][d] dS_band^T[r'][q]
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int g = 0; g < 12; ++g) *reinterpret_cast<uint2*>(bcol + 48 * hh + 4 * g) = make_uint2(0, 0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsk[32 * t + 16 * s2 + 8 * (j >> 2) + 4 * hh + (j & 3)] = f[t][s2][j];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const uint2 lo = *reinterpret_cast<const uint2*>(bcol + 16 * s + 4 * hh);
+      const uint2 hi = *reinterpret_cast<const uint2*>(bcol + 16 * s + 8 + 4 * hh);
+      const bf16x8 bfr = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      const bf16* bk = blk[s >> 1];
+      e0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<KSQ>(bk, 16 * (s & 1), 0, lane), bfr, e0, 0, 0, 0);
+      e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<KSQ>(bk, 16 * (s & 1), 32, lane), bfr, e1, 0, 0, 0);
+    }
+    if (kt + 1 < nkt) {
+      __syncthreads();
+      tile_store_s<KSQ>(sk, rk, tid);
+      ring_chunk_store_s<KSQ>(sring + (kt % 3) * TILE * KSQ, rq, tid);
+      dstore(rnext, kt + 1);
+      if (kt + 3 < nkt) dload(rnext, kt + 3);
+      __syncthreads();
+    }
+  };
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt & 1) step(kt, rdB);
+    else step(kt, rdA);
+  }
+  __syncthreads();   // every wave's reads of the K tile / ring are done before the stages reuse their bytes
+  float* st = reinterpret_cast<float*>(skr) + wv * 32 * 65;
+  const float su = wave_rowsum(st, a0, a1, lane) * p.scale;
+  const float sv = wave_rowsum(st, e0, e1, lane) * p.scale;
+  const long prow = (long)b * (4 * gridDim.x) + blockIdx.x * 4 + wv;
+  if (lane < p.dk) {
+    part[prow * 2 * p.HD + h * p.dk + lane] = su;
+    part[prow * 2 * p.HD + p.HD + h * p.dk + lane] = sv;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    a0[r] += e0[r];
+    a1[r] += e1[r];
+  }
+  if (q0 < p.T)
+    store_transposed(st, a0, a1, p.scale, dqkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, q0, min(32, p.T - q0),
+                     p.dk, lane);
+}
+
 // ------------------------------------------------------------------------------------ dK, dV (+ dS store)
 // grid (ceil(T/128), H, B); wave = 32 keys on the lanes; query tiles of 64 (two 32-query sub-blocks)
 // staged in LDS as q+u, q+v, dO (+ lse, D).  The band for (query tile qt, 128 keys) is 192 rows
@@ -939,17 +1141,7 @@ constexpr int DP_KS = 160;
 constexpr int DP_PADL = 8;             // band image column of r' = 0 (r' = -7 .. 135 are written, 0 .. 127 read)
 constexpr int DP_CH = DP_R / 8 + 1;    // aligned 8-element dS chunks per row (17)
 
-// trfrag_perm with an explicit row stride
-template <int S>
-__device__ __forceinline__ bf16x8 trfrag_perm_s(const bf16* tile, int r0, int c0, int lane) {
-  const int hh = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
-  const bf16* base = tile + (r0 + 4 * hh + q) * S + c0 + 16 * g1 + 4 * p4;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 8 * S));
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
+// (trfrag_perm_s: trfrag_perm with an explicit row stride, defined with the dQ-from-dS kernel above)
 
 struct DposRegs {
   uint4 q[2];         // raw q rows (q + v is formed at store time: converting at load time waits for the load)
@@ -1162,16 +1354,26 @@ int attn_rel_bwd_launch(const void* qkv, const void* dout, const float* lse, con
   bf16* dsbuf = reinterpret_cast<bf16*>(reinterpret_cast<char*>(part) + part_bytes);
   const int ldS = rel_ldS(p.T);
   const dim3 grid(cdiv(p.T, 128), p.H, p.B);
+  // dK / dV (+ the dS buffer), then dQ: from the stored dS (default) or recomputed (cfm_attn_set_mode bit 9)
+  const bool dq_recompute = (g_rel_mode & 512) != 0;
   if (rel_vec(p, rp)) {
     hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                        (bf16*)dqkv, dsbuf, ldS);
-    hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                       (bf16*)dqkv, part);
+    if (dq_recompute)
+      hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, part);
+    else
+      hipLaunchKernelGGL(attn_rel_bwd_dqs_kernel<true>, grid, dim3(256), 0, s, p, rp, (const bf16*)dsbuf, ldS,
+                         (bf16*)dqkv, part);
   } else {
     hipLaunchKernelGGL(attn_rel_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
                        (bf16*)dqkv, dsbuf, ldS);
-    hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
-                       (bf16*)dqkv, part);
+    if (dq_recompute)
+      hipLaunchKernelGGL(attn_rel_bwd_dq2_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dout, lse, ws,
+                         (bf16*)dqkv, part);
+    else
+      hipLaunchKernelGGL(attn_rel_bwd_dqs_kernel<false>, grid, dim3(256), 0, s, p, rp, (const bf16*)dsbuf, ldS,
+                         (bf16*)dqkv, part);
   }
   const size_t ds_bytes = ((size_t)p.B * p.H * p.T * ldS * sizeof(bf16) + 255) & ~(size_t)255;
   float* dpos_part = reinterpret_cast<float*>(reinterpret_cast<char*>(dsbuf) + ds_bytes);
