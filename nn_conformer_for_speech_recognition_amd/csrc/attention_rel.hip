@@ -552,14 +552,12 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
 // coordinates, with the projected table:  dq_i = scale * (sum_j dS_ij k_j + sum_j dS_ij p_{T-1-i+j}).  No scores,
 // softmax, dropout hash or dO x V recompute: per 64-key tile a wave runs 8 + 12 MFMAs (dQ2: 48) and no exp.
 // grid (ceil(T/128), H, B), 4 waves x 32 queries; LDS: the K tile, a ring of 3 band chunks (as dQ2), and per wave
-// one region that holds in turn the tile's dS rows ([query][DSW] bf16, 16-B global loads) and the band-coordinate
-// image of dS^T ([query][SBQ] bf16, as dQ2); after the loop the K tile + ring bytes hold the waves' f32 stages of the
-// du / dv sums and the dq store.
+// the band-coordinate image of dS^T ([query][SBQ] bf16, as dQ2, zeroed once); the dS fragments come straight from
+// the buffer into registers (two 8-B loads per fragment, one tile ahead): the kernel is bound by its LDS instruction
+// count, not by bank conflicts (PMC, profiles/r06/misc/rel_dq_from_ds_ab.txt).  After the loop the K tile + ring
+// bytes hold the waves' f32 stages of the du / dv sums and the dq store.
 // dS entries of keys >= len are not defined in the buffer (the dK/dV kernel leaves them unmasked or unwritten):
 // they are replaced by zeros on the way into LDS.  part: as dQ2.
-// Row strides of the two bf16 images are an odd number of 8-B units (19 and 25: 76 / 100 elements): the
-// 8-B fragment reads of the 32 query rows then hit 32 distinct bank pairs (the 16-B aligned strides -- 144 / 208 B --
-// put rows i and i + 16 on one bank pair: 12 M conflict cycles per L60 launch); the images are written in 8-B pieces.
 // K tile and band ring of the dQ-from-dS kernel: read only through the transposed fragments (ds_read_b64_tr_b16:
 // 4 rows x 64 B per 32-lane half), so 192-B rows (48 dwords: an odd multiple of 16) put the four rows on disjoint
 // bank quarters -- the 144-B rows the score kernels need for their b128 row fragments leave these reads 2-way
@@ -586,10 +584,10 @@ __device__ __forceinline__ void tile_store_s(bf16* t, const uint4 (&reg)[2], int
 }
 template <int STR>
 __device__ __forceinline__ void ring_chunk_store_s(bf16* slot, const uint4 (&reg)[2], int tid) { tile_store_s<STR>(slot, reg, tid); }
-constexpr int DSW = 76;                       // dS tile row stride (bf16 elements): 152 B
+// The band image's row stride is an odd number of 8-B units (25: 100 elements): its 8-B fragment reads of the 32
+// query rows hit 32 distinct bank pairs (a 16-B aligned stride -- 208 B -- puts rows i and i + 16 on one pair).
 constexpr int SBQ = 100;                      // band image row stride (bf16 elements): 200 B
-constexpr int DQS_WAVE = 32 * SBQ * 2;        // per-wave region (bytes): the band image, the larger of the two
-static_assert(32 * DSW * 2 <= DQS_WAVE, "per-wave region");
+constexpr int DQS_WAVE = 32 * SBQ * 2;        // per-wave region (bytes)
 template <bool VEC>
 __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dqs_kernel(AttnM p, RelP rp, const bf16* __restrict__ dsbuf,
                                                                   int ldS, bf16* __restrict__ dqkv,
@@ -608,45 +606,35 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dqs_kernel(AttnM p, RelP 
   const int nkt = (len + TILE - 1) / TILE;
   const int kcol = p.HD + h * p.dk;
   char* wreg = swv + wv * DQS_WAVE;
-  bf16* dimg = reinterpret_cast<bf16*>(wreg);      // [query][DSW] dS rows of the tile
-  bf16* bimg = reinterpret_cast<bf16*>(wreg);      // [query][SBQ] band image of dS^T (after the rows are read)
+  bf16* bimg = reinterpret_cast<bf16*>(wreg);      // [query][SBQ] band image of dS^T
   bf16* bcol = bimg + ii * SBQ;
   bf16* bsk = bcol + 31 - ii;                       // band position of key k (0..63) of query ii: bsk[k]
+  // every tile writes the same band positions of a row (k + 31 - ii, k = 0..63): the rest stay zero from here
+#pragma unroll
+  for (int g = 0; g < 12; ++g) *reinterpret_cast<uint2*>(bcol + 48 * hh + 4 * g) = make_uint2(0, 0);
   const bf16* dsb = dsbuf + ((long)b * p.H + h) * p.T * (long)ldS;
-  // the wave's 32 dS rows of key tile kt: chunk idx = lane + 64 i -> row idx >> 3, keys 8 (idx & 7) .. +7; rows past
-  // T, chunks past the row's ldS, and (below, at the store) keys >= len read as zero.  Two tiles in flight (the
-  // register sets rdA / rdB alternate): one tile's MFMAs are far shorter than an HBM round trip
-  uint4 rdA[4], rdB[4];
-  auto dload = [&](uint4 (&rd)[4], int kt) {
+  // the lane's dS^T B fragments of key tile kt straight from the buffer, in the k order of an accumulator used as the
+  // B operand: fragment 2 t + s of query q0 + ii holds keys 32 t + 16 s + 4 hh + {0..3, 8..11} -- two 8-B loads
+  // (rows past T and runs past the row's ldS read zero; keys >= len are zeroed on the last tile)
+  uint4 fA[4], fB[4];
+  const int qrow = q0 + ii;
+  const bool qok = qrow < p.T;
+  const bf16* dsrow = dsb + (long)(qok ? qrow : 0) * ldS + 4 * hh;
+  auto dload = [&](uint4 (&f)[4], int kt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = lane + 64 * i, row = q0 + (idx >> 3), k = kt * TILE + 8 * (idx & 7);
-      rd[i] = row < p.T && k < ldS ? *reinterpret_cast<const uint4*>(dsb + (long)row * ldS + k) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto dstore = [&](const uint4 (&rd)[4], int kt) {
-    const bool tail = kt * TILE + TILE > len;     // (uniform)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = lane + 64 * i, k = kt * TILE + 8 * (idx & 7);
-      uint4 v = rd[i];
-      if (tail) {
-        bf16x8 e = __builtin_bit_cast(bf16x8, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) e[j] = k + j < len ? e[j] : (bf16)0.f;
-        v = __builtin_bit_cast(uint4, e);
-      }
-      uint2* d2 = reinterpret_cast<uint2*>(dimg + (idx >> 3) * DSW + 8 * (idx & 7));
-      d2[0] = make_uint2(v.x, v.y);
-      d2[1] = make_uint2(v.z, v.w);
+    for (int q = 0; q < 4; ++q) {
+      const int k = kt * TILE + 32 * (q >> 1) + 16 * (q & 1);
+      const uint2 lo = qok && k + 4 * hh < ldS ? *reinterpret_cast<const uint2*>(dsrow + k) : make_uint2(0, 0);
+      const uint2 hi = qok && k + 8 + 4 * hh < ldS ? *reinterpret_cast<const uint2*>(dsrow + k + 8) : make_uint2(0, 0);
+      f[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
     }
   };
   f32x16 a0 = (f32x16){0}, a1 = (f32x16){0}, e0 = (f32x16){0}, e1 = (f32x16){0};   // K-term, band term
   uint4 rk[2], rq[2];
   if (nkt > 0) {
+    dload(fA, 0);
+    if (nkt > 1) dload(fB, 1);
     tile_load<VEC>(p, b, 0, kcol, rk, tid);
-    dload(rdB, 0);
-    if (nkt > 1) dload(rdA, 1);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
 #pragma unroll
@@ -654,12 +642,10 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dqs_kernel(AttnM p, RelP 
       ring_chunk_store_s<KSQ>(sring + ch * TILE * KSQ, rq, tid);
     }
     tile_store_s<KSQ>(sk, rk, tid);
-    dstore(rdB, 0);
-    if (nkt > 2) dload(rdB, 2);
     __syncthreads();
   }
-  // tile kt: rdA holds tile kt + 1 when kt is even, rdB when odd; each is refilled with tile kt + 3 once stored
-  auto step = [&](int kt, uint4 (&rnext)[4]) {
+  // tile kt's fragments: fA when kt is even, fB when odd; refilled with tile kt + 2 after their last use
+  auto step = [&](int kt, uint4 (&fc)[4]) {
     if (kt + 1 < nkt) {                           // the next K tile and band chunk in flight under this tile's MFMAs
       tile_load<VEC>(p, b, (kt + 1) * TILE, kcol, rk, tid);
 #pragma unroll
@@ -671,18 +657,18 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dqs_kernel(AttnM p, RelP 
       const int off = 32 * (3 - wv) + 32 * mm;
       blk[mm] = sring + ((kt + (off >> 6)) % 3) * TILE * KSQ + (off & 63) * KSQ;
     }
-    // B fragments of dS^T (k order of an accumulator used as the B operand: element j of k-step s of key half t is
-    // key 32 t + 16 s + 8 (j >> 2) + 4 hh + (j & 3)): two 8-B runs of query ii's row each
     bf16x8 f[2][2];
+    const bool tail = kt * TILE + TILE > len;     // (uniform)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int q = 0; q < 4; ++q) {
+      bf16x8 e = __builtin_bit_cast(bf16x8, fc[q]);
+      if (tail) {
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16* rowp = dimg + ii * DSW + 32 * t + 16 * s2 + 4 * hh;
-        const uint2 lo = *reinterpret_cast<const uint2*>(rowp);
-        const uint2 hi = *reinterpret_cast<const uint2*>(rowp + 8);
-        f[t][s2] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        for (int j = 0; j < 8; ++j)
+          e[j] = kt * TILE + 32 * (q >> 1) + 16 * (q & 1) + 8 * (j >> 2) + 4 * hh + (j & 3) < len ? e[j] : (bf16)0.f;
       }
+      f[q >> 1][q & 1] = e;
+    }
     // K-term: dQ^T[d][q] += sum_key K[key][d] dS^T[key][q]
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -692,18 +678,15 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dqs_kernel(AttnM p, RelP 
         a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<KSQ>(sk, 32 * t + 16 * s2, 32, lane), f[t][s2], a1, 0, 0,
                                                      0);
       }
-    // band term: dS^T in band coordinates, bf16 image [i][j - i + 31] (zero elsewhere; the region's dS rows are all
-    // read -- LDS operations of a wave complete in order), then dQ^T[d][q] += sum_r' P_band[r'][d] dS_band^T[r'][q]
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int g = 0; g < 12; ++g) *reinterpret_cast<uint2*>(bcol + 48 * hh + 4 * g) = make_uint2(0, 0);
-    __builtin_amdgcn_wave_barrier();
+    // band term: dS^T in band coordinates, bf16 image [i][j - i + 31], then
+    // dQ^T[d][q] += sum_r' P_band[r'][d] dS_band^T[r'][q]
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int j = 0; j < 8; ++j) bsk[32 * t + 16 * s2 + 8 * (j >> 2) + 4 * hh + (j & 3)] = f[t][s2][j];
+    if (kt + 2 < nkt) dload(fc, kt + 2);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
@@ -714,18 +697,17 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dqs_kernel(AttnM p, RelP 
       e0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<KSQ>(bk, 16 * (s & 1), 0, lane), bfr, e0, 0, 0, 0);
       e1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<KSQ>(bk, 16 * (s & 1), 32, lane), bfr, e1, 0, 0, 0);
     }
+    __builtin_amdgcn_wave_barrier();   // this tile's band-image reads before the next tile's scatter
     if (kt + 1 < nkt) {
       __syncthreads();
       tile_store_s<KSQ>(sk, rk, tid);
       ring_chunk_store_s<KSQ>(sring + (kt % 3) * TILE * KSQ, rq, tid);
-      dstore(rnext, kt + 1);
-      if (kt + 3 < nkt) dload(rnext, kt + 3);
       __syncthreads();
     }
   };
   for (int kt = 0; kt < nkt; ++kt) {
-    if (kt & 1) step(kt, rdB);
-    else step(kt, rdA);
+    if (kt & 1) step(kt, fB);
+    else step(kt, fA);
   }
   __syncthreads();   // every wave's reads of the K tile / ring are done before the stages reuse their bytes
   float* st = reinterpret_cast<float*>(skr) + wv * 32 * 65;
