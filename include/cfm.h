@@ -431,7 +431,9 @@ int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* dout, const 
                         int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream);
 /* cfm_attn_bwd (d_ready 0) / cfm_attn_bwd_with_d (d_ready 1) with the projected-table gradient dpos written in
    dtype_dpos: CFM_F32, or CFM_BF16 on the rel-pos MFMA path (each fp32 column sum rounded as cfm_cast rounds
-   it -- the compute-dtype copy the dW_pos GEMM reads, without an fp32 dpos and a cast pass). */
+   it -- the compute-dtype copy the dW_pos GEMM reads, without an fp32 dpos and a cast pass).  d_ready bit 1 (round 6):
+   ws is the full cfm_attn_bwd_ws_bytes workspace (D, if ready, in its first B*H*T floats) -- the non-rel whole-head
+   path (T <= 384) then computes dQ from the dS^T its dK/dV kernel stores there (cfm_attn_bwd always does). */
 int cfm_attn_bwd_ex(const void* qkv, const void* o, const void* dout, const float* lse,
                     const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                     void* dqkv, void* dpos, int dtype_dpos, float* dpos_u, float* dpos_v, int B, int T,

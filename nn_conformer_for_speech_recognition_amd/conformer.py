@@ -342,10 +342,8 @@ def _mha_bwd(g, x, sv, P, R, cfg, seed, lens, grads, rgrads, side, g2=None, nxt=
     if wt is not None and d // H == 64 and cd == torch.bfloat16 and "rowdot" not in ops.DISABLED:
         # D = rowsum(dO * O) per head from the epilogue of the GEMM producing dO (no separate pass); rel-pos: written
         # into the head of the attention backward's workspace
-        if cfg.rel:
-            aws, Dh = ops.attn_ws(B, T, H, d // H, True, g4.device)
-        else:
-            Dh = torch.empty(B * H * T, device=g4.device, dtype=torch.float32)
+        # (the full workspace in both cases: the non-rel whole-head path keeps the dS^T its dQ pass reads there)
+        aws, Dh = ops.attn_ws(B, T, H, d // H, cfg.rel, g4.device)
         do = ops.linear_dgrad(g4, wout, wt=wt, rowdot=(o, Dh, T))
     else:
         Dh = None

@@ -407,10 +407,14 @@ __device__ __forceinline__ void store_acc_rows(const f32x16& a0, const f32x16& a
 // = (bh T + q) T2 + kj/2 (T2 = even T / 2; exact: didx < 2^33), so lanes kj and kj^1 share one 32-bit
 // hash per query: the even lane hashes the query of accumulator register r, the odd lane that of r + 1,
 // and one DPP swap hands each lane its partner's -- one hash per two elements, 32-bit index arithmetic.
+// dsT (round 6, may be null): pass 2 also stores dS^T (bf16, unscaled) key-major -- dsT[(b H + h)][key][query],
+// Tq x Tq per head (Tq = T rounded up to 32), four 8-B runs of consecutive queries per lane and step -- for
+// attn_bwd_dqs_head_kernel.  Key blocks at or past len store nothing (the consumer masks keys >= len).
 __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel(AttnM p, const bf16* __restrict__ dout,
                                                                                  const float* __restrict__ lse,
                                                                                  const float* __restrict__ Dg,
-                                                                                 bf16* __restrict__ dqkv) {
+                                                                                 bf16* __restrict__ dqkv,
+                                                                                 bf16* __restrict__ dsT) {
   const bool drop = p.drop_p > 0.f;
   if (drop) p.seed = salted_seed(p.seed, p.salt);
   const uint32_t dkey = drop_key(p.seed, 0), dthr = drop_thr(p.drop_p);
@@ -537,6 +541,16 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
         }
       }
       if (!kvalid) sf[0] = sf[1] = (bf16x8){0};
+      if (dsT) {   // registers 4g .. 4g+3 = queries q0 + 8g + 4hh + 0..3 of key kj
+        bf16* drow = dsT + ((long)(b * p.H + h) * Tq + kj) * Tq + q0 + 4 * hh;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const bf16x8& v = sf[g >> 1];
+          const int o = 4 * (g & 1);
+          bf16x4 w = {v[o], v[o + 1], v[o + 2], v[o + 3]};
+          *reinterpret_cast<uint2*>(drow + 8 * g) = __builtin_bit_cast(uint2, w);
+        }
+      }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm(sQall, q0 + 16 * s2, 0, lane), sf[s2], dk0, 0, 0, 0);
@@ -552,6 +566,83 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
     }
     store_acc_rows(dk0, dk1, p.scale, obase + p.HD, p.D3, k0w, nvalid, p.dk, v8, lane);
   }
+}
+
+// ------------------------------------------------------------------------------------ dQ from the stored dS^T
+// (round 6 default on the whole-head path when the caller passes the full workspace; cfm_attn_set_mode bit 10 keeps
+// attn_bwd_dq_head_kernel).  dq_i = scale * sum_j dS_ij k_j over the dS^T that attn_bwd_dkdv_wave_kernel stored:
+// 8 MFMAs per 64-key tile and wave, no score / softmax / dropout-hash / dO x V recompute.  grid (ceil(T/128), H, B),
+// 4 waves x 32 queries.  LDS: the K tile (192-B rows: its transposed fragment reads conflict free) and per wave the
+// tile's [64 keys][32 queries] dS^T slice (64-B rows, conflict free for the same reads); keys >= len zeroed on the way
+// in; after the loop the bytes hold the waves' f32 stages of the dq store.
+constexpr int DQH_KS = 96;
+constexpr int DQH_LDS = 4 * 32 * 65 * 4;
+static_assert(TILE * DQH_KS * 2 + 4 * TILE * 32 * 2 <= DQH_LDS, "dQ-from-dS LDS");
+__global__ __launch_bounds__(256, 2) void attn_bwd_dqs_head_kernel(AttnM p, const bf16* __restrict__ dsT,
+                                                                   bf16* __restrict__ dqkv) {
+  __shared__ __attribute__((aligned(16))) char sm[DQH_LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * 128 + wv * 32;
+  const int len = p.len[b];
+  const int Tq = (p.T + 31) / 32 * 32;
+  const int nkt = (len + TILE - 1) / TILE;
+  const bool qok = q0 < Tq;
+  bf16* sk = reinterpret_cast<bf16*>(sm);
+  bf16* simg = reinterpret_cast<bf16*>(sm + TILE * DQH_KS * 2) + wv * TILE * 32;
+  const bf16* dbase = dsT + (long)(b * p.H + h) * Tq * Tq + (qok ? q0 : 0);
+  const int kcol = p.HD + h * p.dk;
+  // the wave's dS^T slice of key tile kt: chunk idx = lane + 64 i -> key row idx >> 2, queries 8 (idx & 3) .. +7
+  uint4 rd[4], rk[2];
+  auto dload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = lane + 64 * i, key = kt * TILE + (idx >> 2);
+      rd[i] = qok && key < len ? *reinterpret_cast<const uint4*>(dbase + (long)key * Tq + 8 * (idx & 3))
+                               : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto dstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = lane + 64 * i;
+      *reinterpret_cast<uint4*>(simg + (idx >> 2) * 32 + 8 * (idx & 3)) = rd[i];
+    }
+  };
+  f32x16 a0 = (f32x16){0}, a1 = (f32x16){0};
+  if (nkt > 0) {
+    dload(0);
+    tile_load<false>(p, b, 0, kcol, rk, tid);
+    tile_store_s<DQH_KS>(sk, rk, tid);
+    dstore();
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) {                   // the next tile in flight under this one's MFMAs
+      dload(kt + 1);
+      tile_load<false>(p, b, (kt + 1) * TILE, kcol, rk, tid);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 bfr = trfrag_perm_s<32>(simg, 32 * t + 16 * s2, 0, lane);   // dS^T: k = keys, columns = queries
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<DQH_KS>(sk, 32 * t + 16 * s2, 0, lane), bfr, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<DQH_KS>(sk, 32 * t + 16 * s2, 32, lane), bfr, a1, 0, 0,
+                                                     0);
+      }
+    if (kt + 1 < nkt) {
+      __syncthreads();
+      tile_store_s<DQH_KS>(sk, rk, tid);
+      dstore();
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  float* st = reinterpret_cast<float*>(sm) + wv * 32 * 65;
+  if (q0 < p.T)
+    store_transposed(st, a0, a1, p.scale, dqkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, q0, min(32, p.T - q0), p.dk,
+                     lane);
 }
 
 size_t dkdv_wave_lds_bytes(int T, int waves) {
@@ -846,16 +937,23 @@ CFM_EXPORT int cfm_attn_fwd(const void* qkv, void* o, float* lse, const int32_t*
   return cfm::check_launch("cfm_attn_fwd");
 }
 
+// the whole-head backward's dS^T buffer (dQ from dS): after D in the full workspace
+static bool dsT_path(int T) { return use_head(T) && !(g_attn_mode & 1024); }
+static size_t d_slot_bytes(int B, int T, int H) { return ((size_t)B * H * T * sizeof(float) + 255) & ~(size_t)255; }
+static size_t dsT_bytes(int B, int T, int H) { const size_t tq = (size_t)cdiv(T, 32) * 32; return (size_t)B * H * tq * tq * 2; }
+
 CFM_EXPORT size_t cfm_attn_bwd_ws_bytes(int B, int T, int H, int dk, int rel, int dtype) {
   if (!use_mfma(dtype, rel ? (const void*)1 : nullptr, dk)) return cfm::attn_simt_ws_bytes(B, T, H);
   if (rel) return cfm::attn_rel_ws_bytes(B, T, H, dk);
+  if (dsT_path(T)) return d_slot_bytes(B, T, H) + dsT_bytes(B, T, H);
   return (size_t)B * H * T * sizeof(float);
 }
 
 static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const float* lse,
                          const int32_t* lengths, const void* pos, const float* pos_u, const float* pos_v,
                          void* dqkv, void* dpos, int dpos_dt, float* dpos_u, float* dpos_v, int B, int T, int H,
-                         int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream, bool d_ready) {
+                         int dk, int dtype, float drop_p, uint64_t seed, float* ws, void* stream, bool d_ready,
+                         bool full_ws) {
   CFM_REQUIRE(qkv && o && dout && lse && lengths && dqkv && ws, CFM_ERR_ARG, "null pointer");
   CFM_REQUIRE(B > 0 && T > 0 && H > 0 && dk > 0, CFM_ERR_SHAPE, "bad shape");
   CFM_REQUIRE(!pos || (pos_u && pos_v && dpos && dpos_u && dpos_v), CFM_ERR_ARG, "rel-pos grads need buffers");
@@ -881,13 +979,20 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
                                     T, H, dk, drop_p, seed, ws, s);
   p.qs = use_head(T) ? head_split(B, H, T) : 1;
   const int hwaves = cdiv(cdiv(T, 32), p.qs);
+  // dQ from the dS^T the dK/dV kernel stores: only when the caller passed the full workspace (cfm_attn_bwd, or
+  // cfm_attn_bwd_ex with d_ready bit 1; cfm_attn_bwd_with_d's ws may be D alone)
+  bf16* dsT = full_ws && dsT_path(T) ? reinterpret_cast<bf16*>(reinterpret_cast<char*>(ws) + d_slot_bytes(B, T, H))
+                                     : nullptr;
   if (use_head(T))
     hipLaunchKernelGGL(attn_bwd_dkdv_wave_kernel, dim3(B * H * p.qs), dim3(64 * hwaves), dkdv_wave_lds_bytes(T, hwaves),
-                       s, p, (const bf16*)dout, lse, ws, (bf16*)dqkv);
+                       s, p, (const bf16*)dout, lse, ws, (bf16*)dqkv, dsT);
   else
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse,
                        ws, (bf16*)dqkv);
-  if (use_head(T))
+  if (dsT)
+    hipLaunchKernelGGL(attn_bwd_dqs_head_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dsT,
+                       (bf16*)dqkv);
+  else if (use_head(T))
     hipLaunchKernelGGL(attn_bwd_dq_head_kernel, dim3(B * H * p.qs), dim3(64 * hwaves), head_lds_bytes(T, hwaves), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);
   else
@@ -901,7 +1006,7 @@ CFM_EXPORT int cfm_attn_bwd(const void* qkv, const void* o, const void* dout, co
                             void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
                             int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
   return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, CFM_F32, dpos_u, dpos_v, B, T, H, dk,
-                       dtype, drop_p, seed, ws, stream, false);
+                       dtype, drop_p, seed, ws, stream, false, true);
 }
 
 CFM_EXPORT int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* dout, const float* lse,
@@ -909,7 +1014,7 @@ CFM_EXPORT int cfm_attn_bwd_with_d(const void* qkv, const void* o, const void* d
                                    void* dqkv, float* dpos, float* dpos_u, float* dpos_v, int B, int T, int H, int dk,
                                    int dtype, float drop_p, uint64_t seed, float* ws, void* stream) {
   return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, CFM_F32, dpos_u, dpos_v, B, T, H, dk,
-                       dtype, drop_p, seed, ws, stream, true);
+                       dtype, drop_p, seed, ws, stream, true, false);
 }
 
 CFM_EXPORT int cfm_attn_bwd_ex(const void* qkv, const void* o, const void* dout, const float* lse,
@@ -918,7 +1023,7 @@ CFM_EXPORT int cfm_attn_bwd_ex(const void* qkv, const void* o, const void* dout,
                                int H, int dk, int dtype, float drop_p, uint64_t seed, int d_ready, float* ws,
                                void* stream) {
   return attn_bwd_impl(qkv, o, dout, lse, lengths, pos, pos_u, pos_v, dqkv, dpos, dtype_dpos, dpos_u, dpos_v, B, T, H,
-                       dk, dtype, drop_p, seed, ws, stream, d_ready != 0);
+                       dk, dtype, drop_p, seed, ws, stream, (d_ready & 1) != 0, (d_ready & 2) != 0);
 }
 
 CFM_EXPORT int cfm_attn_set_mode(int mode) {

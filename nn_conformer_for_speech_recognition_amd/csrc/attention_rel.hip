@@ -563,25 +563,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
 // bank quarters -- the 144-B rows the score kernels need for their b128 row fragments leave these reads 2-way
 // conflicted
 constexpr int KSQ = 96;
-// trfrag_perm with an explicit row stride (also the dpos kernel's)
-template <int STR>
-__device__ __forceinline__ bf16x8 trfrag_perm_s(const bf16* tile, int r0, int c0, int lane) {
-  const int hh = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
-  const bf16* base = tile + (r0 + 4 * hh + q) * STR + c0 + 16 * g1 + 4 * p4;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 8 * STR));
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-template <int STR>
-__device__ __forceinline__ void tile_store_s(bf16* t, const uint4 (&reg)[2], int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int v = tid + 256 * i;
-    *reinterpret_cast<uint4*>(t + (v >> 3) * STR + (v & 7) * 8) = reg[i];
-  }
-}
+// (trfrag_perm_s / tile_store_s: attn_common.h)
 template <int STR>
 __device__ __forceinline__ void ring_chunk_store_s(bf16* slot, const uint4 (&reg)[2], int tid) { tile_store_s<STR>(slot, reg, tid); }
 // The band image's row stride is an odd number of 8-B units (25: 100 elements): its 8-B fragment reads of the 32
@@ -1122,8 +1104,6 @@ constexpr int DP_R = 128;              // relative rows per workgroup
 constexpr int DP_KS = 160;
 constexpr int DP_PADL = 8;             // band image column of r' = 0 (r' = -7 .. 135 are written, 0 .. 127 read)
 constexpr int DP_CH = DP_R / 8 + 1;    // aligned 8-element dS chunks per row (17)
-
-// (trfrag_perm_s: trfrag_perm with an explicit row stride, defined with the dQ-from-dS kernel above)
 
 struct DposRegs {
   uint4 q[2];         // raw q rows (q + v is formed at store time: converting at load time waits for the load)

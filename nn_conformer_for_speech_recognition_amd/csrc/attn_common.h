@@ -94,6 +94,27 @@ __device__ __forceinline__ bf16x8 trfrag_perm(const bf16* tile, int r0, int c0, 
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// trfrag_perm with an explicit row stride (the dQ-from-dS kernels' conflict-free images, the rel-pos dpos kernel)
+template <int STR>
+__device__ __forceinline__ bf16x8 trfrag_perm_s(const bf16* tile, int r0, int c0, int lane) {
+  const int hh = lane >> 5, g1 = (lane >> 4) & 1, q = (lane & 15) >> 2, p4 = lane & 3;
+  const bf16* base = tile + (r0 + 4 * hh + q) * STR + c0 + 16 * g1 + 4 * p4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 8 * STR));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// a [64 rows][64 cols] register tile (tile_load) into LDS rows of STR elements
+template <int STR>
+__device__ __forceinline__ void tile_store_s(bf16* t, const uint4 (&reg)[2], int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + 256 * i;
+    *reinterpret_cast<uint4*>(t + (v >> 3) * STR + (v & 7) * 8) = reg[i];
+  }
+}
+
 // accumulator registers 8s..8s+7 -> bf16 B-operand fragment of k-step s
 __device__ __forceinline__ bf16x8 acc2frag(const f32x16& a, int s) {
   bf16x8 r;

@@ -808,6 +808,7 @@ def attn_bwd(qkv, o, dout, lse, lengths_i32, B, T, H, dk, pos=None, pos_u=None, 
     (linear_dgrad(rowdot=...)); bf16 MFMA path only.  Rel-pos: D must be the head of ws (attn_ws).
     dpos_dtype: torch.bfloat16 returns dpos already in the compute dtype (rel-pos MFMA path, cfm_attn_bwd_ex)."""
     rel = pos is not None
+    full = True     # ws is the whole cfm_attn_bwd_ws_bytes workspace (the non-rel whole-head path keeps dS^T there)
     if D is not None and ws is not None:
         if D.data_ptr() != ws.data_ptr():
             raise L.CfmError("attn_bwd: D must be the first B*H*T floats of ws")
@@ -815,20 +816,17 @@ def attn_bwd(qkv, o, dout, lse, lengths_i32, B, T, H, dk, pos=None, pos_u=None, 
         if rel:
             raise L.CfmError("attn_bwd: rel-pos with a precomputed D needs its workspace (attn_ws)")
         ws = D
+        full = False
     else:
         ws = workspace(L.size_call("cfm_attn_bwd_ws_bytes", B, T, H, dk, int(rel), L.dt(qkv)), qkv.device)
     dqkv = torch.empty_like(qkv)
     dpos = torch.empty(pos.shape, device=qkv.device, dtype=dpos_dtype) if rel else None
     dpu = torch.empty(H * dk, device=qkv.device, dtype=torch.float32) if rel else None
     dpv = torch.empty(H * dk, device=qkv.device, dtype=torch.float32) if rel else None
-    if rel and dpos_dtype != torch.float32:
-        L.call("cfm_attn_bwd_ex", L.ptr(qkv), L.ptr(o), L.ptr(dout), L.ptr(lse), L.ptr(lengths_i32), L.ptr(pos),
-               L.ptr(pos_u), L.ptr(pos_v), L.ptr(dqkv), L.ptr(dpos), L.dt(dpos), L.ptr(dpu), L.ptr(dpv), B, T, H, dk,
-               L.dt(qkv), float(drop_p), int(seed) & (2**64 - 1), int(D is not None), L.ptr(ws), L.stream())
-        return dqkv, dpos, dpu, dpv
-    L.call("cfm_attn_bwd_with_d" if D is not None else "cfm_attn_bwd", L.ptr(qkv), L.ptr(o), L.ptr(dout), L.ptr(lse),
-           L.ptr(lengths_i32), L.ptr(pos), L.ptr(pos_u), L.ptr(pos_v), L.ptr(dqkv), L.ptr(dpos), L.ptr(dpu), L.ptr(dpv),
-           B, T, H, dk, L.dt(qkv), float(drop_p), int(seed) & (2**64 - 1), L.ptr(ws), L.stream())
+    d_ready = (1 if D is not None else 0) | (2 if full else 0)
+    L.call("cfm_attn_bwd_ex", L.ptr(qkv), L.ptr(o), L.ptr(dout), L.ptr(lse), L.ptr(lengths_i32), L.ptr(pos),
+           L.ptr(pos_u), L.ptr(pos_v), L.ptr(dqkv), L.ptr(dpos), L.dt(dpos), L.ptr(dpu), L.ptr(dpv), B, T, H, dk,
+           L.dt(qkv), float(drop_p), int(seed) & (2**64 - 1), d_ready, L.ptr(ws), L.stream())
     return dqkv, dpos, dpu, dpv
 
 

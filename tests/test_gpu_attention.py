@@ -52,6 +52,30 @@ def test_attention_vs_torch(attn_mode, mode, B, T, H):
     assert _rel(dqkv.float(), rg) < 2e-2
 
 
+@pytest.mark.parametrize("B,T,H,dk,lens", [(2, 373, 4, 64, [373, 250]), (3, 97, 2, 64, [97, 40, 1]),
+                                         (2, 373, 4, 36, [373, 301]), (1, 384, 2, 64, [384]), (2, 130, 2, 64, [130, 65])])
+@pytest.mark.parametrize("drop_p", [0.0, 0.1])
+def test_dq_from_stored_ds_matches_recompute(attn_mode, B, T, H, dk, lens, drop_p):
+    """Whole-head backward: dQ from the dS^T the dK/dV kernel stores (default with the full workspace) against the
+    recomputing dQ kernel (cfm_attn_set_mode bit 10): dK / dV bit-identical (the same kernel, plus stores), dQ equal
+    up to the bf16 rounding of the stored dS (the recomputing kernel rounds the same values, in another order);
+    ragged lengths incl. a length-1 utterance and keys past len; dk 36 (Conformer-S); T 384 (Tq = T) and 130."""
+    g = torch.Generator().manual_seed(T + dk + H)
+    qkv = torch.randn(B * T, 3 * H * dk, generator=g).to(DEV, torch.bfloat16)
+    lt = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    do = torch.randn(B * T, H * dk, generator=g).to(DEV, torch.bfloat16)
+    o, lse = ops.attn_fwd(qkv, lt, B, T, H, dk, drop_p=drop_p, seed=3)
+    outs = []
+    for m in (1024, 0):
+        attn_mode(m)
+        dqkv, _, _, _ = ops.attn_bwd(qkv, o, do, lse, lt, B, T, H, dk, drop_p=drop_p, seed=3)
+        outs.append(dqkv.float().view(B * T, 3, H * dk))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][:, 1:], outs[1][:, 1:])
+    assert _rel(outs[1][:, 0], outs[0][:, 0]) < 5e-3
+    assert torch.isfinite(outs[1]).all()
+
+
 def test_attention_kernels_agree_under_dropout(attn_mode):
     B, T, H, dk = 2, 373, 2, 64
     g = torch.Generator().manual_seed(5)
