@@ -571,35 +571,44 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
 // ------------------------------------------------------------------------------------ dQ from the stored dS^T
 // (round 6 default on the whole-head path when the caller passes the full workspace; cfm_attn_set_mode bit 10 keeps
 // attn_bwd_dq_head_kernel).  dq_i = scale * sum_j dS_ij k_j over the dS^T that attn_bwd_dkdv_wave_kernel stored:
-// 8 MFMAs per 64-key tile and wave, no score / softmax / dropout-hash / dO x V recompute.  grid (ceil(T/128), H, B),
-// 4 waves x 32 queries.  LDS: the K tile (192-B rows: its transposed fragment reads conflict free) and per wave the
-// tile's [64 keys][32 queries] dS^T slice (64-B rows, conflict free for the same reads); keys >= len zeroed on the way
-// in; after the loop the bytes hold the waves' f32 stages of the dq store.
+// 8 MFMAs per 64-key tile and wave, no score / softmax / dropout-hash / dO x V recompute.  Whole-head layout like the
+// other head kernels: grid (B*H*qs), one wave per 32-query block; the head's K is staged once (192-B rows: the
+// transposed fragment reads are conflict free), then each wave streams its [64 keys][32 queries] dS^T slices through
+// a private 4 KiB LDS image (64-B rows, conflict free for the same reads; the next slice in registers while the
+// current one runs) -- no workgroup barrier inside the loop.  Keys >= len read as zero.  After the loop the LDS holds
+// the waves' f32 stages of the dq store.
 constexpr int DQH_KS = 96;
-constexpr int DQH_LDS = 4 * 32 * 65 * 4;
-static_assert(TILE * DQH_KS * 2 + 4 * TILE * 32 * 2 <= DQH_LDS, "dQ-from-dS LDS");
-__global__ __launch_bounds__(256, 2) void attn_bwd_dqs_head_kernel(AttnM p, const bf16* __restrict__ dsT,
-                                                                   bf16* __restrict__ dqkv) {
-  __shared__ __attribute__((aligned(16))) char sm[DQH_LDS];
+size_t dqs_head_lds_bytes(int T, int waves) {
+  const size_t tq = (size_t)cdiv(T, 32) * 32;
+  const size_t loop = tq * DQH_KS * 2 + (size_t)waves * TILE * 32 * 2, stage = (size_t)waves * 32 * 65 * 4;
+  return loop > stage ? loop : stage;
+}
+__global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dqs_head_kernel(AttnM p, const bf16* __restrict__ dsT,
+                                                                                bf16* __restrict__ dqkv) {
+  extern __shared__ __attribute__((aligned(16))) bf16 hsm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * 128 + wv * 32;
+  const HeadPart hp = head_part(p);
+  const int b = hp.b, h = hp.h;
   const int len = p.len[b];
-  const int Tq = (p.T + 31) / 32 * 32;
-  const int nkt = (len + TILE - 1) / TILE;
-  const bool qok = q0 < Tq;
-  bf16* sk = reinterpret_cast<bf16*>(sm);
-  bf16* simg = reinterpret_cast<bf16*>(sm + TILE * DQH_KS * 2) + wv * TILE * 32;
-  const bf16* dbase = dsT + (long)(b * p.H + h) * Tq * Tq + (qok ? q0 : 0);
-  const int kcol = p.HD + h * p.dk;
-  // the wave's dS^T slice of key tile kt: chunk idx = lane + 64 i -> key row idx >> 2, queries 8 (idx & 3) .. +7
-  uint4 rd[4], rk[2];
-  auto dload = [&](int kt) {
+  const int nq = (p.T + 31) / 32, Tq = nq * 32;
+  bf16* sK = hsm;
+  bf16* simg = hsm + (long)Tq * DQH_KS + wv * TILE * 32;
+  // the head's K rows [0, Tq) (rows >= T read as zero)
+  const bf16* kbase = p.qkv + (long)b * p.T * p.D3 + p.HD + h * p.dk;
+  for (int i = tid; i < Tq * 8; i += blockDim.x) {
+    const int row = i >> 3, c = (i & 7) * 8;
+    *reinterpret_cast<uint4*>(sK + row * DQH_KS + c) = ld8(kbase, p.D3, row, p.T, c, p.dk, p.vec, p.vec4);
+  }
+  __syncthreads();
+  const int q0 = (hp.blk0 + wv) * 32;
+  const int nkt = q0 < p.T ? (len + TILE - 1) / TILE : 0;
+  const bf16* dbase = dsT + (long)(b * p.H + h) * Tq * Tq + (q0 < Tq ? q0 : 0);
+  uint4 rd[4];
+  auto dload = [&](int kt) {   // chunk idx = lane + 64 i -> key row idx >> 2, queries 8 (idx & 3) .. +7
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = lane + 64 * i, key = kt * TILE + (idx >> 2);
-      rd[i] = qok && key < len ? *reinterpret_cast<const uint4*>(dbase + (long)key * Tq + 8 * (idx & 3))
-                               : make_uint4(0, 0, 0, 0);
+      rd[i] = key < len ? *reinterpret_cast<const uint4*>(dbase + (long)key * Tq + 8 * (idx & 3)) : make_uint4(0, 0, 0, 0);
     }
   };
   auto dstore = [&]() {
@@ -612,34 +621,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dqs_head_kernel(AttnM p, cons
   f32x16 a0 = (f32x16){0}, a1 = (f32x16){0};
   if (nkt > 0) {
     dload(0);
-    tile_load<false>(p, b, 0, kcol, rk, tid);
-    tile_store_s<DQH_KS>(sk, rk, tid);
     dstore();
-    __syncthreads();
   }
   for (int kt = 0; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) {                   // the next tile in flight under this one's MFMAs
-      dload(kt + 1);
-      tile_load<false>(p, b, (kt + 1) * TILE, kcol, rk, tid);
-    }
+    if (kt + 1 < nkt) dload(kt + 1);
+    // (the slice's stores and these reads are one wave's LDS operations: in order)
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const bf16x8 bfr = trfrag_perm_s<32>(simg, 32 * t + 16 * s2, 0, lane);   // dS^T: k = keys, columns = queries
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<DQH_KS>(sk, 32 * t + 16 * s2, 0, lane), bfr, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<DQH_KS>(sk, 32 * t + 16 * s2, 32, lane), bfr, a1, 0, 0,
-                                                     0);
+        const int kr = kt * TILE + 32 * t + 16 * s2;
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<DQH_KS>(sK, kr, 0, lane), bfr, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag_perm_s<DQH_KS>(sK, kr, 32, lane), bfr, a1, 0, 0, 0);
       }
     if (kt + 1 < nkt) {
-      __syncthreads();
-      tile_store_s<DQH_KS>(sk, rk, tid);
+      __builtin_amdgcn_wave_barrier();
       dstore();
-      __syncthreads();
     }
   }
-  __syncthreads();
-  float* st = reinterpret_cast<float*>(sm) + wv * 32 * 65;
+  __syncthreads();   // every wave's reads of K and of its slice are done before the stages reuse the bytes
+  float* st = reinterpret_cast<float*>(hsm) + wv * 32 * 65;
   if (q0 < p.T)
     store_transposed(st, a0, a1, p.scale, dqkv + (long)b * p.T * p.D3 + h * p.dk, p.D3, q0, min(32, p.T - q0), p.dk,
                      lane);
@@ -990,8 +992,8 @@ static int attn_bwd_impl(const void* qkv, const void* o, const void* dout, const
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dout, lse,
                        ws, (bf16*)dqkv);
   if (dsT)
-    hipLaunchKernelGGL(attn_bwd_dqs_head_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, s, p, (const bf16*)dsT,
-                       (bf16*)dqkv);
+    hipLaunchKernelGGL(attn_bwd_dqs_head_kernel, dim3(B * H * p.qs), dim3(64 * hwaves), dqs_head_lds_bytes(T, hwaves), s,
+                       p, (const bf16*)dsT, (bf16*)dqkv);
   else if (use_head(T))
     hipLaunchKernelGGL(attn_bwd_dq_head_kernel, dim3(B * H * p.qs), dim3(64 * hwaves), head_lds_bytes(T, hwaves), s, p,
                        (const bf16*)dout, lse, ws, (bf16*)dqkv);
