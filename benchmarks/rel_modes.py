@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--modes", default="0")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--drop", type=float, default=0.1, help="attention dropout p (0: no hash in either pass)")
     a = ap.parse_args()
     modes = [int(m) for m in a.modes.split(",")]
     B, T, H, dk = 8, 1498, 8, 64
@@ -39,15 +40,15 @@ def main():
     pv = (0.3 * torch.randn(H * dk, generator=g)).cuda()
     do = torch.randn(B * T, H * dk, generator=g).to("cuda", torch.bfloat16)
     lens = torch.full((B,), T, dtype=torch.int32, device="cuda")
-    o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, pos, pu, pv, drop_p=0.1, seed=3)
+    o, lse = ops.attn_fwd(qkv, lens, B, T, H, dk, pos, pu, pv, drop_p=a.drop, seed=3)
     res = {}
     for _ in range(a.reps):
         for m in modes:
             _lib.call("cfm_attn_set_mode", m)
             res.setdefault(f"fwd mode {m}", []).append(
-                timeit(lambda: ops.attn_fwd(qkv, lens, B, T, H, dk, pos, pu, pv, drop_p=0.1, seed=3)))
+                timeit(lambda: ops.attn_fwd(qkv, lens, B, T, H, dk, pos, pu, pv, drop_p=a.drop, seed=3)))
             res.setdefault(f"bwd mode {m}", []).append(
-                timeit(lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, pos, pu, pv, drop_p=0.1, seed=3)))
+                timeit(lambda: ops.attn_bwd(qkv, o, do, lse, lens, B, T, H, dk, pos, pu, pv, drop_p=a.drop, seed=3)))
     _lib.call("cfm_attn_set_mode", 0)
     out = {}
     for k, v in res.items():
