@@ -579,8 +579,8 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dkdv_wave_kernel
 // the waves' f32 stages of the dq store.
 constexpr int DQH_KS = 96;
 size_t dqs_head_lds_bytes(int T, int waves) {
-  const size_t tq = (size_t)cdiv(T, 32) * 32;
-  const size_t loop = tq * DQH_KS * 2 + (size_t)waves * TILE * 32 * 2, stage = (size_t)waves * 32 * 65 * 4;
+  const size_t tk = (size_t)cdiv(T, TILE) * TILE;   // K rows: whole 64-key tiles (rows >= T zero)
+  const size_t loop = tk * DQH_KS * 2 + (size_t)waves * TILE * 32 * 2, stage = (size_t)waves * 32 * 65 * 4;
   return loop > stage ? loop : stage;
 }
 __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dqs_head_kernel(AttnM p, const bf16* __restrict__ dsT,
@@ -591,11 +591,12 @@ __global__ __launch_bounds__(64 * HEAD_TMAX / 32) void attn_bwd_dqs_head_kernel(
   const int b = hp.b, h = hp.h;
   const int len = p.len[b];
   const int nq = (p.T + 31) / 32, Tq = nq * 32;
+  const int Tk = (p.T + TILE - 1) / TILE * TILE;   // the last key tile's rows are all staged (zero past T)
   bf16* sK = hsm;
-  bf16* simg = hsm + (long)Tq * DQH_KS + wv * TILE * 32;
-  // the head's K rows [0, Tq) (rows >= T read as zero)
+  bf16* simg = hsm + (long)Tk * DQH_KS + wv * TILE * 32;
+  // the head's K rows [0, Tk) (rows >= T read as zero)
   const bf16* kbase = p.qkv + (long)b * p.T * p.D3 + p.HD + h * p.dk;
-  for (int i = tid; i < Tq * 8; i += blockDim.x) {
+  for (int i = tid; i < Tk * 8; i += blockDim.x) {
     const int row = i >> 3, c = (i & 7) * 8;
     *reinterpret_cast<uint4*>(sK + row * DQH_KS + c) = ld8(kbase, p.D3, row, p.T, c, p.dk, p.vec, p.vec4);
   }
