@@ -1211,13 +1211,15 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP r
   const int nit = (len > 0 && ihi >= ilo) ? (ihi - it0) / TILE + 1 : 0;
   // four register stages ahead of the LDS double buffer: step it issues tile it+3's loads, computes tile it from
   // LDS and stores tile it+1 (loaded two steps earlier) into the other buffer.  Every load and store is issued
-  // unconditionally (tile indices clamped to the last tile; the surplus steps of the 4-step unroll only skip their
-  // MFMAs, a branch with no memory operation in it), so the compiler's vmcnt waits stay counted -- a conditional
-  // load makes the wait at its join a vmcnt(0) that also waits for the prefetch.
+  // unconditionally (tile indices clamped to the last tile), so the compiler's vmcnt waits stay counted -- a
+  // conditional load makes the wait at its join a vmcnt(0) that also waits for the prefetch.  The 4-step unroll
+  // leaves the loop after the last tile (a workgroup-uniform exit, nothing in flight is needed after it): running the
+  // surplus steps of the last group (loads, band stores and a barrier each, ~1.5 of a workgroup's ~13 tiles at L60)
+  // cost 8 us of 106 (profiles/r06/misc/dpos_exit_ab.txt)
   auto tile_of = [&](int it) { return it0 + min(it, nit - 1) * TILE; };
   auto step = [&](int it, DposRegs& gl, const DposRegs& gs) {
     load(tile_of(it + 3), gl);
-    if (it < nit) {
+    {
       const int cur = it & 1;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -1232,17 +1234,17 @@ __global__ __launch_bounds__(256) void attn_rel_bwd_dpos3_kernel(AttnM p, RelP r
     lds_barrier();
   };
   if (nit > 0) {
-    DposRegs g0, g1, g2, g3;
-    load(tile_of(0), g0);
-    load(tile_of(1), g1);
-    load(tile_of(2), g2);
-    store(0, tile_of(0), g0);
+    DposRegs g[4];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) load(tile_of(k), g[k]);
+    store(0, tile_of(0), g[0]);
     lds_barrier();
     for (int it = 0; it < nit; it += 4) {
-      step(it, g3, g1);
-      step(it + 1, g0, g2);
-      step(it + 2, g1, g3);
-      step(it + 3, g2, g0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {   // (this form keeps the stages in VGPRs; breaks between four named
+        if (k > 0 && it + k >= nit) break;   // stages pushed ~100 registers into AGPRs: one wave per SIMD)
+        step(it + k, g[(k + 3) & 3], g[(k + 1) & 3]);
+      }
     }
   }
   // acc0/acc1: rows d (32 dh + acc_row), lanes rr (64 rq + 32 j + lane&31) -> sO[rr][d] -> the partial rows
