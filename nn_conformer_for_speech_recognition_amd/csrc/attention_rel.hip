@@ -554,7 +554,8 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dq2_kernel(AttnM p, RelP 
 // grid (ceil(T/128), H, B), 4 waves x 32 queries; LDS: the K tile, a ring of 3 band chunks (as dQ2), and per wave
 // the band-coordinate image of dS^T ([query][SBQ] bf16, as dQ2, zeroed once); the dS fragments come straight from
 // the buffer into registers (two 8-B loads per fragment, one tile ahead): the kernel is bound by its LDS instruction
-// count, not by bank conflicts (PMC, profiles/r06/misc/rel_dq_from_ds_ab.txt).  After the loop the K tile + ring
+// count, not by bank conflicts (PMC, profiles/r06/misc/rel_dq_from_ds_ab.txt); the band scatter is 32 explicit 2-byte
+// stores per tile (merged by the compiler, they were misaligned 8-B stores, slower).  After the loop the K tile + ring
 // bytes hold the waves' f32 stages of the du / dv sums and the dq store.
 // dS entries of keys >= len are not defined in the buffer (the dK/dV kernel leaves them unmasked or unwritten):
 // they are replaced by zeros on the way into LDS.  part: as dQ2.
@@ -590,7 +591,7 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dqs_kernel(AttnM p, RelP 
   char* wreg = swv + wv * DQS_WAVE;
   bf16* bimg = reinterpret_cast<bf16*>(wreg);      // [query][SBQ] band image of dS^T
   bf16* bcol = bimg + ii * SBQ;
-  bf16* bsk = bcol + 31 - ii;                       // band position of key k (0..63) of query ii: bsk[k]
+  // band position of key k (0..63) of query ii: bcol[31 - ii + k]
   // every tile writes the same band positions of a row (k + 31 - ii, k = 0..63): the rest stay zero from here
 #pragma unroll
   for (int g = 0; g < 12; ++g) *reinterpret_cast<uint2*>(bcol + 48 * hh + 4 * g) = make_uint2(0, 0);
@@ -665,9 +666,20 @@ __global__ __launch_bounds__(256, 2) void attn_rel_bwd_dqs_kernel(AttnM p, RelP 
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+      for (int s2 = 0; s2 < 2; ++s2) {
+        // explicit 2-byte stores (volatile, from the packed words): the plain element stores were merged by the
+        // compiler into ds_write_b64 at 2-byte-aligned addresses, which the LDS runs slower (dQ 140.5 vs 132.9 us
+        // at L60, profiles/r06/misc/rel_dqs_b16_ab.txt)
+        typedef volatile __attribute__((address_space(3))) unsigned short lds_u16;
+        lds_u16* d = reinterpret_cast<lds_u16*>((__attribute__((address_space(3))) char*)swv + wv * DQS_WAVE) +
+                     ii * SBQ + 31 - ii;
+        const uint4 w = __builtin_bit_cast(uint4, f[t][s2]);
+        const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) bsk[32 * t + 16 * s2 + 8 * (j >> 2) + 4 * hh + (j & 3)] = f[t][s2][j];
+        for (int j = 0; j < 8; ++j)
+          d[32 * t + 16 * s2 + 8 * (j >> 2) + 4 * hh + (j & 3)] =
+              (unsigned short)((j & 1) ? (wd[j >> 1] >> 16) : (wd[j >> 1] & 0xFFFFu));
+      }
     if (kt + 2 < nkt) dload(fc, kt + 2);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
