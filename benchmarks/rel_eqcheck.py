@@ -1,7 +1,7 @@
 """Bit-identity of the rel-pos attention backward across cfm_attn_set_mode values (the first mode is compared
 with the second and with the last):  python benchmarks/rel_eqcheck.py 0,MODE[,MODE2]"""
-import sys, torch
-sys.path.insert(0, '.')
+import os, sys, torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nn_conformer_for_speech_recognition_amd import _lib, ops
 modes = [int(m) for m in sys.argv[1].split(',')]
 for (B, T, H, lens) in [(2, 1498, 3, [1498, 1001]), (3, 373, 2, [373, 300, 41]), (2, 64, 1, [64, 1]), (9, 130, 2, [130] * 8 + [77])]:
