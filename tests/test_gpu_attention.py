@@ -211,6 +211,30 @@ def test_rel_dpos_xcd_kernel_matches_round4(attn_mode, B, T, H, lens):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("B,T,H,lens", [(2, 373, 2, [373, 250]), (2, 1498, 2, [1498, 1001]), (3, 130, 2, [130, 77, 1])])
+@pytest.mark.parametrize("drop_p", [0.0, 0.1])
+def test_rel_dq_from_stored_ds_matches_recompute(attn_mode, B, T, H, lens, drop_p):
+    """Rel-pos backward: dQ from the dS the dK/dV kernel stores (attn_rel_bwd_dqs_kernel, default; its band scatter is
+    explicit 2-byte LDS stores) against the recomputing dQ2 kernel (cfm_attn_set_mode bit 9): dK / dV and dpos
+    bit-identical (the same kernels), dQ and the u / v gradients equal up to the bf16 rounding of the stored dS;
+    ragged lengths incl. a length-1 utterance, T 1498 (L60)."""
+    dk = 64
+    qkv, pos, pu, pv, do, ln = _rel_case(B, T, H, dk, lens, 13)
+    o, lse = ops.attn_fwd(qkv, ln, B, T, H, dk, pos, pu, pv, drop_p=drop_p, seed=5)
+    outs = []
+    for m in (512, 0):
+        attn_mode(m)
+        dqkv, dpos, dpu, dpv = ops.attn_bwd(qkv, o, do, lse, ln, B, T, H, dk, pos, pu, pv, drop_p=drop_p, seed=5)
+        outs.append((dqkv.float().view(B * T, 3, H * dk), dpos.float(), dpu.float(), dpv.float()))
+    torch.cuda.synchronize()
+    (r, rpos, ru, rv), (n, npos, nu, nv) = outs
+    assert torch.isfinite(n).all() and torch.isfinite(npos).all()
+    assert torch.equal(r[:, 1:], n[:, 1:])
+    assert torch.equal(rpos, npos)
+    assert _rel(n[:, 0], r[:, 0]) < 5e-3
+    assert _rel(nu, ru) < 5e-3 and _rel(nv, rv) < 5e-3
+
+
 # ------------------------------------------------------------------------------------ dropout masks, read back
 def _keep(B, T, H, p, seed):
     """numpy restatement of the attention-dropout keep mask (cfm_common.h attn_mix / drop_key, attn_common.h
